@@ -1,0 +1,229 @@
+/*
+ * crgc.h — C ABI of the MI355X-native CRGC garbage-detection hot path.
+ *
+ * This is the drop-in boundary for the reference's `ShadowGraph`
+ * (uigc-akka, src/main/java/edu/illinois/osl/uigc/engines/crgc/ShadowGraph.java).
+ * `LocalGC` (src/main/scala/.../crgc/LocalGC.scala:58) constructs a ShadowGraph
+ * and calls exactly the methods listed below; each entry point names the
+ * reference method it replaces.  A JVM binds these through a ~100-line JNI shim
+ * (see INTEGRATION.md); tests and the bench bind them through Python ctypes.
+ *
+ * Conventions
+ *  - Every function returns 0 (CRGC_OK) or a negative CRGC_E_* code.  Nothing
+ *    throws or aborts across the ABI.
+ *  - One caller thread per handle (LocalGC is a single actor on a
+ *    PinnedDispatcher: CRGC.scala:54-58, reference.conf:11-14).
+ *  - Actor identity: the JVM interns each ActorRef to a uint64 id.  The top 16
+ *    bits of the id are the actor's location (the interned akka Address,
+ *    `ref.path().address()`, ShadowGraph.java:49); the low 48 bits are free.
+ *    Ids CRGC_NO_ACTOR and CRGC_DEAD_ACTOR (and location 0xFFFF) are reserved.
+ *  - Input buffers are caller-owned and only read during the call (the
+ *    reference recycles an Entry right after merging it: LocalGC.scala:167-169).
+ *    `memory` says whether their pointers are host or device (HBM) pointers.
+ *  - Merges are stream-ordered and asynchronous with respect to the host; a
+ *    trace (and every query) synchronises.  Merges between two traces commute
+ *    except for the last-write-wins fields, which follow call order and then
+ *    record order inside a call — exactly the order the reference would have
+ *    applied them in.
+ */
+#ifndef CRGC_H
+#define CRGC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CRGC_ABI_VERSION 1u
+
+/* ---- status codes ------------------------------------------------------- */
+#define CRGC_OK 0
+#define CRGC_E_INVAL (-1)          /* bad argument, reserved id, > F records   */
+#define CRGC_E_NOMEM (-2)          /* device or host allocation failed         */
+#define CRGC_E_DEVICE (-3)         /* a HIP call failed                        */
+#define CRGC_E2BIG (-4)            /* output buffer too small; sizes written   */
+#define CRGC_E_NULL_SUPERVISOR (-5)/* reference NPE, ShadowGraph.java:277      */
+#define CRGC_E_UNDO_NEW_SHADOW (-6)/* reference CME, ShadowGraph.java:162,170  */
+#define CRGC_E_POISONED (-7)       /* handle unusable after a device fault     */
+#define CRGC_E_TIMEOUT (-8)        /* a bounded device spin gave up            */
+
+/* ---- reserved ids ------------------------------------------------------- */
+#define CRGC_NO_ACTOR ((uint64_t)0xFFFFFFFFFFFFFFFFull)   /* Java null        */
+/* A supervisor that points at a removed (collected) shadow incarnation.  Only
+ * appears in crgc_export output; it is non-null for the NPE test. */
+#define CRGC_DEAD_ACTOR ((uint64_t)0xFFFFFFFFFFFFFFFEull)
+#define CRGC_LOCATION_OF(id) ((uint16_t)((uint64_t)(id) >> 48))
+
+/* ---- where a batch lives ----------------------------------------------- */
+#define CRGC_MEM_HOST 0u   /* pageable or pinned host memory (copied H2D)   */
+#define CRGC_MEM_DEVICE 1u /* device pointers on the handle's GPU            */
+
+/* ---- vertex flag bits, as exported ------------------------------------ */
+#define CRGC_F_INTERNED 0x02u
+#define CRGC_F_LOCAL 0x04u
+#define CRGC_F_BUSY 0x08u
+#define CRGC_F_ROOT 0x10u
+#define CRGC_F_HALTED 0x20u
+
+/* Entry.isBusy / Entry.isRoot bits in crgc_entry_batch.flags */
+#define CRGC_ENTRY_BUSY 0x01u
+#define CRGC_ENTRY_ROOT 0x02u
+/* DeltaShadow.interned / isRoot / isBusy bits in crgc_delta_batch.flags */
+#define CRGC_DELTA_INTERNED 0x01u
+#define CRGC_DELTA_ROOT 0x02u
+#define CRGC_DELTA_BUSY 0x04u
+
+typedef struct crgc_graph crgc_graph; /* opaque; owns the HBM shadow graph */
+
+typedef struct crgc_config {
+  uint32_t abi_version;        /* CRGC_ABI_VERSION                          */
+  int32_t device;              /* HIP device ordinal                        */
+  uint32_t entry_field_size;   /* F, uigc.crgc.entry-field-size (default 4) */
+  uint32_t delta_graph_size;   /* uigc.crgc.delta-graph-size (default 64)   */
+  uint64_t vertex_capacity;    /* hint: expected live shadows               */
+  uint64_t edge_capacity;      /* hint: expected live (owner,target) pairs  */
+  void *stream;                /* hipStream_t to run on; NULL = own stream  */
+} crgc_config;
+
+/*
+ * A batch of Entry records in queue order (Entry.java:5-37, filled by
+ * State.flushToEntry, State.java:90-124).  Record order is the order in which
+ * LocalGC would have polled them (LocalGC.scala:152-172).
+ * Per entry i the created/spawned/updated records are the half-open ranges
+ * [x_off[i], x_off[i+1]) of the flat arrays — the reference's null-terminated
+ * prefixes of F-slot arrays (ShadowGraph.java:86,97,108).
+ */
+typedef struct crgc_entry_batch {
+  uint64_t n_entries;
+  const uint64_t *self;           /* [n]   Entry.self                       */
+  const int16_t *recv_count;      /* [n]   Entry.recvCount                  */
+  const uint8_t *flags;           /* [n]   CRGC_ENTRY_BUSY | CRGC_ENTRY_ROOT */
+  const uint32_t *created_off;    /* [n+1]                                  */
+  const uint64_t *created_owner;  /* Entry.createdOwners                    */
+  const uint64_t *created_target; /* Entry.createdTargets                   */
+  const uint32_t *spawned_off;    /* [n+1]                                  */
+  const uint64_t *spawned;        /* Entry.spawnedActors                    */
+  const uint32_t *updated_off;    /* [n+1]                                  */
+  const uint64_t *updated_ref;    /* Entry.updatedRefs                      */
+  const int16_t *updated_info;    /* Entry.updatedInfos (RefobInfo word)    */
+  uint32_t memory;                /* CRGC_MEM_HOST / CRGC_MEM_DEVICE        */
+} crgc_entry_batch;
+
+/*
+ * A batch of DeltaGraph shadows, concatenated in arrival order and, inside one
+ * DeltaGraph, in compressed-id order (ShadowGraph.java:131).  The host decodes
+ * the compressed ids through DeltaGraph.decoder() (DeltaGraph.java:162-169).
+ */
+typedef struct crgc_delta_batch {
+  uint64_t n_shadows;
+  const uint64_t *id;          /* [n] decoder[i]                            */
+  const int32_t *recv_count;   /* [n] DeltaShadow.recvCount                 */
+  const uint64_t *supervisor;  /* [n] decoder[supervisor] or CRGC_NO_ACTOR  */
+  const uint8_t *flags;        /* [n] CRGC_DELTA_*                          */
+  const uint32_t *out_off;     /* [n+1] DeltaShadow.outgoing ranges         */
+  const uint64_t *out_target;  /* decoder[key]                              */
+  const int32_t *out_count;    /* value                                     */
+  uint32_t memory;
+} crgc_delta_batch;
+
+/* An UndoLog (UndoLog.java:16-37) built on the host from delta graphs and
+ * ingress entries (UndoLog.java:39-93). */
+typedef struct crgc_undo_log {
+  uint16_t node_location;        /* UndoLog.nodeAddress                     */
+  uint16_t _pad[3];
+  uint64_t n_fields;
+  const uint64_t *actor;         /* [n] key of UndoLog.admitted             */
+  const int32_t *message_count;  /* [n] Field.messageCount                  */
+  const uint32_t *created_off;   /* [n+1] Field.createdRefs ranges          */
+  const uint64_t *created_target;
+  const int32_t *created_count;
+  uint32_t memory;
+} crgc_undo_log;
+
+typedef struct crgc_trace_stats {
+  uint64_t pseudo_roots;   /* shadows passing isPseudoRoot (:201-203)       */
+  uint64_t edges_scanned;  /* nonzero out-edges of marked non-halted shadows */
+  uint64_t sup_edges;      /* supervisor edges followed (:258-267)          */
+  uint64_t levels;         /* BFS levels run                                */
+  double ms_mark;          /* device time: pseudo-roots + mark              */
+  double ms_sweep;         /* device time: sweep + id compaction            */
+  double ms_total;         /* host wall time of crgc_trace                  */
+} crgc_trace_stats;
+
+typedef struct crgc_trace_out {
+  uint64_t *garbage_ids;   /* caller buffer or NULL (count only)            */
+  uint64_t garbage_cap;
+  uint64_t n_garbage;      /* TracingEvent.numGarbageActors (:275)          */
+  uint64_t *kill_ids;      /* actors told StopMsg (:277-278)                */
+  uint64_t kill_cap;
+  uint64_t n_kill;
+  uint64_t n_live;         /* TracingEvent.numLiveActors (:282)             */
+  crgc_trace_stats stats;
+} crgc_trace_out;
+
+/* Full graph state, for parity tests and debugging (the reference's
+ * ShadowGraph.assertEquals / Shadow.assertEquals, ShadowGraph.java:176-199).
+ * Two-phase: call with NULL arrays to learn n_vertices / n_edges. */
+typedef struct crgc_graph_export {
+  uint64_t vertex_cap, n_vertices;
+  uint64_t *id;
+  int32_t *recv_count;
+  uint8_t *flags;          /* CRGC_F_* bits                                 */
+  uint64_t *supervisor;    /* id, CRGC_NO_ACTOR or CRGC_DEAD_ACTOR          */
+  uint64_t edge_cap, n_edges; /* nonzero counts to live incarnations only   */
+  uint64_t *edge_owner;
+  uint64_t *edge_target;
+  int32_t *edge_count;
+} crgc_graph_export;
+
+/* ShadowGraph(Context) — ShadowGraph.java:17-21 */
+int crgc_create(const crgc_config *cfg, crgc_graph **out);
+void crgc_destroy(crgc_graph *g);
+
+/* N x ShadowGraph.mergeEntry(Entry) — ShadowGraph.java:75-125,
+ * called from LocalGC Wakeup (LocalGC.scala:152-172). */
+int crgc_merge_entries(crgc_graph *g, const crgc_entry_batch *batch);
+
+/* N x ShadowGraph.mergeDelta(DeltaGraph) — ShadowGraph.java:127-156,
+ * called on DeltaMsg (LocalGC.scala:124-136). */
+int crgc_merge_deltas(crgc_graph *g, const crgc_delta_batch *batch);
+
+/* ShadowGraph.mergeUndoLog(UndoLog) — ShadowGraph.java:158-174,
+ * called when an undo log is ready (LocalGC.scala:254-263).
+ * Returns CRGC_E_UNDO_NEW_SHADOW, without mutating the graph, where the
+ * reference would throw ConcurrentModificationException. */
+int crgc_merge_undo(crgc_graph *g, const crgc_undo_log *log);
+
+/* ShadowGraph.trace(shouldKill) — ShadowGraph.java:205-289.
+ * Writes garbage and kill ids (sets; order unspecified) and the counts.
+ * Returns CRGC_E_NULL_SUPERVISOR, without mutating the graph, where the
+ * reference would throw NullPointerException (:277).  On CRGC_E2BIG the trace
+ * HAS happened; n_garbage / n_kill hold the sizes and crgc_last_trace copies
+ * the retained lists into larger buffers. */
+int crgc_trace(crgc_graph *g, int should_kill, crgc_trace_out *out);
+int crgc_last_trace(crgc_graph *g, crgc_trace_out *out);
+
+/* ShadowGraph.startWave() — ShadowGraph.java:291-299: ids to tell WaveMsg. */
+int crgc_local_roots(crgc_graph *g, uint64_t *out, uint64_t cap, uint64_t *n);
+
+/* ShadowGraph.investigateRemotelyHeldActors(Address) — ShadowGraph.java:302-330,
+ * called from LocalGC.scala:234,276. */
+int crgc_count_reachable_from(crgc_graph *g, uint16_t location, int64_t *out);
+
+/* ShadowGraph.totalActorsSeen — ShadowGraph.java:12,46; LocalGC.scala:273. */
+int crgc_total_actors_seen(crgc_graph *g, uint64_t *out);
+
+/* Number of shadows in the graph (|from| == |shadowMap|). */
+int crgc_live_count(crgc_graph *g, uint64_t *out);
+
+int crgc_export(crgc_graph *g, crgc_graph_export *out);
+
+/* Human-readable text for a status code. */
+const char *crgc_strerror(int code);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+#endif /* CRGC_H */

@@ -1,0 +1,33 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for sub in ("uigc-akka_amd", "workload", "oracle", "tests"):
+    p = os.path.join(REPO, sub)
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+    config.addinivalue_line("markers", "slow: long-running parity case")
+
+
+@pytest.fixture(scope="session")
+def oracle_mod():
+    import oracle
+    oracle.build()
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def hip_mod():
+    """The HIP product path.  Fails loudly if the extension or GPU is missing."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test collected on a host without a GPU")
+    import crgc_hip
+    crgc_hip.abi.load_library()
+    return crgc_hip

@@ -1,0 +1,146 @@
+"""Parity of the HIP shadow graph against the CPU oracle (bit-exact sets/state).
+
+Every test drives the product through its C ABI (crgc_hip.ShadowGraph ->
+libcrgc_hip.so) and checks it against oracle.OracleGraph on the same stream.
+"""
+import numpy as np
+import pytest
+
+import fuzz
+import kats
+from crgc_hip import abi
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(hip_mod, oracle_mod, **kw):
+    return hip_mod.ShadowGraph(**kw), oracle_mod.OracleGraph()
+
+
+def _same_trace(rh, ro):
+    assert rh.garbage_set() == ro.garbage_set()
+    assert rh.kill_set() == ro.kill_set()
+    assert len(rh.garbage) == len(ro.garbage), "duplicate garbage ids"
+    assert len(rh.kill) == len(ro.kill), "duplicate kill ids"
+    assert rh.n_live == ro.n_live
+    assert rh.pseudo_roots == ro.pseudo_roots
+    assert rh.sup_edges == ro.sup_edges
+
+
+@pytest.mark.parametrize("name", sorted(kats.SCENARIOS))
+def test_kat_scenarios_on_hip(hip_mod, name):
+    g = hip_mod.ShadowGraph()
+    kats.run_scenario(g, kats.SCENARIOS[name]())
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_random_spec_on_hip(hip_mod, oracle_mod, seed):
+    g = hip_mod.ShadowGraph()
+    collected, everyone = kats.run_random(g, seed=seed, max_actors=400)
+    assert collected == everyone
+
+
+def test_random_spec_hip_matches_oracle_every_wakeup(hip_mod, oracle_mod):
+    w = kats.RandomWorld(seed=7, max_actors=600, wake_every=13)
+    h, o = _pair(hip_mod, oracle_mod)
+    for batch in w.steps():
+        h.merge_entries(batch)
+        o.merge_entries(batch)
+        assert h.export() == o.export()
+        rh, ro = h.trace(True), o.trace(True)
+        _same_trace(rh, ro)
+        w.kill(ro.kill_set())
+    assert h.total_actors_seen() == o.total_actors_seen()
+
+
+@pytest.mark.parametrize("seed,cap", [(11, 0), (12, 0), (13, 64)])
+def test_fuzz_entries_deltas_undo(hip_mod, oracle_mod, seed, cap):
+    # cap=64 starts from a tiny graph so rebuilds (compaction) happen often
+    h, o = _pair(hip_mod, oracle_mod, vertex_capacity=cap, edge_capacity=cap)
+    fz = fuzz.Fuzz(seed)
+    for step in range(14):
+        eb = fz.entries(200 + 50 * step)
+        h.merge_entries(eb); o.merge_entries(eb)
+        if step % 2 == 1:
+            db = fz.deltas(5)
+            h.merge_deltas(db); o.merge_deltas(db)
+        if step == 9:
+            ub = fz.undo(o.export().vertices.keys())
+            h.merge_undo(ub); o.merge_undo(ub)
+        st = o.export()
+        assert h.export() == st
+        for loc in (1, 2, 3):
+            assert h.count_reachable_from(loc) == o.count_reachable_from(loc)
+        assert sorted(h.startWave().tolist()) == sorted(o.local_roots().tolist())
+        rh, ro = h.trace(True), o.trace(True)
+        _same_trace(rh, ro)
+        fz.sync(o.export())
+    assert h.total_actors_seen() == o.total_actors_seen()
+    assert h.export() == o.export()
+
+
+def test_should_kill_false_reports_garbage_but_no_kills(hip_mod, oracle_mod):
+    h, o = _pair(hip_mod, oracle_mod)
+    for st in kats.simple_actor():
+        if st[0] == "merge":
+            h.merge_entries(st[1]); o.merge_entries(st[1])
+        else:
+            rh, ro = h.trace(False), o.trace(False)
+            _same_trace(rh, ro)
+            assert len(rh.kill) == 0
+
+
+def test_null_supervisor_is_reported_like_the_reference_npe(hip_mod, oracle_mod):
+    from crgc_hip import Entry, EntryBatch
+    # A local, non-root actor that was never spawned and is not referenced.
+    a = (1 << 48) | 77
+    b = EntryBatch.from_entries([Entry(self=a)])
+    h, o = _pair(hip_mod, oracle_mod)
+    h.merge_entries(b); o.merge_entries(b)
+    with pytest.raises(abi.CrgcError) as eo:
+        o.trace(True)
+    assert eo.value.code == abi.E_NULL_SUPERVISOR
+    with pytest.raises(abi.CrgcError) as eh:
+        h.trace(True)
+    assert eh.value.code == abi.E_NULL_SUPERVISOR
+
+
+def test_undo_naming_unknown_actor_is_reported_like_the_reference_cme(hip_mod, oracle_mod):
+    from crgc_hip import Entry, EntryBatch, UndoBatch
+    r = (1 << 48) | 1
+    b = EntryBatch.from_entries([Entry(self=r, isRoot=True, createdOwners=[r], createdTargets=[r])])
+    h, o = _pair(hip_mod, oracle_mod)
+    h.merge_entries(b); o.merge_entries(b)
+    log = UndoBatch.from_fields(3, [(r, 1, [((3 << 48) | 9, 1)])])
+    for g in (h, o):
+        with pytest.raises(abi.CrgcError) as e:
+            g.merge_undo(log)
+        assert e.value.code == abi.E_UNDO_NEW_SHADOW
+    assert h.export() == o.export()  # nothing was applied
+
+
+def test_reserved_ids_are_rejected(hip_mod):
+    from crgc_hip import Entry, EntryBatch
+    g = hip_mod.ShadowGraph()
+    g.merge_entries(EntryBatch.from_entries([Entry(self=abi.NO_ACTOR)]))
+    with pytest.raises(abi.CrgcError) as e:
+        g.trace(True)
+    assert e.value.code == abi.E_INVAL
+
+
+def test_device_resident_batches(hip_mod, oracle_mod):
+    w = kats.RandomWorld(seed=3, max_actors=300, wake_every=17)
+    h, o = _pair(hip_mod, oracle_mod)
+    for batch in w.steps():
+        h.merge_entries(batch.to_device())
+        o.merge_entries(batch)
+        _same_trace(h.trace(True), o.trace(True))
+
+
+def test_empty_graph_and_empty_batches(hip_mod, oracle_mod):
+    from crgc_hip import EntryBatch, DeltaBatch
+    h, o = _pair(hip_mod, oracle_mod)
+    h.merge_entries(EntryBatch.empty()); o.merge_entries(EntryBatch.empty())
+    h.merge_deltas(DeltaBatch.from_rows([])); o.merge_deltas(DeltaBatch.from_rows([]))
+    _same_trace(h.trace(True), o.trace(True))
+    assert h.live_count() == 0

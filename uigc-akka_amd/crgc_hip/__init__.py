@@ -1,0 +1,12 @@
+"""crgc_hip — MI355X-native CRGC garbage-detection hot path.
+
+The product is the C-ABI shared library built from ../csrc (libcrgc_hip.so,
+HIP kernels for gfx950); this package is its host-side mirror of the reference
+ShadowGraph surface (ShadowGraph.java), bound through ctypes.
+"""
+from . import abi
+from .batch import Entry, EntryBatch, DeltaBatch, UndoBatch, TraceResult, RefobInfo, GraphState
+from .graph import ShadowGraph
+
+__all__ = ["abi", "Entry", "EntryBatch", "DeltaBatch", "UndoBatch", "TraceResult", "RefobInfo",
+           "GraphState", "ShadowGraph"]

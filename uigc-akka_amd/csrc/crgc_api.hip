@@ -1,0 +1,808 @@
+// crgc_api.hip — the C ABI of include/crgc.h: host orchestration of the HBM
+// shadow graph.  One handle = one ShadowGraph (ShadowGraph.java:9-21).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "crgc_host.hpp"
+
+using namespace crgc;
+
+namespace {
+
+uint64_t pow2ceil(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
+
+struct Caps {
+  uint64_t scap, hcap, pcap, ecap;
+};
+
+// Device arrays of one graph generation.
+struct Arrays {
+  DevGraph d{};
+  Caps caps{};
+  bool allocated = false;
+};
+
+template <class T>
+hipError_t dmalloc(T **p, uint64_t n) {
+  return hipMalloc((void **)p, std::max<uint64_t>(n, 1) * sizeof(T));
+}
+
+void free_arrays(Arrays &a) {
+  if (!a.allocated) return;
+  DevGraph &d = a.d;
+  void *ps[] = {d.hkey, d.hval, d.vid, d.recv, d.flags, d.sup, d.adj, d.ecap, d.vseq, d.sseq,
+                d.enew, d.pool, d.ekey, d.eval, d.edelta, d.vis, d.front[0], d.front[1],
+                d.dirty[0], d.dirty[1], d.out_a, d.out_b};
+  for (void *p : ps)
+    if (p) hipFree(p);
+  a.allocated = false;
+  a.d = DevGraph{};
+}
+
+hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s) {
+  a.caps = c;
+  DevGraph &d = a.d;
+  d = DevGraph{};
+  d.hcap = c.hcap;
+  d.hmask = c.hcap - 1;
+  d.scap = c.scap;
+  d.pcap = c.pcap;
+  d.ecap_tab = c.ecap;
+  d.emask = c.ecap - 1;
+  d.ctr = ctr;
+  hipError_t e = hipSuccess;
+#define A(call)                         \
+  do {                                  \
+    if ((e = (call)) != hipSuccess) {   \
+      a.allocated = true;               \
+      free_arrays(a);                   \
+      return e;                         \
+    }                                   \
+  } while (0)
+  A(dmalloc(&d.hkey, c.hcap));
+  A(dmalloc(&d.hval, c.hcap));
+  A(dmalloc(&d.vid, c.scap));
+  A(dmalloc(&d.recv, c.scap));
+  A(dmalloc(&d.flags, c.scap));
+  A(dmalloc(&d.sup, c.scap));
+  A(dmalloc(&d.adj, c.scap));
+  A(dmalloc(&d.ecap, c.scap));
+  A(dmalloc(&d.vseq, c.scap));
+  A(dmalloc(&d.sseq, c.scap));
+  A(dmalloc(&d.enew, c.scap));
+  A(dmalloc(&d.pool, c.pcap));
+  A(dmalloc(&d.ekey, c.ecap));
+  A(dmalloc(&d.eval, c.ecap));
+  A(dmalloc(&d.edelta, c.ecap));
+  A(dmalloc(&d.vis, c.scap / 32));
+  A(dmalloc(&d.front[0], c.scap));
+  A(dmalloc(&d.front[1], c.scap));
+  A(dmalloc(&d.dirty[0], c.scap / BLK_SLOTS));
+  A(dmalloc(&d.dirty[1], c.scap / BLK_SLOTS));
+  A(dmalloc(&d.out_a, c.scap));
+  A(dmalloc(&d.out_b, c.scap));
+#undef A
+  a.allocated = true;
+  // Default state of every unused slot / bucket.
+  hipMemsetAsync(d.hkey, 0xFF, c.hcap * 8, s);
+  hipMemsetAsync(d.hval, 0xFF, c.hcap * 4, s);
+  hipMemsetAsync(d.recv, 0, c.scap * 4, s);
+  hipMemsetAsync(d.flags, 0, c.scap, s);
+  hipMemsetAsync(d.sup, 0xFF, c.scap * 4, s);
+  hipMemsetAsync(d.adj, 0, c.scap * 8, s);
+  hipMemsetAsync(d.ecap, 0, c.scap * 4, s);
+  hipMemsetAsync(d.vseq, 0, c.scap * 8, s);
+  hipMemsetAsync(d.sseq, 0, c.scap * 8, s);
+  hipMemsetAsync(d.enew, 0, c.scap * 4, s);
+  hipMemsetAsync(d.ekey, 0xFF, c.ecap * 8, s);
+  hipMemsetAsync(d.eval, 0xFF, c.ecap * 4, s);
+  hipMemsetAsync(d.edelta, 0, c.ecap * 4, s);
+  hipMemsetAsync(d.vis, 0, c.scap / 8, s);
+  hipMemsetAsync(d.front[0], 0, c.scap, s);
+  hipMemsetAsync(d.front[1], 0, c.scap, s);
+  hipMemsetAsync(d.dirty[0], 0, c.scap / BLK_SLOTS, s);
+  hipMemsetAsync(d.dirty[1], 0, c.scap / BLK_SLOTS, s);
+  return hipGetLastError();
+}
+
+Caps caps_for(uint64_t live, uint64_t edges, uint64_t ids_pending, uint64_t atoms_pending) {
+  Caps c;
+  c.scap = round_up(std::max<uint64_t>(2 * live + ids_pending, live + 2 * ids_pending) + 8192,
+                    BLK_SLOTS);
+  c.hcap = pow2ceil(c.scap * 3 / 2 + 1024);
+  uint64_t pc = 4 * edges + 8 * atoms_pending + 4 * c.scap + 65536;
+  c.pcap = std::min<uint64_t>(pc, 0xFFFFFFF0ull);
+  c.ecap = pow2ceil((edges + 2 * atoms_pending) * 3 / 2 + 65536);
+  return c;
+}
+
+#define CTR_OFF(f) offsetof(Counters, f)
+
+}  // namespace
+
+struct crgc_graph {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  uint32_t F = 4, DGS = 64;
+  Arrays g;
+  Counters *ctr = nullptr;   // device
+  Counters *hctr = nullptr;  // pinned host mirror
+  unsigned long long epoch = 0;
+  bool poisoned = false;
+  // exact values as of the last synchronisation + upper-bound increments since
+  uint64_t slot_top = 0, pool_top = 0, etab_used = 0, live = 0;
+  uint64_t ids_since = 0, atoms_since = 0;
+  uint64_t inserted_at_trace = 0;  // Counters::inserted when `live` was exact
+  Scratch stage, work;
+  hipEvent_t ev[4] = {};
+  // last trace
+  uint64_t last_garbage = 0, last_kill = 0, last_live = 0;
+  crgc_trace_stats last_stats{};
+  bool have_last = false;
+  uint64_t *roots_buf = nullptr;
+  uint64_t roots_cap = 0;
+};
+
+namespace {
+
+int map_hip(hipError_t e) {
+  if (e == hipSuccess) return CRGC_OK;
+  if (e == hipErrorOutOfMemory) return CRGC_E_NOMEM;
+  return CRGC_E_DEVICE;
+}
+
+#define HIP_TRY(x)                                  \
+  do {                                              \
+    hipError_t _e = (x);                            \
+    if (_e != hipSuccess) return map_hip(_e);       \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    hipGetDevice(&prev);
+    if (prev != dev) hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur;
+    hipGetDevice(&cur);
+    if (prev >= 0 && cur != prev) hipSetDevice(prev);
+  }
+};
+
+// Read back the small counters (blocking).
+hipError_t sync_counters(crgc_graph *h) {
+  hipError_t e = hipMemcpyAsync(h->hctr, h->ctr, offsetof(Counters, ring), hipMemcpyDeviceToHost,
+                                h->stream);
+  if (e != hipSuccess) return e;
+  e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) return e;
+  h->slot_top = h->hctr->slot_top;
+  h->pool_top = h->hctr->pool_top;
+  h->etab_used = h->hctr->etab_used;
+  h->ids_since = h->atoms_since = 0;
+  return hipSuccess;
+}
+
+int device_error(crgc_graph *h) {
+  const uint64_t err = h->hctr->err;
+  if (!err) return CRGC_OK;
+  h->poisoned = true;
+  if (err & (ERR_RESERVED_ID | ERR_TOO_MANY | ERR_BAD_OFFSETS)) return CRGC_E_INVAL;
+  if (err & ERR_SPIN) return CRGC_E_TIMEOUT;
+  return CRGC_E_NOMEM;
+}
+
+// Rebuild into fresh arrays with room for `ids`/`atoms` more, then swap.
+int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms) {
+  HIP_TRY(sync_counters(h));
+  if (int rc = device_error(h)) return rc;
+  const uint64_t src_top = h->slot_top;
+  // live upper bound: live at the last trace + vertices created since
+  const uint64_t live_ub =
+      std::min<uint64_t>(src_top, h->live + (h->hctr->inserted - h->inserted_at_trace));
+  Caps c = caps_for(std::max<uint64_t>(live_ub, 1), h->etab_used, ids, atoms);
+  Arrays dst;
+  HIP_TRY(alloc_arrays(dst, c, h->ctr, h->stream));
+  Scratch tmp;
+  const size_t need = Carver::need({src_top * 4 + 4, c.scap * 8, rebuild_scan_tmp_bytes(c.scap)});
+  if (tmp.ensure(need) != hipSuccess) {
+    free_arrays(dst);
+    return CRGC_E_NOMEM;
+  }
+  Carver cv(tmp.ptr);
+  uint32_t *map = cv.take<uint32_t>(src_top + 1);
+  uint64_t *offs = cv.take<uint64_t>(c.scap);
+  void *scan_tmp = cv.take<uint64_t>(rebuild_scan_tmp_bytes(c.scap) / 8);
+  hipMemsetAsync(offs, 0, c.scap * 8, h->stream);
+  // new generation counters: slot_top, pool_top, etab_used restart
+  hipMemsetAsync((char *)h->ctr + CTR_OFF(slot_top), 0, 8, h->stream);
+  hipMemsetAsync((char *)h->ctr + CTR_OFF(pool_top), 0, 8, h->stream);
+  hipMemsetAsync((char *)h->ctr + CTR_OFF(etab_used), 0, 8, h->stream);
+  // src keeps a view of the old counters' bound via src_top (passed by value)
+  hipError_t e = launch_rebuild(h->g.d, src_top, dst.d, map, nullptr, offs, scan_tmp, h->stream);
+  if (e == hipSuccess) e = sync_counters(h);
+  tmp.release();
+  if (e != hipSuccess) {
+    free_arrays(dst);
+    h->poisoned = true;
+    return map_hip(e);
+  }
+  free_arrays(h->g);
+  h->g = dst;
+  h->live = h->slot_top;
+  h->inserted_at_trace = h->hctr->inserted;
+  if (int rc = device_error(h)) return rc;
+  return CRGC_OK;
+}
+
+// Make sure `ids` more vertices and `atoms` more edge updates fit.
+int ensure_capacity(crgc_graph *h, uint64_t ids, uint64_t atoms) {
+  auto fits = [&](uint64_t st, uint64_t pt, uint64_t eu) {
+    const Caps &c = h->g.caps;
+    return st + ids <= c.scap && (st + ids) * 10 <= c.hcap * 7 &&
+           pt + 2 * eu + 6 * atoms <= c.pcap && (eu + atoms) * 10 <= c.ecap * 7;
+  };
+  // upper bounds since the last sync
+  const uint64_t st = h->slot_top + h->ids_since;
+  const uint64_t eu = h->etab_used + h->atoms_since;
+  const uint64_t pt = h->pool_top + 2 * (h->etab_used + h->atoms_since) + 6 * h->atoms_since;
+  if (fits(st, pt, eu)) return CRGC_OK;
+  HIP_TRY(sync_counters(h));
+  if (int rc = device_error(h)) return rc;
+  if (fits(h->slot_top, h->pool_top, h->etab_used)) return CRGC_OK;
+  return rebuild(h, ids, atoms);
+}
+
+void note_merge(crgc_graph *h, uint64_t ids, uint64_t atoms) {
+  h->ids_since += ids;
+  h->atoms_since += atoms;
+}
+
+// Copy `bytes` from a host or device pointer into the staging area.
+template <class T>
+const T *stage(crgc_graph *h, Carver &cv, const T *src, uint64_t n, uint32_t memory) {
+  if (memory == CRGC_MEM_DEVICE) return src;
+  if (n == 0) return nullptr;
+  T *dst = cv.take<T>(n);
+  hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyHostToDevice, h->stream);
+  return dst;
+}
+
+int check_graph(crgc_graph *h) {
+  if (!h) return CRGC_E_INVAL;
+  if (h->poisoned) return CRGC_E_POISONED;
+  return CRGC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *crgc_strerror(int code) {
+  switch (code) {
+    case CRGC_OK: return "ok";
+    case CRGC_E_INVAL: return "invalid argument";
+    case CRGC_E_NOMEM: return "out of memory";
+    case CRGC_E_DEVICE: return "device error";
+    case CRGC_E2BIG: return "output buffer too small";
+    case CRGC_E_NULL_SUPERVISOR: return "local garbage shadow without supervisor (reference NPE)";
+    case CRGC_E_UNDO_NEW_SHADOW: return "undo log names an unknown actor (reference CME)";
+    case CRGC_E_POISONED: return "graph unusable after an earlier error";
+    case CRGC_E_TIMEOUT: return "device wait bound exceeded";
+    default: return "unknown error";
+  }
+}
+
+int crgc_create(const crgc_config *cfg, crgc_graph **out) {
+  if (!out) return CRGC_E_INVAL;
+  *out = nullptr;
+  if (cfg && cfg->abi_version != CRGC_ABI_VERSION) return CRGC_E_INVAL;
+  crgc_graph *h = new (std::nothrow) crgc_graph();
+  if (!h) return CRGC_E_NOMEM;
+  h->device = cfg ? cfg->device : 0;
+  h->F = (cfg && cfg->entry_field_size) ? cfg->entry_field_size : 4;
+  h->DGS = (cfg && cfg->delta_graph_size) ? cfg->delta_graph_size : 64;
+  DeviceGuard dg(h->device);
+  int rc = CRGC_OK;
+  do {
+    if (cfg && cfg->stream) {
+      h->stream = (hipStream_t)cfg->stream;
+    } else {
+      if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        rc = CRGC_E_DEVICE;
+        break;
+      }
+      h->own_stream = true;
+    }
+    for (auto &e : h->ev)
+      if (hipEventCreate(&e) != hipSuccess) rc = CRGC_E_DEVICE;
+    if (rc) break;
+    if (hipMalloc(&h->ctr, sizeof(Counters)) != hipSuccess ||
+        hipHostMalloc(&h->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess) {
+      rc = CRGC_E_NOMEM;
+      break;
+    }
+    hipMemsetAsync(h->ctr, 0, sizeof(Counters), h->stream);
+    memset(h->hctr, 0, sizeof(Counters));
+    const uint64_t v0 = cfg && cfg->vertex_capacity ? cfg->vertex_capacity : (1u << 16);
+    const uint64_t e0 = cfg && cfg->edge_capacity ? cfg->edge_capacity : 8 * v0;
+    Caps c = caps_for(v0, e0, v0, e0);
+    if (hipError_t e = alloc_arrays(h->g, c, h->ctr, h->stream)) {
+      rc = map_hip(e);
+      break;
+    }
+    if (hipStreamSynchronize(h->stream) != hipSuccess) rc = CRGC_E_DEVICE;
+  } while (0);
+  if (rc) {
+    crgc_destroy(h);
+    return rc;
+  }
+  *out = h;
+  return CRGC_OK;
+}
+
+void crgc_destroy(crgc_graph *h) {
+  if (!h) return;
+  DeviceGuard dg(h->device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  free_arrays(h->g);
+  h->stage.release();
+  h->work.release();
+  if (h->ctr) hipFree(h->ctr);
+  if (h->hctr) hipHostFree(h->hctr);
+  if (h->roots_buf) hipFree(h->roots_buf);
+  for (auto &e : h->ev)
+    if (e) hipEventDestroy(e);
+  if (h->own_stream && h->stream) hipStreamDestroy(h->stream);
+  delete h;
+}
+
+// Shared tail of every merge: the edge pipeline over the staged atoms.
+static int run_edges(crgc_graph *h, uint32_t *ao, uint32_t *at, int32_t *ad, uint64_t max_atoms,
+                     Carver &cv) {
+  if (max_atoms == 0) return CRGC_OK;
+  EdgeArgs ea{};
+  ea.max_atoms = max_atoms;
+  ea.n_atoms_dev = nullptr;
+  ea.atom_o = ao;
+  ea.atom_t = at;
+  ea.atom_d = ad;
+  ea.newlist = cv.take<uint64_t>(max_atoms);
+  ea.touched = cv.take<uint32_t>(max_atoms);
+  ea.reloc = cv.take<uint32_t>(max_atoms);
+  hipMemsetAsync((char *)h->ctr + CTR_OFF(n_touched), 0, 16, h->stream);
+  HIP_TRY(launch_edges(h->g.d, ea, h->stream));
+  return CRGC_OK;
+}
+
+static size_t edge_scratch(uint64_t max_atoms) {
+  return Carver::need({max_atoms * 4, max_atoms * 4, max_atoms * 4, max_atoms * 8, max_atoms * 4,
+                       max_atoms * 4});
+}
+
+int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
+  if (int rc = check_graph(h)) return rc;
+  if (!b || b->memory > CRGC_MEM_DEVICE) return CRGC_E_INVAL;
+  const uint64_t n = b->n_entries;
+  if (n == 0) return CRGC_OK;
+  if (n >= (1ull << 31) / (h->F + 1)) return CRGC_E_INVAL;
+  if (!b->self || !b->recv_count || !b->flags || !b->created_off || !b->spawned_off ||
+      !b->updated_off)
+    return CRGC_E_INVAL;
+  DeviceGuard dg(h->device);
+  uint64_t C, S, U;
+  if (b->memory == CRGC_MEM_HOST) {
+    C = b->created_off[n];
+    S = b->spawned_off[n];
+    U = b->updated_off[n];
+    if (b->created_off[0] || b->spawned_off[0] || b->updated_off[0]) return CRGC_E_INVAL;
+    if (C > n * h->F || S > n * h->F || U > n * h->F) return CRGC_E_INVAL;
+  } else {
+    C = S = U = n * h->F;  // bounds; kernels read the exact offsets
+  }
+  const uint64_t ids = n + 2 * C + S + U;
+  const uint64_t max_atoms = n * 2 * (uint64_t)h->F;
+  if (int rc = ensure_capacity(h, ids, C + U)) return rc;
+
+  const size_t host_bytes =
+      b->memory == CRGC_MEM_HOST
+          ? Carver::need({n * 8, n * 2, n, (n + 1) * 4, C * 8, C * 8, (n + 1) * 4, S * 8,
+                          (n + 1) * 4, U * 8, U * 2})
+          : 0;
+  const size_t work_bytes = Carver::need({n * 4, n * h->F * 4}) + edge_scratch(max_atoms);
+  if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
+    return CRGC_E_NOMEM;
+  Carver sc(h->stage.ptr), wc(h->work.ptr);
+  EntryArgs a{};
+  a.n = n;
+  a.F = h->F;
+  a.epoch = ++h->epoch;
+  a.self = stage(h, sc, b->self, n, b->memory);
+  a.recv = stage(h, sc, b->recv_count, n, b->memory);
+  a.flags = stage(h, sc, b->flags, n, b->memory);
+  a.c_off = stage(h, sc, b->created_off, n + 1, b->memory);
+  a.c_owner = stage(h, sc, b->created_owner, C, b->memory);
+  a.c_target = stage(h, sc, b->created_target, C, b->memory);
+  a.s_off = stage(h, sc, b->spawned_off, n + 1, b->memory);
+  a.spawned = stage(h, sc, b->spawned, S, b->memory);
+  a.u_off = stage(h, sc, b->updated_off, n + 1, b->memory);
+  a.u_ref = stage(h, sc, b->updated_ref, U, b->memory);
+  a.u_info = stage(h, sc, b->updated_info, U, b->memory);
+  a.self_slot = wc.take<uint32_t>(n);
+  a.spawn_slot = wc.take<uint32_t>(n * h->F);
+  a.atom_o = wc.take<uint32_t>(max_atoms);
+  a.atom_t = wc.take<uint32_t>(max_atoms);
+  a.atom_d = wc.take<int32_t>(max_atoms);
+  hipMemsetAsync(a.atom_d, 0, max_atoms * 4, h->stream);
+  HIP_TRY(launch_entries(h->g.d, a, h->stream));
+  if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, max_atoms, wc)) return rc;
+  note_merge(h, ids, C + U);
+  return CRGC_OK;
+}
+
+int crgc_merge_deltas(crgc_graph *h, const crgc_delta_batch *b) {
+  if (int rc = check_graph(h)) return rc;
+  if (!b || b->memory > CRGC_MEM_DEVICE) return CRGC_E_INVAL;
+  const uint64_t n = b->n_shadows;
+  if (n == 0) return CRGC_OK;
+  if (!b->id || !b->recv_count || !b->supervisor || !b->flags || !b->out_off) return CRGC_E_INVAL;
+  DeviceGuard dg(h->device);
+  uint64_t nout;
+  if (b->memory == CRGC_MEM_HOST) {
+    if (b->out_off[0]) return CRGC_E_INVAL;
+    nout = b->out_off[n];
+  } else {
+    uint32_t v = 0;
+    HIP_TRY(hipMemcpy(&v, b->out_off + n, 4, hipMemcpyDeviceToHost));
+    nout = v;
+  }
+  const uint64_t ids = 2 * n + nout;
+  if (int rc = ensure_capacity(h, ids, nout)) return rc;
+  const size_t host_bytes =
+      b->memory == CRGC_MEM_HOST
+          ? Carver::need({n * 8, n * 4, n * 8, n, (n + 1) * 4, nout * 8, nout * 4})
+          : 0;
+  const size_t work_bytes = Carver::need({n * 4, n * 4}) + edge_scratch(nout);
+  if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
+    return CRGC_E_NOMEM;
+  Carver sc(h->stage.ptr), wc(h->work.ptr);
+  DeltaArgs a{};
+  a.n = n;
+  a.epoch = ++h->epoch;
+  a.id = stage(h, sc, b->id, n, b->memory);
+  a.recv = stage(h, sc, b->recv_count, n, b->memory);
+  a.sup = stage(h, sc, b->supervisor, n, b->memory);
+  a.flags = stage(h, sc, b->flags, n, b->memory);
+  a.out_off = stage(h, sc, b->out_off, n + 1, b->memory);
+  a.out_target = stage(h, sc, b->out_target, nout, b->memory);
+  a.out_count = stage(h, sc, b->out_count, nout, b->memory);
+  a.self_slot = wc.take<uint32_t>(n);
+  a.sup_slot = wc.take<uint32_t>(n);
+  a.atom_o = wc.take<uint32_t>(std::max<uint64_t>(nout, 1));
+  a.atom_t = wc.take<uint32_t>(std::max<uint64_t>(nout, 1));
+  a.atom_d = wc.take<int32_t>(std::max<uint64_t>(nout, 1));
+  HIP_TRY(launch_deltas(h->g.d, a, nout, h->stream));
+  if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, nout, wc)) return rc;
+  note_merge(h, ids, nout);
+  return CRGC_OK;
+}
+
+int crgc_merge_undo(crgc_graph *h, const crgc_undo_log *log) {
+  if (int rc = check_graph(h)) return rc;
+  if (!log || log->memory != CRGC_MEM_HOST) return CRGC_E_INVAL;
+  const uint64_t n = log->n_fields;
+  if (n && (!log->actor || !log->message_count || !log->created_off)) return CRGC_E_INVAL;
+  if (n && log->created_off[0]) return CRGC_E_INVAL;
+  DeviceGuard dg(h->device);
+  const uint64_t nc = n ? log->created_off[n] : 0;
+  {
+    // UndoLog.admitted is a map: one field per actor.
+    std::vector<uint64_t> ids(log->actor, log->actor + n);
+    std::sort(ids.begin(), ids.end());
+    if (std::adjacent_find(ids.begin(), ids.end()) != ids.end()) return CRGC_E_INVAL;
+  }
+  if (int rc = ensure_capacity(h, 0, nc)) return rc;
+  const size_t host_bytes = Carver::need({n * 8, n * 4, (n + 1) * 4, nc * 8, nc * 4});
+  const size_t work_bytes = edge_scratch(nc);
+  if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
+    return CRGC_E_NOMEM;
+  Carver sc(h->stage.ptr), wc(h->work.ptr);
+  UndoArgs a{};
+  a.n = n;
+  a.location = log->node_location;
+  a.actor = stage(h, sc, log->actor, n, CRGC_MEM_HOST);
+  a.msg = stage(h, sc, log->message_count, n, CRGC_MEM_HOST);
+  a.c_off = stage(h, sc, log->created_off, n + 1, CRGC_MEM_HOST);
+  a.c_target = stage(h, sc, log->created_target, nc, CRGC_MEM_HOST);
+  a.c_count = stage(h, sc, log->created_count, nc, CRGC_MEM_HOST);
+  a.atom_o = wc.take<uint32_t>(std::max<uint64_t>(nc, 1));
+  a.atom_t = wc.take<uint32_t>(std::max<uint64_t>(nc, 1));
+  a.atom_d = wc.take<int32_t>(std::max<uint64_t>(nc, 1));
+  // Detect the reference's ConcurrentModificationException before mutating.
+  HIP_TRY(launch_undo_check(h->g.d, a, h->stream));
+  HIP_TRY(sync_counters(h));
+  if (h->hctr->err & ERR_UNDO_NEW) {
+    const unsigned long long clear = 0;
+    // leave the graph usable: clear only the undo bit
+    h->hctr->err &= ~(unsigned long long)ERR_UNDO_NEW;
+    HIP_TRY(hipMemcpyAsync((char *)h->ctr + CTR_OFF(err), &h->hctr->err, 8, hipMemcpyHostToDevice,
+                           h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    (void)clear;
+    return CRGC_E_UNDO_NEW_SHADOW;
+  }
+  if (int rc = device_error(h)) return rc;
+  HIP_TRY(launch_undo_apply(h->g.d, a, h->slot_top, h->stream));
+  if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, nc, wc)) return rc;
+  note_merge(h, 0, nc);
+  return CRGC_OK;
+}
+
+// BFS driver shared by trace and count_reachable_from.  Returns levels run.
+static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64_t *levels,
+                      uint64_t *roots) {
+  const uint64_t top = h->slot_top + h->ids_since;
+  LevelArgs la{};
+  la.location = location;
+  la.sparse_thresh = (uint32_t)std::max<uint64_t>(64, (top / BLK_SLOTS) / 4);
+  la.level = 0;
+  HIP_TRY(launch_level(h->g.d, la, true, investigate, top, h->stream));
+  int L = 1;
+  int chunk = 8;
+  std::vector<unsigned long long> ring(LEVEL_RING);
+  for (;;) {
+    for (int k = 0; k < chunk; ++k) {
+      la.level = L + k;
+      HIP_TRY(launch_level(h->g.d, la, false, investigate, top, h->stream));
+    }
+    // counts of levels L-1 .. L+chunk-1
+    const int first = L - 1, last = L + chunk - 1;
+    for (int lv = first; lv <= last;) {
+      const int i0 = lv % LEVEL_RING;
+      const int cnt = std::min(last - lv + 1, LEVEL_RING - i0);
+      HIP_TRY(hipMemcpyAsync(&ring[i0], (char *)h->ctr + CTR_OFF(ring) + i0 * 8, cnt * 8,
+                             hipMemcpyDeviceToHost, h->stream));
+      lv += cnt;
+    }
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (first == 0) *roots = ring[0];
+    for (int lv = first; lv <= last; ++lv) {
+      if (ring[lv % LEVEL_RING] == 0) {
+        *levels = (uint64_t)lv;  // levels 0 .. lv-1 were non-empty
+        return CRGC_OK;
+      }
+    }
+    L += chunk;
+    chunk = std::min(chunk * 2, 512);
+    if ((uint64_t)L > (1ull << 40)) return CRGC_E_TIMEOUT;
+  }
+}
+
+static void reset_trace_counters(crgc_graph *h) {
+  // marked .. n_out, and the level ring
+  const size_t a = CTR_OFF(marked), b = sizeof(Counters);
+  hipMemsetAsync((char *)h->ctr + a, 0, b - a, h->stream);
+  const uint64_t top = h->slot_top + h->ids_since;
+  hipMemsetAsync(h->g.d.vis, 0, round_up(std::min<uint64_t>(top, h->g.caps.scap), BLK_SLOTS) / 8,
+                 h->stream);
+}
+
+static int copy_lists(crgc_graph *h, crgc_trace_out *out) {
+  bool big = false;
+  out->n_garbage = h->last_garbage;
+  out->n_kill = h->last_kill;
+  out->n_live = h->last_live;
+  out->stats = h->last_stats;
+  if (out->garbage_ids) {
+    if (out->garbage_cap < h->last_garbage) big = true;
+    else if (h->last_garbage)
+      HIP_TRY(hipMemcpyAsync(out->garbage_ids, h->g.d.out_a, h->last_garbage * 8,
+                             hipMemcpyDeviceToHost, h->stream));
+  }
+  if (out->kill_ids) {
+    if (out->kill_cap < h->last_kill) big = true;
+    else if (h->last_kill)
+      HIP_TRY(hipMemcpyAsync(out->kill_ids, h->g.d.out_b, h->last_kill * 8, hipMemcpyDeviceToHost,
+                             h->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return big ? CRGC_E2BIG : CRGC_OK;
+}
+
+int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
+  if (int rc = check_graph(h)) return rc;
+  if (!out) return CRGC_E_INVAL;
+  DeviceGuard dg(h->device);
+  const auto t0 = std::chrono::steady_clock::now();
+  // Surface merge-time device errors before tracing.
+  HIP_TRY(sync_counters(h));
+  if (int rc = device_error(h)) return rc;
+  const uint64_t top = h->slot_top;
+  reset_trace_counters(h);
+  HIP_TRY(hipEventRecord(h->ev[0], h->stream));
+  uint64_t levels = 0, roots = 0;
+  if (int rc = run_levels(h, false, 0, &levels, &roots)) return rc;
+  HIP_TRY(hipEventRecord(h->ev[1], h->stream));
+  HIP_TRY(launch_sweep(h->g.d, should_kill ? 1 : 0, top, h->stream));
+  HIP_TRY(launch_commit(h->g.d, top, h->stream));
+  HIP_TRY(hipEventRecord(h->ev[2], h->stream));
+  HIP_TRY(sync_counters(h));
+  const Counters &c = *h->hctr;
+  if (c.npe) return CRGC_E_NULL_SUPERVISOR;  // commit skipped: graph unchanged
+  if (int rc = device_error(h)) return rc;
+  crgc_trace_stats st{};
+  st.pseudo_roots = 0;
+  st.edges_scanned = c.edges_scanned;
+  st.sup_edges = c.sup_edges;
+  st.levels = levels;
+  float ms = 0;
+  hipEventElapsedTime(&ms, h->ev[0], h->ev[1]);
+  st.ms_mark = ms;
+  hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
+  st.ms_sweep = ms;
+  st.pseudo_roots = roots;
+  h->last_garbage = c.n_garbage;
+  h->last_kill = c.n_kill;
+  h->last_live = c.n_live;
+  h->live = c.n_live;
+  h->inserted_at_trace = c.inserted;
+  h->have_last = true;
+  const int rc = copy_lists(h, out);
+  st.ms_total =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  h->last_stats = st;
+  out->stats = st;
+  // Keep the slot space dense: rebuild once dead slots outnumber live ones.
+  if (rc == CRGC_OK && h->slot_top > 65536 && h->slot_top > 2 * h->live) {
+    if (int r2 = rebuild(h, 0, 0)) return r2;
+  }
+  return rc;
+}
+
+int crgc_last_trace(crgc_graph *h, crgc_trace_out *out) {
+  if (int rc = check_graph(h)) return rc;
+  if (!out || !h->have_last) return CRGC_E_INVAL;
+  DeviceGuard dg(h->device);
+  return copy_lists(h, out);
+}
+
+int crgc_local_roots(crgc_graph *h, uint64_t *out, uint64_t cap, uint64_t *n) {
+  if (int rc = check_graph(h)) return rc;
+  if (!n) return CRGC_E_INVAL;
+  DeviceGuard dg(h->device);
+  HIP_TRY(sync_counters(h));
+  if (h->roots_cap < h->g.caps.scap) {
+    if (h->roots_buf) hipFree(h->roots_buf);
+    h->roots_buf = nullptr;
+    h->roots_cap = 0;
+    HIP_TRY(hipMalloc(&h->roots_buf, h->g.caps.scap * 8));
+    h->roots_cap = h->g.caps.scap;
+  }
+  hipMemsetAsync((char *)h->ctr + CTR_OFF(n_out), 0, 8, h->stream);
+  DevGraph d = h->g.d;
+  d.out_a = h->roots_buf;
+  HIP_TRY(launch_local_roots(d, h->slot_top, h->stream));
+  unsigned long long k = 0;
+  HIP_TRY(hipMemcpyAsync(&k, (char *)h->ctr + CTR_OFF(n_out), 8, hipMemcpyDeviceToHost,
+                         h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  *n = k;
+  if (!out) return CRGC_OK;
+  if (cap < k) return CRGC_E2BIG;
+  if (k) HIP_TRY(hipMemcpy(out, h->roots_buf, k * 8, hipMemcpyDeviceToHost));
+  return CRGC_OK;
+}
+
+int crgc_count_reachable_from(crgc_graph *h, uint16_t location, int64_t *out) {
+  if (int rc = check_graph(h)) return rc;
+  if (!out) return CRGC_E_INVAL;
+  DeviceGuard dg(h->device);
+  HIP_TRY(sync_counters(h));
+  if (int rc = device_error(h)) return rc;
+  reset_trace_counters(h);
+  uint64_t levels = 0, roots = 0;
+  if (int rc = run_levels(h, true, location, &levels, &roots)) return rc;
+  HIP_TRY(sync_counters(h));
+  *out = (int64_t)h->hctr->marked;
+  return CRGC_OK;
+}
+
+int crgc_total_actors_seen(crgc_graph *h, uint64_t *out) {
+  if (!h || !out) return CRGC_E_INVAL;
+  DeviceGuard dg(h->device);
+  HIP_TRY(sync_counters(h));
+  *out = h->hctr->inserted;
+  return CRGC_OK;
+}
+
+int crgc_live_count(crgc_graph *h, uint64_t *out) {
+  if (int rc = check_graph(h)) return rc;
+  if (!out) return CRGC_E_INVAL;
+  DeviceGuard dg(h->device);
+  HIP_TRY(sync_counters(h));
+  // alive slots = slot_top minus dead slots: count on the host copy of flags
+  std::vector<uint8_t> fl(h->slot_top);
+  if (h->slot_top)
+    HIP_TRY(hipMemcpy(fl.data(), h->g.d.flags, h->slot_top, hipMemcpyDeviceToHost));
+  uint64_t k = 0;
+  for (uint8_t f : fl) k += (f & FL_ALIVE) ? 1 : 0;
+  *out = k;
+  return CRGC_OK;
+}
+
+int crgc_export(crgc_graph *h, crgc_graph_export *out) {
+  if (int rc = check_graph(h)) return rc;
+  if (!out) return CRGC_E_INVAL;
+  DeviceGuard dg(h->device);
+  HIP_TRY(sync_counters(h));
+  if (int rc = device_error(h)) return rc;
+  const uint64_t top = h->slot_top;
+  std::vector<uint64_t> vid(top);
+  std::vector<int32_t> recv(top);
+  std::vector<uint8_t> fl(top);
+  std::vector<uint32_t> sup(top);
+  std::vector<uint2> adj(top);
+  std::vector<uint64_t> pool(h->pool_top);
+  if (top) {
+    HIP_TRY(hipMemcpy(vid.data(), h->g.d.vid, top * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(recv.data(), h->g.d.recv, top * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(fl.data(), h->g.d.flags, top, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(sup.data(), h->g.d.sup, top * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(adj.data(), h->g.d.adj, top * 8, hipMemcpyDeviceToHost));
+  }
+  if (h->pool_top)
+    HIP_TRY(hipMemcpy(pool.data(), h->g.d.pool, h->pool_top * 8, hipMemcpyDeviceToHost));
+  uint64_t nv = 0, ne = 0;
+  bool big = false;
+  for (uint64_t v = 0; v < top; ++v) {
+    if (!(fl[v] & FL_ALIVE)) continue;
+    if (out->id) {
+      if (nv < out->vertex_cap) {
+        out->id[nv] = vid[v];
+        out->recv_count[nv] = recv[v];
+        out->flags[nv] = fl[v] & (uint8_t)~FL_ALIVE;
+        const uint32_t s = sup[v];
+        out->supervisor[nv] = s == SLOT_NONE                         ? CRGC_NO_ACTOR
+                              : (s < top && (fl[s] & FL_ALIVE)) ? vid[s]
+                                                                    : CRGC_DEAD_ACTOR;
+      } else {
+        big = true;
+      }
+    }
+    ++nv;
+    for (uint32_t e = 0; e < adj[v].y; ++e) {
+      const uint64_t ed = pool[(uint64_t)adj[v].x + e];
+      const uint32_t t = (uint32_t)ed;
+      const int32_t cnt = (int32_t)(uint32_t)(ed >> 32);
+      if (cnt == 0 || t >= top || !(fl[t] & FL_ALIVE)) continue;
+      if (out->edge_owner) {
+        if (ne < out->edge_cap) {
+          out->edge_owner[ne] = vid[v];
+          out->edge_target[ne] = vid[t];
+          out->edge_count[ne] = cnt;
+        } else {
+          big = true;
+        }
+      }
+      ++ne;
+    }
+  }
+  out->n_vertices = nv;
+  out->n_edges = ne;
+  return big ? CRGC_E2BIG : CRGC_OK;
+}
+
+}  // extern "C"

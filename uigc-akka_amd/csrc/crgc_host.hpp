@@ -1,0 +1,148 @@
+// crgc_host.hpp — host-side state of one shadow-graph handle and the kernel
+// launchers each .hip translation unit provides.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "../../include/crgc.h"
+#include "crgc_internal.hpp"
+
+namespace crgc {
+
+// A grow-only device scratch buffer.
+struct Scratch {
+  void *ptr = nullptr;
+  size_t bytes = 0;
+  hipError_t ensure(size_t need) {
+    if (need <= bytes) return hipSuccess;
+    if (ptr) hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+    size_t sz = need + need / 4 + 4096;
+    hipError_t e = hipMalloc(&ptr, sz);
+    if (e == hipSuccess) bytes = sz;
+    return e;
+  }
+  void release() {
+    if (ptr) hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+  }
+};
+
+// Carves aligned sub-buffers out of a Scratch.
+struct Carver {
+  char *base;
+  size_t off = 0;
+  explicit Carver(void *p) : base((char *)p) {}
+  template <class T>
+  T *take(size_t n) {
+    off = (off + 255) & ~(size_t)255;
+    T *p = (T *)(base + off);
+    off += n * sizeof(T);
+    return p;
+  }
+  static size_t need(std::initializer_list<size_t> sizes) {
+    size_t o = 0;
+    for (size_t s : sizes) o = ((o + 255) & ~(size_t)255) + s;
+    return o + 256;
+  }
+};
+
+struct EntryArgs {
+  uint64_t n;
+  uint32_t F;
+  unsigned long long epoch;
+  const uint64_t *self;
+  const int16_t *recv;
+  const uint8_t *flags;
+  const uint32_t *c_off;
+  const uint64_t *c_owner;
+  const uint64_t *c_target;
+  const uint32_t *s_off;
+  const uint64_t *spawned;
+  const uint32_t *u_off;
+  const uint64_t *u_ref;
+  const int16_t *u_info;
+  uint32_t *self_slot;   // [n]
+  uint32_t *spawn_slot;  // [n*F]
+  uint32_t *atom_o;      // [2*n*F]: created atoms, then updated atoms
+  uint32_t *atom_t;
+  int32_t *atom_d;
+};
+
+struct DeltaArgs {
+  uint64_t n;
+  unsigned long long epoch;
+  const uint64_t *id;
+  const int32_t *recv;
+  const uint64_t *sup;
+  const uint8_t *flags;
+  const uint32_t *out_off;
+  const uint64_t *out_target;
+  const int32_t *out_count;
+  uint32_t *self_slot;
+  uint32_t *sup_slot;
+  uint32_t *atom_o;
+  uint32_t *atom_t;
+  int32_t *atom_d;
+};
+
+struct UndoArgs {
+  uint64_t n;
+  uint16_t location;
+  const uint64_t *actor;
+  const int32_t *msg;
+  const uint32_t *c_off;
+  const uint64_t *c_target;
+  const int32_t *c_count;
+  uint32_t *atom_o;
+  uint32_t *atom_t;
+  int32_t *atom_d;
+};
+
+struct EdgeArgs {
+  uint64_t max_atoms;          // grid bound
+  const uint64_t *n_atoms_dev; // exact count on device (or null: use max_atoms)
+  const uint32_t *atom_o;
+  const uint32_t *atom_t;
+  const int32_t *atom_d;
+  uint64_t *newlist;   // [max_atoms] buckets of new edge keys
+  uint32_t *touched;   // [max_atoms] owners that got new edges
+  uint32_t *reloc;     // [max_atoms] new segment offset per touched owner
+};
+
+struct LevelArgs {
+  int level;
+  uint32_t sparse_thresh;
+  uint16_t location;
+};
+
+// ---- launchers (return hipError_t of the launch) ---------------------------
+hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s);
+hipError_t launch_deltas(const DevGraph &g, const DeltaArgs &a, uint64_t n_out, hipStream_t s);
+hipError_t launch_undo_check(const DevGraph &g, const UndoArgs &a, hipStream_t s);
+hipError_t launch_undo_apply(const DevGraph &g, const UndoArgs &a, uint64_t slot_top,
+                             hipStream_t s);
+hipError_t launch_edges(const DevGraph &g, const EdgeArgs &a, hipStream_t s);
+
+hipError_t launch_level(const DevGraph &g, const LevelArgs &a, bool roots, bool investigate,
+                        uint64_t slot_top, hipStream_t s);
+hipError_t launch_sweep(const DevGraph &g, int should_kill, uint64_t slot_top, hipStream_t s);
+hipError_t launch_commit(const DevGraph &g, uint64_t slot_top, hipStream_t s);
+hipError_t launch_local_roots(const DevGraph &g, uint64_t slot_top, hipStream_t s);
+
+// rebuild: compact `src` (live vertices only, purged edges) into `dst`,
+// whose arrays are freshly allocated and initialised by init_graph_arrays.
+hipError_t launch_init_arrays(const DevGraph &g, hipStream_t s);
+hipError_t launch_rebuild(const DevGraph &src, uint64_t src_slot_top, const DevGraph &dst,
+                          uint32_t *map, uint32_t *newdeg, uint64_t *offs, void *scan_tmp,
+                          hipStream_t s);
+size_t rebuild_scan_tmp_bytes(uint64_t n);
+
+int grid_for(uint64_t threads, int block = 256, int cap = 4096);
+
+}  // namespace crgc

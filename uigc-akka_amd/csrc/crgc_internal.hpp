@@ -1,0 +1,301 @@
+// crgc_internal.hpp — HBM layout of the shadow graph and the device helpers
+// shared by the merge, trace and rebuild kernels (gfx950 / CDNA4 only).
+//
+// Layout (DESIGN.md "Data layout in HBM"):
+//   id table   hkey[u64] / hval[u32]   open addressing, linear probing:
+//                                      actor id -> dense vertex slot
+//   vertex SoA, indexed by slot         (ShadowGraph.shadowMap + Shadow fields)
+//     vid[u64]    actor id of the slot
+//     recv[i32]   Shadow.recvCount
+//     flags[u8]   ALIVE|INTERNED|LOCAL|BUSY|ROOT|HALTED
+//     sup[u32]    Shadow.supervisor as a slot (NONE = null, DEAD = collected)
+//     adj[uint2]  {offset, degree} of the slot's out-edge segment in the pool
+//     ecap[u32]   segment capacity
+//   edge pool   pool[u64] = target slot (lo 32) | count (hi 32): Shadow.outgoing
+//   edge table  ekey[u64] = owner<<32|target -> eval[u32] index inside segment
+//   trace state vis bitmap + two frontier byte maps + two block-dirty maps
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace crgc {
+
+constexpr uint64_t KEY_EMPTY = 0xFFFFFFFFFFFFFFFFull;
+constexpr uint64_t KEY_TOMB = 0xFFFFFFFFFFFFFFFEull;
+constexpr uint32_t SLOT_NONE = 0xFFFFFFFFu;  // Java null supervisor
+constexpr uint32_t SLOT_DEAD = 0xFFFFFFFEu;  // supervisor collected (post-rebuild)
+constexpr uint32_t VAL_PENDING = 0xFFFFFFFFu;
+constexpr uint32_t EVAL_NEW = 0x80000000u;   // eval: edge inserted in this merge
+
+// flags bits: ALIVE is internal; the rest equal CRGC_F_* of include/crgc.h
+constexpr uint8_t FL_ALIVE = 0x01, FL_INTERNED = 0x02, FL_LOCAL = 0x04, FL_BUSY = 0x08,
+                  FL_ROOT = 0x10, FL_HALTED = 0x20;
+
+// device error bits (Counters::err)
+constexpr uint32_t ERR_RESERVED_ID = 1u << 0;
+constexpr uint32_t ERR_TOO_MANY = 1u << 1;   // more than F records in an entry
+constexpr uint32_t ERR_IDTAB_FULL = 1u << 2;
+constexpr uint32_t ERR_SLOTS_FULL = 1u << 3;
+constexpr uint32_t ERR_POOL_FULL = 1u << 4;
+constexpr uint32_t ERR_ETAB_FULL = 1u << 5;
+constexpr uint32_t ERR_UNDO_NEW = 1u << 6;
+constexpr uint32_t ERR_SPIN = 1u << 7;
+constexpr uint32_t ERR_BAD_OFFSETS = 1u << 8;
+
+constexpr int WAVE = 64;
+constexpr int BLK_SLOTS = 2048;          // slots per wave-block (64 lanes x 32)
+constexpr int LEVEL_RING = 4096;         // ring of per-level frontier counts
+
+struct Counters {
+  unsigned long long inserted;       // vertices created (totalActorsSeen)
+  unsigned long long slot_top;       // next dense slot
+  unsigned long long pool_top;       // next free edge in pool
+  unsigned long long etab_used;      // edge-table keys ever inserted
+  unsigned long long n_touched;      // owners with new edges in this merge
+  unsigned long long n_new_edges;    // new edge keys in this merge
+  unsigned long long err;
+  unsigned long long spin_max;
+  // trace
+  unsigned long long marked;
+  unsigned long long edges_scanned;
+  unsigned long long sup_edges;
+  unsigned long long n_garbage;
+  unsigned long long n_kill;
+  unsigned long long n_live;
+  unsigned long long npe;
+  unsigned long long n_out;          // generic output counter (local roots)
+  unsigned long long ring[LEVEL_RING];
+};
+
+// Everything a kernel needs, passed by value.
+struct DevGraph {
+  // id table
+  uint64_t hcap, hmask;
+  uint64_t *hkey;
+  uint32_t *hval;
+  // vertex SoA
+  uint64_t scap;  // slot capacity (multiple of BLK_SLOTS)
+  uint64_t *vid;
+  int32_t *recv;
+  uint8_t *flags;
+  uint32_t *sup;
+  uint2 *adj;
+  uint32_t *ecap;
+  unsigned long long *vseq;  // last-write-wins tag for busy/root
+  unsigned long long *sseq;  // last-write-wins tag for supervisor
+  uint32_t *enew;            // new edges per owner in the current merge
+  // edges
+  uint64_t pcap;
+  uint64_t *pool;
+  uint64_t ecap_tab, emask;
+  uint64_t *ekey;
+  uint32_t *eval;
+  int32_t *edelta;
+  // trace
+  uint32_t *vis;
+  uint8_t *front[2];
+  uint8_t *dirty[2];
+  uint64_t *out_a;  // garbage ids / generic
+  uint64_t *out_b;  // kill ids
+  Counters *ctr;
+};
+
+// splitmix64 finaliser
+__host__ __device__ inline uint64_t mix64(uint64_t x) {
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebull;
+  x ^= x >> 31;
+  return x;
+}
+
+__host__ __device__ inline bool reserved_id(uint64_t id) {
+  return id >= KEY_TOMB || (id >> 48) == 0xFFFFull;
+}
+
+__device__ inline void set_err(Counters *c, uint32_t bit) {
+  atomicOr(&c->err, (unsigned long long)bit);
+}
+
+__device__ inline int lane_id() { return threadIdx.x & 63; }
+__device__ inline uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+// Full-wave inclusive scan (all 64 lanes must be active).
+__device__ inline uint32_t wave_incl_scan(uint32_t x) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+__device__ inline uint32_t wave_sum(uint32_t x) { return __shfl(wave_incl_scan(x), 63); }
+
+__device__ inline uint32_t wave_max(uint32_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x = max(x, (uint32_t)__shfl_xor(x, d));
+  return x;
+}
+
+// Wave-aggregated atomic add: one atomic per wave.  ALL 64 lanes must call
+// (v = 0 to abstain).  Returns this lane's exclusive base.
+__device__ inline unsigned long long wave_atomic_add(unsigned long long *p, uint32_t v) {
+  const uint32_t incl = wave_incl_scan(v);
+  const uint32_t total = __shfl(incl, 63);
+  unsigned long long base = 0;
+  if (lane_id() == 0 && total) base = atomicAdd(p, (unsigned long long)total);
+  base = __shfl(base, 0);
+  return base + (incl - v);
+}
+
+// Wave-aggregated 1-bit append: lanes with `pred` get consecutive indices.
+__device__ inline unsigned long long wave_append(unsigned long long *p, bool pred) {
+  const uint64_t ball = __ballot(pred);
+  unsigned long long base = 0;
+  if (lane_id() == 0 && ball) base = atomicAdd(p, (unsigned long long)__popcll(ball));
+  base = __shfl(base, 0);
+  return base + __popcll(ball & lanemask_lt());
+}
+
+// ---- id table --------------------------------------------------------------
+// Resolving an id to its dense slot, inserting it if absent, is split in two
+// so that slot allocation is one atomic per wave and no wave can deadlock:
+//   id_probe   (divergent)  claims the key with a CAS or finds it;
+//   id_settle  (ALL lanes)  the wave allocates slots for the keys it claimed,
+//                           publishes them with memory-side atomic exchanges,
+//                           and only then waits (memory-side atomic reads, so
+//                           no stale per-XCD L2 line can satisfy the wait) for
+//                           keys another wave claimed but has not published.
+// Every wave publishes before it waits, so a wait always ends.
+constexpr uint32_t SLOT_INVALID = 0xFFFFFFFDu;  // published on overflow
+enum : int { RS_NONE = 0, RS_FOUND = 1, RS_INSERTED = 2, RS_PENDING = 3 };
+
+__device__ inline int id_probe(const DevGraph &g, uint64_t id, uint64_t &bucket,
+                               uint32_t &slot) {
+  uint64_t h = mix64(id) & g.hmask;
+  for (uint64_t probe = 0; probe < g.hcap; ++probe) {
+    uint64_t k = g.hkey[h];
+    if (k == KEY_EMPTY) {
+      k = atomicCAS((unsigned long long *)&g.hkey[h], (unsigned long long)KEY_EMPTY,
+                    (unsigned long long)id);
+      if (k == KEY_EMPTY) {
+        bucket = h;
+        return RS_INSERTED;
+      }
+    }
+    if (k == id) {
+      bucket = h;
+      uint32_t v = g.hval[h];
+      if (v != VAL_PENDING) {
+        slot = v;
+        return RS_FOUND;
+      }
+      return RS_PENDING;
+    }
+    h = (h + 1) & g.hmask;
+  }
+  set_err(g.ctr, ERR_IDTAB_FULL);
+  slot = SLOT_INVALID;
+  return RS_FOUND;
+}
+
+__device__ inline uint32_t id_settle(const DevGraph &g, uint64_t id, uint64_t bucket,
+                                     uint32_t slot, int state) {
+  const bool ins = state == RS_INSERTED;
+  const unsigned long long s = wave_append(&g.ctr->slot_top, ins);
+  const uint64_t ball = __ballot(ins);
+  if (lane_id() == 0 && ball) atomicAdd(&g.ctr->inserted, (unsigned long long)__popcll(ball));
+  if (ins) {
+    if (s >= g.scap) {
+      set_err(g.ctr, ERR_SLOTS_FULL);
+      slot = SLOT_INVALID;
+    } else {
+      slot = (uint32_t)s;
+      g.vid[s] = id;
+      g.flags[s] = FL_ALIVE;
+    }
+    atomicExch(&g.hval[bucket], slot);
+  }
+  if (state == RS_PENDING) {
+    slot = SLOT_INVALID;
+    for (uint32_t spin = 0; spin < (1u << 24); ++spin) {
+      uint32_t v = atomicOr(&g.hval[bucket], 0u);
+      if (v != VAL_PENDING) {
+        slot = v;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (slot == SLOT_INVALID) set_err(g.ctr, ERR_SPIN);
+  }
+  return state == RS_NONE ? SLOT_INVALID : slot;
+}
+
+// Uniform helper: every lane calls; lanes with !has get SLOT_INVALID.
+__device__ inline uint32_t id_resolve(const DevGraph &g, bool has, uint64_t id) {
+  uint64_t bucket = 0;
+  uint32_t slot = SLOT_INVALID;
+  int st = RS_NONE;
+  if (has) st = id_probe(g, id, bucket, slot);
+  return id_settle(g, id, bucket, slot, st);
+}
+
+// Lookup without insertion (tombstones are skipped, EMPTY ends the chain).
+__device__ inline uint32_t id_find(const DevGraph &g, uint64_t id, uint64_t *bucket = nullptr) {
+  uint64_t h = mix64(id) & g.hmask;
+  for (uint64_t probe = 0; probe < g.hcap; ++probe) {
+    uint64_t k = g.hkey[h];
+    if (k == id) {
+      if (bucket) *bucket = h;
+      return g.hval[h];
+    }
+    if (k == KEY_EMPTY) return SLOT_NONE;
+    h = (h + 1) & g.hmask;
+  }
+  return SLOT_NONE;
+}
+
+// ---- edge table ------------------------------------------------------------
+__device__ inline uint64_t edge_key(uint32_t owner, uint32_t target) {
+  return ((uint64_t)owner << 32) | target;
+}
+
+// Returns the bucket of `key`; *inserted tells whether this thread created it.
+__device__ inline uint64_t edge_find_or_insert(const DevGraph &g, uint64_t key, bool *inserted) {
+  uint64_t h = mix64(key) & g.emask;
+  *inserted = false;
+  for (uint64_t probe = 0; probe < g.ecap_tab; ++probe) {
+    uint64_t k = g.ekey[h];
+    if (k == KEY_EMPTY) {
+      k = atomicCAS((unsigned long long *)&g.ekey[h], (unsigned long long)KEY_EMPTY,
+                    (unsigned long long)key);
+      if (k == KEY_EMPTY) {
+        *inserted = true;
+        return h;
+      }
+    }
+    if (k == key) return h;
+    h = (h + 1) & g.emask;
+  }
+  set_err(g.ctr, ERR_ETAB_FULL);
+  return KEY_EMPTY;
+}
+
+__device__ inline uint64_t pack_edge(uint32_t target, int32_t count) {
+  return ((uint64_t)(uint32_t)count << 32) | target;
+}
+__device__ inline uint32_t edge_target(uint64_t e) { return (uint32_t)e; }
+__device__ inline int32_t edge_count(uint64_t e) { return (int32_t)(uint32_t)(e >> 32); }
+__device__ inline int32_t *edge_count_ptr(uint64_t *pool, uint64_t i) {
+  return reinterpret_cast<int32_t *>(pool + i) + 1;
+}
+
+// RefobInfo.count / isActive (RefobInfo.java:23-29)
+__device__ inline int32_t refob_count(int16_t info) { return (int16_t)(((int32_t)info) >> 1); }
+__device__ inline bool refob_deactivated(int16_t info) { return (info & 1) != 0; }
+
+}  // namespace crgc

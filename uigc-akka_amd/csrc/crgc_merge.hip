@@ -1,0 +1,452 @@
+// crgc_merge.hip — entry / delta / undo-log merge kernels (gfx950).
+//
+// A merge call replaces N sequential ShadowGraph.mergeEntry / mergeDelta calls
+// (ShadowGraph.java:75-156) by one data-parallel pass, exact because the merge
+// is commutative except for last-write-wins fields:
+//   * recvCount        += deltas          -> wrapping int32 atomics
+//   * outgoing[o][t]   += deltas          -> edge pipeline (k_edge_* below)
+//   * interned/isLocal |= ...             -> written by the LWW winner (every
+//                                            record that sets busy/root sets them)
+//   * isBusy/isRoot     last write wins   -> atomicMax of (epoch<<32 | seq) tags,
+//   * supervisor        last write wins      then the winner writes the field.
+// `epoch` counts merge calls, `seq` is the record's position inside the call,
+// so "last" is exactly the reference's order (LocalGC.scala:152-172).
+#include "crgc_host.hpp"
+
+namespace crgc {
+
+__device__ inline bool vs(uint32_t s) { return s < 0xFFFFFFF0u; }
+
+// ---------------------------------------------------------------------------
+// Entries — ShadowGraph.mergeEntry, ShadowGraph.java:75-125.
+// One thread per entry; the created / spawned / updated records are walked in
+// wave-uniform rounds so that id resolution (id_resolve) can aggregate slot
+// allocation per wave.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_entries_resolve(DevGraph g, EntryArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool valid = i < a.n;
+  uint64_t self = 0;
+  uint32_t c0 = 0, c1 = 0, s0 = 0, s1 = 0, u0 = 0, u1 = 0;
+  int16_t rc = 0;
+  bool ok = valid;
+  const uint32_t ctot = a.c_off[a.n];
+  if (valid) {
+    self = a.self[i];
+    rc = a.recv[i];
+    c0 = a.c_off[i]; c1 = a.c_off[i + 1];
+    s0 = a.s_off[i]; s1 = a.s_off[i + 1];
+    u0 = a.u_off[i]; u1 = a.u_off[i + 1];
+    if (c1 < c0 || s1 < s0 || u1 < u0 || c1 > a.n * a.F || s1 > a.n * a.F || u1 > a.n * a.F) {
+      set_err(g.ctr, ERR_BAD_OFFSETS);
+      ok = false;
+    } else if (c1 - c0 > a.F || s1 - s0 > a.F || u1 - u0 > a.F) {
+      set_err(g.ctr, ERR_TOO_MANY);
+      ok = false;
+    }
+    if (reserved_id(self)) {
+      set_err(g.ctr, ERR_RESERVED_ID);
+      ok = false;
+    }
+  }
+  const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
+
+  // Local information (:77-82): recv delta and the busy/root LWW tag.
+  const uint32_t me = id_resolve(g, ok, self);
+  if (valid) a.self_slot[i] = ok ? me : SLOT_INVALID;
+  if (ok && vs(me)) {
+    if (rc != 0) atomicAdd(&g.recv[me], (int32_t)rc);
+    atomicMax(&g.vseq[me], tag);
+  }
+
+  // Created refs (:85-93): outgoing[owner][target] += 1.  Target first.
+  const uint32_t nc = ok ? c1 - c0 : 0;
+  for (uint32_t k = 0; __ballot(k < nc); ++k) {
+    bool has = k < nc;
+    uint64_t tid = 0, oid = 0;
+    if (has) {
+      tid = a.c_target[c0 + k];
+      oid = a.c_owner[c0 + k];
+      if (reserved_id(tid) || reserved_id(oid)) {
+        set_err(g.ctr, ERR_RESERVED_ID);
+        has = false;
+      }
+    }
+    const uint32_t ts = id_resolve(g, has, tid);
+    const uint32_t os = id_resolve(g, has, oid);
+    if (k < nc) {
+      a.atom_o[c0 + k] = os;
+      a.atom_t[c0 + k] = ts;
+      a.atom_d[c0 + k] = (has && vs(os) && vs(ts)) ? 1 : 0;
+    }
+  }
+
+  // Spawned actors (:96-104): child.supervisor = self, last write wins.
+  const uint32_t ns = ok ? s1 - s0 : 0;
+  for (uint32_t k = 0; __ballot(k < ns); ++k) {
+    bool has = k < ns;
+    uint64_t cid = 0;
+    if (has) {
+      cid = a.spawned[s0 + k];
+      if (reserved_id(cid)) {
+        set_err(g.ctr, ERR_RESERVED_ID);
+        has = false;
+      }
+    }
+    const uint32_t cs = id_resolve(g, has, cid);
+    if (k < ns) {
+      const bool good = has && vs(cs) && vs(me);
+      a.spawn_slot[s0 + k] = good ? cs : SLOT_INVALID;
+      if (good) atomicMax(&g.sseq[cs], tag);
+    }
+  }
+
+  // Updated refs (:107-123): target.recv -= count; deactivation -> -1 edge.
+  const uint32_t nu = ok ? u1 - u0 : 0;
+  for (uint32_t k = 0; __ballot(k < nu); ++k) {
+    bool has = k < nu;
+    uint64_t rid = 0;
+    int16_t info = 0;
+    if (has) {
+      rid = a.u_ref[u0 + k];
+      info = a.u_info[u0 + k];
+      if (reserved_id(rid)) {
+        set_err(g.ctr, ERR_RESERVED_ID);
+        has = false;
+      }
+    }
+    const uint32_t ts = id_resolve(g, has, rid);
+    if (k < nu) {
+      const bool good = has && vs(ts) && vs(me);
+      const int32_t cnt = refob_count(info);
+      if (good && cnt > 0) atomicAdd(&g.recv[ts], -cnt);
+      const uint64_t at = (uint64_t)ctot + u0 + k;
+      a.atom_o[at] = me;
+      a.atom_t[at] = ts;
+      a.atom_d[at] = (good && refob_deactivated(info)) ? -1 : 0;
+    }
+  }
+}
+
+// The LWW winners write the flag byte and the supervisor slot.
+__global__ __launch_bounds__(256) void k_entries_lww(DevGraph g, EntryArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const uint32_t me = a.self_slot[i];
+  if (!vs(me)) return;
+  const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
+  if (g.vseq[me] == tag) {
+    const uint8_t ef = a.flags[i];
+    uint8_t f = g.flags[me] & (uint8_t)~(FL_BUSY | FL_ROOT);
+    f |= FL_INTERNED | FL_LOCAL;
+    if (ef & CRGC_ENTRY_BUSY) f |= FL_BUSY;
+    if (ef & CRGC_ENTRY_ROOT) f |= FL_ROOT;
+    g.flags[me] = f;
+  }
+  const uint32_t s0 = a.s_off[i], s1 = a.s_off[i + 1];
+  for (uint32_t k = s0; k < s1; ++k) {
+    const uint32_t cs = a.spawn_slot[k];
+    if (vs(cs) && g.sseq[cs] == tag) g.sup[cs] = me;
+  }
+}
+
+hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  const int blocks = (int)((a.n + 255) / 256);
+  hipLaunchKernelGGL(k_entries_resolve, dim3(blocks), dim3(256), 0, s, g, a);
+  hipLaunchKernelGGL(k_entries_lww, dim3(blocks), dim3(256), 0, s, g, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Deltas — ShadowGraph.mergeDelta, ShadowGraph.java:127-156.  One thread per
+// delta shadow, in arrival order (seq).  Flags only when the shadow is
+// interned (:139-146); isLocal is never set (:135).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_deltas_resolve(DevGraph g, DeltaArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool valid = i < a.n;
+  uint64_t id = 0, sid = CRGC_NO_ACTOR;
+  uint32_t o0 = 0, o1 = 0;
+  uint8_t fl = 0;
+  int32_t rc = 0;
+  bool ok = valid;
+  if (valid) {
+    id = a.id[i];
+    sid = a.sup[i];
+    fl = a.flags[i];
+    rc = a.recv[i];
+    o0 = a.out_off[i];
+    o1 = a.out_off[i + 1];
+    if (o1 < o0) {
+      set_err(g.ctr, ERR_BAD_OFFSETS);
+      ok = false;
+    }
+    if (reserved_id(id) || (sid != CRGC_NO_ACTOR && reserved_id(sid))) {
+      set_err(g.ctr, ERR_RESERVED_ID);
+      ok = false;
+    }
+  }
+  const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
+  const uint32_t me = id_resolve(g, ok, id);
+  if (valid) a.self_slot[i] = ok ? me : SLOT_INVALID;
+  if (ok && vs(me)) {
+    if (rc != 0) atomicAdd(&g.recv[me], rc);
+    if (fl & CRGC_DELTA_INTERNED) atomicMax(&g.vseq[me], tag);
+  }
+  const bool has_sup = ok && sid != CRGC_NO_ACTOR;
+  const uint32_t ss = id_resolve(g, has_sup, sid);
+  if (valid) a.sup_slot[i] = (has_sup && vs(ss) && vs(me)) ? ss : SLOT_INVALID;
+  if (has_sup && vs(ss) && vs(me)) atomicMax(&g.sseq[me], tag);
+
+  const uint32_t no = ok ? o1 - o0 : 0;
+  for (uint32_t k = 0; __ballot(k < no); ++k) {
+    bool has = k < no;
+    uint64_t tid = 0;
+    if (has) {
+      tid = a.out_target[o0 + k];
+      if (reserved_id(tid)) {
+        set_err(g.ctr, ERR_RESERVED_ID);
+        has = false;
+      }
+    }
+    const uint32_t ts = id_resolve(g, has, tid);
+    if (k < no) {
+      a.atom_o[o0 + k] = me;
+      a.atom_t[o0 + k] = ts;
+      a.atom_d[o0 + k] = (has && vs(ts) && vs(me)) ? a.out_count[o0 + k] : 0;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_deltas_lww(DevGraph g, DeltaArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const uint32_t me = a.self_slot[i];
+  if (!vs(me)) return;
+  const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
+  const uint8_t df = a.flags[i];
+  if ((df & CRGC_DELTA_INTERNED) && g.vseq[me] == tag) {
+    uint8_t f = g.flags[me] & (uint8_t)~(FL_BUSY | FL_ROOT);
+    f |= FL_INTERNED;
+    if (df & CRGC_DELTA_BUSY) f |= FL_BUSY;
+    if (df & CRGC_DELTA_ROOT) f |= FL_ROOT;
+    g.flags[me] = f;
+  }
+  const uint32_t ss = a.sup_slot[i];
+  if (vs(ss) && g.sseq[me] == tag) g.sup[me] = ss;
+}
+
+hipError_t launch_deltas(const DevGraph &g, const DeltaArgs &a, uint64_t n_out, hipStream_t s) {
+  (void)n_out;
+  if (a.n == 0) return hipSuccess;
+  const int blocks = (int)((a.n + 255) / 256);
+  hipLaunchKernelGGL(k_deltas_resolve, dim3(blocks), dim3(256), 0, s, g, a);
+  hipLaunchKernelGGL(k_deltas_lww, dim3(blocks), dim3(256), 0, s, g, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Undo logs — ShadowGraph.mergeUndoLog, ShadowGraph.java:158-174.
+// ---------------------------------------------------------------------------
+// The reference throws ConcurrentModificationException when a created-ref
+// target of an admitted actor is not yet in the graph: detect it.
+__global__ __launch_bounds__(256) void k_undo_check(DevGraph g, UndoArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  if (id_find(g, a.actor[i]) == SLOT_NONE) return;  // field ignored (:166-167)
+  for (uint32_t k = a.c_off[i]; k < a.c_off[i + 1]; ++k)
+    if (id_find(g, a.c_target[k]) == SLOT_NONE) set_err(g.ctr, ERR_UNDO_NEW);
+}
+
+// 1. every shadow at the downed location becomes halted (:163-165)
+__global__ __launch_bounds__(256) void k_undo_halt(DevGraph g, uint16_t loc, uint64_t slot_top) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= slot_top) return;
+  const uint8_t f = g.flags[v];
+  if ((f & FL_ALIVE) && (uint16_t)(g.vid[v] >> 48) == loc) g.flags[v] = f | FL_HALTED;
+}
+
+// 2./3. undelivered messages and created refs of admitted actors (:166-172)
+__global__ __launch_bounds__(256) void k_undo_fields(DevGraph g, UndoArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const uint32_t s = id_find(g, a.actor[i]);
+  const bool ok = s != SLOT_NONE;
+  if (ok && a.msg[i] != 0) atomicAdd(&g.recv[s], a.msg[i]);
+  for (uint32_t k = a.c_off[i]; k < a.c_off[i + 1]; ++k) {
+    const uint32_t t = ok ? id_find(g, a.c_target[k]) : SLOT_NONE;
+    a.atom_o[k] = s;
+    a.atom_t[k] = t;
+    a.atom_d[k] = (ok && t != SLOT_NONE) ? a.c_count[k] : 0;
+  }
+}
+
+hipError_t launch_undo_check(const DevGraph &g, const UndoArgs &a, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_undo_check, dim3((a.n + 255) / 256), dim3(256), 0, s, g, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_undo_apply(const DevGraph &g, const UndoArgs &a, uint64_t slot_top,
+                             hipStream_t s) {
+  if (slot_top)
+    hipLaunchKernelGGL(k_undo_halt, dim3((slot_top + 255) / 256), dim3(256), 0, s, g,
+                       a.location, slot_top);
+  if (a.n)
+    hipLaunchKernelGGL(k_undo_fields, dim3((a.n + 255) / 256), dim3(256), 0, s, g, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Edge pipeline — outgoing[o][t] += d  (ShadowGraph.updateOutgoing, :64-73).
+// Absent == 0, so zero counts are simply kept (they are never traced) until a
+// rebuild drops them.
+//   1. k_edge_apply: find-or-insert (o,t) in the edge table.  Existing edges
+//      get a memory-side atomic add on their pool count; keys new in this merge
+//      accumulate in edelta[bucket] and take a rank among the owner's new edges.
+//   2. k_edge_plan:  owners whose segment overflows get a new segment
+//      (pow2 capacity), one atomic per wave on pool_top.
+//   3. k_edge_move:  one wave per relocated owner copies its segment.
+//   4. k_edge_append: new edges are written after the owner's old degree.
+//   5. k_edge_finish: degrees advance, per-owner counters reset.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_edge_apply(DevGraph g, EdgeArgs a) {
+  const uint64_t n = a.n_atoms_dev ? *a.n_atoms_dev : a.max_atoms;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t base = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); base < n;
+       base += stride) {
+    const uint64_t i = base + lane_id();
+    const bool valid = i < n;
+    uint32_t o = 0, t = 0;
+    int32_t d = 0;
+    if (valid) {
+      o = a.atom_o[i];
+      t = a.atom_t[i];
+      d = a.atom_d[i];
+    }
+    bool active = valid && d != 0 && vs(o) && vs(t);
+    bool ins = false;
+    uint64_t b = 0;
+    if (active) {
+      b = edge_find_or_insert(g, edge_key(o, t), &ins);
+      if (b == KEY_EMPTY) active = ins = false;
+    }
+    uint32_t rank = 0;
+    if (ins) {
+      rank = atomicAdd(&g.enew[o], 1u);
+      g.eval[b] = EVAL_NEW | rank;
+      atomicAdd(&g.edelta[b], d);
+    } else if (active) {
+      const uint32_t v = g.eval[b];
+      if (v & EVAL_NEW)
+        atomicAdd(&g.edelta[b], d);
+      else
+        atomicAdd(edge_count_ptr(g.pool, (uint64_t)g.adj[o].x + v), d);
+    }
+    const unsigned long long li = wave_append(&g.ctr->n_new_edges, ins);
+    if (ins) a.newlist[li] = b;
+    const uint64_t insb = __ballot(ins);
+    if (lane_id() == 0 && insb) atomicAdd(&g.ctr->etab_used, (unsigned long long)__popcll(insb));
+    const bool first = ins && rank == 0;
+    const unsigned long long ti = wave_append(&g.ctr->n_touched, first);
+    if (first) a.touched[ti] = o;
+  }
+}
+
+__device__ inline uint32_t seg_cap(uint32_t need) {
+  uint32_t c = 4;
+  while (c < need) c <<= 1;
+  return c;
+}
+
+__global__ __launch_bounds__(256) void k_edge_plan(DevGraph g, EdgeArgs a) {
+  const uint64_t n = g.ctr->n_touched;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t base = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); base < n;
+       base += stride) {
+    const uint64_t i = base + lane_id();
+    uint32_t want = 0;
+    if (i < n) {
+      const uint32_t o = a.touched[i];
+      const uint32_t need = g.adj[o].y + g.enew[o];
+      if (need > g.ecap[o]) want = seg_cap(need);
+    }
+    const unsigned long long off = wave_atomic_add(&g.ctr->pool_top, want);
+    if (i < n) {
+      uint32_t r = 0xFFFFFFFFu;  // no move
+      if (want) {
+        if (off + want > g.pcap) {
+          set_err(g.ctr, ERR_POOL_FULL);
+          r = 0xFFFFFFFEu;
+        } else {
+          r = (uint32_t)off;
+        }
+      }
+      a.reloc[i] = r;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_edge_move(DevGraph g, EdgeArgs a) {
+  const uint64_t n = g.ctr->n_touched;
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += nw) {
+    const uint32_t r = a.reloc[i];
+    if (r >= 0xFFFFFFFEu) continue;
+    const uint32_t o = a.touched[i];
+    const uint2 ad = g.adj[o];
+    for (uint32_t e = lane_id(); e < ad.y; e += 64) g.pool[(uint64_t)r + e] = g.pool[(uint64_t)ad.x + e];
+    if (lane_id() == 0) {
+      g.adj[o].x = r;
+      g.ecap[o] = seg_cap(ad.y + g.enew[o]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_edge_append(DevGraph g, EdgeArgs a) {
+  const uint64_t n = g.ctr->n_new_edges;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const uint64_t b = a.newlist[i];
+    const uint64_t key = g.ekey[b];
+    const uint32_t o = (uint32_t)(key >> 32), t = (uint32_t)key;
+    const uint32_t rank = g.eval[b] & ~EVAL_NEW;
+    const uint2 ad = g.adj[o];
+    const uint32_t idx = ad.y + rank;
+    if (idx >= g.ecap[o]) continue;  // relocation failed: ERR_POOL_FULL already set
+    g.pool[(uint64_t)ad.x + idx] = pack_edge(t, g.edelta[b]);
+    g.eval[b] = idx;
+    g.edelta[b] = 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_edge_finish(DevGraph g, EdgeArgs a) {
+  const uint64_t n = g.ctr->n_touched;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const uint32_t o = a.touched[i];
+    g.adj[o].y += g.enew[o];
+    g.enew[o] = 0;
+  }
+}
+
+int grid_for(uint64_t threads, int block, int cap) {
+  uint64_t b = (threads + block - 1) / block;
+  if (b < 1) b = 1;
+  if (b > (uint64_t)cap) b = cap;
+  return (int)b;
+}
+
+hipError_t launch_edges(const DevGraph &g, const EdgeArgs &a, hipStream_t s) {
+  if (a.max_atoms == 0) return hipSuccess;
+  const int grid = grid_for(a.max_atoms, 256, 8192);
+  hipLaunchKernelGGL(k_edge_apply, dim3(grid), dim3(256), 0, s, g, a);
+  hipLaunchKernelGGL(k_edge_plan, dim3(grid), dim3(256), 0, s, g, a);
+  hipLaunchKernelGGL(k_edge_move, dim3(grid), dim3(256), 0, s, g, a);
+  hipLaunchKernelGGL(k_edge_append, dim3(grid), dim3(256), 0, s, g, a);
+  hipLaunchKernelGGL(k_edge_finish, dim3(grid), dim3(256), 0, s, g, a);
+  return hipGetLastError();
+}
+
+}  // namespace crgc

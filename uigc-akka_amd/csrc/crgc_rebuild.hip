@@ -1,0 +1,206 @@
+// crgc_rebuild.hip — compaction of the HBM shadow graph.
+//
+// Collected shadows leave a tombstone in the id table and a dead slot whose
+// pool segment and incoming edges linger; slots are never reused before a
+// rebuild, which makes the lingering edges harmless (they point at a slot no
+// live id maps to, exactly like the reference's outgoing keys that still name
+// a collected Shadow object — SURVEY E9).  A rebuild renumbers the live slots
+// densely, drops zero-count edges and edges to dead slots, re-packs every
+// segment at power-of-two capacity and rebuilds both hash tables.  It runs
+// when a capacity would be exceeded, never on the per-wakeup path unless the
+// graph has grown.
+#include "crgc_host.hpp"
+
+namespace crgc {
+
+__device__ inline uint32_t rb_cap(uint32_t k) {
+  if (k == 0) return 0;
+  uint32_t c = 4;
+  while (c < k) c <<= 1;
+  return c;
+}
+
+// 1. live vertices -> dense new slots, id table rebuilt.
+__global__ __launch_bounds__(256) void k_rb_vertices(DevGraph src, uint64_t src_top, DevGraph dst,
+                                                     uint32_t *map) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t base = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); base < src_top;
+       base += stride) {
+    const uint64_t v = base + lane_id();
+    const bool alive = v < src_top && (src.flags[v] & FL_ALIVE);
+    const unsigned long long ns = wave_append(&dst.ctr->slot_top, alive);
+    if (v < src_top) map[v] = alive ? (uint32_t)ns : SLOT_NONE;
+    if (!alive) continue;
+    if (ns >= dst.scap) {
+      set_err(dst.ctr, ERR_SLOTS_FULL);
+      continue;
+    }
+    const uint64_t id = src.vid[v];
+    dst.vid[ns] = id;
+    dst.recv[ns] = src.recv[v];
+    dst.flags[ns] = src.flags[v];
+    uint64_t h = mix64(id) & dst.hmask;
+    for (uint64_t p = 0; p < dst.hcap; ++p) {
+      if (atomicCAS((unsigned long long *)&dst.hkey[h], (unsigned long long)KEY_EMPTY,
+                    (unsigned long long)id) == KEY_EMPTY) {
+        dst.hval[h] = (uint32_t)ns;
+        break;
+      }
+      h = (h + 1) & dst.hmask;
+    }
+  }
+}
+
+// 2. kept out-degree of every live vertex: nonzero count, live target.
+__global__ __launch_bounds__(256) void k_rb_count(DevGraph src, uint64_t src_top, const uint32_t *map,
+                                                  uint64_t *caps) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < src_top; v += stride) {
+    const uint32_t ns = map[v];
+    if (ns == SLOT_NONE) continue;
+    const uint2 ad = src.adj[v];
+    uint32_t k = 0;
+    for (uint32_t e = 0; e < ad.y; ++e) {
+      const uint64_t ed = src.pool[(uint64_t)ad.x + e];
+      if (edge_count(ed) != 0 && (src.flags[edge_target(ed)] & FL_ALIVE)) ++k;
+    }
+    caps[ns] = rb_cap(k);
+  }
+}
+
+// 4. copy kept edges (targets remapped), rebuild the edge table, remap the
+//    supervisor (a collected supervisor becomes SLOT_DEAD: non-null, unmarked).
+__global__ __launch_bounds__(256) void k_rb_edges(DevGraph src, uint64_t src_top, DevGraph dst,
+                                                  const uint32_t *map, const uint64_t *offs) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t base = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); base < src_top;
+       base += stride) {
+    const uint64_t v = base + lane_id();
+    uint32_t kept = 0;
+    if (v < src_top) {
+      const uint32_t ns = map[v];
+      if (ns != SLOT_NONE && ns < dst.scap) {
+        const uint2 ad = src.adj[v];
+        const uint64_t off = offs[ns];
+        for (uint32_t e = 0; e < ad.y; ++e) {
+          const uint64_t ed = src.pool[(uint64_t)ad.x + e];
+          const uint32_t t = edge_target(ed);
+          if (edge_count(ed) == 0 || !(src.flags[t] & FL_ALIVE)) continue;
+          const uint32_t nt = map[t];
+          dst.pool[off + kept] = pack_edge(nt, edge_count(ed));
+          const uint64_t key = edge_key(ns, nt);
+          uint64_t h = mix64(key) & dst.emask;
+          for (uint64_t p = 0; p < dst.ecap_tab; ++p) {
+            if (atomicCAS((unsigned long long *)&dst.ekey[h], (unsigned long long)KEY_EMPTY,
+                          (unsigned long long)key) == KEY_EMPTY) {
+              dst.eval[h] = kept;
+              break;
+            }
+            h = (h + 1) & dst.emask;
+          }
+          ++kept;
+        }
+        dst.adj[ns] = make_uint2((uint32_t)off, kept);
+        dst.ecap[ns] = rb_cap(kept);
+        const uint32_t s = src.sup[v];
+        uint32_t nsup = SLOT_NONE;
+        if (s == SLOT_DEAD) nsup = SLOT_DEAD;
+        else if (s != SLOT_NONE) nsup = (src.flags[s] & FL_ALIVE) ? map[s] : SLOT_DEAD;
+        dst.sup[ns] = nsup;
+      }
+    }
+    wave_atomic_add(&dst.ctr->etab_used, kept);
+  }
+}
+
+// ---- exclusive scan of uint64 (in place), 2048 elements per block ----------
+constexpr int SCAN_ITEMS = 8;
+constexpr int SCAN_TILE = 256 * SCAN_ITEMS;
+
+__device__ inline uint64_t block_excl_scan_u64(uint64_t x, uint64_t *total) {
+  __shared__ uint64_t warp_tot[4];
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  uint64_t incl = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint64_t y = __shfl_up(incl, d);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) warp_tot[wv] = incl;
+  __syncthreads();
+  uint64_t pre = 0, tot = 0;
+  for (int w = 0; w < 4; ++w) {
+    if (w < wv) pre += warp_tot[w];
+    tot += warp_tot[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + incl - x;
+}
+
+__global__ __launch_bounds__(256) void k_scan_tiles(uint64_t *data, uint64_t n, uint64_t *partials) {
+  const uint64_t t0 = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+  uint64_t v[SCAN_ITEMS];
+  uint64_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    v[k] = (t0 + k < n) ? data[t0 + k] : 0;
+    sum += v[k];
+  }
+  uint64_t tot;
+  uint64_t run = block_excl_scan_u64(sum, &tot);
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    if (t0 + k < n) data[t0 + k] = run;
+    run += v[k];
+  }
+  if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_scan_partials(uint64_t *partials, uint64_t nb, uint64_t *grand) {
+  uint64_t carry = 0;
+  for (uint64_t b0 = 0; b0 < nb; b0 += 256) {
+    const uint64_t i = b0 + threadIdx.x;
+    const uint64_t x = i < nb ? partials[i] : 0;
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan_u64(x, &tot);
+    if (i < nb) partials[i] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) *grand = carry;
+}
+
+__global__ __launch_bounds__(256) void k_scan_add(uint64_t *data, uint64_t n, const uint64_t *partials) {
+  const uint64_t t0 = (uint64_t)blockIdx.x * SCAN_TILE;
+  const uint64_t add = partials[blockIdx.x];
+  for (int k = threadIdx.x; k < SCAN_TILE; k += 256)
+    if (t0 + k < n) data[t0 + k] += add;
+}
+
+size_t rebuild_scan_tmp_bytes(uint64_t n) { return ((n + SCAN_TILE - 1) / SCAN_TILE + 2) * 8; }
+
+// scan_tmp layout: [partials (nb)] [grand total]
+static void exclusive_scan(uint64_t *data, uint64_t n, uint64_t *tmp, hipStream_t s) {
+  const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+  if (nb == 0) return;
+  hipLaunchKernelGGL(k_scan_tiles, dim3(nb), dim3(256), 0, s, data, n, tmp);
+  hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(256), 0, s, tmp, nb, tmp + nb);
+  hipLaunchKernelGGL(k_scan_add, dim3(nb), dim3(256), 0, s, data, n, tmp);
+}
+
+__global__ void k_rb_pool_top(Counters *c, const uint64_t *grand) { c->pool_top = *grand; }
+
+hipError_t launch_rebuild(const DevGraph &src, uint64_t src_top, const DevGraph &dst, uint32_t *map,
+                          uint32_t *newdeg, uint64_t *offs, void *scan_tmp, hipStream_t s) {
+  (void)newdeg;
+  const int grid = grid_for(src_top, 256, 8192);
+  hipLaunchKernelGGL(k_rb_vertices, dim3(grid), dim3(256), 0, s, src, src_top, dst, map);
+  hipLaunchKernelGGL(k_rb_count, dim3(grid), dim3(256), 0, s, src, src_top, map, offs);
+  exclusive_scan(offs, dst.scap, (uint64_t *)scan_tmp, s);
+  const uint64_t nb = (dst.scap + SCAN_TILE - 1) / SCAN_TILE;
+  hipLaunchKernelGGL(k_rb_pool_top, dim3(1), dim3(1), 0, s, dst.ctr, (uint64_t *)scan_tmp + nb);
+  hipLaunchKernelGGL(k_rb_edges, dim3(grid), dim3(256), 0, s, src, src_top, dst, map, offs);
+  return hipGetLastError();
+}
+
+}  // namespace crgc
