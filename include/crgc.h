@@ -146,8 +146,9 @@ typedef struct crgc_trace_stats {
   uint64_t pseudo_roots;   /* shadows passing isPseudoRoot (:201-203)       */
   uint64_t edges_scanned;  /* nonzero out-edges of marked non-halted shadows */
   uint64_t sup_edges;      /* supervisor edges followed (:258-267)          */
-  uint64_t levels;         /* BFS levels run                                */
-  double ms_mark;          /* device time: pseudo-roots + mark              */
+  uint64_t levels;         /* non-empty BFS levels                          */
+  uint64_t launches;       /* level-kernel launches (incl. trailing empty)  */
+  double ms_mark;          /* device time of the pseudo-root + level kernels*/
   double ms_sweep;         /* device time: sweep + id compaction            */
   double ms_total;         /* host wall time of crgc_trace                  */
 } crgc_trace_stats;

@@ -106,6 +106,7 @@ class CrgcTraceStats(C.Structure):
         ("edges_scanned", _U64),
         ("sup_edges", _U64),
         ("levels", _U64),
+        ("launches", _U64),
         ("ms_mark", C.c_double),
         ("ms_sweep", C.c_double),
         ("ms_total", C.c_double),

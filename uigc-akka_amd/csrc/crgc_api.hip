@@ -151,6 +151,8 @@ struct crgc_graph {
   uint64_t last_garbage = 0, last_kill = 0, last_live = 0;
   crgc_trace_stats last_stats{};
   bool have_last = false;
+  uint64_t last_levels = 0;
+  std::vector<hipEvent_t> lvl_ev;  // per-level-kernel event pairs
   uint64_t *roots_buf = nullptr;
   uint64_t roots_cap = 0;
 };
@@ -366,6 +368,7 @@ void crgc_destroy(crgc_graph *h) {
   if (h->roots_buf) hipFree(h->roots_buf);
   for (auto &e : h->ev)
     if (e) hipEventDestroy(e);
+  for (auto &e : h->lvl_ev) hipEventDestroy(e);
   if (h->own_stream && h->stream) hipStreamDestroy(h->stream);
   delete h;
 }
@@ -551,23 +554,41 @@ int crgc_merge_undo(crgc_graph *h, const crgc_undo_log *log) {
   return CRGC_OK;
 }
 
-// BFS driver shared by trace and count_reachable_from.  Returns levels run.
-static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64_t *levels,
-                      uint64_t *roots) {
-  const uint64_t top = h->slot_top + h->ids_since;
+// BFS driver shared by trace and count_reachable_from.  Every level kernel is
+// bracketed by its own event pair, so `kernel_ms` is device time of the level
+// kernels only (no host round-trip gaps).  Levels are enqueued in chunks; the
+// first chunk is as deep as the previous trace, so a steady-state wakeup needs
+// one host synchronisation.
+static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64_t top,
+                      uint64_t *levels, uint64_t *roots, double *kernel_ms, uint64_t *launches) {
   LevelArgs la{};
   la.location = location;
   la.sparse_thresh = (uint32_t)std::max<uint64_t>(64, (top / BLK_SLOTS) / 4);
-  la.level = 0;
-  HIP_TRY(launch_level(h->g.d, la, true, investigate, top, h->stream));
+  size_t nl = 0;
+  auto launch = [&](int level, bool rootk) -> hipError_t {
+    if (h->lvl_ev.size() < 2 * (nl + 1)) {
+      for (int k = 0; k < 2; ++k) {
+        hipEvent_t e;
+        hipError_t r = hipEventCreate(&e);
+        if (r != hipSuccess) return r;
+        h->lvl_ev.push_back(e);
+      }
+    }
+    hipError_t r = hipEventRecord(h->lvl_ev[2 * nl], h->stream);
+    if (r != hipSuccess) return r;
+    la.level = level;
+    r = launch_level(h->g.d, la, rootk, investigate, top, h->stream);
+    if (r != hipSuccess) return r;
+    r = hipEventRecord(h->lvl_ev[2 * nl + 1], h->stream);
+    ++nl;
+    return r;
+  };
+  HIP_TRY(launch(0, true));
   int L = 1;
-  int chunk = 8;
+  int chunk = (int)std::min<uint64_t>(std::max<uint64_t>(4, h->last_levels + 1), 512);
   std::vector<unsigned long long> ring(LEVEL_RING);
   for (;;) {
-    for (int k = 0; k < chunk; ++k) {
-      la.level = L + k;
-      HIP_TRY(launch_level(h->g.d, la, false, investigate, top, h->stream));
-    }
+    for (int k = 0; k < chunk; ++k) HIP_TRY(launch(L + k, false));
     // counts of levels L-1 .. L+chunk-1
     const int first = L - 1, last = L + chunk - 1;
     for (int lv = first; lv <= last;) {
@@ -582,6 +603,14 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
     for (int lv = first; lv <= last; ++lv) {
       if (ring[lv % LEVEL_RING] == 0) {
         *levels = (uint64_t)lv;  // levels 0 .. lv-1 were non-empty
+        double ms = 0;
+        for (size_t i = 0; i < nl; ++i) {
+          float t = 0;
+          hipEventElapsedTime(&t, h->lvl_ev[2 * i], h->lvl_ev[2 * i + 1]);
+          ms += t;
+        }
+        *kernel_ms = ms;
+        *launches = nl;
         return CRGC_OK;
       }
     }
@@ -628,13 +657,13 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   DeviceGuard dg(h->device);
   const auto t0 = std::chrono::steady_clock::now();
   // Surface merge-time device errors before tracing.
-  HIP_TRY(sync_counters(h));
-  if (int rc = device_error(h)) return rc;
-  const uint64_t top = h->slot_top;
+  // Grids are sized from an upper bound of slot_top; the kernels read the
+  // exact value from the device counters, so no synchronisation is needed here.
+  const uint64_t top = h->slot_top + h->ids_since;
   reset_trace_counters(h);
-  HIP_TRY(hipEventRecord(h->ev[0], h->stream));
-  uint64_t levels = 0, roots = 0;
-  if (int rc = run_levels(h, false, 0, &levels, &roots)) return rc;
+  uint64_t levels = 0, roots = 0, launches = 0;
+  double mark_ms = 0;
+  if (int rc = run_levels(h, false, 0, top, &levels, &roots, &mark_ms, &launches)) return rc;
   HIP_TRY(hipEventRecord(h->ev[1], h->stream));
   HIP_TRY(launch_sweep(h->g.d, should_kill ? 1 : 0, top, h->stream));
   HIP_TRY(launch_commit(h->g.d, top, h->stream));
@@ -648,9 +677,9 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   st.edges_scanned = c.edges_scanned;
   st.sup_edges = c.sup_edges;
   st.levels = levels;
+  st.launches = launches;
+  st.ms_mark = mark_ms;
   float ms = 0;
-  hipEventElapsedTime(&ms, h->ev[0], h->ev[1]);
-  st.ms_mark = ms;
   hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
   st.ms_sweep = ms;
   st.pseudo_roots = roots;
@@ -660,6 +689,7 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   h->live = c.n_live;
   h->inserted_at_trace = c.inserted;
   h->have_last = true;
+  h->last_levels = levels;
   const int rc = copy_lists(h, out);
   st.ms_total =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -713,8 +743,12 @@ int crgc_count_reachable_from(crgc_graph *h, uint16_t location, int64_t *out) {
   HIP_TRY(sync_counters(h));
   if (int rc = device_error(h)) return rc;
   reset_trace_counters(h);
-  uint64_t levels = 0, roots = 0;
-  if (int rc = run_levels(h, true, location, &levels, &roots)) return rc;
+  uint64_t levels = 0, roots = 0, launches = 0;
+  double ms = 0;
+  const uint64_t saved = h->last_levels;
+  const int rl = run_levels(h, true, location, h->slot_top, &levels, &roots, &ms, &launches);
+  h->last_levels = saved;
+  if (rl) return rl;
   HIP_TRY(sync_counters(h));
   *out = (int64_t)h->hctr->marked;
   return CRGC_OK;

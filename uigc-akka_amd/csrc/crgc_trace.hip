@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256) void k_level(DevGraph g, LevelArgs a) {
       m &= m - 1;
       s_front[wv][pos++] = (uint32_t)(base + j);
     }
-    n_front += total;
+    n_front += cnt;  // per lane; summed over the wave below
     wave_lds_fence();
 
     // Expand, 64 frontier shadows at a time.

@@ -1,0 +1,129 @@
+"""ctypes wrapper of world.cpp: seeded synthetic CRGC entry streams (C1-C4)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(_HERE), "uigc-akka_amd"))
+from crgc_hip.batch import EntryBatch  # noqa: E402
+
+LIB = os.path.join(_HERE, "_build", "libcrgc_workload.so")
+
+
+class WlBatch(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("C", C.c_uint64), ("S", C.c_uint64), ("U", C.c_uint64)] + \
+        [(k, C.c_void_p) for k in ("self", "recv", "flags", "c_off", "c_owner", "c_target",
+                                   "s_off", "spawned", "u_off", "u_ref", "u_info")]
+
+
+def build(force=False) -> str:
+    src = os.path.join(_HERE, "world.cpp")
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+        os.makedirs(os.path.dirname(LIB), exist_ok=True)
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", LIB, src])
+    return LIB
+
+
+_lib = None
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        build()
+        lib = C.CDLL(LIB)
+        lib.wl_create.restype = C.c_void_p
+        lib.wl_create.argtypes = [C.c_uint64, C.c_uint32, C.c_uint16]
+        lib.wl_destroy.argtypes = [C.c_void_p]
+        lib.wl_set_mix.argtypes = [C.c_void_p] + [C.c_double] * 5
+        lib.wl_bulk_graph.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_double,
+                                      C.c_uint32, C.c_uint64]
+        lib.wl_chain_graph.argtypes = [C.c_void_p] + [C.c_uint32] * 6
+        lib.wl_simulate.argtypes = [C.c_void_p, C.c_uint64]
+        for f in ("wl_queued", "wl_n_actors", "wl_n_refobs_held"):
+            getattr(lib, f).restype = C.c_uint64
+            getattr(lib, f).argtypes = [C.c_void_p]
+        lib.wl_take.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(WlBatch)]
+        lib.wl_compact.argtypes = [C.c_void_p]
+        _lib = lib
+    return _lib
+
+
+def _arr(ptr, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype)
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dtype))),
+                                 shape=(n,)).copy()
+
+
+class World:
+    """A simulated node: `seed`, entry-field size F, location id."""
+
+    def __init__(self, seed: int, F: int = 4, location: int = 1):
+        self.lib = _load()
+        self.h = self.lib.wl_create(seed, F, location)
+
+    def close(self):
+        if self.h:
+            self.lib.wl_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_mix(self, send=0.4, share=0.2, release=0.2, spawn=0.1, actions_per_msg=1.5):
+        self.lib.wl_set_mix(self.h, send, share, release, spawn, actions_per_msg)
+
+    def bulk_graph(self, n_actors, n_edges, alpha=2.1, n_roots=None, cap=100000):
+        n_roots = n_roots if n_roots is not None else max(1, n_actors // 100)
+        self.lib.wl_bulk_graph(self.h, n_actors, n_edges, alpha, n_roots, cap)
+
+    def chain_graph(self, n_chains=100, chain_len=10000, n_sup_chains=10, sup_depth=1000,
+                    n_rings=100, ring_len=100):
+        self.lib.wl_chain_graph(self.h, n_chains, chain_len, n_sup_chains, sup_depth,
+                                n_rings, ring_len)
+
+    def simulate(self, n_entries):
+        self.lib.wl_simulate(self.h, n_entries)
+
+    def queued(self) -> int:
+        return self.lib.wl_queued(self.h)
+
+    def n_actors(self) -> int:
+        return self.lib.wl_n_actors(self.h)
+
+    def n_refs(self) -> int:
+        return self.lib.wl_n_refobs_held(self.h)
+
+    def take(self, max_entries) -> EntryBatch:
+        b = WlBatch()
+        self.lib.wl_take(self.h, max_entries, C.byref(b))
+        n, nc, ns, nu = b.n, b.C, b.S, b.U
+        eb = EntryBatch(
+            _arr(b.self, n, np.uint64), _arr(b.recv, n, np.int16), _arr(b.flags, n, np.uint8),
+            _arr(b.c_off, n + 1, np.uint32), _arr(b.c_owner, nc, np.uint64),
+            _arr(b.c_target, nc, np.uint64), _arr(b.s_off, n + 1, np.uint32),
+            _arr(b.spawned, ns, np.uint64), _arr(b.u_off, n + 1, np.uint32),
+            _arr(b.u_ref, nu, np.uint64), _arr(b.u_info, nu, np.int16))
+        self.lib.wl_compact(self.h)
+        return eb
+
+    def batches(self, batch_size):
+        """Drain the queue in batches of `batch_size` entries."""
+        while self.queued():
+            yield self.take(batch_size)
+
+    def wakeup_batch(self, n_entries) -> EntryBatch:
+        """Simulate until n_entries are queued and take exactly those."""
+        need = n_entries - self.queued()
+        if need > 0:
+            self.simulate(need)
+        return self.take(n_entries)
