@@ -96,7 +96,8 @@ class OracleGraph:
         self._chk(self.lib.oracle_trace(self.h, int(bool(should_kill)), C.byref(out)), "trace")
         st = out.stats
         return TraceResult(g[:out.n_garbage].copy(), k[:out.n_kill].copy(), int(out.n_live),
-                           st.pseudo_roots, st.edges_scanned, st.sup_edges, st.levels)
+                           st.pseudo_roots, st.edges_scanned, st.sup_edges, st.levels,
+                           st.launches)
 
     def local_roots(self):
         n = C.c_uint64()

@@ -1,0 +1,66 @@
+"""Interleaved A/B timing of trace variants on one resident C2 graph.
+
+Variants are selected by environment switches read per trace (CRGC_* in
+crgc_api.hip); results must be identical, only timings differ.
+
+    python tools/ab_trace.py --actors 10000000 --edges 100000000 --rounds 8 \
+        --variant CRGC_MARK_CHECK=0 --variant CRGC_MARK_CHECK=1
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for sub in ("uigc-akka_amd", "workload"):
+    sys.path.insert(0, os.path.join(REPO, sub))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--actors", type=int, default=10_000_000)
+    ap.add_argument("--edges", type=int, default=100_000_000)
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--variant", action="append", default=[])
+    args = ap.parse_args()
+    import torch
+    import crgc_hip
+    import world
+    w = world.World(seed=0x5EED + 2)
+    w.bulk_graph(args.actors, args.edges, alpha=2.1, n_roots=max(1, args.actors // 1000))
+    g = crgc_hip.ShadowGraph(vertex_capacity=int(args.actors * 1.2),
+                             edge_capacity=int(args.edges * 1.2))
+    for b in w.batches(1_000_000):
+        g.merge_entries(b.to_device("cuda"))
+    g.trace_counts(True)
+    g.merge_entries(w.wakeup_batch(1_000_000).to_device("cuda"))
+    g.trace_counts(True)
+    variants = args.variant or ["BASE=0"]
+    res = {v: [] for v in variants}
+    ref = None
+    for r in range(args.rounds):
+        for v in variants:
+            k, val = v.split("=")
+            os.environ[k] = val
+            t = time.perf_counter()
+            out, ng, nk = g.trace_counts(True)
+            wall = (time.perf_counter() - t) * 1e3
+            key = (out.n_live, out.edges_scanned, out.levels, ng)
+            ref = ref or key
+            assert key == ref, (v, key, ref)
+            res[v].append((out.ms_mark, out.ms_sweep, wall))
+            del os.environ[k]
+    summary = {}
+    for v, xs in res.items():
+        summary[v] = {"mark_ms_median": statistics.median(x[0] for x in xs),
+                      "mark_ms_min": min(x[0] for x in xs),
+                      "sweep_ms_median": statistics.median(x[1] for x in xs),
+                      "wall_ms_median": statistics.median(x[2] for x in xs)}
+    print(json.dumps({"shape": {"live": ref[0], "edges_scanned": ref[1], "levels": ref[2]},
+                      "variants": summary}))
+
+
+if __name__ == "__main__":
+    main()

@@ -332,6 +332,7 @@ class TraceResult:
     edges_scanned: int = 0
     sup_edges: int = 0
     levels: int = 0
+    launches: int = 0
     ms_mark: float = 0.0
     ms_sweep: float = 0.0
     ms_total: float = 0.0

@@ -100,37 +100,53 @@ class ShadowGraph:
     mergeUndoLog = merge_undo
 
     # -- trace ----------------------------------------------------------------
-    def trace(self, shouldKill: bool = True, capacity: Optional[int] = None) -> TraceResult:
-        self.flush()
-        cap = capacity if capacity is not None else self.live_count_upper()
-        g = np.zeros(max(cap, 1), np.uint64)
-        k = np.zeros(max(cap, 1), np.uint64)
+    @staticmethod
+    def _result(out, g, k) -> TraceResult:
+        st = out.stats
+        return TraceResult(g, k, int(out.n_live), int(st.pseudo_roots), int(st.edges_scanned),
+                           int(st.sup_edges), int(st.levels), int(st.launches), st.ms_mark,
+                           st.ms_sweep, st.ms_total)
+
+    def _trace_into(self, shouldKill, g, k):
         out = abi.CrgcTraceOut()
-        out.garbage_ids, out.garbage_cap = _ptr(g), cap
-        out.kill_ids, out.kill_cap = _ptr(k), cap
+        out.garbage_ids, out.garbage_cap = _ptr(g), len(g)
+        out.kill_ids, out.kill_cap = _ptr(k), len(k)
         rc = self.lib.crgc_trace(self.h, int(bool(shouldKill)), C.byref(out))
+        return rc, out
+
+    def trace(self, shouldKill: bool = True) -> TraceResult:
+        """ShadowGraph.trace(shouldKill): returns the garbage and kill id sets."""
+        r, ng, nk = self.trace_kill_ids(shouldKill)
+        return TraceResult(r.garbage[:ng].copy(), r.kill[:nk].copy(), *[
+            getattr(r, f) for f in ("n_live", "pseudo_roots", "edges_scanned", "sup_edges",
+                                    "levels", "launches", "ms_mark", "ms_sweep", "ms_total")])
+
+    def trace_kill_ids(self, shouldKill: bool = True):
+        """trace() into reusable host buffers: (result with buffer views, n_garbage, n_kill)."""
+        self.flush()
+        if getattr(self, "_gbuf", None) is None:
+            self._gbuf = np.zeros(1 << 16, np.uint64)
+            self._kbuf = np.zeros(1 << 16, np.uint64)
+        rc, out = self._trace_into(shouldKill, self._gbuf, self._kbuf)
         if rc == abi.E2BIG:
-            g = np.zeros(max(int(out.n_garbage), 1), np.uint64)
-            k = np.zeros(max(int(out.n_kill), 1), np.uint64)
-            out.garbage_ids, out.garbage_cap = _ptr(g), int(out.n_garbage)
-            out.kill_ids, out.kill_cap = _ptr(k), int(out.n_kill)
+            if out.n_garbage > len(self._gbuf):
+                self._gbuf = np.zeros(int(out.n_garbage) * 2, np.uint64)
+            if out.n_kill > len(self._kbuf):
+                self._kbuf = np.zeros(int(out.n_kill) * 2, np.uint64)
+            out.garbage_ids, out.garbage_cap = _ptr(self._gbuf), len(self._gbuf)
+            out.kill_ids, out.kill_cap = _ptr(self._kbuf), len(self._kbuf)
             rc = self.lib.crgc_last_trace(self.h, C.byref(out))
         self._chk(rc, "crgc_trace")
-        st = out.stats
-        return TraceResult(g[:out.n_garbage].copy(), k[:out.n_kill].copy(), int(out.n_live),
-                           int(st.pseudo_roots), int(st.edges_scanned), int(st.sup_edges),
-                           int(st.levels), st.ms_mark, st.ms_sweep, st.ms_total)
+        ng, nk = int(out.n_garbage), int(out.n_kill)
+        return self._result(out, self._gbuf[:ng], self._kbuf[:nk]), ng, nk
 
-    def trace_counts(self, shouldKill: bool = True) -> TraceResult:
+    def trace_counts(self, shouldKill: bool = True):
         """trace() without copying the id lists back (counts and timings only)."""
         self.flush()
         out = abi.CrgcTraceOut()
         self._chk(self.lib.crgc_trace(self.h, int(bool(shouldKill)), C.byref(out)), "crgc_trace")
-        st = out.stats
         e = np.zeros(0, np.uint64)
-        return TraceResult(e, e, int(out.n_live), int(st.pseudo_roots), int(st.edges_scanned),
-                           int(st.sup_edges), int(st.levels), st.ms_mark, st.ms_sweep,
-                           st.ms_total), int(out.n_garbage), int(out.n_kill)
+        return self._result(out, e, e), int(out.n_garbage), int(out.n_kill)
 
     # -- queries --------------------------------------------------------------
     def startWave(self) -> np.ndarray:
@@ -168,9 +184,6 @@ class ShadowGraph:
         v = C.c_uint64()
         self._chk(self.lib.crgc_live_count(self.h, C.byref(v)), "crgc_live_count")
         return v.value
-
-    def live_count_upper(self) -> int:
-        return self.totalActorsSeen  # every live shadow was created at some point
 
     def export(self):
         self.flush()

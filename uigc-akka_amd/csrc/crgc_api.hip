@@ -43,7 +43,8 @@ void free_arrays(Arrays &a) {
   DevGraph &d = a.d;
   void *ps[] = {d.hkey, d.hval, d.vid, d.recv, d.flags, d.sup, d.adj, d.ecap, d.vseq, d.sseq,
                 d.enew, d.pool, d.ekey, d.eval, d.edelta, d.vis, d.front[0], d.front[1],
-                d.dirty[0], d.dirty[1], d.out_a, d.out_b};
+                d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat,
+                d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill, d.fbits[0], d.fbits[1]};
   for (void *p : ps)
     if (p) hipFree(p);
   a.allocated = false;
@@ -92,6 +93,18 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s) 
   A(dmalloc(&d.dirty[1], c.scap / BLK_SLOTS));
   A(dmalloc(&d.out_a, c.scap));
   A(dmalloc(&d.out_b, c.scap));
+  d.qn_cap = c.scap;
+  d.qh_cap = c.pcap / 128 + 1024;
+  A(dmalloc(&d.qn_buf, d.qn_cap));
+  A(dmalloc(&d.qh_buf, d.qh_cap));
+  A(dmalloc(&d.qn_tag, c.scap / BLK_SLOTS));
+  A(dmalloc(&d.blkstat, (uint64_t)STAT_WG * 4));
+  A(dmalloc(&d.sweep_cnt, 2 * (c.scap / BLK_SLOTS)));
+  A(dmalloc(&d.sweep_off, 2 * (c.scap / BLK_SLOTS)));
+  A(dmalloc(&d.out_ids, c.scap));
+  A(dmalloc(&d.out_kill, c.scap));
+  A(dmalloc(&d.fbits[0], c.scap / 32));
+  A(dmalloc(&d.fbits[1], c.scap / 32));
 #undef A
   a.allocated = true;
   // Default state of every unused slot / bucket.
@@ -113,6 +126,8 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s) 
   hipMemsetAsync(d.front[1], 0, c.scap, s);
   hipMemsetAsync(d.dirty[0], 0, c.scap / BLK_SLOTS, s);
   hipMemsetAsync(d.dirty[1], 0, c.scap / BLK_SLOTS, s);
+  hipMemsetAsync(d.fbits[0], 0, c.scap / 8, s);
+  hipMemsetAsync(d.fbits[1], 0, c.scap / 8, s);
   return hipGetLastError();
 }
 
@@ -204,6 +219,7 @@ int device_error(crgc_graph *h) {
   h->poisoned = true;
   if (err & (ERR_RESERVED_ID | ERR_TOO_MANY | ERR_BAD_OFFSETS)) return CRGC_E_INVAL;
   if (err & ERR_SPIN) return CRGC_E_TIMEOUT;
+  if (err & ERR_QUEUE_FULL) return CRGC_E_DEVICE;
   return CRGC_E_NOMEM;
 }
 
@@ -563,6 +579,10 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
                       uint64_t *levels, uint64_t *roots, double *kernel_ms, uint64_t *launches) {
   LevelArgs la{};
   la.location = location;
+  // Tuning switch for A/B runs (results are identical either way).
+  la.flags = LV_CHECK_BEFORE_STORE;
+  if (const char *m = getenv("CRGC_MARK_CHECK")) la.flags = atoi(m) ? LV_CHECK_BEFORE_STORE : 0;
+  if (const char *m = getenv("CRGC_MARK_BITS")) la.flags |= atoi(m) ? LV_BITMAP_FRONT : 0;
   la.sparse_thresh = (uint32_t)std::max<uint64_t>(64, (top / BLK_SLOTS) / 4);
   size_t nl = 0;
   auto launch = [&](int level, bool rootk) -> hipError_t {
@@ -625,6 +645,8 @@ static void reset_trace_counters(crgc_graph *h) {
   const size_t a = CTR_OFF(marked), b = sizeof(Counters);
   hipMemsetAsync((char *)h->ctr + a, 0, b - a, h->stream);
   const uint64_t top = h->slot_top + h->ids_since;
+  hipMemsetAsync(h->g.d.blkstat, 0, (size_t)STAT_WG * 4 * 8, h->stream);
+  hipMemsetAsync(h->g.d.qn_tag, 0, h->g.caps.scap / BLK_SLOTS * 4, h->stream);
   hipMemsetAsync(h->g.d.vis, 0, round_up(std::min<uint64_t>(top, h->g.caps.scap), BLK_SLOTS) / 8,
                  h->stream);
 }
@@ -638,13 +660,13 @@ static int copy_lists(crgc_graph *h, crgc_trace_out *out) {
   if (out->garbage_ids) {
     if (out->garbage_cap < h->last_garbage) big = true;
     else if (h->last_garbage)
-      HIP_TRY(hipMemcpyAsync(out->garbage_ids, h->g.d.out_a, h->last_garbage * 8,
+      HIP_TRY(hipMemcpyAsync(out->garbage_ids, h->g.d.out_ids, h->last_garbage * 8,
                              hipMemcpyDeviceToHost, h->stream));
   }
   if (out->kill_ids) {
     if (out->kill_cap < h->last_kill) big = true;
     else if (h->last_kill)
-      HIP_TRY(hipMemcpyAsync(out->kill_ids, h->g.d.out_b, h->last_kill * 8, hipMemcpyDeviceToHost,
+      HIP_TRY(hipMemcpyAsync(out->kill_ids, h->g.d.out_kill, h->last_kill * 8, hipMemcpyDeviceToHost,
                              h->stream));
   }
   HIP_TRY(hipStreamSynchronize(h->stream));
@@ -665,8 +687,9 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   double mark_ms = 0;
   if (int rc = run_levels(h, false, 0, top, &levels, &roots, &mark_ms, &launches)) return rc;
   HIP_TRY(hipEventRecord(h->ev[1], h->stream));
+  HIP_TRY(launch_trace_stats(h->g.d, h->stream));
   HIP_TRY(launch_sweep(h->g.d, should_kill ? 1 : 0, top, h->stream));
-  HIP_TRY(launch_commit(h->g.d, top, h->stream));
+
   HIP_TRY(hipEventRecord(h->ev[2], h->stream));
   HIP_TRY(sync_counters(h));
   const Counters &c = *h->hctr;

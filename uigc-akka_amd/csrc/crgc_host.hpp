@@ -115,9 +115,14 @@ struct EdgeArgs {
   uint32_t *reloc;     // [max_atoms] new segment offset per touched owner
 };
 
+constexpr uint32_t LV_CHECK_BEFORE_STORE = 1;  // read the candidate byte before storing it
+constexpr uint32_t LV_BITMAP_FRONT = 2;        // candidates as a bitmap set by atomicOr
+
 struct LevelArgs {
   int level;
   uint32_t sparse_thresh;
+  uint32_t frontier_grid;  // workgroups of k_frontier (set by launch_level)
+  uint32_t flags;          // LV_*
   uint16_t location;
 };
 
@@ -131,8 +136,10 @@ hipError_t launch_edges(const DevGraph &g, const EdgeArgs &a, hipStream_t s);
 
 hipError_t launch_level(const DevGraph &g, const LevelArgs &a, bool roots, bool investigate,
                         uint64_t slot_top, hipStream_t s);
+hipError_t launch_trace_stats(const DevGraph &g, hipStream_t s);
+// sweep + id compaction + removal of the garbage (skipped on a reference NPE)
 hipError_t launch_sweep(const DevGraph &g, int should_kill, uint64_t slot_top, hipStream_t s);
-hipError_t launch_commit(const DevGraph &g, uint64_t slot_top, hipStream_t s);
+int level_grid(uint64_t slot_top);
 hipError_t launch_local_roots(const DevGraph &g, uint64_t slot_top, hipStream_t s);
 
 // rebuild: compact `src` (live vertices only, purged edges) into `dst`,

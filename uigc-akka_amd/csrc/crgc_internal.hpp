@@ -42,10 +42,12 @@ constexpr uint32_t ERR_ETAB_FULL = 1u << 5;
 constexpr uint32_t ERR_UNDO_NEW = 1u << 6;
 constexpr uint32_t ERR_SPIN = 1u << 7;
 constexpr uint32_t ERR_BAD_OFFSETS = 1u << 8;
+constexpr uint32_t ERR_QUEUE_FULL = 1u << 9;
 
 constexpr int WAVE = 64;
 constexpr int BLK_SLOTS = 2048;          // slots per wave-block (64 lanes x 32)
 constexpr int LEVEL_RING = 4096;         // ring of per-level frontier counts
+constexpr int STAT_WG = 2048;            // max workgroups of the level / sweep kernels
 
 struct Counters {
   unsigned long long inserted;       // vertices created (totalActorsSeen)
@@ -65,6 +67,7 @@ struct Counters {
   unsigned long long n_live;
   unsigned long long npe;
   unsigned long long n_out;          // generic output counter (local roots)
+  unsigned long long qn[2], qh[2];   // per-level edge-range queue lengths
   unsigned long long ring[LEVEL_RING];
 };
 
@@ -96,8 +99,18 @@ struct DevGraph {
   uint32_t *vis;
   uint8_t *front[2];
   uint8_t *dirty[2];
-  uint64_t *out_a;  // garbage ids / generic
-  uint64_t *out_b;  // kill ids
+  uint32_t *fbits[2];  // candidate bitmaps (LV_BITMAP_FRONT variant)
+  uint2 *qn_buf;     // per-block regions of light edge ranges {offset, degree}
+  uint32_t *qn_tag;   // per block: (level+1) << 12 | number of light ranges
+  uint2 *qh_buf;      // RANGE_MAX-edge pieces of hub segments
+  uint64_t qn_cap, qh_cap;
+  uint64_t *blkstat;  // STAT_WG x 4 per-workgroup statistics partials
+  uint32_t *sweep_cnt;  // per block: garbage, kill counts
+  uint64_t *sweep_off;  // per block: exclusive offsets of the above
+  uint64_t *out_a;    // per-block regions: garbage slots (u32) / generic ids
+  uint64_t *out_b;    // per-block regions: kill slots (u32)
+  uint64_t *out_ids;  // dense garbage ids
+  uint64_t *out_kill; // dense kill ids
   Counters *ctr;
 };
 

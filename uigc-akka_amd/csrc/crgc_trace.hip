@@ -6,21 +6,24 @@
 // Reachability does not depend on visiting order, so a level-synchronous
 // sweep marks exactly the reference's `to` set.
 //
-// Frontier representation, no atomics on the per-edge path:
+// Frontier state, no atomics on the per-edge path:
 //   vis     1 bit / slot   marked set as of the start of the level
-//   front   1 byte / slot  candidates for the next level; discovered targets
-//                          get a plain byte store (idempotent, so concurrent
-//                          stores from any XCD merge correctly at write-back)
+//   front   1 byte / slot  candidates for the next level: a discovered target
+//                          gets a plain byte store (idempotent, so concurrent
+//                          stores from any XCD merge correctly at write-back),
+//                          skipped when the byte is already set
 //   dirty   1 byte / 2048 slots, only in sparse levels: which blocks to scan
-// A wave owns 2048 consecutive slots (32 per lane = one vis word per lane).
-// It turns its candidate bytes into new frontier bits (cand & ~vis), sets
-// them in vis (it is the only writer of those words), compacts the frontier
-// slots into LDS with a wave scan of popcounts, and expands them with a
-// load-balanced merge over the concatenated edge segments (degree scan +
-// binary search in LDS), 64 edges per step.
+//
+// No hot global counters either (one word saturates at ~88 atomics/us on
+// MI355X): frontier ranges go to per-block regions with level-tagged counts,
+// statistics to per-workgroup partials reduced by a single block.
 #include "crgc_host.hpp"
 
 namespace crgc {
+
+constexpr uint32_t RANGE_MAX = 256;  // longer segments (hubs) are cut into pieces
+constexpr int EXP_UNROLL = 4;        // independent edge loads in flight per lane
+constexpr int STAT_FRONT = 0, STAT_SUP = 1, STAT_EDGES = 2, STAT_LIVE = 3;
 
 __device__ inline bool sparse_level(const Counters *c, int L, uint32_t thr) {
   if (L <= 1) return false;
@@ -34,23 +37,53 @@ __device__ inline void wave_lds_fence() {
 }
 
 __device__ inline void mark_target(const DevGraph &g, uint8_t *Fn, uint8_t *Dn, bool sp_next,
-                                   uint32_t t) {
+                                   uint32_t t, bool check = false) {
   const uint32_t w = g.vis[t >> 5];
   if (!((w >> (t & 31)) & 1u)) {
-    Fn[t] = 1;
-    if (sp_next) Dn[t >> 11] = 1;
+    if (!check || Fn[t] == 0) Fn[t] = 1;
+    if (sp_next && Dn[t >> 11] == 0) Dn[t >> 11] = 1;
   }
 }
 
+// Bitmap variant of the candidate set: a plain (possibly stale) read filters,
+// a memory-side atomicOr sets.  Fbits is 1 bit per slot.
+__device__ inline void mark_target_bits(const DevGraph &g, uint32_t *Fbits, uint8_t *Dn,
+                                        bool sp_next, uint32_t t) {
+  const uint32_t bit = 1u << (t & 31);
+  if ((g.vis[t >> 5] | Fbits[t >> 5]) & bit) return;
+  atomicOr(&Fbits[t >> 5], bit);
+  if (sp_next && Dn[t >> 11] == 0) Dn[t >> 11] = 1;
+}
+
+// Workgroup reduction of one value per wave; thread 0 gets the sum.
+__device__ inline uint64_t block_sum4(uint64_t v) {
+  __shared__ uint64_t part[4];
+  const uint64_t w = __shfl(wave_incl_scan((uint32_t)v), 63);  // per-wave totals fit u32
+  if (lane_id() == 0) part[threadIdx.x >> 6] = w;
+  __syncthreads();
+  const uint64_t s = part[0] + part[1] + part[2] + part[3];
+  __syncthreads();  // `part` is reused by the next call
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// k_frontier: one wave per 2048-slot block.  Candidate bytes (or, at level 0,
+// the pseudo-root predicate) -> new frontier bits -> vis (the wave owns those
+// words); frontier shadows are compacted in LDS with a ballot/popc scan; their
+// supervisor edges are followed; their edge segments go to the block's region
+// of `qn` (light) or, cut into RANGE_MAX pieces, to `qh` (hubs).
+// ---------------------------------------------------------------------------
 template <bool ROOTS, bool INVESTIGATE>
-__global__ __launch_bounds__(256) void k_level(DevGraph g, LevelArgs a) {
+__global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
   __shared__ uint32_t s_front[4][BLK_SLOTS];
-  __shared__ uint32_t s_start[4][64];
-  __shared__ uint32_t s_off[4][64];
   Counters *c = g.ctr;
   const int L = a.level;
   if (blockIdx.x == 0 && threadIdx.x == 0) c->ring[(L + 1) % LEVEL_RING] = 0;
-  if (!ROOTS && c->ring[(L - 1) % LEVEL_RING] == 0) return;  // previous level was empty
+  uint64_t *stat = g.blkstat + (uint64_t)blockIdx.x * 4;
+  if (!ROOTS && c->ring[(L - 1) % LEVEL_RING] == 0) {  // previous level was empty
+    if (threadIdx.x == 0) stat[STAT_FRONT] = 0;
+    return;
+  }
   const bool sp_cur = !ROOTS && sparse_level(c, L, a.sparse_thresh);
   const bool sp_next = sparse_level(c, L + 1, a.sparse_thresh);
   const uint64_t slot_top = c->slot_top;
@@ -63,7 +96,10 @@ __global__ __launch_bounds__(256) void k_level(DevGraph g, LevelArgs a) {
   uint8_t *Fn = g.front[(L + 1) & 1];
   uint8_t *Dc = g.dirty[L & 1];
   uint8_t *Dn = g.dirty[(L + 1) & 1];
-  uint32_t n_front = 0, n_edges = 0, n_sup = 0;
+  unsigned long long *qh_cnt = &c->qh[L & 1];
+  const uint32_t tag = (uint32_t)(L + 1) << 12;
+  const bool bitmode = a.flags & LV_BITMAP_FRONT;
+  uint32_t n_front = 0, n_sup = 0;
 
   for (uint32_t blk = gw; blk < nblk; blk += nw) {
     if (sp_cur && Dc[blk] == 0) continue;
@@ -73,21 +109,31 @@ __global__ __launch_bounds__(256) void k_level(DevGraph g, LevelArgs a) {
     if (ROOTS) {
       const uint4 f4[2] = {*(const uint4 *)(g.flags + base), *(const uint4 *)(g.flags + base + 16)};
       const uint8_t *fb = (const uint8_t *)f4;
+      if (INVESTIGATE) {
+        // investigateRemotelyHeldActors: every shadow at `location` (:305-310)
 #pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        const uint8_t f = fb[j];
-        if (!(f & FL_ALIVE)) continue;
-        bool root;
-        if (INVESTIGATE) {
-          // investigateRemotelyHeldActors: every shadow at `location` (:305-310)
-          root = (uint16_t)(g.vid[base + j] >> 48) == a.location;
-        } else {
-          // isPseudoRoot (:201-203)
-          root = ((f & (FL_ROOT | FL_BUSY)) || !(f & FL_INTERNED) || g.recv[base + j] != 0) &&
-                 !(f & FL_HALTED);
+        for (int j = 0; j < 32; ++j)
+          if ((fb[j] & FL_ALIVE) && (uint16_t)(g.vid[base + j] >> 48) == a.location) m |= 1u << j;
+      } else {
+        // isPseudoRoot (:201-203): 32 flag bytes + 32 receive counts per lane
+        int4 r4[8];
+        const int4 *rp = (const int4 *)(g.recv + base);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) r4[q] = rp[q];
+        const int32_t *rb = (const int32_t *)r4;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+          const uint8_t f = fb[j];
+          const bool root = (f & FL_ALIVE) && !(f & FL_HALTED) &&
+                            ((f & (FL_ROOT | FL_BUSY)) || !(f & FL_INTERNED) || rb[j] != 0);
+          m |= root ? (1u << j) : 0u;
         }
-        if (root) m |= 1u << j;
       }
+    } else if (bitmode) {
+      uint32_t *fw = g.fbits[L & 1] + (uint64_t)blk * 64 + lane;
+      const uint32_t bits = *fw;
+      if (bits) *fw = 0;
+      m = bits & ~word;
     } else {
       uint4 *fp = (uint4 *)(Fc + base);
       const uint4 x0 = fp[0], x1 = fp[1];
@@ -120,85 +166,226 @@ __global__ __launch_bounds__(256) void k_level(DevGraph g, LevelArgs a) {
       m &= m - 1;
       s_front[wv][pos++] = (uint32_t)(base + j);
     }
-    n_front += cnt;  // per lane; summed over the wave below
+    n_front += cnt;
     wave_lds_fence();
 
-    // Expand, 64 frontier shadows at a time.
+    // Frontier shadows -> supervisor marks + edge ranges.
+    uint32_t nlight = 0;
+    uint2 *region = g.qn_buf + (uint64_t)blk * BLK_SLOTS;
     for (uint32_t c0 = 0; c0 < total; c0 += 64) {
       const uint32_t idx = c0 + lane;
       const bool valid = idx < total;
       const uint32_t v = valid ? s_front[wv][idx] : 0;
       const uint8_t f = valid ? g.flags[v] : 0;
-      const bool expand = valid && !(f & FL_HALTED);
+      const bool expand = valid && !(f & FL_HALTED);  // halted: marked, not expanded (:226)
       const uint2 ad = expand ? g.adj[v] : make_uint2(0, 0);
       if (!INVESTIGATE && expand) {
         const uint32_t s = g.sup[v];  // supervisor edge (:258-267)
-        if (s < 0xFFFFFFF0u) {  // not null, not collected
+        if (s < 0xFFFFFFF0u) {         // not null, not collected
           n_sup++;
-          mark_target(g, Fn, Dn, sp_next, s);
+          if (bitmode) mark_target_bits(g, g.fbits[(L + 1) & 1], Dn, sp_next, s);
+          else mark_target(g, Fn, Dn, sp_next, s);
         }
       }
-      const uint32_t deg = ad.y;
-      const uint32_t dincl = wave_incl_scan(deg);
-      const uint32_t dtot = __shfl(dincl, 63);
-      wave_lds_fence();
-      s_start[wv][lane] = dincl - deg;
-      s_off[wv][lane] = ad.x;
-      wave_lds_fence();
-      for (uint32_t e = lane; e < dtot; e += 64) {
-        int lo = 0, hi = 63;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (s_start[wv][mid] <= e) lo = mid;
-          else hi = mid - 1;
+      const bool light = ad.y > 0 && ad.y <= RANGE_MAX;
+      const uint64_t ball = __ballot(light);
+      if (light) region[nlight + __popcll(ball & lanemask_lt())] = ad;
+      nlight += __popcll(ball);
+      const uint32_t pieces = ad.y > RANGE_MAX ? (ad.y + RANGE_MAX - 1) / RANGE_MAX : 0;
+      if (__ballot(pieces != 0)) {  // hubs are rare: a wave-aggregated append
+        const unsigned long long hi = wave_atomic_add(qh_cnt, pieces);
+        for (uint32_t k = 0; k < pieces; ++k) {
+          const uint32_t len = min(RANGE_MAX, ad.y - k * RANGE_MAX);
+          if (hi + k < g.qh_cap) g.qh_buf[hi + k] = make_uint2(ad.x + k * RANGE_MAX, len);
+          else set_err(c, ERR_QUEUE_FULL);
         }
-        const uint64_t ptr = (uint64_t)s_off[wv][lo] + (e - s_start[wv][lo]);
-        const uint64_t ed = g.pool[ptr];
-        const int32_t cntv = edge_count(ed);
-        n_edges += cntv != 0;
-        if (cntv > 0) mark_target(g, Fn, Dn, sp_next, edge_target(ed));  // (:231-241)
       }
-      wave_lds_fence();
     }
+    if (lane == 0 && nlight) g.qn_tag[blk] = tag | nlight;
+    wave_lds_fence();
   }
-  const uint32_t tf = wave_sum(n_front), te = wave_sum(n_edges), ts = wave_sum(n_sup);
-  if (lane == 0) {
-    if (tf) {
-      atomicAdd(&c->ring[L % LEVEL_RING], (unsigned long long)tf);
-      atomicAdd(&c->marked, (unsigned long long)tf);
-    }
-    if (te) atomicAdd(&c->edges_scanned, (unsigned long long)te);
-    if (ts) atomicAdd(&c->sup_edges, (unsigned long long)ts);
+  const uint64_t tf = block_sum4(n_front);
+  const uint64_t ts = block_sum4(n_sup);
+  if (threadIdx.x == 0) {
+    stat[STAT_FRONT] = tf;
+    stat[STAT_SUP] += ts;
   }
 }
 
-static int level_grid(uint64_t slot_top) {
+__device__ inline void expand_edge(const DevGraph &g, uint8_t *Fn, uint8_t *Dn, bool sp_next, bool check,
+                                   uint64_t ed, uint32_t &n_edges, uint32_t *Fbits) {
+  const int32_t cntv = edge_count(ed);
+  n_edges += cntv != 0;
+  if (cntv > 0) {  // (:231-241)
+    if (Fbits) mark_target_bits(g, Fbits, Dn, sp_next, edge_target(ed));
+    else mark_target(g, Fn, Dn, sp_next, edge_target(ed), check);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_expand: every wave of the grid walks the level's ranges, 64 light ranges
+// per step (degree scan + binary search in LDS assigns edges to lanes) or one
+// hub piece per step, EXP_UNROLL independent edge loads per lane.  Block 0
+// also turns k_frontier's per-workgroup counts into the level count.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
+  __shared__ uint32_t s_start[4][65];
+  __shared__ uint32_t s_off[4][64];
+  Counters *c = g.ctr;
+  const int L = a.level;
+  if (L > 0 && c->ring[(L - 1) % LEVEL_RING] == 0) return;  // nothing was found this level
+  const uint64_t nh = min(c->qh[L & 1], (unsigned long long)g.qh_cap);
+  if (blockIdx.x == 0) {
+    // level count = sum of k_frontier's per-workgroup frontier counts
+    uint64_t s = 0;
+    for (uint32_t b = threadIdx.x; b < a.frontier_grid; b += 256) s += g.blkstat[b * 4 + STAT_FRONT];
+    __shared__ uint64_t red[256];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+      if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      c->ring[L % LEVEL_RING] = red[0];
+      c->marked += red[0];
+      c->qh[(L + 1) & 1] = 0;  // next level's hub queue (last read by the previous k_expand)
+    }
+  }
+  const bool sp_next = sparse_level(c, L + 1, a.sparse_thresh);
+  const bool check = a.flags & LV_CHECK_BEFORE_STORE;
+  uint32_t *Fbits = (a.flags & LV_BITMAP_FRONT) ? g.fbits[(L + 1) & 1] : nullptr;
+  uint8_t *Fn = g.front[(L + 1) & 1];
+  uint8_t *Dn = g.dirty[(L + 1) & 1];
+  const int wv = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const uint64_t gw = (uint64_t)blockIdx.x * 4 + wv;
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  const uint32_t want = (uint32_t)(L + 1);
+  const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
+  uint32_t n_edges = 0;
+
+  // light ranges: chunk (block b, k-th 64) of every block's region; chunk ids
+  // run over blocks first so consecutive waves take different blocks
+  for (uint64_t cid = gw; cid < nblk * 32; cid += nw) {
+    const uint64_t b = cid % nblk;
+    const uint32_t k = (uint32_t)(cid / nblk);
+    const uint32_t t = g.qn_tag[b];
+    if ((t >> 12) != want) continue;
+    const uint32_t cnt = t & 0xFFFu;
+    if (cnt <= k * 64) continue;
+    const uint32_t qi = k * 64 + lane;
+    const uint2 r = qi < cnt ? g.qn_buf[b * BLK_SLOTS + qi] : make_uint2(0, 0);
+    const uint32_t incl = wave_incl_scan(r.y);
+    const uint32_t dtot = __shfl(incl, 63);
+    s_start[wv][lane] = incl - r.y;
+    s_off[wv][lane] = r.x;
+    wave_lds_fence();
+    for (uint32_t e0 = 0; e0 < dtot; e0 += 64 * EXP_UNROLL) {
+      uint64_t ed[EXP_UNROLL];
+#pragma unroll
+      for (int u = 0; u < EXP_UNROLL; ++u) {
+        const uint32_t e = e0 + u * 64 + lane;
+        ed[u] = 0;  // count 0: neither traced nor counted
+        if (e < dtot) {
+          int lo = 0, hi = 63;
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_start[wv][mid] <= e) lo = mid;
+            else hi = mid - 1;
+          }
+          ed[u] = g.pool[(uint64_t)s_off[wv][lo] + (e - s_start[wv][lo])];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < EXP_UNROLL; ++u)
+        expand_edge(g, Fn, Dn, sp_next, check, ed[u], n_edges, Fbits);
+    }
+    wave_lds_fence();
+  }
+  // hub pieces: one per step
+  for (uint64_t hi = gw; hi < nh; hi += nw) {
+    const uint2 r = g.qh_buf[hi];
+    for (uint32_t e0 = 0; e0 < r.y; e0 += 64 * EXP_UNROLL) {
+      uint64_t ed[EXP_UNROLL];
+#pragma unroll
+      for (int u = 0; u < EXP_UNROLL; ++u) {
+        const uint32_t e = e0 + u * 64 + lane;
+        ed[u] = e < r.y ? g.pool[(uint64_t)r.x + e] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < EXP_UNROLL; ++u)
+        expand_edge(g, Fn, Dn, sp_next, check, ed[u], n_edges, Fbits);
+    }
+  }
+  const uint64_t te = block_sum4(n_edges);
+  if (threadIdx.x == 0 && te) g.blkstat[(uint64_t)blockIdx.x * 4 + STAT_EDGES] += te;
+}
+
+int level_grid(uint64_t slot_top) {
   const uint64_t blocks = (slot_top + BLK_SLOTS - 1) / BLK_SLOTS;  // wave-blocks
   uint64_t wg = (blocks + 3) / 4;
   if (wg < 1) wg = 1;
-  if (wg > 2048) wg = 2048;  // 8 workgroups of 4 waves per CU
+  if (wg > STAT_WG) wg = STAT_WG;
   return (int)wg;
 }
 
-hipError_t launch_level(const DevGraph &g, const LevelArgs &a, bool roots, bool investigate,
+hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool investigate,
                         uint64_t slot_top, hipStream_t s) {
+  LevelArgs a = a0;
   const int grid = level_grid(slot_top);
+  a.frontier_grid = grid;
   if (roots && investigate)
-    hipLaunchKernelGGL((k_level<true, true>), dim3(grid), dim3(256), 0, s, g, a);
+    hipLaunchKernelGGL((k_frontier<true, true>), dim3(grid), dim3(256), 0, s, g, a);
   else if (roots)
-    hipLaunchKernelGGL((k_level<true, false>), dim3(grid), dim3(256), 0, s, g, a);
+    hipLaunchKernelGGL((k_frontier<true, false>), dim3(grid), dim3(256), 0, s, g, a);
   else if (investigate)
-    hipLaunchKernelGGL((k_level<false, true>), dim3(grid), dim3(256), 0, s, g, a);
+    hipLaunchKernelGGL((k_frontier<false, true>), dim3(grid), dim3(256), 0, s, g, a);
   else
-    hipLaunchKernelGGL((k_level<false, false>), dim3(grid), dim3(256), 0, s, g, a);
+    hipLaunchKernelGGL((k_frontier<false, false>), dim3(grid), dim3(256), 0, s, g, a);
+  hipLaunchKernelGGL(k_expand, dim3(STAT_WG), dim3(256), 0, s, g, a);  // 8 WGs of 4 waves per CU
+  return hipGetLastError();
+}
+
+// Sum of the per-workgroup sup/edge partials into the counters (once per trace).
+__global__ __launch_bounds__(256) void k_trace_stats(DevGraph g) {
+  __shared__ uint64_t red[2][256];
+  uint64_t su = 0, ed = 0;
+  for (uint32_t b = threadIdx.x; b < STAT_WG; b += 256) {
+    su += g.blkstat[b * 4 + STAT_SUP];
+    ed += g.blkstat[b * 4 + STAT_EDGES];
+  }
+  red[0][threadIdx.x] = su;
+  red[1][threadIdx.x] = ed;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + k];
+      red[1][threadIdx.x] += red[1][threadIdx.x + k];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    g.ctr->sup_edges = red[0][0];
+    g.ctr->edges_scanned = red[1][0];
+  }
+}
+
+hipError_t launch_trace_stats(const DevGraph &g, hipStream_t s) {
+  hipLaunchKernelGGL(k_trace_stats, dim3(1), dim3(256), 0, s, g);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
 // Sweep (:270-284): unmarked shadows are garbage; a local one is told StopMsg
 // when its supervisor is marked and it is not halted.  A local garbage shadow
-// without a supervisor is the reference's NullPointerException: counted here,
-// and the commit pass below then leaves the graph untouched.
+// without a supervisor is the reference's NullPointerException: counted, and
+// the gather pass then leaves the graph untouched.
+//   k_sweep   one wave per 2048-slot block: garbage / kill slots into the
+//             block's own region of out_a / out_b, counts per block
+//   k_sweep_scan   one workgroup: exclusive offsets of the per-block counts
+//   k_sweep_gather one wave per block: slots -> ids, packed densely; unless an
+//             NPE was seen, removes the garbage from shadowMap (:276)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_sweep(DevGraph g, int should_kill) {
   Counters *c = g.ctr;
@@ -233,56 +420,122 @@ __global__ __launch_bounds__(256) void k_sweep(DevGraph g, int should_kill) {
         }
       }
     }
-    const unsigned long long gbase = wave_atomic_add(&c->n_garbage, __popc(garbage));
-    const unsigned long long kbase = wave_atomic_add(&c->n_kill, __popc(kill));
-    uint32_t k = 0;
+    const uint32_t gc = __popc(garbage), kc = __popc(kill);
+    const uint32_t gi = wave_incl_scan(gc), ki = wave_incl_scan(kc);
+    uint32_t gp = gi - gc, kp = ki - kc;
+    uint32_t *ga = (uint32_t *)g.out_a + (uint64_t)blk * BLK_SLOTS;
+    uint32_t *ka = (uint32_t *)g.out_b + (uint64_t)blk * BLK_SLOTS;
     gm = garbage;
     while (gm) {
       const int j = __ffs(gm) - 1;
       gm &= gm - 1;
-      g.out_a[gbase + k++] = g.vid[base + j];
+      ga[gp++] = (uint32_t)(base + j);
     }
-    k = 0;
     uint32_t km = kill;
     while (km) {
       const int j = __ffs(km) - 1;
       km &= km - 1;
-      g.out_b[kbase + k++] = g.vid[base + j];
+      ka[kp++] = (uint32_t)(base + j);
+    }
+    if (lane == 63) {
+      g.sweep_cnt[2 * (uint64_t)blk] = gi;
+      g.sweep_cnt[2 * (uint64_t)blk + 1] = ki;
     }
   }
-  const uint32_t tl = wave_sum(n_live), tn = wave_sum(n_npe);
-  if (lane == 0) {
-    if (tl) atomicAdd(&c->n_live, (unsigned long long)tl);
+  const uint64_t tl = block_sum4(n_live);
+  const uint64_t tn = block_sum4(n_npe);
+  if (threadIdx.x == 0) {
+    g.blkstat[(uint64_t)blockIdx.x * 4 + STAT_LIVE] = tl;
     if (tn) atomicAdd(&c->npe, (unsigned long long)tn);
   }
 }
 
-// Remove the garbage from shadowMap (:276): tombstone its id-table bucket and
-// clear its slot.  Slots and pool segments are reclaimed by the next rebuild,
-// which also purges edges pointing at them.
-__global__ __launch_bounds__(256) void k_commit(DevGraph g) {
+// One workgroup: exclusive offsets over the per-block (garbage, kill) counts,
+// totals into the counters, and the live count from the sweep partials.
+__global__ __launch_bounds__(1024) void k_sweep_scan(DevGraph g, uint32_t sweep_grid) {
+  __shared__ uint64_t wsum[2][16];
+  __shared__ uint64_t carry[2];
   Counters *c = g.ctr;
-  if (c->npe) return;
-  const uint64_t slot_top = c->slot_top;
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < slot_top; v += stride) {
-    const uint8_t f = g.flags[v];
-    if (!(f & FL_ALIVE)) continue;
-    if ((g.vis[v >> 5] >> (v & 31)) & 1u) continue;
-    uint64_t bucket = KEY_EMPTY;
-    id_find(g, g.vid[v], &bucket);
-    if (bucket != KEY_EMPTY) g.hkey[bucket] = KEY_TOMB;
-    g.flags[v] = 0;
+  const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry[0] = carry[1] = 0;
+  __syncthreads();
+  for (uint64_t b0 = 0; b0 < nblk; b0 += 1024) {
+    const uint64_t b = b0 + threadIdx.x;
+    const uint32_t gv = b < nblk ? g.sweep_cnt[2 * b] : 0;
+    const uint32_t kv = b < nblk ? g.sweep_cnt[2 * b + 1] : 0;
+    const uint32_t gi = wave_incl_scan(gv), ki = wave_incl_scan(kv);
+    if (lane == 63) {
+      wsum[0][wv] = gi;
+      wsum[1][wv] = ki;
+    }
+    __syncthreads();
+    uint64_t gpre = carry[0], kpre = carry[1], gtot = 0, ktot = 0;
+    for (int w = 0; w < 16; ++w) {
+      if (w < wv) {
+        gpre += wsum[0][w];
+        kpre += wsum[1][w];
+      }
+      gtot += wsum[0][w];
+      ktot += wsum[1][w];
+    }
+    if (b < nblk) {
+      g.sweep_off[2 * b] = gpre + gi - gv;
+      g.sweep_off[2 * b + 1] = kpre + ki - kv;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      carry[0] += gtot;
+      carry[1] += ktot;
+    }
+    __syncthreads();
+  }
+  uint64_t live = 0;
+  for (uint32_t b = threadIdx.x; b < sweep_grid; b += 1024) live += g.blkstat[b * 4 + STAT_LIVE];
+  const uint64_t wl = __shfl(wave_incl_scan((uint32_t)live), 63);
+  if (lane == 0) wsum[0][wv] = wl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < 16; ++w) t += wsum[0][w];
+    c->n_live = t;
+    c->n_garbage = carry[0];
+    c->n_kill = carry[1];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_sweep_gather(DevGraph g) {
+  Counters *c = g.ctr;
+  const bool commit = c->npe == 0;
+  const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
+  const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t blk = gw; blk < nblk; blk += nw) {
+    const uint32_t gn = g.sweep_cnt[2 * blk], kn = g.sweep_cnt[2 * blk + 1];
+    if (gn == 0) continue;
+    const uint64_t go = g.sweep_off[2 * blk], ko = g.sweep_off[2 * blk + 1];
+    const uint32_t *ga = (const uint32_t *)g.out_a + blk * BLK_SLOTS;
+    const uint32_t *ka = (const uint32_t *)g.out_b + blk * BLK_SLOTS;
+    for (uint32_t i = lane_id(); i < gn; i += 64) {
+      const uint32_t v = ga[i];
+      const uint64_t id = g.vid[v];
+      g.out_ids[go + i] = id;
+      if (commit) {
+        uint64_t bucket = KEY_EMPTY;
+        id_find(g, id, &bucket);
+        if (bucket != KEY_EMPTY) g.hkey[bucket] = KEY_TOMB;
+        g.flags[v] = 0;
+      }
+    }
+    for (uint32_t i = lane_id(); i < kn; i += 64) g.out_kill[ko + i] = g.vid[ka[i]];
   }
 }
 
 hipError_t launch_sweep(const DevGraph &g, int should_kill, uint64_t slot_top, hipStream_t s) {
-  hipLaunchKernelGGL(k_sweep, dim3(level_grid(slot_top)), dim3(256), 0, s, g, should_kill);
-  return hipGetLastError();
-}
-
-hipError_t launch_commit(const DevGraph &g, uint64_t slot_top, hipStream_t s) {
-  hipLaunchKernelGGL(k_commit, dim3(grid_for(slot_top, 256, 8192)), dim3(256), 0, s, g);
+  const int grid = level_grid(slot_top);
+  hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(256), 0, s, g, should_kill);
+  hipLaunchKernelGGL(k_sweep_scan, dim3(1), dim3(1024), 0, s, g, (uint32_t)grid);
+  hipLaunchKernelGGL(k_sweep_gather, dim3(grid), dim3(256), 0, s, g);
   return hipGetLastError();
 }
 
