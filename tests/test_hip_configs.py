@@ -1,0 +1,119 @@
+"""HIP vs oracle on the BASELINE.json configurations (C1, C2 scaled, C3, C5).
+
+Bit-exact parity is checked on garbage and kill *sets*, live counts and the
+exported graph state, wakeup by wakeup, at sizes the oracle finishes in
+seconds.  The full-size C2 graph is checked by size-independent properties
+(test_c2_full_size_properties).
+"""
+import numpy as np
+import pytest
+
+import cluster
+import world
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(rh, ro):
+    assert rh.garbage_set() == ro.garbage_set()
+    assert rh.kill_set() == ro.kill_set()
+    assert len(rh.garbage) == len(ro.garbage) and len(rh.kill) == len(ro.kill)
+    assert rh.n_live == ro.n_live
+    assert rh.pseudo_roots == ro.pseudo_roots
+    assert rh.sup_edges == ro.sup_edges
+
+
+def _load(g, w, batch):
+    for b in w.batches(batch):
+        g.merge_entries(b)
+
+
+@pytest.mark.parametrize("actors,edges,batch,wakeups", [
+    (100_000, 1_000_000, 10_000, 6),       # C1: the reference's CPU-runnable case
+    (1_000_000, 10_000_000, 100_000, 2),   # C2 shape at 1/10 scale
+])
+def test_power_law_wakeups_match_oracle(hip_mod, oracle_mod, actors, edges, batch, wakeups):
+    w = world.World(seed=0x5EED + 1)
+    w.bulk_graph(actors, edges, alpha=2.1, n_roots=max(1, actors // 100))
+    h = hip_mod.ShadowGraph(vertex_capacity=actors, edge_capacity=edges)
+    o = oracle_mod.OracleGraph()
+    for b in w.batches(1 << 20):
+        h.merge_entries(b)
+        o.merge_entries(b)
+    _same(h.trace(True), o.trace(True))
+    for _ in range(wakeups):
+        b = w.wakeup_batch(batch)
+        h.merge_entries(b.to_device())
+        o.merge_entries(b)
+        _same(h.trace(True), o.trace(True))
+    if actors <= 100_000:
+        assert h.export() == o.export()
+    assert h.total_actors_seen() == o.total_actors_seen()
+
+
+def test_c3_deep_chains_and_dead_rings(hip_mod, oracle_mod):
+    w = world.World(seed=0x5EED + 3)
+    w.chain_graph(n_chains=20, chain_len=3000, n_sup_chains=5, sup_depth=400,
+                  n_rings=30, ring_len=60)
+    h = hip_mod.ShadowGraph()
+    o = oracle_mod.OracleGraph()
+    for b in w.batches(50_000):
+        h.merge_entries(b)
+        o.merge_entries(b)
+    rh, ro = h.trace(True), o.trace(True)
+    _same(rh, ro)
+    assert len(ro.garbage) == 30 * 60 and len(ro.kill) == 30 * 60
+    assert rh.levels >= 3000  # one BFS level per chain link
+    assert h.export() == o.export()
+
+
+def test_c5_cluster_deltas_and_undo(hip_mod, oracle_mod):
+    cw = cluster.ClusterWorld(seed=9, n_nodes=8, max_actors=3000)
+    h = hip_mod.ShadowGraph()
+    o = oracle_mod.OracleGraph()
+    merged = []
+    for _ in range(8):
+        cw.run_turns(500)
+        own, deltas = cw.flush(0)
+        for k, g in deltas:
+            b = g.to_batch()
+            h.merge_deltas(b)
+            o.merge_deltas(b)
+            merged.append((k, g))
+        h.merge_entries(own)
+        o.merge_entries(own)
+        _same(h.trace(True), o.trace(True))
+    assert h.export() == o.export()
+    # node 8 (index 7) is downed: replay its undo log, then trace
+    log = cw.undo_log(7, merged).to_batch(restrict_to=set(o.export().vertices))
+    h.merge_undo(log)
+    o.merge_undo(log)
+    assert h.export() == o.export()
+    assert h.count_reachable_from(8) == o.count_reachable_from(8)
+    _same(h.trace(True), o.trace(True))
+
+
+@pytest.mark.slow
+def test_c2_full_size_properties(hip_mod):
+    """1e7 actors / 1e8 edges: properties that need no oracle."""
+    w = world.World(seed=0x5EED + 2)
+    w.bulk_graph(10_000_000, 100_000_000, alpha=2.1, n_roots=10_000)
+    h = hip_mod.ShadowGraph(vertex_capacity=12_000_000, edge_capacity=120_000_000)
+    for b in w.batches(1_000_000):
+        h.merge_entries(b.to_device())
+    seen = h.total_actors_seen()
+    r0 = h.trace(True)
+    assert r0.n_live + len(r0.garbage) == seen          # every shadow is live or garbage
+    for _ in range(2):
+        b = w.wakeup_batch(1_000_000)
+        h.merge_entries(b.to_device())
+        pre = h.live_count()
+        r = h.trace(True)
+        g = r.garbage
+        assert len(np.unique(g)) == len(g)                 # no duplicates
+        assert r.kill_set() <= r.garbage_set()             # kills are garbage
+        assert r.n_live + len(g) == pre                    # partition of the graph
+        assert h.live_count() == r.n_live
+    # idempotence: with no new entries a second trace finds no garbage
+    r2 = h.trace(True)
+    assert len(r2.garbage) == 0 and r2.n_live == h.live_count()

@@ -25,6 +25,24 @@ def _same_trace(rh, ro):
     assert rh.n_live == ro.n_live
     assert rh.pseudo_roots == ro.pseudo_roots
     assert rh.sup_edges == ro.sup_edges
+    assert rh.edges_scanned == ro.edges_scanned
+
+
+# Traversal directions.  "pull" forces every level after the roots to pull
+# (in-candidate scan) and "push" disables pulling; "auto" is the product
+# default (pull only for large dense levels, i.e. push at these sizes).
+DIRECTIONS = {
+    "auto": {},
+    "push": {"CRGC_PULL": "0", "CRGC_SPARSE_THRESH": "0"},
+    "pull": {"CRGC_PULL": "1", "CRGC_PULL_THRESH": "1", "CRGC_SPARSE_THRESH": "0"},
+}
+
+
+@pytest.fixture(params=sorted(DIRECTIONS))
+def direction(request, monkeypatch):
+    for k, v in DIRECTIONS[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param
 
 
 @pytest.mark.parametrize("name", sorted(kats.SCENARIOS))
@@ -40,7 +58,7 @@ def test_random_spec_on_hip(hip_mod, oracle_mod, seed):
     assert collected == everyone
 
 
-def test_random_spec_hip_matches_oracle_every_wakeup(hip_mod, oracle_mod):
+def test_random_spec_hip_matches_oracle_every_wakeup(hip_mod, oracle_mod, direction):
     w = kats.RandomWorld(seed=7, max_actors=600, wake_every=13)
     h, o = _pair(hip_mod, oracle_mod)
     for batch in w.steps():
@@ -54,7 +72,7 @@ def test_random_spec_hip_matches_oracle_every_wakeup(hip_mod, oracle_mod):
 
 
 @pytest.mark.parametrize("seed,cap", [(11, 0), (12, 0), (13, 64)])
-def test_fuzz_entries_deltas_undo(hip_mod, oracle_mod, seed, cap):
+def test_fuzz_entries_deltas_undo(hip_mod, oracle_mod, seed, cap, direction):
     # cap=64 starts from a tiny graph so rebuilds (compaction) happen often
     h, o = _pair(hip_mod, oracle_mod, vertex_capacity=cap, edge_capacity=cap)
     fz = fuzz.Fuzz(seed)

@@ -42,8 +42,9 @@ def main():
     ref = None
     for r in range(args.rounds):
         for v in variants:
-            k, val = v.split("=")
-            os.environ[k] = val
+            kv = [x.split("=") for x in v.split(",")]
+            for k, val in kv:
+                os.environ[k] = val
             t = time.perf_counter()
             out, ng, nk = g.trace_counts(True)
             wall = (time.perf_counter() - t) * 1e3
@@ -51,7 +52,8 @@ def main():
             ref = ref or key
             assert key == ref, (v, key, ref)
             res[v].append((out.ms_mark, out.ms_sweep, wall))
-            del os.environ[k]
+            for k, _ in kv:
+                del os.environ[k]
     summary = {}
     for v, xs in res.items():
         summary[v] = {"mark_ms_median": statistics.median(x[0] for x in xs),

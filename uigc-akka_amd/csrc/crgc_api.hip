@@ -44,7 +44,8 @@ void free_arrays(Arrays &a) {
   void *ps[] = {d.hkey, d.hval, d.vid, d.recv, d.flags, d.sup, d.adj, d.ecap, d.vseq, d.sseq,
                 d.enew, d.pool, d.ekey, d.eval, d.edelta, d.vis, d.front[0], d.front[1],
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat,
-                d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill, d.fbits[0], d.fbits[1]};
+                d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill, d.fbits[0], d.fbits[1],
+                d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.fx};
   for (void *p : ps)
     if (p) hipFree(p);
   a.allocated = false;
@@ -105,6 +106,13 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s) 
   A(dmalloc(&d.out_kill, c.scap));
   A(dmalloc(&d.fbits[0], c.scap / 32));
   A(dmalloc(&d.fbits[1], c.scap / 32));
+  d.rpcap = c.pcap;
+  A(dmalloc(&d.nzdeg, c.scap));
+  A(dmalloc(&d.radj, c.scap));
+  A(dmalloc(&d.rcap, c.scap));
+  A(dmalloc(&d.rnew, c.scap));
+  A(dmalloc(&d.rpool, d.rpcap));
+  A(dmalloc(&d.fx, c.scap / 32));
 #undef A
   a.allocated = true;
   // Default state of every unused slot / bucket.
@@ -128,6 +136,11 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s) 
   hipMemsetAsync(d.dirty[1], 0, c.scap / BLK_SLOTS, s);
   hipMemsetAsync(d.fbits[0], 0, c.scap / 8, s);
   hipMemsetAsync(d.fbits[1], 0, c.scap / 8, s);
+  hipMemsetAsync(d.nzdeg, 0, c.scap * 4, s);
+  hipMemsetAsync(d.radj, 0, c.scap * 8, s);
+  hipMemsetAsync(d.rcap, 0, c.scap * 4, s);
+  hipMemsetAsync(d.rnew, 0, c.scap * 4, s);
+  hipMemsetAsync(d.fx, 0, c.scap / 8, s);
   return hipGetLastError();
 }
 
@@ -157,7 +170,7 @@ struct crgc_graph {
   unsigned long long epoch = 0;
   bool poisoned = false;
   // exact values as of the last synchronisation + upper-bound increments since
-  uint64_t slot_top = 0, pool_top = 0, etab_used = 0, live = 0;
+  uint64_t slot_top = 0, pool_top = 0, rpool_top = 0, etab_used = 0, live = 0;
   uint64_t ids_since = 0, atoms_since = 0;
   uint64_t inserted_at_trace = 0;  // Counters::inserted when `live` was exact
   Scratch stage, work;
@@ -208,6 +221,7 @@ hipError_t sync_counters(crgc_graph *h) {
   if (e != hipSuccess) return e;
   h->slot_top = h->hctr->slot_top;
   h->pool_top = h->hctr->pool_top;
+  h->rpool_top = h->hctr->rpool_top;
   h->etab_used = h->hctr->etab_used;
   h->ids_since = h->atoms_since = 0;
   return hipSuccess;
@@ -248,6 +262,7 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   // new generation counters: slot_top, pool_top, etab_used restart
   hipMemsetAsync((char *)h->ctr + CTR_OFF(slot_top), 0, 8, h->stream);
   hipMemsetAsync((char *)h->ctr + CTR_OFF(pool_top), 0, 8, h->stream);
+  hipMemsetAsync((char *)h->ctr + CTR_OFF(rpool_top), 0, 8, h->stream);
   hipMemsetAsync((char *)h->ctr + CTR_OFF(etab_used), 0, 8, h->stream);
   // src keeps a view of the old counters' bound via src_top (passed by value)
   hipError_t e = launch_rebuild(h->g.d, src_top, dst.d, map, nullptr, offs, scan_tmp, h->stream);
@@ -268,19 +283,22 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms) {
 
 // Make sure `ids` more vertices and `atoms` more edge updates fit.
 int ensure_capacity(crgc_graph *h, uint64_t ids, uint64_t atoms) {
-  auto fits = [&](uint64_t st, uint64_t pt, uint64_t eu) {
+  // A merge's relocations need at most 2*(stored + new) + 4*touched pool
+  // entries in either direction (power-of-two segments).
+  auto fits = [&](uint64_t st, uint64_t pt, uint64_t rt, uint64_t eu) {
     const Caps &c = h->g.caps;
     return st + ids <= c.scap && (st + ids) * 10 <= c.hcap * 7 &&
-           pt + 2 * eu + 6 * atoms <= c.pcap && (eu + atoms) * 10 <= c.ecap * 7;
+           pt + 2 * eu + 6 * atoms <= c.pcap && rt + 2 * eu + 6 * atoms <= c.pcap &&
+           (eu + atoms) * 10 <= c.ecap * 7;
   };
   // upper bounds since the last sync
   const uint64_t st = h->slot_top + h->ids_since;
   const uint64_t eu = h->etab_used + h->atoms_since;
-  const uint64_t pt = h->pool_top + 2 * (h->etab_used + h->atoms_since) + 6 * h->atoms_since;
-  if (fits(st, pt, eu)) return CRGC_OK;
+  const uint64_t grow = 2 * (h->etab_used + h->atoms_since) + 6 * h->atoms_since;
+  if (fits(st, h->pool_top + grow, h->rpool_top + grow, eu)) return CRGC_OK;
   HIP_TRY(sync_counters(h));
   if (int rc = device_error(h)) return rc;
-  if (fits(h->slot_top, h->pool_top, h->etab_used)) return CRGC_OK;
+  if (fits(h->slot_top, h->pool_top, h->rpool_top, h->etab_used)) return CRGC_OK;
   return rebuild(h, ids, atoms);
 }
 
@@ -400,16 +418,19 @@ static int run_edges(crgc_graph *h, uint32_t *ao, uint32_t *at, int32_t *ad, uin
   ea.atom_t = at;
   ea.atom_d = ad;
   ea.newlist = cv.take<uint64_t>(max_atoms);
+  ea.rrank = cv.take<uint32_t>(max_atoms);
   ea.touched = cv.take<uint32_t>(max_atoms);
   ea.reloc = cv.take<uint32_t>(max_atoms);
-  hipMemsetAsync((char *)h->ctr + CTR_OFF(n_touched), 0, 16, h->stream);
+  ea.rtouched = cv.take<uint32_t>(max_atoms);
+  ea.rreloc = cv.take<uint32_t>(max_atoms);
+  hipMemsetAsync((char *)h->ctr + CTR_OFF(n_touched), 0, 3 * 8, h->stream);
   HIP_TRY(launch_edges(h->g.d, ea, h->stream));
   return CRGC_OK;
 }
 
 static size_t edge_scratch(uint64_t max_atoms) {
   return Carver::need({max_atoms * 4, max_atoms * 4, max_atoms * 4, max_atoms * 8, max_atoms * 4,
-                       max_atoms * 4});
+                       max_atoms * 4, max_atoms * 4, max_atoms * 4, max_atoms * 4});
 }
 
 int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
@@ -584,6 +605,17 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   if (const char *m = getenv("CRGC_MARK_CHECK")) la.flags = atoi(m) ? LV_CHECK_BEFORE_STORE : 0;
   if (const char *m = getenv("CRGC_MARK_BITS")) la.flags |= atoi(m) ? LV_BITMAP_FRONT : 0;
   la.sparse_thresh = (uint32_t)std::max<uint64_t>(64, (top / BLK_SLOTS) / 4);
+  // Direction optimisation: dense levels after a frontier of >= top/div shadows pull.
+  uint64_t pull_div = 16;
+  la.flags |= LV_PULL;
+  if (const char *m = getenv("CRGC_PULL")) {
+    if (!atoi(m)) la.flags &= ~LV_PULL;
+  }
+  if (const char *m = getenv("CRGC_PULL_DIV")) pull_div = std::max<uint64_t>(1, strtoull(m, nullptr, 10));
+  la.pull_thresh = std::max<uint64_t>(1, top / pull_div);
+  // Test hooks: absolute thresholds (0 disables sparse levels entirely).
+  if (const char *m = getenv("CRGC_PULL_THRESH")) la.pull_thresh = strtoull(m, nullptr, 10);
+  if (const char *m = getenv("CRGC_SPARSE_THRESH")) la.sparse_thresh = (uint32_t)strtoul(m, nullptr, 10);
   size_t nl = 0;
   auto launch = [&](int level, bool rootk) -> hipError_t {
     if (h->lvl_ev.size() < 2 * (nl + 1)) {

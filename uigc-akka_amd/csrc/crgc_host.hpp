@@ -111,16 +111,21 @@ struct EdgeArgs {
   const uint32_t *atom_t;
   const int32_t *atom_d;
   uint64_t *newlist;   // [max_atoms] buckets of new edge keys
+  uint32_t *rrank;     // [max_atoms] rank of each new key among its target's new candidates
   uint32_t *touched;   // [max_atoms] owners that got new edges
   uint32_t *reloc;     // [max_atoms] new segment offset per touched owner
+  uint32_t *rtouched;  // [max_atoms] targets that got new candidates
+  uint32_t *rreloc;    // [max_atoms] new candidate-segment offset per touched target
 };
 
 constexpr uint32_t LV_CHECK_BEFORE_STORE = 1;  // read the candidate byte before storing it
 constexpr uint32_t LV_BITMAP_FRONT = 2;        // candidates as a bitmap set by atomicOr
+constexpr uint32_t LV_PULL = 4;                // dense levels scan in-candidates (pull)
 
 struct LevelArgs {
   int level;
   uint32_t sparse_thresh;
+  uint64_t pull_thresh;    // a level pulls when the previous frontier had >= this many shadows
   uint32_t frontier_grid;  // workgroups of k_frontier (set by launch_level)
   uint32_t flags;          // LV_*
   uint16_t location;

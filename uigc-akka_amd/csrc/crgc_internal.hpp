@@ -53,9 +53,12 @@ struct Counters {
   unsigned long long inserted;       // vertices created (totalActorsSeen)
   unsigned long long slot_top;       // next dense slot
   unsigned long long pool_top;       // next free edge in pool
+  unsigned long long rpool_top;      // next free reverse-candidate entry
   unsigned long long etab_used;      // edge-table keys ever inserted
+  // per-merge lists (reset together before every edge pipeline)
   unsigned long long n_touched;      // owners with new edges in this merge
   unsigned long long n_new_edges;    // new edge keys in this merge
+  unsigned long long n_rtouched;     // targets with new candidates in this merge
   unsigned long long err;
   unsigned long long spin_max;
   // trace
@@ -88,6 +91,15 @@ struct DevGraph {
   unsigned long long *vseq;  // last-write-wins tag for busy/root
   unsigned long long *sseq;  // last-write-wins tag for supervisor
   uint32_t *enew;            // new edges per owner in the current merge
+  uint32_t *nzdeg;           // out-edges with count != 0 (reference `outgoing.size()`)
+  // reverse candidates (pull BFS): owners that ever created an edge key to the
+  // slot; a candidate is verified against the forward count when used
+  uint2 *radj;               // {offset, length} into rpool
+  uint32_t *rcap;
+  uint32_t *rnew;            // new candidates per target in the current merge
+  uint32_t *rpool;
+  uint64_t rpcap;
+  uint32_t *fx;              // expandable frontier bitmap (frontier & !halted)
   // edges
   uint64_t pcap;
   uint64_t *pool;
@@ -296,6 +308,20 @@ __device__ inline uint64_t edge_find_or_insert(const DevGraph &g, uint64_t key, 
   }
   set_err(g.ctr, ERR_ETAB_FULL);
   return KEY_EMPTY;
+}
+
+// Lookup only: the entry offset of edge (owner -> target) in owner's segment,
+// or SLOT_NONE when the key was never created.
+__device__ inline uint32_t edge_find(const DevGraph &g, uint32_t owner, uint32_t target) {
+  const uint64_t key = edge_key(owner, target);
+  uint64_t h = mix64(key) & g.emask;
+  for (uint64_t probe = 0; probe < g.ecap_tab; ++probe) {
+    const uint64_t k = g.ekey[h];
+    if (k == key) return g.eval[h];
+    if (k == KEY_EMPTY) break;
+    h = (h + 1) & g.emask;
+  }
+  return SLOT_NONE;
 }
 
 __device__ inline uint64_t pack_edge(uint32_t target, int32_t count) {

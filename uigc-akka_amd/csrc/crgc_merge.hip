@@ -301,15 +301,18 @@ hipError_t launch_undo_apply(const DevGraph &g, const UndoArgs &a, uint64_t slot
 // ---------------------------------------------------------------------------
 // Edge pipeline — outgoing[o][t] += d  (ShadowGraph.updateOutgoing, :64-73).
 // Absent == 0, so zero counts are simply kept (they are never traced) until a
-// rebuild drops them.
+// rebuild drops them; nzdeg[o] tracks how many of o's counts are nonzero (the
+// reference's outgoing.size(), :231) so traced-edge counts stay exact.
 //   1. k_edge_apply: find-or-insert (o,t) in the edge table.  Existing edges
 //      get a memory-side atomic add on their pool count; keys new in this merge
-//      accumulate in edelta[bucket] and take a rank among the owner's new edges.
-//   2. k_edge_plan:  owners whose segment overflows get a new segment
-//      (pow2 capacity), one atomic per wave on pool_top.
-//   3. k_edge_move:  one wave per relocated owner copies its segment.
-//   4. k_edge_append: new edges are written after the owner's old degree.
-//   5. k_edge_finish: degrees advance, per-owner counters reset.
+//      accumulate in edelta[bucket], take a rank among the owner's new edges and
+//      among the target's new reverse candidates.
+//   2. k_seg_plan:  owners (targets) whose forward (candidate) segment
+//      overflows get a new power-of-two segment, one atomic per wave.
+//   3. k_seg_move:  one wave per relocated segment copies it.
+//   4. k_edge_append: new edges written after the owner's old degree, the
+//      owner appended to the target's candidate list.
+//   5. k_seg_finish: degrees advance, per-merge counters reset.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_edge_apply(DevGraph g, EdgeArgs a) {
   const uint64_t n = a.n_atoms_dev ? *a.n_atoms_dev : a.max_atoms;
@@ -332,25 +335,35 @@ __global__ __launch_bounds__(256) void k_edge_apply(DevGraph g, EdgeArgs a) {
       b = edge_find_or_insert(g, edge_key(o, t), &ins);
       if (b == KEY_EMPTY) active = ins = false;
     }
-    uint32_t rank = 0;
+    uint32_t rank = 0, rrank = 0;
     if (ins) {
       rank = atomicAdd(&g.enew[o], 1u);
+      rrank = atomicAdd(&g.rnew[t], 1u);
       g.eval[b] = EVAL_NEW | rank;
       atomicAdd(&g.edelta[b], d);
     } else if (active) {
       const uint32_t v = g.eval[b];
-      if (v & EVAL_NEW)
+      if (v & EVAL_NEW) {
         atomicAdd(&g.edelta[b], d);
-      else
-        atomicAdd(edge_count_ptr(g.pool, (uint64_t)g.adj[o].x + v), d);
+      } else {
+        const int32_t old = atomicAdd(edge_count_ptr(g.pool, (uint64_t)g.adj[o].x + v), d);
+        const int32_t now = (int32_t)((uint32_t)old + (uint32_t)d);
+        if ((old != 0) != (now != 0)) atomicAdd(&g.nzdeg[o], now != 0 ? 1u : 0xFFFFFFFFu);
+      }
     }
     const unsigned long long li = wave_append(&g.ctr->n_new_edges, ins);
-    if (ins) a.newlist[li] = b;
+    if (ins) {
+      a.newlist[li] = b;
+      a.rrank[li] = rrank;
+    }
     const uint64_t insb = __ballot(ins);
     if (lane_id() == 0 && insb) atomicAdd(&g.ctr->etab_used, (unsigned long long)__popcll(insb));
     const bool first = ins && rank == 0;
     const unsigned long long ti = wave_append(&g.ctr->n_touched, first);
     if (first) a.touched[ti] = o;
+    const bool rfirst = ins && rrank == 0;
+    const unsigned long long ri = wave_append(&g.ctr->n_rtouched, rfirst);
+    if (rfirst) a.rtouched[ri] = t;
   }
 }
 
@@ -360,47 +373,74 @@ __device__ inline uint32_t seg_cap(uint32_t need) {
   return c;
 }
 
-__global__ __launch_bounds__(256) void k_edge_plan(DevGraph g, EdgeArgs a) {
-  const uint64_t n = g.ctr->n_touched;
+// One direction's segmented store: forward edges (u64) or reverse candidates (u32).
+template <typename T>
+struct Seg {
+  uint2 *adj;
+  uint32_t *cap;
+  uint32_t *nnew;
+  T *pool;
+  uint64_t pcap;
+  unsigned long long *top;
+  const unsigned long long *ntouched;
+  const uint32_t *touched;
+  uint32_t *reloc;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_seg_plan(Seg<T> s, Counters *c) {
+  const uint64_t n = *s.ntouched;
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t base = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); base < n;
        base += stride) {
     const uint64_t i = base + lane_id();
     uint32_t want = 0;
     if (i < n) {
-      const uint32_t o = a.touched[i];
-      const uint32_t need = g.adj[o].y + g.enew[o];
-      if (need > g.ecap[o]) want = seg_cap(need);
+      const uint32_t o = s.touched[i];
+      const uint32_t need = s.adj[o].y + s.nnew[o];
+      if (need > s.cap[o]) want = seg_cap(need);
     }
-    const unsigned long long off = wave_atomic_add(&g.ctr->pool_top, want);
+    const unsigned long long off = wave_atomic_add(s.top, want);
     if (i < n) {
       uint32_t r = 0xFFFFFFFFu;  // no move
       if (want) {
-        if (off + want > g.pcap) {
-          set_err(g.ctr, ERR_POOL_FULL);
+        if (off + want > s.pcap) {
+          set_err(c, ERR_POOL_FULL);
           r = 0xFFFFFFFEu;
         } else {
           r = (uint32_t)off;
         }
       }
-      a.reloc[i] = r;
+      s.reloc[i] = r;
     }
   }
 }
 
-__global__ __launch_bounds__(256) void k_edge_move(DevGraph g, EdgeArgs a) {
-  const uint64_t n = g.ctr->n_touched;
+template <typename T>
+__global__ __launch_bounds__(256) void k_seg_move(Seg<T> s) {
+  const uint64_t n = *s.ntouched;
   const uint64_t nw = (uint64_t)gridDim.x * 4;
   for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += nw) {
-    const uint32_t r = a.reloc[i];
+    const uint32_t r = s.reloc[i];
     if (r >= 0xFFFFFFFEu) continue;
-    const uint32_t o = a.touched[i];
-    const uint2 ad = g.adj[o];
-    for (uint32_t e = lane_id(); e < ad.y; e += 64) g.pool[(uint64_t)r + e] = g.pool[(uint64_t)ad.x + e];
+    const uint32_t o = s.touched[i];
+    const uint2 ad = s.adj[o];
+    for (uint32_t e = lane_id(); e < ad.y; e += 64) s.pool[(uint64_t)r + e] = s.pool[(uint64_t)ad.x + e];
     if (lane_id() == 0) {
-      g.adj[o].x = r;
-      g.ecap[o] = seg_cap(ad.y + g.enew[o]);
+      s.adj[o].x = r;
+      s.cap[o] = seg_cap(ad.y + s.nnew[o]);
     }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_seg_finish(Seg<T> s) {
+  const uint64_t n = *s.ntouched;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const uint32_t o = s.touched[i];
+    s.adj[o].y += s.nnew[o];
+    s.nnew[o] = 0;
   }
 }
 
@@ -415,19 +455,14 @@ __global__ __launch_bounds__(256) void k_edge_append(DevGraph g, EdgeArgs a) {
     const uint2 ad = g.adj[o];
     const uint32_t idx = ad.y + rank;
     if (idx >= g.ecap[o]) continue;  // relocation failed: ERR_POOL_FULL already set
-    g.pool[(uint64_t)ad.x + idx] = pack_edge(t, g.edelta[b]);
+    const int32_t d = g.edelta[b];
+    g.pool[(uint64_t)ad.x + idx] = pack_edge(t, d);
     g.eval[b] = idx;
     g.edelta[b] = 0;
-  }
-}
-
-__global__ __launch_bounds__(256) void k_edge_finish(DevGraph g, EdgeArgs a) {
-  const uint64_t n = g.ctr->n_touched;
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    const uint32_t o = a.touched[i];
-    g.adj[o].y += g.enew[o];
-    g.enew[o] = 0;
+    if (d != 0) atomicAdd(&g.nzdeg[o], 1u);
+    const uint2 rd = g.radj[t];
+    const uint32_t ridx = rd.y + a.rrank[i];
+    if (ridx < g.rcap[t]) g.rpool[(uint64_t)rd.x + ridx] = o;
   }
 }
 
@@ -441,11 +476,18 @@ int grid_for(uint64_t threads, int block, int cap) {
 hipError_t launch_edges(const DevGraph &g, const EdgeArgs &a, hipStream_t s) {
   if (a.max_atoms == 0) return hipSuccess;
   const int grid = grid_for(a.max_atoms, 256, 8192);
+  Seg<uint64_t> fw{g.adj, g.ecap, g.enew, g.pool, g.pcap, &g.ctr->pool_top,
+                   &g.ctr->n_touched, a.touched, a.reloc};
+  Seg<uint32_t> rv{g.radj, g.rcap, g.rnew, g.rpool, g.rpcap, &g.ctr->rpool_top,
+                   &g.ctr->n_rtouched, a.rtouched, a.rreloc};
   hipLaunchKernelGGL(k_edge_apply, dim3(grid), dim3(256), 0, s, g, a);
-  hipLaunchKernelGGL(k_edge_plan, dim3(grid), dim3(256), 0, s, g, a);
-  hipLaunchKernelGGL(k_edge_move, dim3(grid), dim3(256), 0, s, g, a);
+  hipLaunchKernelGGL(k_seg_plan<uint64_t>, dim3(grid), dim3(256), 0, s, fw, g.ctr);
+  hipLaunchKernelGGL(k_seg_plan<uint32_t>, dim3(grid), dim3(256), 0, s, rv, g.ctr);
+  hipLaunchKernelGGL(k_seg_move<uint64_t>, dim3(grid), dim3(256), 0, s, fw);
+  hipLaunchKernelGGL(k_seg_move<uint32_t>, dim3(grid), dim3(256), 0, s, rv);
   hipLaunchKernelGGL(k_edge_append, dim3(grid), dim3(256), 0, s, g, a);
-  hipLaunchKernelGGL(k_edge_finish, dim3(grid), dim3(256), 0, s, g, a);
+  hipLaunchKernelGGL(k_seg_finish<uint64_t>, dim3(grid), dim3(256), 0, s, fw);
+  hipLaunchKernelGGL(k_seg_finish<uint32_t>, dim3(grid), dim3(256), 0, s, rv);
   return hipGetLastError();
 }
 

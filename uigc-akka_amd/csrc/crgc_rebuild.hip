@@ -88,6 +88,7 @@ __global__ __launch_bounds__(256) void k_rb_edges(DevGraph src, uint64_t src_top
           if (edge_count(ed) == 0 || !(src.flags[t] & FL_ALIVE)) continue;
           const uint32_t nt = map[t];
           dst.pool[off + kept] = pack_edge(nt, edge_count(ed));
+          atomicAdd(&dst.rnew[nt], 1u);  // in-degree, for the candidate lists
           const uint64_t key = edge_key(ns, nt);
           uint64_t h = mix64(key) & dst.emask;
           for (uint64_t p = 0; p < dst.ecap_tab; ++p) {
@@ -102,6 +103,12 @@ __global__ __launch_bounds__(256) void k_rb_edges(DevGraph src, uint64_t src_top
         }
         dst.adj[ns] = make_uint2((uint32_t)off, kept);
         dst.ecap[ns] = rb_cap(kept);
+        // The reference keeps nonzero counts toward collected shadows in
+        // `outgoing` (their Shadow objects stay keys there), so they still
+        // count in outgoing.size(): carry the owner's count over unchanged.
+        // The purged entries can never change again (their ids now map to
+        // fresh shadows).
+        dst.nzdeg[ns] = src.nzdeg[v];
         const uint32_t s = src.sup[v];
         uint32_t nsup = SLOT_NONE;
         if (s == SLOT_DEAD) nsup = SLOT_DEAD;
@@ -189,6 +196,39 @@ static void exclusive_scan(uint64_t *data, uint64_t n, uint64_t *tmp, hipStream_
 }
 
 __global__ void k_rb_pool_top(Counters *c, const uint64_t *grand) { c->pool_top = *grand; }
+__global__ void k_rb_rpool_top(Counters *c, const uint64_t *grand) { c->rpool_top = *grand; }
+
+// 5. reverse candidate lists from the kept edges: capacities from the
+//    in-degrees counted in k_rb_edges, offsets by scan, then a fill pass.
+__global__ __launch_bounds__(256) void k_rb_rcaps(DevGraph dst, uint64_t *caps) {
+  const uint64_t n = dst.ctr->slot_top;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < dst.scap; v += stride)
+    caps[v] = v < n ? rb_cap(dst.rnew[v]) : 0;
+}
+
+__global__ __launch_bounds__(256) void k_rb_rsetup(DevGraph dst, const uint64_t *offs) {
+  const uint64_t n = dst.ctr->slot_top;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < n; v += stride) {
+    dst.rcap[v] = rb_cap(dst.rnew[v]);
+    dst.radj[v] = make_uint2((uint32_t)offs[v], 0);
+    dst.rnew[v] = 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rb_rfill(DevGraph dst) {
+  const uint64_t n = dst.ctr->slot_top;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t o = (uint64_t)blockIdx.x * 256 + threadIdx.x; o < n; o += stride) {
+    const uint2 ad = dst.adj[o];
+    for (uint32_t e = 0; e < ad.y; ++e) {
+      const uint32_t t = edge_target(dst.pool[(uint64_t)ad.x + e]);
+      const uint32_t pos = atomicAdd(&dst.radj[t].y, 1u);
+      dst.rpool[(uint64_t)dst.radj[t].x + pos] = (uint32_t)o;
+    }
+  }
+}
 
 hipError_t launch_rebuild(const DevGraph &src, uint64_t src_top, const DevGraph &dst, uint32_t *map,
                           uint32_t *newdeg, uint64_t *offs, void *scan_tmp, hipStream_t s) {
@@ -200,6 +240,12 @@ hipError_t launch_rebuild(const DevGraph &src, uint64_t src_top, const DevGraph 
   const uint64_t nb = (dst.scap + SCAN_TILE - 1) / SCAN_TILE;
   hipLaunchKernelGGL(k_rb_pool_top, dim3(1), dim3(1), 0, s, dst.ctr, (uint64_t *)scan_tmp + nb);
   hipLaunchKernelGGL(k_rb_edges, dim3(grid), dim3(256), 0, s, src, src_top, dst, map, offs);
+  const int dgrid = grid_for(dst.scap, 256, 8192);
+  hipLaunchKernelGGL(k_rb_rcaps, dim3(dgrid), dim3(256), 0, s, dst, offs);
+  exclusive_scan(offs, dst.scap, (uint64_t *)scan_tmp, s);
+  hipLaunchKernelGGL(k_rb_rpool_top, dim3(1), dim3(1), 0, s, dst.ctr, (uint64_t *)scan_tmp + nb);
+  hipLaunchKernelGGL(k_rb_rsetup, dim3(dgrid), dim3(256), 0, s, dst, offs);
+  hipLaunchKernelGGL(k_rb_rfill, dim3(dgrid), dim3(256), 0, s, dst);
   return hipGetLastError();
 }
 

@@ -30,6 +30,15 @@ __device__ inline bool sparse_level(const Counters *c, int L, uint32_t thr) {
   return c->ring[(L - 2) % LEVEL_RING] < thr;
 }
 
+// Direction choice for level L (same answer in k_frontier and k_expand): pull
+// when the previous frontier was large; the level is then dense, so every
+// block of the slot range is scanned and `fx` is complete.
+__device__ inline bool pull_level(const Counters *c, int L, const LevelArgs &a) {
+  if (!(a.flags & LV_PULL) || (a.flags & LV_BITMAP_FRONT) || L < 1) return false;
+  if (sparse_level(c, L, a.sparse_thresh) || sparse_level(c, L + 1, a.sparse_thresh)) return false;
+  return c->ring[(L - 1) % LEVEL_RING] >= a.pull_thresh;
+}
+
 __device__ inline void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -99,7 +108,8 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
   unsigned long long *qh_cnt = &c->qh[L & 1];
   const uint32_t tag = (uint32_t)(L + 1) << 12;
   const bool bitmode = a.flags & LV_BITMAP_FRONT;
-  uint32_t n_front = 0, n_sup = 0;
+  const bool pull = !ROOTS && pull_level(c, L, a);
+  uint32_t n_front = 0, n_sup = 0, n_edges = 0;
 
   for (uint32_t blk = gw; blk < nblk; blk += nw) {
     if (sp_cur && Dc[blk] == 0) continue;
@@ -161,6 +171,15 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
     const uint32_t incl = wave_incl_scan(cnt);
     const uint32_t total = __shfl(incl, 63);
     uint32_t pos = incl - cnt;
+    if (pull) {
+      // expandable frontier = frontier minus halted shadows (this wave owns the words)
+      const uint4 f4[2] = {*(const uint4 *)(g.flags + base), *(const uint4 *)(g.flags + base + 16)};
+      const uint8_t *fb = (const uint8_t *)f4;
+      uint32_t halted = 0;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) halted |= (fb[j] & FL_HALTED) ? (1u << j) : 0u;
+      g.fx[(uint64_t)blk * 64 + lane] = m & ~halted;
+    }
     while (m) {
       const int j = __ffs(m) - 1;
       m &= m - 1;
@@ -169,7 +188,7 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
     n_front += cnt;
     wave_lds_fence();
 
-    // Frontier shadows -> supervisor marks + edge ranges.
+    // Frontier shadows -> supervisor marks + edge ranges (push levels).
     uint32_t nlight = 0;
     uint2 *region = g.qn_buf + (uint64_t)blk * BLK_SLOTS;
     for (uint32_t c0 = 0; c0 < total; c0 += 64) {
@@ -178,7 +197,9 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
       const uint32_t v = valid ? s_front[wv][idx] : 0;
       const uint8_t f = valid ? g.flags[v] : 0;
       const bool expand = valid && !(f & FL_HALTED);  // halted: marked, not expanded (:226)
-      const uint2 ad = expand ? g.adj[v] : make_uint2(0, 0);
+      // traced edges = nonzero out-edges of expanded shadows (:231)
+      if (expand) n_edges += g.nzdeg[v];
+      const uint2 ad = (expand && !pull) ? g.adj[v] : make_uint2(0, 0);
       if (!INVESTIGATE && expand) {
         const uint32_t s = g.sup[v];  // supervisor edge (:258-267)
         if (s < 0xFFFFFFF0u) {         // not null, not collected
@@ -206,16 +227,17 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
   }
   const uint64_t tf = block_sum4(n_front);
   const uint64_t ts = block_sum4(n_sup);
+  const uint64_t te = block_sum4(n_edges);
   if (threadIdx.x == 0) {
     stat[STAT_FRONT] = tf;
     stat[STAT_SUP] += ts;
+    stat[STAT_EDGES] += te;
   }
 }
 
 __device__ inline void expand_edge(const DevGraph &g, uint8_t *Fn, uint8_t *Dn, bool sp_next, bool check,
-                                   uint64_t ed, uint32_t &n_edges, uint32_t *Fbits) {
+                                   uint64_t ed, uint32_t *Fbits) {
   const int32_t cntv = edge_count(ed);
-  n_edges += cntv != 0;
   if (cntv > 0) {  // (:231-241)
     if (Fbits) mark_target_bits(g, Fbits, Dn, sp_next, edge_target(ed));
     else mark_target(g, Fn, Dn, sp_next, edge_target(ed), check);
@@ -263,7 +285,59 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   const uint64_t nw = (uint64_t)gridDim.x * 4;
   const uint32_t want = (uint32_t)(L + 1);
   const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
-  uint32_t n_edges = 0;
+
+  if (pull_level(c, L, a)) {
+    // Pull: each unmarked, not-yet-found shadow looks for an expandable
+    // frontier shadow among its in-candidates and stops at the first one
+    // whose edge to it has a positive count.  A wave owns its block's bytes.
+    for (uint64_t blk = gw; blk < nblk; blk += nw) {
+      const uint64_t base = blk * BLK_SLOTS + (uint64_t)lane * 32;
+      const uint32_t word = g.vis[blk * 64 + lane];
+      const uint4 f4[2] = {*(const uint4 *)(g.flags + base), *(const uint4 *)(g.flags + base + 16)};
+      const uint8_t *fb = (const uint8_t *)f4;
+      uint4 *fp = (uint4 *)(Fn + base);
+      const uint4 x0 = fp[0], x1 = fp[1];
+      uint32_t xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      uint32_t un = 0;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        const bool cand = (xs[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+        un |= ((fb[j] & FL_ALIVE) && !cand) ? (1u << j) : 0u;
+      }
+      un &= ~word;
+      uint32_t found = 0;
+      while (un) {
+        const int j = __ffs(un) - 1;
+        un &= un - 1;
+        const uint32_t v = (uint32_t)(base + j);
+        const uint2 rd = g.radj[v];
+        bool hit = false;
+        for (uint32_t i = 0; i < rd.y && !hit; i += 4) {
+          uint32_t u[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) u[q] = i + q < rd.y ? g.rpool[rd.x + i + q] : SLOT_NONE;
+          uint32_t fw[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) fw[q] = u[q] != SLOT_NONE ? g.fx[u[q] >> 5] : 0u;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (hit || !((fw[q] >> (u[q] & 31)) & 1u)) continue;
+            const uint32_t idx = edge_find(g, u[q], v);
+            if (idx != SLOT_NONE && edge_count(g.pool[(uint64_t)g.adj[u[q]].x + idx]) > 0) hit = true;
+          }
+        }
+        if (hit) found |= 1u << j;
+      }
+      if (found) {
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+          if ((found >> j) & 1u) xs[j >> 2] |= 1u << (8 * (j & 3));
+        fp[0] = make_uint4(xs[0], xs[1], xs[2], xs[3]);
+        fp[1] = make_uint4(xs[4], xs[5], xs[6], xs[7]);
+      }
+    }
+    return;
+  }
 
   // light ranges: chunk (block b, k-th 64) of every block's region; chunk ids
   // run over blocks first so consecutive waves take different blocks
@@ -299,7 +373,7 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < EXP_UNROLL; ++u)
-        expand_edge(g, Fn, Dn, sp_next, check, ed[u], n_edges, Fbits);
+        expand_edge(g, Fn, Dn, sp_next, check, ed[u], Fbits);
     }
     wave_lds_fence();
   }
@@ -315,11 +389,9 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < EXP_UNROLL; ++u)
-        expand_edge(g, Fn, Dn, sp_next, check, ed[u], n_edges, Fbits);
+        expand_edge(g, Fn, Dn, sp_next, check, ed[u], Fbits);
     }
   }
-  const uint64_t te = block_sum4(n_edges);
-  if (threadIdx.x == 0 && te) g.blkstat[(uint64_t)blockIdx.x * 4 + STAT_EDGES] += te;
 }
 
 int level_grid(uint64_t slot_top) {
