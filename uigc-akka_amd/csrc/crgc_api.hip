@@ -45,7 +45,7 @@ void free_arrays(Arrays &a) {
                 d.enew, d.pool, d.ekey, d.eval, d.edelta, d.vis, d.front[0], d.front[1],
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill, d.fbits[0], d.fbits[1],
-                d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.fx};
+                d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.fx, d.erev};
   for (void *p : ps)
     if (p) hipFree(p);
   a.allocated = false;
@@ -56,6 +56,8 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s) 
   a.caps = c;
   DevGraph &d = a.d;
   d = DevGraph{};
+  // slots are u32 below SLOT_DEAD, and reverse candidates keep bit 31 (RC_POS)
+  if (c.scap >= (1ull << 31)) return hipErrorOutOfMemory;
   d.hcap = c.hcap;
   d.hmask = c.hcap - 1;
   d.scap = c.scap;
@@ -86,6 +88,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s) 
   A(dmalloc(&d.pool, c.pcap));
   A(dmalloc(&d.ekey, c.ecap));
   A(dmalloc(&d.eval, c.ecap));
+  A(dmalloc(&d.erev, c.ecap));
   A(dmalloc(&d.edelta, c.ecap));
   A(dmalloc(&d.vis, c.scap / 32));
   A(dmalloc(&d.front[0], c.scap));
@@ -423,14 +426,16 @@ static int run_edges(crgc_graph *h, uint32_t *ao, uint32_t *at, int32_t *ad, uin
   ea.reloc = cv.take<uint32_t>(max_atoms);
   ea.rtouched = cv.take<uint32_t>(max_atoms);
   ea.rreloc = cv.take<uint32_t>(max_atoms);
-  hipMemsetAsync((char *)h->ctr + CTR_OFF(n_touched), 0, 3 * 8, h->stream);
+  ea.flips = cv.take<uint64_t>(max_atoms);
+  // n_touched, n_new_edges, n_rtouched, n_flips
+  hipMemsetAsync((char *)h->ctr + CTR_OFF(n_touched), 0, 4 * 8, h->stream);
   HIP_TRY(launch_edges(h->g.d, ea, h->stream));
   return CRGC_OK;
 }
 
 static size_t edge_scratch(uint64_t max_atoms) {
   return Carver::need({max_atoms * 4, max_atoms * 4, max_atoms * 4, max_atoms * 8, max_atoms * 4,
-                       max_atoms * 4, max_atoms * 4, max_atoms * 4, max_atoms * 4});
+                       max_atoms * 4, max_atoms * 4, max_atoms * 4, max_atoms * 4, max_atoms * 8});
 }
 
 int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
@@ -656,10 +661,18 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
       if (ring[lv % LEVEL_RING] == 0) {
         *levels = (uint64_t)lv;  // levels 0 .. lv-1 were non-empty
         double ms = 0;
+        const bool log = getenv("CRGC_LEVEL_LOG") != nullptr;
         for (size_t i = 0; i < nl; ++i) {
           float t = 0;
           hipEventElapsedTime(&t, h->lvl_ev[2 * i], h->lvl_ev[2 * i + 1]);
           ms += t;
+          if (log)
+            fprintf(stderr, "[crgc] level %zu frontier %llu  %.1f us%s\n", i,
+                    i <= (size_t)last ? ring[i % LEVEL_RING] : 0ull, t * 1e3,
+                    (la.flags & LV_PULL) && i >= 1 && i <= (size_t)last &&
+                            ring[(i - 1) % LEVEL_RING] >= la.pull_thresh
+                        ? " (pull?)"
+                        : "");
         }
         *kernel_ms = ms;
         *launches = nl;

@@ -116,6 +116,7 @@ struct EdgeArgs {
   uint32_t *reloc;     // [max_atoms] new segment offset per touched owner
   uint32_t *rtouched;  // [max_atoms] targets that got new candidates
   uint32_t *rreloc;    // [max_atoms] new candidate-segment offset per touched target
+  uint64_t *flips;     // [max_atoms] buckets of edges whose count changed sign
 };
 
 constexpr uint32_t LV_CHECK_BEFORE_STORE = 1;  // read the candidate byte before storing it

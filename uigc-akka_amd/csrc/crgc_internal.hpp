@@ -27,6 +27,7 @@ constexpr uint32_t SLOT_NONE = 0xFFFFFFFFu;  // Java null supervisor
 constexpr uint32_t SLOT_DEAD = 0xFFFFFFFEu;  // supervisor collected (post-rebuild)
 constexpr uint32_t VAL_PENDING = 0xFFFFFFFFu;
 constexpr uint32_t EVAL_NEW = 0x80000000u;   // eval: edge inserted in this merge
+constexpr uint32_t RC_POS = 0x80000000u;     // reverse candidate: the edge's count is > 0
 
 // flags bits: ALIVE is internal; the rest equal CRGC_F_* of include/crgc.h
 constexpr uint8_t FL_ALIVE = 0x01, FL_INTERNED = 0x02, FL_LOCAL = 0x04, FL_BUSY = 0x08,
@@ -59,6 +60,7 @@ struct Counters {
   unsigned long long n_touched;      // owners with new edges in this merge
   unsigned long long n_new_edges;    // new edge keys in this merge
   unsigned long long n_rtouched;     // targets with new candidates in this merge
+  unsigned long long n_flips;        // existing edges whose count changed sign in this merge
   unsigned long long err;
   unsigned long long spin_max;
   // trace
@@ -97,7 +99,7 @@ struct DevGraph {
   uint2 *radj;               // {offset, length} into rpool
   uint32_t *rcap;
   uint32_t *rnew;            // new candidates per target in the current merge
-  uint32_t *rpool;
+  uint32_t *rpool;           // owner slot | RC_POS while count(owner -> slot) > 0
   uint64_t rpcap;
   uint32_t *fx;              // expandable frontier bitmap (frontier & !halted)
   // edges
@@ -106,6 +108,7 @@ struct DevGraph {
   uint64_t ecap_tab, emask;
   uint64_t *ekey;
   uint32_t *eval;
+  uint32_t *erev;   // index of the edge's candidate entry in the target's reverse segment
   int32_t *edelta;
   // trace
   uint32_t *vis;

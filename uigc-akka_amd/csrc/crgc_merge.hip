@@ -329,7 +329,7 @@ __global__ __launch_bounds__(256) void k_edge_apply(DevGraph g, EdgeArgs a) {
       d = a.atom_d[i];
     }
     bool active = valid && d != 0 && vs(o) && vs(t);
-    bool ins = false;
+    bool ins = false, flip = false;
     uint64_t b = 0;
     if (active) {
       b = edge_find_or_insert(g, edge_key(o, t), &ins);
@@ -349,8 +349,13 @@ __global__ __launch_bounds__(256) void k_edge_apply(DevGraph g, EdgeArgs a) {
         const int32_t old = atomicAdd(edge_count_ptr(g.pool, (uint64_t)g.adj[o].x + v), d);
         const int32_t now = (int32_t)((uint32_t)old + (uint32_t)d);
         if ((old != 0) != (now != 0)) atomicAdd(&g.nzdeg[o], now != 0 ? 1u : 0xFFFFFFFFu);
+        flip = (old > 0) != (now > 0);
       }
     }
+    // sign changes of existing counts: their candidate entries are refreshed
+    // from the final count after the merge (k_edge_flip)
+    const unsigned long long fi = wave_append(&g.ctr->n_flips, flip);
+    if (flip) a.flips[fi] = b;
     const unsigned long long li = wave_append(&g.ctr->n_new_edges, ins);
     if (ins) {
       a.newlist[li] = b;
@@ -462,7 +467,23 @@ __global__ __launch_bounds__(256) void k_edge_append(DevGraph g, EdgeArgs a) {
     if (d != 0) atomicAdd(&g.nzdeg[o], 1u);
     const uint2 rd = g.radj[t];
     const uint32_t ridx = rd.y + a.rrank[i];
-    if (ridx < g.rcap[t]) g.rpool[(uint64_t)rd.x + ridx] = o;
+    g.erev[b] = ridx;
+    if (ridx < g.rcap[t]) g.rpool[(uint64_t)rd.x + ridx] = o | (d > 0 ? RC_POS : 0u);
+  }
+}
+
+// 6. candidate entries of edges whose count changed sign: the final count
+//    decides (an edge may be listed more than once; every copy writes the same).
+__global__ __launch_bounds__(256) void k_edge_flip(DevGraph g, EdgeArgs a) {
+  const uint64_t n = g.ctr->n_flips;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const uint64_t b = a.flips[i];
+    const uint64_t key = g.ekey[b];
+    const uint32_t o = (uint32_t)(key >> 32), t = (uint32_t)key;
+    const int32_t cnt = edge_count(g.pool[(uint64_t)g.adj[o].x + g.eval[b]]);
+    const uint32_t r = g.erev[b];
+    if (r < g.radj[t].y) g.rpool[(uint64_t)g.radj[t].x + r] = o | (cnt > 0 ? RC_POS : 0u);
   }
 }
 
@@ -488,6 +509,7 @@ hipError_t launch_edges(const DevGraph &g, const EdgeArgs &a, hipStream_t s) {
   hipLaunchKernelGGL(k_edge_append, dim3(grid), dim3(256), 0, s, g, a);
   hipLaunchKernelGGL(k_seg_finish<uint64_t>, dim3(grid), dim3(256), 0, s, fw);
   hipLaunchKernelGGL(k_seg_finish<uint32_t>, dim3(grid), dim3(256), 0, s, rv);
+  hipLaunchKernelGGL(k_edge_flip, dim3(grid), dim3(256), 0, s, g, a);
   return hipGetLastError();
 }
 

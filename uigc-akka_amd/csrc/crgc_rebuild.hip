@@ -223,9 +223,15 @@ __global__ __launch_bounds__(256) void k_rb_rfill(DevGraph dst) {
   for (uint64_t o = (uint64_t)blockIdx.x * 256 + threadIdx.x; o < n; o += stride) {
     const uint2 ad = dst.adj[o];
     for (uint32_t e = 0; e < ad.y; ++e) {
-      const uint32_t t = edge_target(dst.pool[(uint64_t)ad.x + e]);
+      const uint64_t ed = dst.pool[(uint64_t)ad.x + e];
+      const uint32_t t = edge_target(ed);
       const uint32_t pos = atomicAdd(&dst.radj[t].y, 1u);
-      dst.rpool[(uint64_t)dst.radj[t].x + pos] = (uint32_t)o;
+      dst.rpool[(uint64_t)dst.radj[t].x + pos] = (uint32_t)o | (edge_count(ed) > 0 ? RC_POS : 0u);
+      // the edge's bucket, for its candidate index
+      const uint64_t key = edge_key((uint32_t)o, t);
+      uint64_t hb = mix64(key) & dst.emask;
+      for (uint64_t p = 0; p < dst.ecap_tab && dst.ekey[hb] != key; ++p) hb = (hb + 1) & dst.emask;
+      if (dst.ekey[hb] == key) dst.erev[hb] = pos;
     }
   }
 }

@@ -288,8 +288,8 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
 
   if (pull_level(c, L, a)) {
     // Pull: each unmarked, not-yet-found shadow looks for an expandable
-    // frontier shadow among its in-candidates and stops at the first one
-    // whose edge to it has a positive count.  A wave owns its block's bytes.
+    // frontier shadow among its in-candidates whose edge to it has a
+    // positive count, and stops at the first.  A wave owns its block's bytes.
     for (uint64_t blk = gw; blk < nblk; blk += nw) {
       const uint64_t base = blk * BLK_SLOTS + (uint64_t)lane * 32;
       const uint32_t word = g.vis[blk * 64 + lane];
@@ -316,14 +316,12 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
           uint32_t u[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) u[q] = i + q < rd.y ? g.rpool[rd.x + i + q] : SLOT_NONE;
-          uint32_t fw[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) fw[q] = u[q] != SLOT_NONE ? g.fx[u[q] >> 5] : 0u;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            if (hit || !((fw[q] >> (u[q] & 31)) & 1u)) continue;
-            const uint32_t idx = edge_find(g, u[q], v);
-            if (idx != SLOT_NONE && edge_count(g.pool[(uint64_t)g.adj[u[q]].x + idx]) > 0) hit = true;
+            // a candidate counts only while its edge count is positive (RC_POS)
+            const bool pos = u[q] != SLOT_NONE && (u[q] & RC_POS);
+            const uint32_t s = u[q] & ~RC_POS;
+            if (pos && ((g.fx[s >> 5] >> (s & 31)) & 1u)) hit = true;
           }
         }
         if (hit) found |= 1u << j;
