@@ -30,11 +30,16 @@ def _same_trace(rh, ro):
 
 # Traversal directions.  "pull" forces every level after the roots to pull
 # (in-candidate scan) and "push" disables pulling; "auto" is the product
-# default (pull only for large dense levels, i.e. push at these sizes).
+# default (pull only for large dense levels, i.e. push at these sizes, and
+# k_tail once a sparse level's frontier is narrow).
 DIRECTIONS = {
     "auto": {},
     "push": {"CRGC_PULL": "0", "CRGC_SPARSE_THRESH": "0"},
     "pull": {"CRGC_PULL": "1", "CRGC_PULL_THRESH": "1", "CRGC_SPARSE_THRESH": "0"},
+    # narrow-frontier workgroup (k_tail) off, and on at every sparse level with
+    # a bail back to the level kernels whenever a round finds more than 3
+    "notail": {"CRGC_TAIL": "0"},
+    "tailbail": {"CRGC_TAIL_START": "65536", "CRGC_TAIL_MAX": "3"},
 }
 
 

@@ -14,7 +14,7 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for sub in ("uigc-akka_amd", "workload"):
+for sub in ("uigc-akka_amd", "workload", ""):
     sys.path.insert(0, os.path.join(REPO, sub))
 
 
@@ -23,20 +23,21 @@ def main():
     ap.add_argument("--actors", type=int, default=10_000_000)
     ap.add_argument("--edges", type=int, default=100_000_000)
     ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--wakeups", type=int, default=3, help="bench wakeups applied before timing")
     ap.add_argument("--variant", action="append", default=[])
     args = ap.parse_args()
     import torch
     import crgc_hip
     import world
-    w = world.World(seed=0x5EED + 2)
-    w.bulk_graph(args.actors, args.edges, alpha=2.1, n_roots=max(1, args.actors // 1000))
-    g = crgc_hip.ShadowGraph(vertex_capacity=int(args.actors * 1.2),
-                             edge_capacity=int(args.edges * 1.2))
-    for b in w.batches(1_000_000):
-        g.merge_entries(b.to_device("cuda"))
-    g.trace_counts(True)
-    g.merge_entries(w.wakeup_batch(1_000_000).to_device("cuda"))
-    g.trace_counts(True)
+    import bench
+    ns = argparse.Namespace(actors=args.actors, edges=args.edges, batch=1_000_000)
+    stream = torch.cuda.Stream()
+    w, g = bench.build_graph(crgc_hip, world, 0, 0, stream.cuda_stream, ns)  # bench's C2 graph
+    for _ in range(args.wakeups):
+        b = w.wakeup_batch(1_000_000).to_device("cuda")
+        torch.cuda.synchronize()  # uploaded on torch's stream, merged on the graph's
+        g.merge_entries(b)
+        g.trace_counts(True)
     variants = args.variant or ["BASE=0"]
     res = {v: [] for v in variants}
     ref = None

@@ -41,11 +41,11 @@ hipError_t dmalloc(T **p, uint64_t n) {
 void free_arrays(Arrays &a) {
   if (!a.allocated) return;
   DevGraph &d = a.d;
-  void *ps[] = {d.hkey, d.hval, d.vid, d.recv, d.flags, d.sup, d.adj, d.ecap, d.vseq, d.sseq,
-                d.enew, d.pool, d.ekey, d.eval, d.edelta, d.vis, d.front[0], d.front[1],
+  void *ps[] = {d.htab, d.vid, d.recv, d.flags, d.sup, d.adj, d.ecap, d.vseq, d.sseq,
+                d.enew, d.pool, d.etab, d.edelta, d.vis, d.front[0], d.front[1],
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill, d.fbits[0], d.fbits[1],
-                d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.fx, d.erev};
+                d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.fx, d.tq};
   for (void *p : ps)
     if (p) hipFree(p);
   a.allocated = false;
@@ -74,8 +74,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s) 
       return e;                         \
     }                                   \
   } while (0)
-  A(dmalloc(&d.hkey, c.hcap));
-  A(dmalloc(&d.hval, c.hcap));
+  A(dmalloc(&d.htab, c.hcap));
   A(dmalloc(&d.vid, c.scap));
   A(dmalloc(&d.recv, c.scap));
   A(dmalloc(&d.flags, c.scap));
@@ -86,9 +85,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s) 
   A(dmalloc(&d.sseq, c.scap));
   A(dmalloc(&d.enew, c.scap));
   A(dmalloc(&d.pool, c.pcap));
-  A(dmalloc(&d.ekey, c.ecap));
-  A(dmalloc(&d.eval, c.ecap));
-  A(dmalloc(&d.erev, c.ecap));
+  A(dmalloc(&d.etab, c.ecap));
   A(dmalloc(&d.edelta, c.ecap));
   A(dmalloc(&d.vis, c.scap / 32));
   A(dmalloc(&d.front[0], c.scap));
@@ -116,11 +113,11 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s) 
   A(dmalloc(&d.rnew, c.scap));
   A(dmalloc(&d.rpool, d.rpcap));
   A(dmalloc(&d.fx, c.scap / 32));
+  A(dmalloc(&d.tq, 2 * (uint64_t)TAIL_QCAP));
 #undef A
   a.allocated = true;
   // Default state of every unused slot / bucket.
-  hipMemsetAsync(d.hkey, 0xFF, c.hcap * 8, s);
-  hipMemsetAsync(d.hval, 0xFF, c.hcap * 4, s);
+  hipMemsetAsync(d.htab, 0xFF, c.hcap * sizeof(IdBucket), s);
   hipMemsetAsync(d.recv, 0, c.scap * 4, s);
   hipMemsetAsync(d.flags, 0, c.scap, s);
   hipMemsetAsync(d.sup, 0xFF, c.scap * 4, s);
@@ -129,8 +126,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s) 
   hipMemsetAsync(d.vseq, 0, c.scap * 8, s);
   hipMemsetAsync(d.sseq, 0, c.scap * 8, s);
   hipMemsetAsync(d.enew, 0, c.scap * 4, s);
-  hipMemsetAsync(d.ekey, 0xFF, c.ecap * 8, s);
-  hipMemsetAsync(d.eval, 0xFF, c.ecap * 4, s);
+  hipMemsetAsync(d.etab, 0xFF, c.ecap * sizeof(EdgeBucket), s);
   hipMemsetAsync(d.edelta, 0, c.ecap * 4, s);
   hipMemsetAsync(d.vis, 0, c.scap / 8, s);
   hipMemsetAsync(d.front[0], 0, c.scap, s);
@@ -602,7 +598,8 @@ int crgc_merge_undo(crgc_graph *h, const crgc_undo_log *log) {
 // first chunk is as deep as the previous trace, so a steady-state wakeup needs
 // one host synchronisation.
 static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64_t top,
-                      uint64_t *levels, uint64_t *roots, double *kernel_ms, uint64_t *launches) {
+                      uint64_t *levels, uint64_t *roots, double *kernel_ms, uint64_t *launches,
+                      uint64_t *depth = nullptr) {
   LevelArgs la{};
   la.location = location;
   // Tuning switch for A/B runs (results are identical either way).
@@ -621,6 +618,17 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   // Test hooks: absolute thresholds (0 disables sparse levels entirely).
   if (const char *m = getenv("CRGC_PULL_THRESH")) la.pull_thresh = strtoull(m, nullptr, 10);
   if (const char *m = getenv("CRGC_SPARSE_THRESH")) la.sparse_thresh = (uint32_t)strtoul(m, nullptr, 10);
+  // Narrow frontiers: one workgroup finishes the mark (k_tail).
+  la.flags |= LV_TAIL;
+  la.tail_start = 8192;
+  la.tail_max = 32768;
+  if (const char *m = getenv("CRGC_TAIL")) {
+    if (!atoi(m)) la.flags &= ~LV_TAIL;
+  }
+  if (const char *m = getenv("CRGC_TAIL_START")) la.tail_start = (uint32_t)strtoul(m, nullptr, 10);
+  if (const char *m = getenv("CRGC_TAIL_MAX")) la.tail_max = (uint32_t)strtoul(m, nullptr, 10);
+  la.tail_start = std::min<uint32_t>(la.tail_start, TAIL_QCAP);
+  la.tail_max = std::min<uint32_t>(std::max(la.tail_max, 1u), TAIL_QCAP);
   size_t nl = 0;
   auto launch = [&](int level, bool rootk) -> hipError_t {
     if (h->lvl_ev.size() < 2 * (nl + 1)) {
@@ -644,6 +652,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   int L = 1;
   int chunk = (int)std::min<uint64_t>(std::max<uint64_t>(4, h->last_levels + 1), 512);
   std::vector<unsigned long long> ring(LEVEL_RING);
+  unsigned long long tail[3] = {0, 0, 0};
   for (;;) {
     for (int k = 0; k < chunk; ++k) HIP_TRY(launch(L + k, false));
     // counts of levels L-1 .. L+chunk-1
@@ -655,11 +664,21 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
                              hipMemcpyDeviceToHost, h->stream));
       lv += cnt;
     }
+    HIP_TRY(hipMemcpyAsync(tail, (char *)h->ctr + CTR_OFF(tail_state), 24, hipMemcpyDeviceToHost,
+                           h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     if (first == 0) *roots = ring[0];
+    if (tail[0] == TAIL_BAILED) {  // k_tail handed a wide frontier back: resume there
+      HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(tail_state), 0, 8, h->stream));
+      L = (int)tail[1];
+      continue;
+    }
     for (int lv = first; lv <= last; ++lv) {
-      if (ring[lv % LEVEL_RING] == 0) {
-        *levels = (uint64_t)lv;  // levels 0 .. lv-1 were non-empty
+      if (tail[0] == TAIL_DONE || ring[lv % LEVEL_RING] == 0) {
+        // levels 0 .. lv-1 were non-empty
+        *levels = tail[0] == TAIL_DONE ? (uint64_t)tail[1] : (uint64_t)lv;
+        // level launches that did work: the first chunk of the next trace
+        if (depth) *depth = tail[0] == TAIL_DONE ? (uint64_t)tail[2] + 1 : (uint64_t)lv;
         double ms = 0;
         const bool log = getenv("CRGC_LEVEL_LOG") != nullptr;
         for (size_t i = 0; i < nl; ++i) {
@@ -728,9 +747,9 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   // exact value from the device counters, so no synchronisation is needed here.
   const uint64_t top = h->slot_top + h->ids_since;
   reset_trace_counters(h);
-  uint64_t levels = 0, roots = 0, launches = 0;
+  uint64_t levels = 0, roots = 0, launches = 0, depth = 0;
   double mark_ms = 0;
-  if (int rc = run_levels(h, false, 0, top, &levels, &roots, &mark_ms, &launches)) return rc;
+  if (int rc = run_levels(h, false, 0, top, &levels, &roots, &mark_ms, &launches, &depth)) return rc;
   HIP_TRY(hipEventRecord(h->ev[1], h->stream));
   HIP_TRY(launch_trace_stats(h->g.d, h->stream));
   HIP_TRY(launch_sweep(h->g.d, should_kill ? 1 : 0, top, h->stream));
@@ -757,7 +776,7 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   h->live = c.n_live;
   h->inserted_at_trace = c.inserted;
   h->have_last = true;
-  h->last_levels = levels;
+  h->last_levels = depth;
   const int rc = copy_lists(h, out);
   st.ms_total =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -122,11 +122,15 @@ struct EdgeArgs {
 constexpr uint32_t LV_CHECK_BEFORE_STORE = 1;  // read the candidate byte before storing it
 constexpr uint32_t LV_BITMAP_FRONT = 2;        // candidates as a bitmap set by atomicOr
 constexpr uint32_t LV_PULL = 4;                // dense levels scan in-candidates (pull)
+constexpr uint32_t LV_TAIL = 8;                // narrow frontiers go to one workgroup (k_tail)
+constexpr uint32_t LV_INVESTIGATE = 16;        // set by launch_level: no supervisor edges
 
 struct LevelArgs {
   int level;
   uint32_t sparse_thresh;
   uint64_t pull_thresh;    // a level pulls when the previous frontier had >= this many shadows
+  uint32_t tail_start;     // k_tail takes over after a level of <= this many shadows
+  uint32_t tail_max;       // ... whose candidates number <= this, and bails above it
   uint32_t frontier_grid;  // workgroups of k_frontier (set by launch_level)
   uint32_t flags;          // LV_*
   uint16_t location;

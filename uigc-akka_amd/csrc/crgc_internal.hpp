@@ -2,7 +2,7 @@
 // shared by the merge, trace and rebuild kernels (gfx950 / CDNA4 only).
 //
 // Layout (DESIGN.md "Data layout in HBM"):
-//   id table   hkey[u64] / hval[u32]   open addressing, linear probing:
+//   id table   htab[{key u64, slot u32}] 16-B buckets, linear probing:
 //                                      actor id -> dense vertex slot
 //   vertex SoA, indexed by slot         (ShadowGraph.shadowMap + Shadow fields)
 //     vid[u64]    actor id of the slot
@@ -12,7 +12,8 @@
 //     adj[uint2]  {offset, degree} of the slot's out-edge segment in the pool
 //     ecap[u32]   segment capacity
 //   edge pool   pool[u64] = target slot (lo 32) | count (hi 32): Shadow.outgoing
-//   edge table  ekey[u64] = owner<<32|target -> eval[u32] index inside segment
+//   edge table  etab[{key u64 = owner<<32|target, val u32 = index inside the
+//               segment, rev u32 = index of its reverse candidate}] 16-B buckets
 //   trace state vis bitmap + two frontier byte maps + two block-dirty maps
 #pragma once
 
@@ -49,6 +50,8 @@ constexpr int WAVE = 64;
 constexpr int BLK_SLOTS = 2048;          // slots per wave-block (64 lanes x 32)
 constexpr int LEVEL_RING = 4096;         // ring of per-level frontier counts
 constexpr int STAT_WG = 2048;            // max workgroups of the level / sweep kernels
+constexpr int TAIL_QCAP = 1 << 16;       // narrow-frontier queue capacity (per buffer)
+constexpr unsigned long long TAIL_DONE = 1, TAIL_BAILED = 2;
 
 struct Counters {
   unsigned long long inserted;       // vertices created (totalActorsSeen)
@@ -72,16 +75,35 @@ struct Counters {
   unsigned long long n_live;
   unsigned long long npe;
   unsigned long long n_out;          // generic output counter (local roots)
+  unsigned long long tail_state;     // narrow-frontier kernel: 0 idle, TAIL_DONE, TAIL_BAILED
+  unsigned long long tail_level;     // DONE: levels traced; BAILED: level to resume at
+  unsigned long long tail_from;      // level at which k_tail took over
+  unsigned long long tl_n;           // sparse level: frontier slots listed in tq (k_frontier)
   unsigned long long qn[2], qh[2];   // per-level edge-range queue lengths
   unsigned long long ring[LEVEL_RING];
 };
+
+// Hash buckets: key and value share one 16-B line, so a probe is one load.
+struct alignas(16) IdBucket {
+  uint64_t key;  // actor id, KEY_EMPTY or KEY_TOMB
+  uint32_t val;  // dense slot, VAL_PENDING while the inserting wave allocates it
+  uint32_t pad;
+};
+struct alignas(16) EdgeBucket {
+  uint64_t key;  // owner << 32 | target
+  uint32_t val;  // entry index in the owner's segment (EVAL_NEW | rank during a merge)
+  uint32_t rev;  // entry index in the target's reverse-candidate segment
+};
+
+__device__ inline uint64_t bucket_key(const uint4 &b) { return (uint64_t)b.x | ((uint64_t)b.y << 32); }
+template <class B>
+__device__ inline uint4 load_bucket(const B *p) { return *reinterpret_cast<const uint4 *>(p); }
 
 // Everything a kernel needs, passed by value.
 struct DevGraph {
   // id table
   uint64_t hcap, hmask;
-  uint64_t *hkey;
-  uint32_t *hval;
+  IdBucket *htab;
   // vertex SoA
   uint64_t scap;  // slot capacity (multiple of BLK_SLOTS)
   uint64_t *vid;
@@ -102,13 +124,12 @@ struct DevGraph {
   uint32_t *rpool;           // owner slot | RC_POS while count(owner -> slot) > 0
   uint64_t rpcap;
   uint32_t *fx;              // expandable frontier bitmap (frontier & !halted)
+  uint32_t *tq;              // narrow-frontier queues, 2 x TAIL_QCAP slots
   // edges
   uint64_t pcap;
   uint64_t *pool;
   uint64_t ecap_tab, emask;
-  uint64_t *ekey;
-  uint32_t *eval;
-  uint32_t *erev;   // index of the edge's candidate entry in the target's reverse segment
+  EdgeBucket *etab;
   int32_t *edelta;
   // trace
   uint32_t *vis;
@@ -206,18 +227,20 @@ __device__ inline int id_probe(const DevGraph &g, uint64_t id, uint64_t &bucket,
                                uint32_t &slot) {
   uint64_t h = mix64(id) & g.hmask;
   for (uint64_t probe = 0; probe < g.hcap; ++probe) {
-    uint64_t k = g.hkey[h];
+    const uint4 b = load_bucket(&g.htab[h]);
+    uint64_t k = bucket_key(b);
+    uint32_t v = b.z;
     if (k == KEY_EMPTY) {
-      k = atomicCAS((unsigned long long *)&g.hkey[h], (unsigned long long)KEY_EMPTY,
+      k = atomicCAS((unsigned long long *)&g.htab[h].key, (unsigned long long)KEY_EMPTY,
                     (unsigned long long)id);
       if (k == KEY_EMPTY) {
         bucket = h;
         return RS_INSERTED;
       }
+      v = g.htab[h].val;  // someone else's fresh key: its slot may still be pending
     }
     if (k == id) {
       bucket = h;
-      uint32_t v = g.hval[h];
       if (v != VAL_PENDING) {
         slot = v;
         return RS_FOUND;
@@ -246,12 +269,12 @@ __device__ inline uint32_t id_settle(const DevGraph &g, uint64_t id, uint64_t bu
       g.vid[s] = id;
       g.flags[s] = FL_ALIVE;
     }
-    atomicExch(&g.hval[bucket], slot);
+    atomicExch(&g.htab[bucket].val, slot);
   }
   if (state == RS_PENDING) {
     slot = SLOT_INVALID;
     for (uint32_t spin = 0; spin < (1u << 24); ++spin) {
-      uint32_t v = atomicOr(&g.hval[bucket], 0u);
+      uint32_t v = atomicOr(&g.htab[bucket].val, 0u);
       if (v != VAL_PENDING) {
         slot = v;
         break;
@@ -276,10 +299,11 @@ __device__ inline uint32_t id_resolve(const DevGraph &g, bool has, uint64_t id) 
 __device__ inline uint32_t id_find(const DevGraph &g, uint64_t id, uint64_t *bucket = nullptr) {
   uint64_t h = mix64(id) & g.hmask;
   for (uint64_t probe = 0; probe < g.hcap; ++probe) {
-    uint64_t k = g.hkey[h];
+    const uint4 b = load_bucket(&g.htab[h]);
+    const uint64_t k = bucket_key(b);
     if (k == id) {
       if (bucket) *bucket = h;
-      return g.hval[h];
+      return b.z;
     }
     if (k == KEY_EMPTY) return SLOT_NONE;
     h = (h + 1) & g.hmask;
@@ -292,19 +316,25 @@ __device__ inline uint64_t edge_key(uint32_t owner, uint32_t target) {
   return ((uint64_t)owner << 32) | target;
 }
 
-// Returns the bucket of `key`; *inserted tells whether this thread created it.
-__device__ inline uint64_t edge_find_or_insert(const DevGraph &g, uint64_t key, bool *inserted) {
+// Returns the bucket of `key`; *inserted tells whether this thread created it,
+// *val is the bucket's value as loaded (a key created during the current merge
+// reads as EVAL_NEW | rank, or as the all-ones fill before its rank is stored).
+__device__ inline uint64_t edge_find_or_insert(const DevGraph &g, uint64_t key, bool *inserted,
+                                               uint32_t *val) {
   uint64_t h = mix64(key) & g.emask;
   *inserted = false;
   for (uint64_t probe = 0; probe < g.ecap_tab; ++probe) {
-    uint64_t k = g.ekey[h];
+    const uint4 b = load_bucket(&g.etab[h]);
+    uint64_t k = bucket_key(b);
+    *val = b.z;
     if (k == KEY_EMPTY) {
-      k = atomicCAS((unsigned long long *)&g.ekey[h], (unsigned long long)KEY_EMPTY,
+      k = atomicCAS((unsigned long long *)&g.etab[h].key, (unsigned long long)KEY_EMPTY,
                     (unsigned long long)key);
       if (k == KEY_EMPTY) {
         *inserted = true;
         return h;
       }
+      *val = g.etab[h].val;
     }
     if (k == key) return h;
     h = (h + 1) & g.emask;
@@ -319,8 +349,9 @@ __device__ inline uint32_t edge_find(const DevGraph &g, uint32_t owner, uint32_t
   const uint64_t key = edge_key(owner, target);
   uint64_t h = mix64(key) & g.emask;
   for (uint64_t probe = 0; probe < g.ecap_tab; ++probe) {
-    const uint64_t k = g.ekey[h];
-    if (k == key) return g.eval[h];
+    const uint4 b = load_bucket(&g.etab[h]);
+    const uint64_t k = bucket_key(b);
+    if (k == key) return b.z;
     if (k == KEY_EMPTY) break;
     h = (h + 1) & g.emask;
   }

@@ -331,18 +331,18 @@ __global__ __launch_bounds__(256) void k_edge_apply(DevGraph g, EdgeArgs a) {
     bool active = valid && d != 0 && vs(o) && vs(t);
     bool ins = false, flip = false;
     uint64_t b = 0;
+    uint32_t v = 0;
     if (active) {
-      b = edge_find_or_insert(g, edge_key(o, t), &ins);
+      b = edge_find_or_insert(g, edge_key(o, t), &ins, &v);
       if (b == KEY_EMPTY) active = ins = false;
     }
     uint32_t rank = 0, rrank = 0;
     if (ins) {
       rank = atomicAdd(&g.enew[o], 1u);
       rrank = atomicAdd(&g.rnew[t], 1u);
-      g.eval[b] = EVAL_NEW | rank;
+      g.etab[b].val = EVAL_NEW | rank;
       atomicAdd(&g.edelta[b], d);
     } else if (active) {
-      const uint32_t v = g.eval[b];
       if (v & EVAL_NEW) {
         atomicAdd(&g.edelta[b], d);
       } else {
@@ -454,20 +454,21 @@ __global__ __launch_bounds__(256) void k_edge_append(DevGraph g, EdgeArgs a) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
     const uint64_t b = a.newlist[i];
-    const uint64_t key = g.ekey[b];
+    const uint4 bk = load_bucket(&g.etab[b]);
+    const uint64_t key = bucket_key(bk);
     const uint32_t o = (uint32_t)(key >> 32), t = (uint32_t)key;
-    const uint32_t rank = g.eval[b] & ~EVAL_NEW;
+    const uint32_t rank = bk.z & ~EVAL_NEW;
     const uint2 ad = g.adj[o];
     const uint32_t idx = ad.y + rank;
     if (idx >= g.ecap[o]) continue;  // relocation failed: ERR_POOL_FULL already set
     const int32_t d = g.edelta[b];
     g.pool[(uint64_t)ad.x + idx] = pack_edge(t, d);
-    g.eval[b] = idx;
+    g.etab[b].val = idx;
     g.edelta[b] = 0;
     if (d != 0) atomicAdd(&g.nzdeg[o], 1u);
     const uint2 rd = g.radj[t];
     const uint32_t ridx = rd.y + a.rrank[i];
-    g.erev[b] = ridx;
+    g.etab[b].rev = ridx;
     if (ridx < g.rcap[t]) g.rpool[(uint64_t)rd.x + ridx] = o | (d > 0 ? RC_POS : 0u);
   }
 }
@@ -479,10 +480,11 @@ __global__ __launch_bounds__(256) void k_edge_flip(DevGraph g, EdgeArgs a) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
     const uint64_t b = a.flips[i];
-    const uint64_t key = g.ekey[b];
+    const uint4 bk = load_bucket(&g.etab[b]);
+    const uint64_t key = bucket_key(bk);
     const uint32_t o = (uint32_t)(key >> 32), t = (uint32_t)key;
-    const int32_t cnt = edge_count(g.pool[(uint64_t)g.adj[o].x + g.eval[b]]);
-    const uint32_t r = g.erev[b];
+    const int32_t cnt = edge_count(g.pool[(uint64_t)g.adj[o].x + bk.z]);
+    const uint32_t r = bk.w;
     if (r < g.radj[t].y) g.rpool[(uint64_t)g.radj[t].x + r] = o | (cnt > 0 ? RC_POS : 0u);
   }
 }

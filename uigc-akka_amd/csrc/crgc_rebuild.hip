@@ -41,9 +41,9 @@ __global__ __launch_bounds__(256) void k_rb_vertices(DevGraph src, uint64_t src_
     dst.flags[ns] = src.flags[v];
     uint64_t h = mix64(id) & dst.hmask;
     for (uint64_t p = 0; p < dst.hcap; ++p) {
-      if (atomicCAS((unsigned long long *)&dst.hkey[h], (unsigned long long)KEY_EMPTY,
+      if (atomicCAS((unsigned long long *)&dst.htab[h].key, (unsigned long long)KEY_EMPTY,
                     (unsigned long long)id) == KEY_EMPTY) {
-        dst.hval[h] = (uint32_t)ns;
+        dst.htab[h].val = (uint32_t)ns;
         break;
       }
       h = (h + 1) & dst.hmask;
@@ -92,9 +92,9 @@ __global__ __launch_bounds__(256) void k_rb_edges(DevGraph src, uint64_t src_top
           const uint64_t key = edge_key(ns, nt);
           uint64_t h = mix64(key) & dst.emask;
           for (uint64_t p = 0; p < dst.ecap_tab; ++p) {
-            if (atomicCAS((unsigned long long *)&dst.ekey[h], (unsigned long long)KEY_EMPTY,
+            if (atomicCAS((unsigned long long *)&dst.etab[h].key, (unsigned long long)KEY_EMPTY,
                           (unsigned long long)key) == KEY_EMPTY) {
-              dst.eval[h] = kept;
+              dst.etab[h].val = kept;
               break;
             }
             h = (h + 1) & dst.emask;
@@ -230,8 +230,8 @@ __global__ __launch_bounds__(256) void k_rb_rfill(DevGraph dst) {
       // the edge's bucket, for its candidate index
       const uint64_t key = edge_key((uint32_t)o, t);
       uint64_t hb = mix64(key) & dst.emask;
-      for (uint64_t p = 0; p < dst.ecap_tab && dst.ekey[hb] != key; ++p) hb = (hb + 1) & dst.emask;
-      if (dst.ekey[hb] == key) dst.erev[hb] = pos;
+      for (uint64_t p = 0; p < dst.ecap_tab && dst.etab[hb].key != key; ++p) hb = (hb + 1) & dst.emask;
+      if (dst.etab[hb].key == key) dst.etab[hb].rev = pos;
     }
   }
 }

@@ -87,6 +87,7 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
   __shared__ uint32_t s_front[4][BLK_SLOTS];
   Counters *c = g.ctr;
   const int L = a.level;
+  if (c->tail_state) return;  // k_tail finished the mark (or bailed to a later level)
   if (blockIdx.x == 0 && threadIdx.x == 0) c->ring[(L + 1) % LEVEL_RING] = 0;
   uint64_t *stat = g.blkstat + (uint64_t)blockIdx.x * 4;
   if (!ROOTS && c->ring[(L - 1) % LEVEL_RING] == 0) {  // previous level was empty
@@ -109,6 +110,7 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
   const uint32_t tag = (uint32_t)(L + 1) << 12;
   const bool bitmode = a.flags & LV_BITMAP_FRONT;
   const bool pull = !ROOTS && pull_level(c, L, a);
+  const bool listing = sp_cur && (a.flags & LV_TAIL);
   uint32_t n_front = 0, n_sup = 0, n_edges = 0;
 
   for (uint32_t blk = gw; blk < nblk; blk += nw) {
@@ -187,6 +189,13 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
     }
     n_front += cnt;
     wave_lds_fence();
+    if (listing && total) {  // sparse level: list the frontier for k_tail
+      unsigned long long lb = 0;
+      if (lane == 0) lb = atomicAdd(&c->tl_n, (unsigned long long)total);
+      lb = __shfl(lb, 0);
+      for (uint32_t i = lane; i < total; i += 64)
+        if (lb + i < TAIL_QCAP) g.tq[lb + i] = s_front[wv][i];
+    }
 
     // Frontier shadows -> supervisor marks + edge ranges (push levels).
     uint32_t nlight = 0;
@@ -255,6 +264,7 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   __shared__ uint32_t s_off[4][64];
   Counters *c = g.ctr;
   const int L = a.level;
+  if (c->tail_state) return;
   if (L > 0 && c->ring[(L - 1) % LEVEL_RING] == 0) return;  // nothing was found this level
   const uint64_t nh = min(c->qh[L & 1], (unsigned long long)g.qh_cap);
   if (blockIdx.x == 0) {
@@ -289,50 +299,45 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   if (pull_level(c, L, a)) {
     // Pull: each unmarked, not-yet-found shadow looks for an expandable
     // frontier shadow among its in-candidates whose edge to it has a
-    // positive count, and stops at the first.  A wave owns its block's bytes.
-    for (uint64_t blk = gw; blk < nblk; blk += nw) {
-      const uint64_t base = blk * BLK_SLOTS + (uint64_t)lane * 32;
-      const uint32_t word = g.vis[blk * 64 + lane];
-      const uint4 f4[2] = {*(const uint4 *)(g.flags + base), *(const uint4 *)(g.flags + base + 16)};
-      const uint8_t *fb = (const uint8_t *)f4;
-      uint4 *fp = (uint4 *)(Fn + base);
-      const uint4 x0 = fp[0], x1 = fp[1];
-      uint32_t xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-      uint32_t un = 0;
+    // positive count (RC_POS), and stops at the first.  A thread owns 4
+    // consecutive slots (their candidate bytes are one u32), so loads of
+    // flags / bytes / radj are coalesced across the wave.
+    const uint64_t nq = (c->slot_top + 3) / 4;
+    const uint64_t gs = (uint64_t)gridDim.x * 256;
+    for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += gs) {
+      const uint64_t v0 = q * 4;
+      const uint32_t fl = *(const uint32_t *)(g.flags + v0);
+      const uint32_t cand = *(const uint32_t *)(Fn + v0);
+      const uint32_t vb = (g.vis[v0 >> 5] >> (v0 & 31)) & 0xFu;
+      uint32_t todo = 0;
 #pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        const bool cand = (xs[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-        un |= ((fb[j] & FL_ALIVE) && !cand) ? (1u << j) : 0u;
-      }
-      un &= ~word;
+      for (int j = 0; j < 4; ++j)
+        todo |= (((fl >> (8 * j)) & FL_ALIVE) && !((cand >> (8 * j)) & 0xFFu) && !((vb >> j) & 1u))
+                    ? (1u << j) : 0u;
+      if (!todo) continue;
+      const uint4 r01 = *(const uint4 *)(g.radj + v0);
+      const uint4 r23 = *(const uint4 *)(g.radj + v0 + 2);
+      const uint32_t ro[4] = {r01.x, r01.z, r23.x, r23.z};
+      const uint32_t rl[4] = {r01.y, r01.w, r23.y, r23.w};
       uint32_t found = 0;
-      while (un) {
-        const int j = __ffs(un) - 1;
-        un &= un - 1;
-        const uint32_t v = (uint32_t)(base + j);
-        const uint2 rd = g.radj[v];
+      for (int j = 0; j < 4; ++j) {
+        if (!((todo >> j) & 1u)) continue;
+        const uint32_t *rp = g.rpool + ro[j];
+        const uint32_t n = rl[j];
         bool hit = false;
-        for (uint32_t i = 0; i < rd.y && !hit; i += 4) {
+        for (uint32_t i = 0; i < n && !hit; i += 4) {
           uint32_t u[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) u[q] = i + q < rd.y ? g.rpool[rd.x + i + q] : SLOT_NONE;
+          for (int k = 0; k < 4; ++k) u[k] = i + k < n ? rp[i + k] : 0u;  // 0: no RC_POS
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            // a candidate counts only while its edge count is positive (RC_POS)
-            const bool pos = u[q] != SLOT_NONE && (u[q] & RC_POS);
-            const uint32_t s = u[q] & ~RC_POS;
-            if (pos && ((g.fx[s >> 5] >> (s & 31)) & 1u)) hit = true;
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t sl = u[k] & ~RC_POS;
+            if ((u[k] & RC_POS) && ((g.fx[sl >> 5] >> (sl & 31)) & 1u)) hit = true;
           }
         }
-        if (hit) found |= 1u << j;
+        if (hit) found |= 1u << (8 * j);
       }
-      if (found) {
-#pragma unroll
-        for (int j = 0; j < 32; ++j)
-          if ((found >> j) & 1u) xs[j >> 2] |= 1u << (8 * (j & 3));
-        fp[0] = make_uint4(xs[0], xs[1], xs[2], xs[3]);
-        fp[1] = make_uint4(xs[4], xs[5], xs[6], xs[7]);
-      }
+      if (found) *(uint32_t *)(Fn + v0) = cand | found;
     }
     return;
   }
@@ -392,6 +397,172 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// k_tail: one workgroup finishes the mark once a sparse level's frontier is
+// narrow (deep chains and rings, the last levels of a wide trace): rounds over
+// a queue in place of kernel pairs, a claim = atomicOr on `vis`.  It replaces
+// k_expand of the level it starts at (the frontier listed by k_frontier), and
+// hands back to the level kernels when a round discovers more than tail_max
+// shadows: the pending ones become candidate bytes of level L+2.
+// ---------------------------------------------------------------------------
+constexpr int TAIL_THREADS = 1024;
+
+// Exclusive scan over the workgroup; `total` gets the sum.
+__device__ inline uint32_t tail_scan(uint32_t v, uint32_t *s_w, uint32_t &total) {
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const uint32_t incl = wave_incl_scan(v);
+  if (lane == 63) s_w[w] = incl;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const uint32_t x = threadIdx.x < TAIL_THREADS / 64 ? s_w[threadIdx.x] : 0;
+    const uint32_t xi = wave_incl_scan(x);
+    if (threadIdx.x < TAIL_THREADS / 64) s_w[16 + threadIdx.x] = xi - x;
+    if (threadIdx.x == TAIL_THREADS / 64 - 1) s_w[32] = xi;
+  }
+  __syncthreads();
+  total = s_w[32];
+  const uint32_t r = s_w[16 + w] + incl - v;
+  __syncthreads();
+  return r;
+}
+
+// Claim t for the next round; without queue room it becomes a candidate byte
+// of the resume level instead (and the round ends in a bail).
+__device__ inline void tail_claim(const DevGraph &g, uint32_t t, uint32_t *nxt, uint32_t *s_next,
+                                  uint8_t *Fb, uint8_t *Db, int32_t &claims) {
+  const uint32_t bit = 1u << (t & 31);
+  if (g.vis[t >> 5] & bit) return;
+  if (atomicOr(&g.vis[t >> 5], bit) & bit) return;
+  const uint32_t pos = atomicAdd(s_next, 1u);
+  if (pos < TAIL_QCAP) {
+    nxt[pos] = t;
+    ++claims;
+  } else {
+    atomicAnd(&g.vis[t >> 5], ~bit);
+    Fb[t] = 1;
+    Db[t >> 11] = 1;
+  }
+}
+
+__global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) {
+  __shared__ uint32_t s_start[TAIL_THREADS + 1];
+  __shared__ uint32_t s_off[TAIL_THREADS];
+  __shared__ uint32_t s_w[40];
+  __shared__ uint32_t s_next;
+  Counters *c = g.ctr;
+  const int L = a.level;
+  if (c->tail_state) return;
+  const uint64_t n0 = c->tl_n;
+  __syncthreads();
+  if (!(a.flags & LV_TAIL) || n0 == 0 || n0 > a.tail_start) {
+    if (threadIdx.x == 0) c->tl_n = 0;  // declined: the level kernels go on
+    return;
+  }
+  const bool investigate = a.flags & LV_INVESTIGATE;
+  uint8_t *Fn = g.front[(L + 1) & 1];  // k_frontier(L)'s supervisor pushes, redone here
+  uint8_t *Dn = g.dirty[(L + 1) & 1];
+  uint8_t *Fb = g.front[L & 1];        // bail: candidates of level L+2
+  uint8_t *Db = g.dirty[L & 1];
+  uint32_t *cur = g.tq, *nxt = g.tq + TAIL_QCAP;
+  uint32_t n = (uint32_t)n0;
+  uint32_t n_sup = 0, n_edges = 0, rounds = 0;
+  int32_t claims = 0;
+  bool first = true, bailed = false;
+  for (;;) {
+    if (threadIdx.x == 0) s_next = 0;
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < n; c0 += TAIL_THREADS) {
+      const uint32_t i = c0 + threadIdx.x;
+      const bool valid = i < n;
+      const uint32_t v = valid ? cur[i] : 0;
+      const uint8_t f = valid ? g.flags[v] : 0;
+      const bool expand = valid && !(f & FL_HALTED);  // (:226-229)
+      uint2 ad = make_uint2(0, 0);
+      if (expand) {
+        ad = g.adj[v];
+        if (!first) n_edges += g.nzdeg[v];  // level L's were counted by k_frontier
+        if (!investigate) {
+          const uint32_t s = g.sup[v];  // (:258-267)
+          if (s < 0xFFFFFFF0u) {
+            if (first) {
+              Fn[s] = 0;
+              Dn[s >> 11] = 0;
+            } else {
+              ++n_sup;
+            }
+            tail_claim(g, s, nxt, &s_next, Fb, Db, claims);
+          }
+        }
+      }
+      uint32_t total;
+      const uint32_t st = tail_scan(ad.y, s_w, total);
+      s_start[threadIdx.x] = st;
+      s_off[threadIdx.x] = ad.x;
+      if (threadIdx.x == 0) s_start[TAIL_THREADS] = total;
+      __syncthreads();
+      for (uint32_t e = threadIdx.x; e < total; e += TAIL_THREADS) {
+        int lo = 0, hi = TAIL_THREADS - 1;  // last item whose start <= e
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (s_start[mid] <= e) lo = mid;
+          else hi = mid - 1;
+        }
+        const uint64_t ed = g.pool[(uint64_t)s_off[lo] + (e - s_start[lo])];
+        if (edge_count(ed) > 0) tail_claim(g, edge_target(ed), nxt, &s_next, Fb, Db, claims);
+      }
+      __syncthreads();
+    }
+    __syncthreads();
+    const uint32_t nn = s_next;
+    first = false;
+    ++rounds;
+    if (nn == 0) break;
+    if (nn > a.tail_max) {
+      // hand the pending shadows to the level kernels as level L+2 candidates
+      const uint32_t m = min(nn, (uint32_t)TAIL_QCAP);
+      for (uint32_t i = threadIdx.x; i < m; i += TAIL_THREADS) {
+        const uint32_t t = nxt[i];
+        atomicAnd(&g.vis[t >> 5], ~(1u << (t & 31)));
+        Fb[t] = 1;
+        Db[t >> 11] = 1;
+      }
+      bailed = true;
+      n = m;
+      break;
+    }
+    uint32_t *tmp = cur;
+    cur = nxt;
+    nxt = tmp;
+    n = nn;
+    __syncthreads();
+  }
+  // statistics: claims became marked shadows (k_frontier(L) counted level L)
+  uint32_t tot_claims, tot_sup, tot_edges;
+  tail_scan((uint32_t)claims, s_w, tot_claims);
+  tail_scan(n_sup, s_w, tot_sup);
+  tail_scan(n_edges, s_w, tot_edges);
+  if (threadIdx.x == 0) {
+    const uint64_t marked_new = (uint64_t)tot_claims - (bailed ? n : 0);  // queued claims undone
+    c->ring[L % LEVEL_RING] = n0;
+    c->marked += n0 + marked_new;
+    g.blkstat[STAT_SUP] += tot_sup;
+    g.blkstat[STAT_EDGES] += tot_edges;
+    c->tl_n = 0;
+    c->tail_from = L;
+    if (bailed) {
+      c->ring[L % LEVEL_RING] = 1;  // level L+2 runs sparse over the dirty blocks
+      c->ring[(L + 1) % LEVEL_RING] = n;
+      c->qh[L & 1] = 0;
+      c->tail_level = L + 2;
+      c->tail_state = TAIL_BAILED;
+    } else {
+      c->tail_level = L + rounds;  // levels 0 .. L+rounds-1 were non-empty
+      c->tail_state = TAIL_DONE;
+    }
+  }
+}
+
 int level_grid(uint64_t slot_top) {
   const uint64_t blocks = (slot_top + BLK_SLOTS - 1) / BLK_SLOTS;  // wave-blocks
   uint64_t wg = (blocks + 3) / 4;
@@ -405,6 +576,7 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
   LevelArgs a = a0;
   const int grid = level_grid(slot_top);
   a.frontier_grid = grid;
+  if (investigate) a.flags |= LV_INVESTIGATE;
   if (roots && investigate)
     hipLaunchKernelGGL((k_frontier<true, true>), dim3(grid), dim3(256), 0, s, g, a);
   else if (roots)
@@ -413,6 +585,8 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
     hipLaunchKernelGGL((k_frontier<false, true>), dim3(grid), dim3(256), 0, s, g, a);
   else
     hipLaunchKernelGGL((k_frontier<false, false>), dim3(grid), dim3(256), 0, s, g, a);
+  if (!roots && (a.flags & LV_TAIL))
+    hipLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, g, a);
   hipLaunchKernelGGL(k_expand, dim3(STAT_WG), dim3(256), 0, s, g, a);  // 8 WGs of 4 waves per CU
   return hipGetLastError();
 }
@@ -593,7 +767,7 @@ __global__ __launch_bounds__(256) void k_sweep_gather(DevGraph g) {
       if (commit) {
         uint64_t bucket = KEY_EMPTY;
         id_find(g, id, &bucket);
-        if (bucket != KEY_EMPTY) g.hkey[bucket] = KEY_TOMB;
+        if (bucket != KEY_EMPTY) g.htab[bucket].key = KEY_TOMB;
         g.flags[v] = 0;
       }
     }
