@@ -4,7 +4,7 @@ Variants are selected by environment switches read per trace (CRGC_* in
 crgc_api.hip); results must be identical, only timings differ.
 
     python tools/ab_trace.py --actors 10000000 --edges 100000000 --rounds 8 \
-        --variant CRGC_MARK_CHECK=0 --variant CRGC_MARK_CHECK=1
+        --variant CRGC_PULL=0 --variant CRGC_PULL=1,CRGC_PULL_DIV=32
 """
 import argparse
 import json

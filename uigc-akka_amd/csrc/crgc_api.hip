@@ -45,7 +45,7 @@ void free_arrays(Arrays &a) {
                 d.enew, d.pool, d.etab, d.edelta, d.vis, d.front[0], d.front[1],
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill, d.fbits[0], d.fbits[1],
-                d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.fx, d.tq};
+                d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.fx, d.tq, d.tl_buf, d.tl_tag};
   for (void *p : ps)
     if (p) hipFree(p);
   a.allocated = false;
@@ -114,6 +114,8 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s) 
   A(dmalloc(&d.rpool, d.rpcap));
   A(dmalloc(&d.fx, c.scap / 32));
   A(dmalloc(&d.tq, 2 * (uint64_t)TAIL_QCAP));
+  A(dmalloc(&d.tl_buf, c.scap));
+  A(dmalloc(&d.tl_tag, c.scap / BLK_SLOTS));
 #undef A
   a.allocated = true;
   // Default state of every unused slot / bucket.
@@ -614,9 +616,13 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
     if (!atoi(m)) la.flags &= ~LV_PULL;
   }
   if (const char *m = getenv("CRGC_PULL_DIV")) pull_div = std::max<uint64_t>(1, strtoull(m, nullptr, 10));
-  la.pull_thresh = std::max<uint64_t>(1, top / pull_div);
+  la.pull_div = (uint32_t)pull_div;  // against the exact slot count, on the device
+  la.pull_thresh = 0;
   // Test hooks: absolute thresholds (0 disables sparse levels entirely).
-  if (const char *m = getenv("CRGC_PULL_THRESH")) la.pull_thresh = strtoull(m, nullptr, 10);
+  if (const char *m = getenv("CRGC_PULL_THRESH")) {
+    la.pull_thresh = strtoull(m, nullptr, 10);
+    la.pull_div = 0;
+  }
   if (const char *m = getenv("CRGC_SPARSE_THRESH")) la.sparse_thresh = (uint32_t)strtoul(m, nullptr, 10);
   // Narrow frontiers: one workgroup finishes the mark (k_tail).
   la.flags |= LV_TAIL;
@@ -689,7 +695,8 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
             fprintf(stderr, "[crgc] level %zu frontier %llu  %.1f us%s\n", i,
                     i <= (size_t)last ? ring[i % LEVEL_RING] : 0ull, t * 1e3,
                     (la.flags & LV_PULL) && i >= 1 && i <= (size_t)last &&
-                            ring[(i - 1) % LEVEL_RING] >= la.pull_thresh
+                            ring[(i - 1) % LEVEL_RING] * std::max<uint64_t>(la.pull_div, 1) >=
+                                (la.pull_div ? h->slot_top : la.pull_thresh)
                         ? " (pull?)"
                         : "");
         }
@@ -711,6 +718,7 @@ static void reset_trace_counters(crgc_graph *h) {
   const uint64_t top = h->slot_top + h->ids_since;
   hipMemsetAsync(h->g.d.blkstat, 0, (size_t)STAT_WG * 4 * 8, h->stream);
   hipMemsetAsync(h->g.d.qn_tag, 0, h->g.caps.scap / BLK_SLOTS * 4, h->stream);
+  hipMemsetAsync(h->g.d.tl_tag, 0, h->g.caps.scap / BLK_SLOTS * 4, h->stream);
   hipMemsetAsync(h->g.d.vis, 0, round_up(std::min<uint64_t>(top, h->g.caps.scap), BLK_SLOTS) / 8,
                  h->stream);
 }

@@ -124,11 +124,13 @@ constexpr uint32_t LV_BITMAP_FRONT = 2;        // candidates as a bitmap set by 
 constexpr uint32_t LV_PULL = 4;                // dense levels scan in-candidates (pull)
 constexpr uint32_t LV_TAIL = 8;                // narrow frontiers go to one workgroup (k_tail)
 constexpr uint32_t LV_INVESTIGATE = 16;        // set by launch_level: no supervisor edges
+constexpr uint32_t LV_ROOTS = 32;              // set by launch_level: the pseudo-root level
 
 struct LevelArgs {
   int level;
   uint32_t sparse_thresh;
-  uint64_t pull_thresh;    // a level pulls when the previous frontier had >= this many shadows
+  uint64_t pull_thresh;    // pull_div == 0: a level pulls after a frontier of >= this many shadows
+  uint32_t pull_div;       // else: after a frontier of >= slot_top / pull_div shadows
   uint32_t tail_start;     // k_tail takes over after a level of <= this many shadows
   uint32_t tail_max;       // ... whose candidates number <= this, and bails above it
   uint32_t frontier_grid;  // workgroups of k_frontier (set by launch_level)

@@ -78,7 +78,6 @@ struct Counters {
   unsigned long long tail_state;     // narrow-frontier kernel: 0 idle, TAIL_DONE, TAIL_BAILED
   unsigned long long tail_level;     // DONE: levels traced; BAILED: level to resume at
   unsigned long long tail_from;      // level at which k_tail took over
-  unsigned long long tl_n;           // sparse level: frontier slots listed in tq (k_frontier)
   unsigned long long qn[2], qh[2];   // per-level edge-range queue lengths
   unsigned long long ring[LEVEL_RING];
 };
@@ -125,6 +124,8 @@ struct DevGraph {
   uint64_t rpcap;
   uint32_t *fx;              // expandable frontier bitmap (frontier & !halted)
   uint32_t *tq;              // narrow-frontier queues, 2 x TAIL_QCAP slots
+  uint32_t *tl_buf;          // per-block regions: a listed level's frontier slots
+  uint32_t *tl_tag;          // per block: (level+1) << 12 | listed slots
   // edges
   uint64_t pcap;
   uint64_t *pool;

@@ -36,7 +36,15 @@ __device__ inline bool sparse_level(const Counters *c, int L, uint32_t thr) {
 __device__ inline bool pull_level(const Counters *c, int L, const LevelArgs &a) {
   if (!(a.flags & LV_PULL) || (a.flags & LV_BITMAP_FRONT) || L < 1) return false;
   if (sparse_level(c, L, a.sparse_thresh) || sparse_level(c, L + 1, a.sparse_thresh)) return false;
-  return c->ring[(L - 1) % LEVEL_RING] >= a.pull_thresh;
+  const uint64_t prev = c->ring[(L - 1) % LEVEL_RING];
+  return a.pull_div ? prev * a.pull_div >= c->slot_top : prev >= a.pull_thresh;
+}
+
+// Whether level L lists its frontier for k_tail (same answer in k_frontier and
+// k_tail): the level may be narrow (sparse, or after a narrow level).
+__device__ inline bool listing_level(const Counters *c, int L, const LevelArgs &a) {
+  if (!(a.flags & LV_TAIL) || (a.flags & LV_ROOTS) || L < 1) return false;
+  return sparse_level(c, L, a.sparse_thresh) || c->ring[(L - 1) % LEVEL_RING] <= a.tail_max;
 }
 
 __device__ inline void wave_lds_fence() {
@@ -110,7 +118,7 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
   const uint32_t tag = (uint32_t)(L + 1) << 12;
   const bool bitmode = a.flags & LV_BITMAP_FRONT;
   const bool pull = !ROOTS && pull_level(c, L, a);
-  const bool listing = sp_cur && (a.flags & LV_TAIL);
+  const bool listing = !ROOTS && listing_level(c, L, a);
   uint32_t n_front = 0, n_sup = 0, n_edges = 0;
 
   for (uint32_t blk = gw; blk < nblk; blk += nw) {
@@ -189,12 +197,9 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
     }
     n_front += cnt;
     wave_lds_fence();
-    if (listing && total) {  // sparse level: list the frontier for k_tail
-      unsigned long long lb = 0;
-      if (lane == 0) lb = atomicAdd(&c->tl_n, (unsigned long long)total);
-      lb = __shfl(lb, 0);
-      for (uint32_t i = lane; i < total; i += 64)
-        if (lb + i < TAIL_QCAP) g.tq[lb + i] = s_front[wv][i];
+    if (listing && total) {  // into the block's own region: no shared counter
+      for (uint32_t i = lane; i < total; i += 64) g.tl_buf[(uint64_t)blk * BLK_SLOTS + i] = s_front[wv][i];
+      if (lane == 0) g.tl_tag[blk] = tag | total;
     }
 
     // Frontier shadows -> supervisor marks + edge ranges (push levels).
@@ -256,8 +261,7 @@ __device__ inline void expand_edge(const DevGraph &g, uint8_t *Fn, uint8_t *Dn, 
 // ---------------------------------------------------------------------------
 // k_expand: every wave of the grid walks the level's ranges, 64 light ranges
 // per step (degree scan + binary search in LDS assigns edges to lanes) or one
-// hub piece per step, EXP_UNROLL independent edge loads per lane.  Block 0
-// also turns k_frontier's per-workgroup counts into the level count.
+// hub piece per step, EXP_UNROLL independent edge loads per lane.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   __shared__ uint32_t s_start[4][65];
@@ -267,23 +271,6 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   if (c->tail_state) return;
   if (L > 0 && c->ring[(L - 1) % LEVEL_RING] == 0) return;  // nothing was found this level
   const uint64_t nh = min(c->qh[L & 1], (unsigned long long)g.qh_cap);
-  if (blockIdx.x == 0) {
-    // level count = sum of k_frontier's per-workgroup frontier counts
-    uint64_t s = 0;
-    for (uint32_t b = threadIdx.x; b < a.frontier_grid; b += 256) s += g.blkstat[b * 4 + STAT_FRONT];
-    __shared__ uint64_t red[256];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int k = 128; k > 0; k >>= 1) {
-      if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-      c->ring[L % LEVEL_RING] = red[0];
-      c->marked += red[0];
-      c->qh[(L + 1) & 1] = 0;  // next level's hub queue (last read by the previous k_expand)
-    }
-  }
   const bool sp_next = sparse_level(c, L + 1, a.sparse_thresh);
   const bool check = a.flags & LV_CHECK_BEFORE_STORE;
   uint32_t *Fbits = (a.flags & LV_BITMAP_FRONT) ? g.fbits[(L + 1) & 1] : nullptr;
@@ -450,21 +437,52 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
   __shared__ uint32_t s_off[TAIL_THREADS];
   __shared__ uint32_t s_w[40];
   __shared__ uint32_t s_next;
+  __shared__ unsigned long long s_red[TAIL_THREADS];
   Counters *c = g.ctr;
   const int L = a.level;
   if (c->tail_state) return;
-  const uint64_t n0 = c->tl_n;
+  // Level count = sum of k_frontier's per-workgroup frontier counts.
+  unsigned long long part = 0;
+  for (uint32_t b = threadIdx.x; b < a.frontier_grid; b += TAIL_THREADS)
+    part += g.blkstat[b * 4 + STAT_FRONT];
+  s_red[threadIdx.x] = part;
   __syncthreads();
-  if (!(a.flags & LV_TAIL) || n0 == 0 || n0 > a.tail_start) {
-    if (threadIdx.x == 0) c->tl_n = 0;  // declined: the level kernels go on
+  for (int k = TAIL_THREADS / 2; k > 0; k >>= 1) {
+    if (threadIdx.x < k) s_red[threadIdx.x] += s_red[threadIdx.x + k];
+    __syncthreads();
+  }
+  const uint64_t n0 = s_red[0];
+  if (!listing_level(c, L, a) || n0 == 0 || n0 > a.tail_start) {
+    if (threadIdx.x == 0) {  // the level kernels go on
+      c->ring[L % LEVEL_RING] = n0;
+      c->marked += n0;
+      c->qh[(L + 1) & 1] = 0;  // next level's hub queue (last read by k_expand(L-1))
+    }
     return;
+  }
+  // Take over: gather the listed frontier from the per-block regions.
+  uint32_t *cur = g.tq, *nxt = g.tq + TAIL_QCAP;
+  {
+    const uint32_t nblk = (uint32_t)((c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS);
+    const uint32_t want = (uint32_t)(L + 1);
+    uint32_t base = 0;
+    for (uint32_t b0 = 0; b0 < nblk; b0 += TAIL_THREADS) {
+      const uint32_t b = b0 + threadIdx.x;
+      const uint32_t t = b < nblk ? g.tl_tag[b] : 0;
+      const uint32_t cnt = (t >> 12) == want ? (t & 0xFFFu) : 0u;
+      uint32_t tot;
+      const uint32_t off = base + tail_scan(cnt, s_w, tot);
+      for (uint32_t i = 0; i < cnt; ++i)
+        if (off + i < TAIL_QCAP) cur[off + i] = g.tl_buf[(uint64_t)b * BLK_SLOTS + i];
+      base += tot;
+    }
+    __syncthreads();
   }
   const bool investigate = a.flags & LV_INVESTIGATE;
   uint8_t *Fn = g.front[(L + 1) & 1];  // k_frontier(L)'s supervisor pushes, redone here
   uint8_t *Dn = g.dirty[(L + 1) & 1];
   uint8_t *Fb = g.front[L & 1];        // bail: candidates of level L+2
   uint8_t *Db = g.dirty[L & 1];
-  uint32_t *cur = g.tq, *nxt = g.tq + TAIL_QCAP;
   uint32_t n = (uint32_t)n0;
   uint32_t n_sup = 0, n_edges = 0, rounds = 0;
   int32_t claims = 0;
@@ -548,7 +566,6 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
     c->marked += n0 + marked_new;
     g.blkstat[STAT_SUP] += tot_sup;
     g.blkstat[STAT_EDGES] += tot_edges;
-    c->tl_n = 0;
     c->tail_from = L;
     if (bailed) {
       c->ring[L % LEVEL_RING] = 1;  // level L+2 runs sparse over the dirty blocks
@@ -577,6 +594,7 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
   const int grid = level_grid(slot_top);
   a.frontier_grid = grid;
   if (investigate) a.flags |= LV_INVESTIGATE;
+  if (roots) a.flags |= LV_ROOTS;
   if (roots && investigate)
     hipLaunchKernelGGL((k_frontier<true, true>), dim3(grid), dim3(256), 0, s, g, a);
   else if (roots)
@@ -585,8 +603,8 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
     hipLaunchKernelGGL((k_frontier<false, true>), dim3(grid), dim3(256), 0, s, g, a);
   else
     hipLaunchKernelGGL((k_frontier<false, false>), dim3(grid), dim3(256), 0, s, g, a);
-  if (!roots && (a.flags & LV_TAIL))
-    hipLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, g, a);
+  // level controller: the level count, and the narrow-frontier takeover
+  hipLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, g, a);
   hipLaunchKernelGGL(k_expand, dim3(STAT_WG), dim3(256), 0, s, g, a);  // 8 WGs of 4 waves per CU
   return hipGetLastError();
 }
