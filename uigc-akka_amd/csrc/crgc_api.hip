@@ -465,7 +465,9 @@ int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
           ? Carver::need({n * 8, n * 2, n, (n + 1) * 4, C * 8, C * 8, (n + 1) * 4, S * 8,
                           (n + 1) * 4, U * 8, U * 2})
           : 0;
-  const size_t work_bytes = Carver::need({n * 4, n * h->F * 4}) + edge_scratch(max_atoms);
+  const size_t work_bytes =
+      Carver::need({n * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4}) +
+      edge_scratch(max_atoms);
   if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
     return CRGC_E_NOMEM;
   Carver sc(h->stage.ptr), wc(h->work.ptr);
@@ -486,6 +488,9 @@ int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
   a.u_info = stage(h, sc, b->updated_info, U, b->memory);
   a.self_slot = wc.take<uint32_t>(n);
   a.spawn_slot = wc.take<uint32_t>(n * h->F);
+  a.ct_slot = wc.take<uint32_t>(n * h->F);
+  a.co_slot = wc.take<uint32_t>(n * h->F);
+  a.u_slot = wc.take<uint32_t>(n * h->F);
   a.atom_o = wc.take<uint32_t>(max_atoms);
   a.atom_t = wc.take<uint32_t>(max_atoms);
   a.atom_d = wc.take<int32_t>(max_atoms);
@@ -518,7 +523,8 @@ int crgc_merge_deltas(crgc_graph *h, const crgc_delta_batch *b) {
       b->memory == CRGC_MEM_HOST
           ? Carver::need({n * 8, n * 4, n * 8, n, (n + 1) * 4, nout * 8, nout * 4})
           : 0;
-  const size_t work_bytes = Carver::need({n * 4, n * 4}) + edge_scratch(nout);
+  const size_t work_bytes =
+      Carver::need({n * 4, n * 4, std::max<uint64_t>(nout, 1) * 4}) + edge_scratch(nout);
   if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
     return CRGC_E_NOMEM;
   Carver sc(h->stage.ptr), wc(h->work.ptr);
@@ -534,6 +540,7 @@ int crgc_merge_deltas(crgc_graph *h, const crgc_delta_batch *b) {
   a.out_count = stage(h, sc, b->out_count, nout, b->memory);
   a.self_slot = wc.take<uint32_t>(n);
   a.sup_slot = wc.take<uint32_t>(n);
+  a.ot_slot = wc.take<uint32_t>(std::max<uint64_t>(nout, 1));
   a.atom_o = wc.take<uint32_t>(std::max<uint64_t>(nout, 1));
   a.atom_t = wc.take<uint32_t>(std::max<uint64_t>(nout, 1));
   a.atom_d = wc.take<int32_t>(std::max<uint64_t>(nout, 1));

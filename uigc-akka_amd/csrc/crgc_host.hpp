@@ -52,6 +52,20 @@ struct Carver {
   }
 };
 
+// Flattened id resolution (k_ids): up to 5 segments of ids, one slot each.
+struct IdSeg {
+  const uint64_t *ids;
+  uint32_t *slots;
+  uint64_t n;              // bound (grid sizing)
+  const uint32_t *n_dev;   // exact count on the device (an offsets array's last entry), or null
+  bool none_ok;            // CRGC_NO_ACTOR means "none" here (SLOT_INVALID, no error)
+};
+struct IdArgs {
+  IdSeg seg[5];
+  int nseg;
+};
+hipError_t launch_ids(const DevGraph &g, const IdArgs &a, hipStream_t s);
+
 struct EntryArgs {
   uint64_t n;
   uint32_t F;
@@ -69,6 +83,9 @@ struct EntryArgs {
   const int16_t *u_info;
   uint32_t *self_slot;   // [n]
   uint32_t *spawn_slot;  // [n*F]
+  uint32_t *ct_slot;     // [n*F] created targets, resolved by k_ids
+  uint32_t *co_slot;     // [n*F] created owners
+  uint32_t *u_slot;      // [n*F] updated refs
   uint32_t *atom_o;      // [2*n*F]: created atoms, then updated atoms
   uint32_t *atom_t;
   int32_t *atom_d;
@@ -86,6 +103,7 @@ struct DeltaArgs {
   const int32_t *out_count;
   uint32_t *self_slot;
   uint32_t *sup_slot;
+  uint32_t *ot_slot;     // [nout] outgoing targets, resolved by k_ids
   uint32_t *atom_o;
   uint32_t *atom_t;
   int32_t *atom_d;

@@ -202,6 +202,39 @@ __device__ inline unsigned long long wave_atomic_add(unsigned long long *p, uint
   return base + (incl - v);
 }
 
+// Workgroup-aggregated appends to K counters: one atomic per counter per
+// workgroup (a counter that every wave bumps saturates near 88 atomics/us).
+// Every thread of the block must call it; v[k] is this thread's count for
+// ctr[k], out[k] its exclusive base.  Up to 1024 threads.
+template <int K>
+__device__ inline void block_append(unsigned long long *const (&ctr)[K], const uint32_t (&v)[K],
+                                    unsigned long long (&out)[K]) {
+  __shared__ uint32_t s_wave[16][K];
+  __shared__ unsigned long long s_base[K];
+  const int w = threadIdx.x >> 6, nw = (int)(blockDim.x >> 6);
+  uint32_t incl[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    incl[k] = wave_incl_scan(v[k]);
+    if ((threadIdx.x & 63) == 63) s_wave[w][k] = incl[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < (unsigned)K) {
+    const int k = threadIdx.x;
+    uint32_t run = 0;
+    for (int j = 0; j < nw; ++j) {
+      const uint32_t t = s_wave[j][k];
+      s_wave[j][k] = run;
+      run += t;
+    }
+    s_base[k] = run ? atomicAdd(ctr[k], (unsigned long long)run) : 0ull;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) out[k] = s_base[k] + s_wave[w][k] + incl[k] - v[k];
+  __syncthreads();
+}
+
 // Wave-aggregated 1-bit append: lanes with `pred` get consecutive indices.
 __device__ inline unsigned long long wave_append(unsigned long long *p, bool pred) {
   const uint64_t ball = __ballot(pred);
@@ -278,6 +311,43 @@ __device__ inline uint32_t id_settle(const DevGraph &g, uint64_t id, uint64_t bu
       uint32_t v = atomicOr(&g.htab[bucket].val, 0u);
       if (v != VAL_PENDING) {
         slot = v;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (slot == SLOT_INVALID) set_err(g.ctr, ERR_SPIN);
+  }
+  return state == RS_NONE ? SLOT_INVALID : slot;
+}
+
+// Workgroup form of id_settle: one slot_top / inserted atomic per workgroup.
+// Every thread of the block must call it; every thread publishes its claims
+// before any waits, so the protocol above still cannot deadlock.
+__device__ inline uint32_t id_settle_block(const DevGraph &g, uint64_t id, uint64_t bucket,
+                                           uint32_t slot, int state) {
+  const bool ins = state == RS_INSERTED;
+  unsigned long long *const ctrs[2] = {&g.ctr->slot_top, &g.ctr->inserted};
+  const uint32_t v[2] = {ins ? 1u : 0u, ins ? 1u : 0u};
+  unsigned long long base[2];
+  block_append<2>(ctrs, v, base);
+  if (ins) {
+    const unsigned long long s = base[0];
+    if (s >= g.scap) {
+      set_err(g.ctr, ERR_SLOTS_FULL);
+      slot = SLOT_INVALID;
+    } else {
+      slot = (uint32_t)s;
+      g.vid[s] = id;
+      g.flags[s] = FL_ALIVE;
+    }
+    atomicExch(&g.htab[bucket].val, slot);
+  }
+  if (state == RS_PENDING) {
+    slot = SLOT_INVALID;
+    for (uint32_t spin = 0; spin < (1u << 24); ++spin) {
+      uint32_t v2 = atomicOr(&g.htab[bucket].val, 0u);
+      if (v2 != VAL_PENDING) {
+        slot = v2;
         break;
       }
       __builtin_amdgcn_s_sleep(1);

@@ -18,113 +18,109 @@ namespace crgc {
 __device__ inline bool vs(uint32_t s) { return s < 0xFFFFFFF0u; }
 
 // ---------------------------------------------------------------------------
-// Entries — ShadowGraph.mergeEntry, ShadowGraph.java:75-125.
-// One thread per entry; the created / spawned / updated records are walked in
-// wave-uniform rounds so that id resolution (id_resolve) can aggregate slot
-// allocation per wave.
+// Id resolution, flattened: one thread per id reference of the batch (every
+// self / created target and owner / spawned / updated ref of the entries, or
+// every delta id / supervisor / outgoing target), no per-entry loops.  Slot
+// allocation for new shadows is one atomic per 1024-thread workgroup.  Which
+// thread creates a shadow does not matter: creation order only affects the
+// reference's `from` order.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_entries_resolve(DevGraph g, EntryArgs a) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  const bool valid = i < a.n;
-  uint64_t self = 0;
-  uint32_t c0 = 0, c1 = 0, s0 = 0, s1 = 0, u0 = 0, u1 = 0;
-  int16_t rc = 0;
-  bool ok = valid;
-  const uint32_t ctot = a.c_off[a.n];
-  if (valid) {
-    self = a.self[i];
-    rc = a.recv[i];
-    c0 = a.c_off[i]; c1 = a.c_off[i + 1];
-    s0 = a.s_off[i]; s1 = a.s_off[i + 1];
-    u0 = a.u_off[i]; u1 = a.u_off[i + 1];
-    if (c1 < c0 || s1 < s0 || u1 < u0 || c1 > a.n * a.F || s1 > a.n * a.F || u1 > a.n * a.F) {
-      set_err(g.ctr, ERR_BAD_OFFSETS);
-      ok = false;
-    } else if (c1 - c0 > a.F || s1 - s0 > a.F || u1 - u0 > a.F) {
-      set_err(g.ctr, ERR_TOO_MANY);
-      ok = false;
-    }
-    if (reserved_id(self)) {
-      set_err(g.ctr, ERR_RESERVED_ID);
-      ok = false;
-    }
-  }
-  const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
+constexpr int IDS_THREADS = 1024;
 
+__global__ __launch_bounds__(IDS_THREADS) void k_ids(DevGraph g, IdArgs a) {
+  uint64_t cnt[5], total = 0;
+  for (int k = 0; k < 5; ++k) {
+    cnt[k] = k < a.nseg ? (a.seg[k].n_dev ? (uint64_t)*a.seg[k].n_dev : a.seg[k].n) : 0;
+    if (cnt[k] > a.seg[k].n) cnt[k] = a.seg[k].n;  // bad offsets: flagged by the apply kernel
+    total += cnt[k];
+  }
+  const uint64_t stride = (uint64_t)gridDim.x * IDS_THREADS;
+  for (uint64_t base = (uint64_t)blockIdx.x * IDS_THREADS; base < total; base += stride) {
+    uint64_t r = base + threadIdx.x;
+    int k = 0;
+    bool has = r < total;
+    if (has)
+      while (r >= cnt[k]) r -= cnt[k++];
+    const IdSeg &sg = a.seg[has ? k : 0];
+    uint64_t id = has ? sg.ids[r] : 0;
+    if (has && id == CRGC_NO_ACTOR && sg.none_ok) has = false;
+    else if (has && reserved_id(id)) {
+      set_err(g.ctr, ERR_RESERVED_ID);
+      has = false;
+    }
+    uint64_t bucket = 0;
+    uint32_t slot = SLOT_INVALID;
+    int st = RS_NONE;
+    if (has) st = id_probe(g, id, bucket, slot);
+    slot = id_settle_block(g, id, bucket, slot, st);
+    if (base + threadIdx.x < total) sg.slots[r] = slot;
+  }
+}
+
+hipError_t launch_ids(const DevGraph &g, const IdArgs &a, hipStream_t s) {
+  uint64_t n = 0;
+  for (int k = 0; k < a.nseg; ++k) n += a.seg[k].n;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ids, dim3(grid_for(n, IDS_THREADS, 1024)), dim3(IDS_THREADS), 0, s, g, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Entries — ShadowGraph.mergeEntry, ShadowGraph.java:75-125.  One thread per
+// entry over slots resolved by k_ids: receive counts, the LWW tags, and the
+// edge atoms.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_entries_apply(DevGraph g, EntryArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const uint32_t c0 = a.c_off[i], c1 = a.c_off[i + 1];
+  const uint32_t s0 = a.s_off[i], s1 = a.s_off[i + 1];
+  const uint32_t u0 = a.u_off[i], u1 = a.u_off[i + 1];
+  const uint64_t cmax = a.n * a.F;
+  bool ok = true;
+  if (c1 < c0 || s1 < s0 || u1 < u0 || c1 > cmax || s1 > cmax || u1 > cmax) {
+    set_err(g.ctr, ERR_BAD_OFFSETS);
+    ok = false;
+  } else if (c1 - c0 > a.F || s1 - s0 > a.F || u1 - u0 > a.F) {
+    set_err(g.ctr, ERR_TOO_MANY);
+    ok = false;
+  }
+  const uint32_t me = ok ? a.self_slot[i] : SLOT_INVALID;
+  if (!ok) a.self_slot[i] = SLOT_INVALID;
+  const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
+  const int16_t rc = a.recv[i];
   // Local information (:77-82): recv delta and the busy/root LWW tag.
-  const uint32_t me = id_resolve(g, ok, self);
-  if (valid) a.self_slot[i] = ok ? me : SLOT_INVALID;
-  if (ok && vs(me)) {
+  if (vs(me)) {
     if (rc != 0) atomicAdd(&g.recv[me], (int32_t)rc);
     atomicMax(&g.vseq[me], tag);
   }
-
-  // Created refs (:85-93): outgoing[owner][target] += 1.  Target first.
-  const uint32_t nc = ok ? c1 - c0 : 0;
-  for (uint32_t k = 0; __ballot(k < nc); ++k) {
-    bool has = k < nc;
-    uint64_t tid = 0, oid = 0;
-    if (has) {
-      tid = a.c_target[c0 + k];
-      oid = a.c_owner[c0 + k];
-      if (reserved_id(tid) || reserved_id(oid)) {
-        set_err(g.ctr, ERR_RESERVED_ID);
-        has = false;
-      }
-    }
-    const uint32_t ts = id_resolve(g, has, tid);
-    const uint32_t os = id_resolve(g, has, oid);
-    if (k < nc) {
-      a.atom_o[c0 + k] = os;
-      a.atom_t[c0 + k] = ts;
-      a.atom_d[c0 + k] = (has && vs(os) && vs(ts)) ? 1 : 0;
-    }
+  if (!ok) return;
+  const uint32_t ctot = a.c_off[a.n];
+  // Created refs (:85-93): outgoing[owner][target] += 1.
+  for (uint32_t k = c0; k < c1; ++k) {
+    const uint32_t os = a.co_slot[k], ts = a.ct_slot[k];
+    a.atom_o[k] = os;
+    a.atom_t[k] = ts;
+    a.atom_d[k] = (vs(me) && vs(os) && vs(ts)) ? 1 : 0;
   }
-
   // Spawned actors (:96-104): child.supervisor = self, last write wins.
-  const uint32_t ns = ok ? s1 - s0 : 0;
-  for (uint32_t k = 0; __ballot(k < ns); ++k) {
-    bool has = k < ns;
-    uint64_t cid = 0;
-    if (has) {
-      cid = a.spawned[s0 + k];
-      if (reserved_id(cid)) {
-        set_err(g.ctr, ERR_RESERVED_ID);
-        has = false;
-      }
-    }
-    const uint32_t cs = id_resolve(g, has, cid);
-    if (k < ns) {
-      const bool good = has && vs(cs) && vs(me);
-      a.spawn_slot[s0 + k] = good ? cs : SLOT_INVALID;
-      if (good) atomicMax(&g.sseq[cs], tag);
-    }
+  for (uint32_t k = s0; k < s1; ++k) {
+    const uint32_t cs = a.spawn_slot[k];
+    const bool good = vs(cs) && vs(me);
+    if (!good) a.spawn_slot[k] = SLOT_INVALID;
+    if (good) atomicMax(&g.sseq[cs], tag);
   }
-
   // Updated refs (:107-123): target.recv -= count; deactivation -> -1 edge.
-  const uint32_t nu = ok ? u1 - u0 : 0;
-  for (uint32_t k = 0; __ballot(k < nu); ++k) {
-    bool has = k < nu;
-    uint64_t rid = 0;
-    int16_t info = 0;
-    if (has) {
-      rid = a.u_ref[u0 + k];
-      info = a.u_info[u0 + k];
-      if (reserved_id(rid)) {
-        set_err(g.ctr, ERR_RESERVED_ID);
-        has = false;
-      }
-    }
-    const uint32_t ts = id_resolve(g, has, rid);
-    if (k < nu) {
-      const bool good = has && vs(ts) && vs(me);
-      const int32_t cnt = refob_count(info);
-      if (good && cnt > 0) atomicAdd(&g.recv[ts], -cnt);
-      const uint64_t at = (uint64_t)ctot + u0 + k;
-      a.atom_o[at] = me;
-      a.atom_t[at] = ts;
-      a.atom_d[at] = (good && refob_deactivated(info)) ? -1 : 0;
-    }
+  for (uint32_t k = u0; k < u1; ++k) {
+    const uint32_t ts = a.u_slot[k];
+    const int16_t info = a.u_info[k];
+    const bool good = vs(ts) && vs(me);
+    const int32_t cnt = refob_count(info);
+    if (good && cnt > 0) atomicAdd(&g.recv[ts], -cnt);
+    const uint64_t at = (uint64_t)ctot + k;
+    a.atom_o[at] = me;
+    a.atom_t[at] = ts;
+    a.atom_d[at] = (good && refob_deactivated(info)) ? -1 : 0;
   }
 }
 
@@ -152,8 +148,17 @@ __global__ __launch_bounds__(256) void k_entries_lww(DevGraph g, EntryArgs a) {
 
 hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
+  const uint64_t nf = a.n * a.F;
+  IdArgs ia{};
+  ia.nseg = 5;
+  ia.seg[0] = IdSeg{a.self, a.self_slot, a.n, nullptr, false};
+  ia.seg[1] = IdSeg{a.c_target, a.ct_slot, nf, a.c_off + a.n, false};
+  ia.seg[2] = IdSeg{a.c_owner, a.co_slot, nf, a.c_off + a.n, false};
+  ia.seg[3] = IdSeg{a.spawned, a.spawn_slot, nf, a.s_off + a.n, false};
+  ia.seg[4] = IdSeg{a.u_ref, a.u_slot, nf, a.u_off + a.n, false};
+  if (hipError_t e = launch_ids(g, ia, s)) return e;
   const int blocks = (int)((a.n + 255) / 256);
-  hipLaunchKernelGGL(k_entries_resolve, dim3(blocks), dim3(256), 0, s, g, a);
+  hipLaunchKernelGGL(k_entries_apply, dim3(blocks), dim3(256), 0, s, g, a);
   hipLaunchKernelGGL(k_entries_lww, dim3(blocks), dim3(256), 0, s, g, a);
   return hipGetLastError();
 }
@@ -163,59 +168,34 @@ hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s) 
 // delta shadow, in arrival order (seq).  Flags only when the shadow is
 // interned (:139-146); isLocal is never set (:135).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_deltas_resolve(DevGraph g, DeltaArgs a) {
+__global__ __launch_bounds__(256) void k_deltas_apply(DevGraph g, DeltaArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  const bool valid = i < a.n;
-  uint64_t id = 0, sid = CRGC_NO_ACTOR;
-  uint32_t o0 = 0, o1 = 0;
-  uint8_t fl = 0;
-  int32_t rc = 0;
-  bool ok = valid;
-  if (valid) {
-    id = a.id[i];
-    sid = a.sup[i];
-    fl = a.flags[i];
-    rc = a.recv[i];
-    o0 = a.out_off[i];
-    o1 = a.out_off[i + 1];
-    if (o1 < o0) {
-      set_err(g.ctr, ERR_BAD_OFFSETS);
-      ok = false;
-    }
-    if (reserved_id(id) || (sid != CRGC_NO_ACTOR && reserved_id(sid))) {
-      set_err(g.ctr, ERR_RESERVED_ID);
-      ok = false;
-    }
+  if (i >= a.n) return;
+  const uint32_t o0 = a.out_off[i], o1 = a.out_off[i + 1];
+  bool ok = true;
+  if (o1 < o0) {
+    set_err(g.ctr, ERR_BAD_OFFSETS);
+    ok = false;
   }
+  const uint32_t me = ok ? a.self_slot[i] : SLOT_INVALID;
+  if (!ok) a.self_slot[i] = SLOT_INVALID;
   const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
-  const uint32_t me = id_resolve(g, ok, id);
-  if (valid) a.self_slot[i] = ok ? me : SLOT_INVALID;
-  if (ok && vs(me)) {
+  const uint8_t fl = a.flags[i];
+  const int32_t rc = a.recv[i];
+  if (vs(me)) {
     if (rc != 0) atomicAdd(&g.recv[me], rc);
     if (fl & CRGC_DELTA_INTERNED) atomicMax(&g.vseq[me], tag);
   }
-  const bool has_sup = ok && sid != CRGC_NO_ACTOR;
-  const uint32_t ss = id_resolve(g, has_sup, sid);
-  if (valid) a.sup_slot[i] = (has_sup && vs(ss) && vs(me)) ? ss : SLOT_INVALID;
-  if (has_sup && vs(ss) && vs(me)) atomicMax(&g.sseq[me], tag);
-
-  const uint32_t no = ok ? o1 - o0 : 0;
-  for (uint32_t k = 0; __ballot(k < no); ++k) {
-    bool has = k < no;
-    uint64_t tid = 0;
-    if (has) {
-      tid = a.out_target[o0 + k];
-      if (reserved_id(tid)) {
-        set_err(g.ctr, ERR_RESERVED_ID);
-        has = false;
-      }
-    }
-    const uint32_t ts = id_resolve(g, has, tid);
-    if (k < no) {
-      a.atom_o[o0 + k] = me;
-      a.atom_t[o0 + k] = ts;
-      a.atom_d[o0 + k] = (has && vs(ts) && vs(me)) ? a.out_count[o0 + k] : 0;
-    }
+  const uint32_t ss = a.sup_slot[i];  // SLOT_INVALID: no supervisor in this delta
+  const bool sup_ok = vs(ss) && vs(me);
+  a.sup_slot[i] = sup_ok ? ss : SLOT_INVALID;
+  if (sup_ok) atomicMax(&g.sseq[me], tag);
+  if (!ok) return;
+  for (uint32_t k = o0; k < o1; ++k) {
+    const uint32_t ts = a.ot_slot[k];
+    a.atom_o[k] = me;
+    a.atom_t[k] = ts;
+    a.atom_d[k] = (vs(ts) && vs(me)) ? a.out_count[k] : 0;
   }
 }
 
@@ -238,10 +218,15 @@ __global__ __launch_bounds__(256) void k_deltas_lww(DevGraph g, DeltaArgs a) {
 }
 
 hipError_t launch_deltas(const DevGraph &g, const DeltaArgs &a, uint64_t n_out, hipStream_t s) {
-  (void)n_out;
   if (a.n == 0) return hipSuccess;
+  IdArgs ia{};
+  ia.nseg = 3;
+  ia.seg[0] = IdSeg{a.id, a.self_slot, a.n, nullptr, false};
+  ia.seg[1] = IdSeg{a.sup, a.sup_slot, a.n, nullptr, true};
+  ia.seg[2] = IdSeg{a.out_target, a.ot_slot, n_out, a.out_off + a.n, false};
+  if (hipError_t e = launch_ids(g, ia, s)) return e;
   const int blocks = (int)((a.n + 255) / 256);
-  hipLaunchKernelGGL(k_deltas_resolve, dim3(blocks), dim3(256), 0, s, g, a);
+  hipLaunchKernelGGL(k_deltas_apply, dim3(blocks), dim3(256), 0, s, g, a);
   hipLaunchKernelGGL(k_deltas_lww, dim3(blocks), dim3(256), 0, s, g, a);
   return hipGetLastError();
 }
@@ -314,12 +299,16 @@ hipError_t launch_undo_apply(const DevGraph &g, const UndoArgs &a, uint64_t slot
 //      owner appended to the target's candidate list.
 //   5. k_seg_finish: degrees advance, per-merge counters reset.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_edge_apply(DevGraph g, EdgeArgs a) {
+constexpr int EDGE_THREADS = 1024;
+
+__global__ __launch_bounds__(EDGE_THREADS) void k_edge_apply(DevGraph g, EdgeArgs a) {
   const uint64_t n = a.n_atoms_dev ? *a.n_atoms_dev : a.max_atoms;
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t base = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); base < n;
-       base += stride) {
-    const uint64_t i = base + lane_id();
+  const uint64_t stride = (uint64_t)gridDim.x * EDGE_THREADS;
+  Counters *c = g.ctr;
+  unsigned long long *const lists[5] = {&c->n_new_edges, &c->n_touched, &c->n_rtouched,
+                                        &c->n_flips, &c->etab_used};
+  for (uint64_t base = (uint64_t)blockIdx.x * EDGE_THREADS; base < n; base += stride) {
+    const uint64_t i = base + threadIdx.x;
     const bool valid = i < n;
     uint32_t o = 0, t = 0;
     int32_t d = 0;
@@ -352,23 +341,20 @@ __global__ __launch_bounds__(256) void k_edge_apply(DevGraph g, EdgeArgs a) {
         flip = (old > 0) != (now > 0);
       }
     }
-    // sign changes of existing counts: their candidate entries are refreshed
-    // from the final count after the merge (k_edge_flip)
-    const unsigned long long fi = wave_append(&g.ctr->n_flips, flip);
-    if (flip) a.flips[fi] = b;
-    const unsigned long long li = wave_append(&g.ctr->n_new_edges, ins);
+    // List appends, one atomic per list per workgroup.  Sign changes of
+    // existing counts: their candidate entries are refreshed from the final
+    // count after the merge (k_edge_flip).
+    const bool first = ins && rank == 0, rfirst = ins && rrank == 0;
+    const uint32_t cnt[5] = {ins, first, rfirst, flip, ins};
+    unsigned long long at[5];
+    block_append<5>(lists, cnt, at);
     if (ins) {
-      a.newlist[li] = b;
-      a.rrank[li] = rrank;
+      a.newlist[at[0]] = b;
+      a.rrank[at[0]] = rrank;
     }
-    const uint64_t insb = __ballot(ins);
-    if (lane_id() == 0 && insb) atomicAdd(&g.ctr->etab_used, (unsigned long long)__popcll(insb));
-    const bool first = ins && rank == 0;
-    const unsigned long long ti = wave_append(&g.ctr->n_touched, first);
-    if (first) a.touched[ti] = o;
-    const bool rfirst = ins && rrank == 0;
-    const unsigned long long ri = wave_append(&g.ctr->n_rtouched, rfirst);
-    if (rfirst) a.rtouched[ri] = t;
+    if (first) a.touched[at[1]] = o;
+    if (rfirst) a.rtouched[at[2]] = t;
+    if (flip) a.flips[at[3]] = b;
   }
 }
 
@@ -393,19 +379,22 @@ struct Seg {
 };
 
 template <typename T>
-__global__ __launch_bounds__(256) void k_seg_plan(Seg<T> s, Counters *c) {
+__global__ __launch_bounds__(EDGE_THREADS) void k_seg_plan(Seg<T> s, Counters *c) {
   const uint64_t n = *s.ntouched;
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t base = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); base < n;
-       base += stride) {
-    const uint64_t i = base + lane_id();
+  const uint64_t stride = (uint64_t)gridDim.x * EDGE_THREADS;
+  unsigned long long *const tops[1] = {s.top};
+  for (uint64_t base = (uint64_t)blockIdx.x * EDGE_THREADS; base < n; base += stride) {
+    const uint64_t i = base + threadIdx.x;
     uint32_t want = 0;
     if (i < n) {
       const uint32_t o = s.touched[i];
       const uint32_t need = s.adj[o].y + s.nnew[o];
       if (need > s.cap[o]) want = seg_cap(need);
     }
-    const unsigned long long off = wave_atomic_add(s.top, want);
+    const uint32_t v[1] = {want};
+    unsigned long long offs[1];
+    block_append<1>(tops, v, offs);  // one pool allocation per workgroup
+    const unsigned long long off = offs[0];
     if (i < n) {
       uint32_t r = 0xFFFFFFFFu;  // no move
       if (want) {
@@ -503,9 +492,10 @@ hipError_t launch_edges(const DevGraph &g, const EdgeArgs &a, hipStream_t s) {
                    &g.ctr->n_touched, a.touched, a.reloc};
   Seg<uint32_t> rv{g.radj, g.rcap, g.rnew, g.rpool, g.rpcap, &g.ctr->rpool_top,
                    &g.ctr->n_rtouched, a.rtouched, a.rreloc};
-  hipLaunchKernelGGL(k_edge_apply, dim3(grid), dim3(256), 0, s, g, a);
-  hipLaunchKernelGGL(k_seg_plan<uint64_t>, dim3(grid), dim3(256), 0, s, fw, g.ctr);
-  hipLaunchKernelGGL(k_seg_plan<uint32_t>, dim3(grid), dim3(256), 0, s, rv, g.ctr);
+  const int wgrid = grid_for(a.max_atoms, EDGE_THREADS, 2048);
+  hipLaunchKernelGGL(k_edge_apply, dim3(wgrid), dim3(EDGE_THREADS), 0, s, g, a);
+  hipLaunchKernelGGL(k_seg_plan<uint64_t>, dim3(wgrid), dim3(EDGE_THREADS), 0, s, fw, g.ctr);
+  hipLaunchKernelGGL(k_seg_plan<uint32_t>, dim3(wgrid), dim3(EDGE_THREADS), 0, s, rv, g.ctr);
   hipLaunchKernelGGL(k_seg_move<uint64_t>, dim3(grid), dim3(256), 0, s, fw);
   hipLaunchKernelGGL(k_seg_move<uint32_t>, dim3(grid), dim3(256), 0, s, rv);
   hipLaunchKernelGGL(k_edge_append, dim3(grid), dim3(256), 0, s, g, a);
