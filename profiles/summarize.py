@@ -1,7 +1,7 @@
 """Summarise a rocprofv3 kernel trace: steady-state per-kernel time per wakeup.
 
 usage: python profiles/summarize.py <run_kernel_trace.csv> [n_steps]
-Takes the last n_steps wakeups (each starts at a k_entries_resolve launch).
+Takes the last n_steps wakeups (each starts at a k_ids launch).
 """
 import collections
 import csv
@@ -10,7 +10,7 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if "k_entries_resolve" in r["Kernel_Name"]]
+idx = [i for i, r in enumerate(rows) if "k_ids" in r["Kernel_Name"]]
 start = idx[-n]
 agg = collections.defaultdict(lambda: [0, 0.0])
 for r in rows[start:]:
