@@ -66,6 +66,7 @@ extern "C" {
 #define CRGC_F_BUSY 0x08u
 #define CRGC_F_ROOT 0x10u
 #define CRGC_F_HALTED 0x20u
+#define CRGC_F_PROXY 0x40u   /* internal (sharded graphs); never exported   */
 
 /* Entry.isBusy / Entry.isRoot bits in crgc_entry_batch.flags */
 #define CRGC_ENTRY_BUSY 0x01u
@@ -77,14 +78,42 @@ extern "C" {
 
 typedef struct crgc_graph crgc_graph; /* opaque; owns the HBM shadow graph */
 
+/*
+ * Hash-partitioned graphs (more shadows than one GPU should hold, or more
+ * throughput): G shards, shard r holding the shadows whose actor id hashes to
+ * r (crgc_shard_of).  Each shard is one crgc_graph on its own GPU; the shards
+ * exchange marked frontier ids, kill requests and garbage ids through a
+ * transport.  With G > 1 every entry point that changes or traces the graph is
+ * COLLECTIVE: all G shards call it, in the same order (one thread or process
+ * per shard).  Queries (live count, export, local roots, total actors seen)
+ * are per shard; their union / sum is the whole graph's.
+ */
+typedef struct crgc_transport crgc_transport;
+/* One process per GPU: RCCL over xGMI.  Shard 0 makes the id and shares it
+ * out of band (e.g. torch.distributed); every shard then creates its
+ * transport (collective, like ncclCommInitRank). */
+int crgc_transport_rccl_id(uint8_t id[128]);
+int crgc_transport_rccl(const uint8_t id[128], uint32_t n_shards, uint32_t shard, int32_t device,
+                        crgc_transport **out);
+/* One process, G shards (possibly on one GPU), one host thread per shard:
+ * device-to-device copies.  Shared by the G handles. */
+int crgc_transport_local(uint32_t n_shards, crgc_transport **out);
+/* Destroy after every handle using it. */
+void crgc_transport_destroy(crgc_transport *t);
+/* Home shard of an actor id. */
+uint32_t crgc_shard_of(uint64_t id, uint32_t n_shards);
+
 typedef struct crgc_config {
   uint32_t abi_version;        /* CRGC_ABI_VERSION                          */
   int32_t device;              /* HIP device ordinal                        */
   uint32_t entry_field_size;   /* F, uigc.crgc.entry-field-size (default 4) */
   uint32_t delta_graph_size;   /* uigc.crgc.delta-graph-size (default 64)   */
-  uint64_t vertex_capacity;    /* hint: expected live shadows               */
+  uint64_t vertex_capacity;    /* hint: expected live shadows (this shard)  */
   uint64_t edge_capacity;      /* hint: expected live (owner,target) pairs  */
   void *stream;                /* hipStream_t to run on; NULL = own stream  */
+  uint32_t n_shards;           /* 0 or 1: unsharded                         */
+  uint32_t shard;              /* this handle's shard, < n_shards           */
+  crgc_transport *transport;   /* required when n_shards > 1                */
 } crgc_config;
 
 /*
@@ -151,6 +180,14 @@ typedef struct crgc_trace_stats {
   double ms_mark;          /* device time of the pseudo-root + level kernels*/
   double ms_sweep;         /* device time: sweep + id compaction            */
   double ms_total;         /* host wall time of crgc_trace                  */
+  /* per level kernel (device time summed over the trace's launches) */
+  double ms_frontier;      /* k_frontier: pseudo-roots / frontier, sup edges */
+  double ms_tail;          /* k_tail: level controller, narrow frontiers    */
+  double ms_expand;        /* k_expand: out-edges of the frontier           */
+  /* sharded graphs */
+  uint64_t rounds;         /* exchange rounds (1 + frontier all-to-alls)    */
+  uint64_t ids_sent;       /* frontier ids sent to other shards             */
+  double ms_exchange;      /* host wall time spent in exchanges             */
 } crgc_trace_stats;
 
 typedef struct crgc_trace_out {

@@ -1,0 +1,185 @@
+"""Hash-partitioned shadow graph against the unsharded CPU oracle.
+
+G logical shards run on the one GPU of the test box, each shard a crgc_graph
+handle driven by its own host thread, exchanging through the in-process
+transport (device copies) — the same protocol the RCCL transport runs with one
+process per GPU.  Every check is bit-exact against oracle.OracleGraph (an
+unsharded restatement of ShadowGraph.java): the union of the shards' garbage
+and kill sets, the sums of their counts, and the union of their exported
+state must equal the oracle's, wakeup by wakeup.
+"""
+import numpy as np
+import pytest
+
+import cluster
+import fuzz
+import kats
+import world
+from crgc_hip import abi
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(rh, ro):
+    assert rh.garbage_set() == ro.garbage_set()
+    assert rh.kill_set() == ro.kill_set()
+    assert len(rh.garbage) == len(ro.garbage), "a garbage id reported twice"
+    assert len(rh.kill) == len(ro.kill), "a kill id reported twice"
+    assert rh.n_live == ro.n_live
+    assert rh.pseudo_roots == ro.pseudo_roots
+    assert rh.sup_edges == ro.sup_edges
+    assert rh.edges_scanned == ro.edges_scanned
+
+
+@pytest.fixture
+def sharded(hip_mod):
+    made = []
+
+    def make(G, **kw):
+        g = hip_mod.ShardedShadowGraph(G, **kw)
+        made.append(g)
+        return g
+    yield make
+    for g in made:
+        g.close()
+
+
+def test_shard_of_partitions_ids(hip_mod):
+    ids = np.arange(1, 20001, dtype=np.uint64) | np.uint64(1 << 48)
+    for G in (2, 3, 8):
+        homes = [hip_mod.shard_of(int(i), G) for i in ids]
+        counts = np.bincount(homes, minlength=G)
+        assert counts.min() > 0.8 * len(ids) / G  # balanced
+    assert hip_mod.shard_of(12345, 1) == 0
+
+
+@pytest.mark.parametrize("G", [2, 3])
+@pytest.mark.parametrize("name", sorted(kats.SCENARIOS))
+def test_kat_scenarios_sharded(sharded, name, G):
+    kats.run_scenario(sharded(G), kats.SCENARIOS[name]())
+
+
+@pytest.mark.parametrize("G,split", [(2, False), (4, True)])
+def test_random_spec_sharded_matches_oracle_every_wakeup(sharded, oracle_mod, G, split):
+    w = kats.RandomWorld(seed=7, max_actors=600, wake_every=13)
+    h, o = sharded(G), oracle_mod.OracleGraph()
+    for batch in w.steps():
+        h.merge_entries(batch, split=split)
+        o.merge_entries(batch)
+        assert h.export() == o.export()
+        rh, ro = h.trace(True), o.trace(True)
+        _same(rh, ro)
+        w.kill(ro.kill_set())
+    assert h.total_actors_seen() == o.total_actors_seen()
+    assert h.live_count() == 1
+
+
+@pytest.mark.parametrize("G,seed,cap", [(2, 11, 0), (3, 12, 0), (4, 13, 64)])
+def test_fuzz_sharded(sharded, oracle_mod, G, seed, cap):
+    h, o = sharded(G, vertex_capacity=cap, edge_capacity=cap), oracle_mod.OracleGraph()
+    fz = fuzz.Fuzz(seed)
+    for step in range(14):
+        eb = fz.entries(200 + 50 * step)
+        h.merge_entries(eb, split=step % 2 == 0)
+        o.merge_entries(eb)
+        if step % 2 == 1:
+            db = fz.deltas(5)
+            h.merge_deltas(db); o.merge_deltas(db)
+        if step == 9:
+            ub = fz.undo(o.export().vertices.keys())
+            h.merge_undo(ub); o.merge_undo(ub)
+        assert h.export() == o.export()
+        for loc in (1, 2, 3):
+            assert h.count_reachable_from(loc) == o.count_reachable_from(loc)
+        assert sorted(h.startWave().tolist()) == sorted(o.local_roots().tolist())
+        _same(h.trace(True), o.trace(True))
+        fz.sync(o.export())
+    assert h.total_actors_seen() == o.total_actors_seen()
+    assert h.export() == o.export()
+
+
+def test_power_law_c1_sharded(sharded, oracle_mod):
+    w = world.World(seed=0x5EED + 1)
+    w.bulk_graph(100_000, 1_000_000, alpha=2.1, n_roots=1000)
+    h, o = sharded(4), oracle_mod.OracleGraph()
+    for b in w.batches(1 << 18):
+        h.merge_entries(b, split=True)
+        o.merge_entries(b)
+    _same(h.trace(True), o.trace(True))
+    for _ in range(3):
+        b = w.wakeup_batch(10_000)
+        h.merge_entries(b, split=True)
+        o.merge_entries(b)
+        rh = h.trace(True)
+        _same(rh, o.trace(True))
+        assert rh.rounds >= 2  # marks crossed shards
+    assert h.export() == o.export()
+    assert h.total_actors_seen() == o.total_actors_seen()
+
+
+def test_c3_chains_sharded(sharded, oracle_mod):
+    w = world.World(seed=0x5EED + 3)
+    w.chain_graph(n_chains=5, chain_len=300, n_sup_chains=3, sup_depth=100,
+                  n_rings=10, ring_len=40)
+    h, o = sharded(2), oracle_mod.OracleGraph()
+    for b in w.batches(50_000):
+        h.merge_entries(b)
+        o.merge_entries(b)
+    rh, ro = h.trace(True), o.trace(True)
+    _same(rh, ro)
+    assert len(ro.garbage) == 10 * 40
+    assert h.export() == o.export()
+    _same(h.trace(True), o.trace(True))
+
+
+def test_c5_cluster_deltas_and_undo_sharded(sharded, oracle_mod):
+    cw = cluster.ClusterWorld(seed=9, n_nodes=8, max_actors=2000)
+    h, o = sharded(2), oracle_mod.OracleGraph()
+    merged = []
+    for _ in range(6):
+        cw.run_turns(400)
+        own, deltas = cw.flush(0)
+        for k, g in deltas:
+            b = g.to_batch()
+            h.merge_deltas(b)
+            o.merge_deltas(b)
+            merged.append((k, g))
+        h.merge_entries(own)
+        o.merge_entries(own)
+        _same(h.trace(True), o.trace(True))
+    assert h.export() == o.export()
+    log = cw.undo_log(7, merged).to_batch(restrict_to=set(o.export().vertices))
+    h.merge_undo(log)
+    o.merge_undo(log)
+    assert h.export() == o.export()
+    assert h.count_reachable_from(8) == o.count_reachable_from(8)
+    _same(h.trace(True), o.trace(True))
+
+
+def test_npe_and_cme_are_collective(sharded, oracle_mod):
+    from crgc_hip import Entry, EntryBatch, UndoBatch
+    h = sharded(2)
+    a = (1 << 48) | 77
+    h.merge_entries(EntryBatch.from_entries([Entry(self=a)]))
+    with pytest.raises(abi.CrgcError) as e:
+        h.trace(True)
+    assert e.value.code == abi.E_NULL_SUPERVISOR
+    h2 = sharded(2)
+    r = (1 << 48) | 1
+    h2.merge_entries(EntryBatch.from_entries(
+        [Entry(self=r, isRoot=True, createdOwners=[r], createdTargets=[r])]))
+    before = h2.export()
+    with pytest.raises(abi.CrgcError) as e:
+        h2.merge_undo(UndoBatch.from_fields(3, [(r, 1, [((3 << 48) | 9, 1)])]))
+    assert e.value.code == abi.E_UNDO_NEW_SHADOW
+    assert h2.export() == before
+
+
+def test_device_resident_batches_sharded(sharded, oracle_mod):
+    w = kats.RandomWorld(seed=3, max_actors=300, wake_every=17)
+    h, o = sharded(3), oracle_mod.OracleGraph()
+    for batch in w.steps():
+        parts = batch.split(3)
+        h._all(lambda s, b: s.merge_entries(b.to_device()), [(p,) for p in parts])
+        o.merge_entries(batch)
+        _same(h.trace(True), o.trace(True))

@@ -6,7 +6,7 @@ ShadowGraph surface (ShadowGraph.java), bound through ctypes.
 """
 from . import abi
 from .batch import Entry, EntryBatch, DeltaBatch, UndoBatch, TraceResult, RefobInfo, GraphState
-from .graph import ShadowGraph
+from .graph import ShadowGraph, ShardedShadowGraph, Transport, shard_of
 
 __all__ = ["abi", "Entry", "EntryBatch", "DeltaBatch", "UndoBatch", "TraceResult", "RefobInfo",
-           "GraphState", "ShadowGraph"]
+           "GraphState", "ShadowGraph", "ShardedShadowGraph", "Transport", "shard_of"]

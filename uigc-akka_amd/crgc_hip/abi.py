@@ -31,6 +31,7 @@ F_LOCAL = 0x04
 F_BUSY = 0x08
 F_ROOT = 0x10
 F_HALTED = 0x20
+F_PROXY = 0x40
 
 ENTRY_BUSY = 0x01
 ENTRY_ROOT = 0x02
@@ -51,6 +52,9 @@ class CrgcConfig(C.Structure):
         ("vertex_capacity", _U64),
         ("edge_capacity", _U64),
         ("stream", _P),
+        ("n_shards", C.c_uint32),
+        ("shard", C.c_uint32),
+        ("transport", _P),
     ]
 
 
@@ -110,6 +114,12 @@ class CrgcTraceStats(C.Structure):
         ("ms_mark", C.c_double),
         ("ms_sweep", C.c_double),
         ("ms_total", C.c_double),
+        ("ms_frontier", C.c_double),
+        ("ms_tail", C.c_double),
+        ("ms_expand", C.c_double),
+        ("rounds", _U64),
+        ("ids_sent", _U64),
+        ("ms_exchange", C.c_double),
     ]
 
 
@@ -157,6 +167,11 @@ EXPORTED_SYMBOLS = (
     "crgc_live_count",
     "crgc_export",
     "crgc_strerror",
+    "crgc_transport_rccl_id",
+    "crgc_transport_rccl",
+    "crgc_transport_local",
+    "crgc_transport_destroy",
+    "crgc_shard_of",
 )
 
 
@@ -206,6 +221,17 @@ def load_library(path: str | None = None) -> C.CDLL:
     lib.crgc_last_trace.argtypes = [_P, C.POINTER(CrgcTraceOut)]
     lib.crgc_strerror.restype = C.c_char_p
     lib.crgc_strerror.argtypes = [C.c_int]
+    lib.crgc_transport_rccl_id.restype = C.c_int
+    lib.crgc_transport_rccl_id.argtypes = [C.c_char_p]
+    lib.crgc_transport_rccl.restype = C.c_int
+    lib.crgc_transport_rccl.argtypes = [C.c_char_p, C.c_uint32, C.c_uint32, C.c_int32,
+                                        C.POINTER(_P)]
+    lib.crgc_transport_local.restype = C.c_int
+    lib.crgc_transport_local.argtypes = [C.c_uint32, C.POINTER(_P)]
+    lib.crgc_transport_destroy.restype = None
+    lib.crgc_transport_destroy.argtypes = [_P]
+    lib.crgc_shard_of.restype = C.c_uint32
+    lib.crgc_shard_of.argtypes = [_U64, C.c_uint32]
     _declare(lib, "crgc_")
     if path is None:
         _lib = lib

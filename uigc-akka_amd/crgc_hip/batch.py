@@ -165,6 +165,12 @@ class EntryBatch:
             (uo[lo:hi + 1] - uo[lo]).astype(np.uint32),
             self.updated_ref[uo[lo]:uo[hi]].copy(), self.updated_info[uo[lo]:uo[hi]].copy())
 
+    def split(self, k: int) -> List["EntryBatch"]:
+        """k consecutive host parts (part r = entries [n*r/k, n*(r+1)/k))."""
+        n = self.n_entries
+        b = [n * i // k for i in range(k + 1)]
+        return [self.slice(b[i], b[i + 1]) for i in range(k)]
+
     def to_entries(self) -> List[Entry]:
         assert self.memory == abi.MEM_HOST
         out = []
@@ -241,6 +247,10 @@ class DeltaBatch:
             _offsets([len(r[4]) for r in rows]),
             np.array([t for r in rows for t, _ in r[4]], dtype=np.uint64),
             np.array([c for r in rows for _, c in r[4]], dtype=np.int32))
+
+    @staticmethod
+    def empty() -> "DeltaBatch":
+        return DeltaBatch.from_rows([])
 
     @staticmethod
     def concat(batches: Sequence["DeltaBatch"]) -> "DeltaBatch":
@@ -336,6 +346,12 @@ class TraceResult:
     ms_mark: float = 0.0
     ms_sweep: float = 0.0
     ms_total: float = 0.0
+    ms_frontier: float = 0.0
+    ms_tail: float = 0.0
+    ms_expand: float = 0.0
+    rounds: int = 1
+    ids_sent: int = 0
+    ms_exchange: float = 0.0
 
     def garbage_set(self):
         return set(int(x) for x in self.garbage)

@@ -8,7 +8,8 @@ import subprocess
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(PKG, "lib")
-SOURCES = ["crgc_api.hip", "crgc_merge.hip", "crgc_trace.hip", "crgc_rebuild.hip"]
+SOURCES = ["crgc_api.hip", "crgc_merge.hip", "crgc_trace.hip", "crgc_rebuild.hip",
+           "crgc_transport.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall",
          "-Wno-unused-function", "-Wno-unused-result", "-Wno-unused-value", "-munsafe-fp-atomics"]
@@ -41,7 +42,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
             if r.returncode:
                 raise RuntimeError(f"hipcc failed: {cmd[-3]}")
     if force or jobs or _stale(lib, objs):
-        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib, *objs]
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib, *objs,
+               "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode:
             print(r.stdout, r.stderr)

@@ -21,19 +21,24 @@ There is no CPU fallback: without the built library this raises.
 from __future__ import annotations
 
 import ctypes as C
+import dataclasses
 from typing import List, Optional
 
 import numpy as np
 
 from . import abi
-from .batch import (Entry, EntryBatch, DeltaBatch, UndoBatch, TraceResult, _ptr,
+from .batch import (Entry, EntryBatch, DeltaBatch, UndoBatch, TraceResult, GraphState, _ptr,
                     export_to_state)
 
 
 class ShadowGraph:
     def __init__(self, entry_field_size: int = 4, delta_graph_size: int = 64,
                  device: int = 0, vertex_capacity: int = 0, edge_capacity: int = 0,
-                 stream: Optional[int] = None):
+                 stream: Optional[int] = None, n_shards: int = 1, shard: int = 0,
+                 transport=None):
+        """One shadow graph, or (n_shards > 1) shard `shard` of a hash-partitioned
+        one whose shards exchange through `transport` (a Transport).  Merges,
+        traces and investigateRemotelyHeldActors are then collective."""
         self.lib = abi.load_library()
         cfg = abi.CrgcConfig()
         cfg.abi_version = abi.ABI_VERSION
@@ -43,6 +48,11 @@ class ShadowGraph:
         cfg.vertex_capacity = vertex_capacity
         cfg.edge_capacity = edge_capacity
         cfg.stream = stream or None
+        cfg.n_shards = n_shards
+        cfg.shard = shard
+        cfg.transport = transport.t if transport is not None else None
+        self.n_shards, self.shard = n_shards, shard
+        self._transport = transport  # keeps it alive at least as long as this handle
         h = C.c_void_p()
         self._chk(self.lib.crgc_create(C.byref(cfg), C.byref(h)), "crgc_create")
         self.h = h
@@ -105,7 +115,8 @@ class ShadowGraph:
         st = out.stats
         return TraceResult(g, k, int(out.n_live), int(st.pseudo_roots), int(st.edges_scanned),
                            int(st.sup_edges), int(st.levels), int(st.launches), st.ms_mark,
-                           st.ms_sweep, st.ms_total)
+                           st.ms_sweep, st.ms_total, st.ms_frontier, st.ms_tail, st.ms_expand,
+                           int(st.rounds), int(st.ids_sent), st.ms_exchange)
 
     def _trace_into(self, shouldKill, g, k):
         out = abi.CrgcTraceOut()
@@ -117,9 +128,7 @@ class ShadowGraph:
     def trace(self, shouldKill: bool = True) -> TraceResult:
         """ShadowGraph.trace(shouldKill): returns the garbage and kill id sets."""
         r, ng, nk = self.trace_kill_ids(shouldKill)
-        return TraceResult(r.garbage[:ng].copy(), r.kill[:nk].copy(), *[
-            getattr(r, f) for f in ("n_live", "pseudo_roots", "edges_scanned", "sup_edges",
-                                    "levels", "launches", "ms_mark", "ms_sweep", "ms_total")])
+        return dataclasses.replace(r, garbage=r.garbage[:ng].copy(), kill=r.kill[:nk].copy())
 
     def trace_kill_ids(self, shouldKill: bool = True):
         """trace() into reusable host buffers: (result with buffer views, n_garbage, n_kill)."""
@@ -188,3 +197,130 @@ class ShadowGraph:
     def export(self):
         self.flush()
         return export_to_state(self.lib.crgc_export, self.h)
+
+
+class Transport:
+    """A shard transport (include/crgc.h): RCCL over xGMI between processes, or
+    in-process device copies between G shards driven by G host threads."""
+
+    def __init__(self, handle, lib):
+        self.t, self.lib = handle, lib
+
+    @classmethod
+    def local(cls, n_shards: int) -> "Transport":
+        lib = abi.load_library()
+        t = C.c_void_p()
+        ShadowGraph._chk(lib.crgc_transport_local(n_shards, C.byref(t)), "crgc_transport_local")
+        return cls(t, lib)
+
+    @staticmethod
+    def rccl_unique_id() -> bytes:
+        lib = abi.load_library()
+        buf = C.create_string_buffer(128)
+        ShadowGraph._chk(lib.crgc_transport_rccl_id(buf), "crgc_transport_rccl_id")
+        return buf.raw
+
+    @classmethod
+    def rccl(cls, uid: bytes, n_shards: int, shard: int, device: int) -> "Transport":
+        lib = abi.load_library()
+        t = C.c_void_p()
+        ShadowGraph._chk(lib.crgc_transport_rccl(uid, n_shards, shard, device, C.byref(t)),
+                         "crgc_transport_rccl")
+        return cls(t, lib)
+
+    def close(self):
+        if self.t:
+            self.lib.crgc_transport_destroy(self.t)
+            self.t = None
+
+
+def shard_of(actor_id: int, n_shards: int) -> int:
+    """Home shard of an actor id (crgc_shard_of)."""
+    return int(abi.load_library().crgc_shard_of(actor_id, n_shards))
+
+
+class ShardedShadowGraph:
+    """G shards of one hash-partitioned shadow graph in this process, each on
+    its own host thread (collective calls run on all shards at once) over the
+    in-process transport.  `devices` may repeat a GPU: G logical shards on one
+    MI355X run exactly the protocol of G shards on G GPUs, with device copies
+    in place of RCCL.  Results are the union over shards (garbage, kill) or
+    sums (counts), which is what one unsharded ShadowGraph returns.
+    """
+
+    def __init__(self, n_shards: int, devices=None, entry_field_size: int = 4,
+                 vertex_capacity: int = 0, edge_capacity: int = 0):
+        import concurrent.futures as cf
+        self.G = n_shards
+        devices = list(devices) if devices is not None else [0] * n_shards
+        self.transport = Transport.local(n_shards)
+        self.shards = [ShadowGraph(entry_field_size=entry_field_size, device=devices[r],
+                                   vertex_capacity=vertex_capacity, edge_capacity=edge_capacity,
+                                   n_shards=n_shards, shard=r, transport=self.transport)
+                       for r in range(n_shards)]
+        self._pool = cf.ThreadPoolExecutor(max_workers=n_shards)
+
+    def _all(self, fn, args=None):
+        args = args if args is not None else [()] * self.G
+        futs = [self._pool.submit(fn, s, *a) for s, a in zip(self.shards, args)]
+        return [f.result() for f in futs]
+
+    def close(self):
+        for s in self.shards:
+            s.close()
+        self.transport.close()
+        self._pool.shutdown()
+
+    # -- collective -------------------------------------------------------------
+    def merge_entries(self, batch, split: bool = False):
+        """Merge one batch.  By default shard 0 contributes it and the others
+        contribute nothing; with split=True it is cut into G consecutive parts,
+        shard r contributing part r (the merge applies them in shard order, so
+        the result is the same)."""
+        parts = batch.split(self.G) if split else [batch] + [None] * (self.G - 1)
+        self._all(lambda s, b: s.merge_entries(b if b is not None else EntryBatch.empty()),
+                  [(p,) for p in parts])
+
+    def merge_deltas(self, batch):
+        self._all(lambda s, b: s.merge_deltas(b if b is not None else DeltaBatch.empty()),
+                  [(batch,)] + [(None,)] * (self.G - 1))
+
+    def merge_undo(self, log):
+        self._all(lambda s: s.merge_undo(log))
+
+    def trace(self, shouldKill: bool = True) -> TraceResult:
+        rs = self._all(lambda s: s.trace(shouldKill))
+        return TraceResult(
+            np.concatenate([r.garbage for r in rs]), np.concatenate([r.kill for r in rs]),
+            sum(r.n_live for r in rs), sum(r.pseudo_roots for r in rs),
+            sum(r.edges_scanned for r in rs), sum(r.sup_edges for r in rs),
+            max(r.levels for r in rs), sum(r.launches for r in rs),
+            max(r.ms_mark for r in rs), max(r.ms_sweep for r in rs), max(r.ms_total for r in rs),
+            max(r.ms_frontier for r in rs), max(r.ms_tail for r in rs),
+            max(r.ms_expand for r in rs), max(r.rounds for r in rs),
+            sum(r.ids_sent for r in rs), max(r.ms_exchange for r in rs))
+
+    def count_reachable_from(self, location: int) -> int:
+        vals = self._all(lambda s: s.count_reachable_from(location))
+        assert len(set(vals)) == 1, vals
+        return vals[0]
+
+    # -- per shard ------------------------------------------------------------
+    def total_actors_seen(self) -> int:
+        return sum(s.total_actors_seen() for s in self.shards)
+
+    def live_count(self) -> int:
+        return sum(s.live_count() for s in self.shards)
+
+    def startWave(self):
+        return np.concatenate([s.startWave() for s in self.shards])
+
+    def export(self):
+        parts = [s.export() for s in self.shards]
+        verts, edges = {}, {}
+        for p in parts:
+            assert not (verts.keys() & p.vertices.keys()), "a shadow on two shards"
+            verts.update(p.vertices)
+            assert not (edges.keys() & p.edges.keys()), "an edge on two shards"
+            edges.update(p.edges)
+        return GraphState(verts, edges)

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "crgc_host.hpp"
+#include "crgc_transport.hpp"
 
 using namespace crgc;
 
@@ -45,17 +46,21 @@ void free_arrays(Arrays &a) {
                 d.enew, d.pool, d.etab, d.edelta, d.vis, d.front[0], d.front[1],
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill, d.fbits[0], d.fbits[1],
-                d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.fx, d.tq, d.tl_buf, d.tl_tag};
+                d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.fx, d.tq, d.tl_buf, d.tl_tag,
+                d.xp_buf, d.xp_cnt, d.rq_buf, d.rq_cnt};
   for (void *p : ps)
     if (p) hipFree(p);
   a.allocated = false;
   a.d = DevGraph{};
 }
 
-hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s) {
+hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, uint32_t n_shards,
+                        uint32_t shard) {
   a.caps = c;
   DevGraph &d = a.d;
   d = DevGraph{};
+  d.n_shards = n_shards;
+  d.shard = shard;
   // slots are u32 below SLOT_DEAD, and reverse candidates keep bit 31 (RC_POS)
   if (c.scap >= (1ull << 31)) return hipErrorOutOfMemory;
   d.hcap = c.hcap;
@@ -116,6 +121,12 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s) 
   A(dmalloc(&d.tq, 2 * (uint64_t)TAIL_QCAP));
   A(dmalloc(&d.tl_buf, c.scap));
   A(dmalloc(&d.tl_tag, c.scap / BLK_SLOTS));
+  if (n_shards > 1) {
+    A(dmalloc(&d.xp_buf, c.scap));
+    A(dmalloc(&d.xp_cnt, c.scap / BLK_SLOTS));
+    A(dmalloc(&d.rq_buf, c.scap));
+    A(dmalloc(&d.rq_cnt, c.scap / BLK_SLOTS));
+  }
 #undef A
   a.allocated = true;
   // Default state of every unused slot / bucket.
@@ -142,6 +153,10 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s) 
   hipMemsetAsync(d.rcap, 0, c.scap * 4, s);
   hipMemsetAsync(d.rnew, 0, c.scap * 4, s);
   hipMemsetAsync(d.fx, 0, c.scap / 8, s);
+  if (n_shards > 1) {
+    hipMemsetAsync(d.xp_cnt, 0, c.scap / BLK_SLOTS * 4, s);
+    hipMemsetAsync(d.rq_cnt, 0, c.scap / BLK_SLOTS * 4, s);
+  }
   return hipGetLastError();
 }
 
@@ -181,9 +196,15 @@ struct crgc_graph {
   crgc_trace_stats last_stats{};
   bool have_last = false;
   uint64_t last_levels = 0;
-  std::vector<hipEvent_t> lvl_ev;  // per-level-kernel event pairs
+  std::vector<hipEvent_t> lvl_ev;  // 4 per level launch: k_frontier | k_tail | k_expand |
   uint64_t *roots_buf = nullptr;
   uint64_t roots_cap = 0;
+  // sharded graphs (G > 1): transport and exchange buffers
+  crgc_transport *tp = nullptr;
+  uint32_t G = 1, shard = 0;
+  uint64_t n_proxy = 0;              // alive proxy slots at the last sweep
+  Scratch x_send, x_slot, x_recv, x_ans, x_ans_back, x_small, x_pack, x_pack_recv;
+  uint64_t *h_small = nullptr;       // pinned host staging for small all-gathers
 };
 
 namespace {
@@ -248,7 +269,7 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms) {
       std::min<uint64_t>(src_top, h->live + (h->hctr->inserted - h->inserted_at_trace));
   Caps c = caps_for(std::max<uint64_t>(live_ub, 1), h->etab_used, ids, atoms);
   Arrays dst;
-  HIP_TRY(alloc_arrays(dst, c, h->ctr, h->stream));
+  HIP_TRY(alloc_arrays(dst, c, h->ctr, h->stream, h->G, h->shard));
   Scratch tmp;
   const size_t need = Carver::need({src_top * 4 + 4, c.scap * 8, rebuild_scan_tmp_bytes(c.scap)});
   if (tmp.ensure(need) != hipSuccess) {
@@ -352,6 +373,17 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
   h->device = cfg ? cfg->device : 0;
   h->F = (cfg && cfg->entry_field_size) ? cfg->entry_field_size : 4;
   h->DGS = (cfg && cfg->delta_graph_size) ? cfg->delta_graph_size : 64;
+  if (cfg && cfg->n_shards > 1) {
+    if (cfg->n_shards > MAX_SHARDS || cfg->shard >= cfg->n_shards || !cfg->transport ||
+        cfg->transport->n_shards != cfg->n_shards ||
+        !cfg->transport->accepts(cfg->shard, cfg->device)) {
+      delete h;
+      return CRGC_E_INVAL;
+    }
+    h->G = cfg->n_shards;
+    h->shard = cfg->shard;
+    h->tp = cfg->transport;
+  }
   DeviceGuard dg(h->device);
   int rc = CRGC_OK;
   do {
@@ -368,7 +400,9 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
       if (hipEventCreate(&e) != hipSuccess) rc = CRGC_E_DEVICE;
     if (rc) break;
     if (hipMalloc(&h->ctr, sizeof(Counters)) != hipSuccess ||
-        hipHostMalloc(&h->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc(&h->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&h->h_small, 8 * (size_t)MAX_SHARDS * (MAX_SHARDS + 8), hipHostMallocDefault) !=
+            hipSuccess) {
       rc = CRGC_E_NOMEM;
       break;
     }
@@ -377,7 +411,7 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     const uint64_t v0 = cfg && cfg->vertex_capacity ? cfg->vertex_capacity : (1u << 16);
     const uint64_t e0 = cfg && cfg->edge_capacity ? cfg->edge_capacity : 8 * v0;
     Caps c = caps_for(v0, e0, v0, e0);
-    if (hipError_t e = alloc_arrays(h->g, c, h->ctr, h->stream)) {
+    if (hipError_t e = alloc_arrays(h->g, c, h->ctr, h->stream, h->G, h->shard)) {
       rc = map_hip(e);
       break;
     }
@@ -398,8 +432,12 @@ void crgc_destroy(crgc_graph *h) {
   free_arrays(h->g);
   h->stage.release();
   h->work.release();
+  for (Scratch *x : {&h->x_send, &h->x_slot, &h->x_recv, &h->x_ans, &h->x_ans_back, &h->x_small,
+                     &h->x_pack, &h->x_pack_recv})
+    x->release();
   if (h->ctr) hipFree(h->ctr);
   if (h->hctr) hipHostFree(h->hctr);
+  if (h->h_small) hipHostFree(h->h_small);
   if (h->roots_buf) hipFree(h->roots_buf);
   for (auto &e : h->ev)
     if (e) hipEventDestroy(e);
@@ -436,37 +474,202 @@ static size_t edge_scratch(uint64_t max_atoms) {
                        max_atoms * 4, max_atoms * 4, max_atoms * 4, max_atoms * 4, max_atoms * 8});
 }
 
-int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
-  if (int rc = check_graph(h)) return rc;
+}  // extern "C"
+
+namespace {
+// ---- sharded graphs: collective helpers ---------------------------------------
+// All-gather K u64 per shard: `parts` device sources concatenated -> out[G*K] (host).
+static int ag_u64(crgc_graph *h, std::initializer_list<std::pair<const void *, uint32_t>> parts,
+                  uint64_t *out) {
+  uint32_t K = 0;
+  for (auto &p : parts) K += p.second;
+  const size_t bytes = (size_t)K * 8;
+  if (h->x_small.ensure(bytes * (h->G + 1)) != hipSuccess) return CRGC_E_NOMEM;
+  char *snd = (char *)h->x_small.ptr, *rcv = snd + bytes;
+  size_t at = 0;
+  for (auto &p : parts) {
+    HIP_TRY(hipMemcpyAsync(snd + at, p.first, (size_t)p.second * 8, hipMemcpyDefault, h->stream));
+    at += (size_t)p.second * 8;
+  }
+  if (int rc = h->tp->allgather(h->shard, snd, rcv, bytes, h->stream)) {
+    h->poisoned = true;
+    return rc;
+  }
+  HIP_TRY(hipMemcpyAsync(h->h_small, rcv, bytes * h->G, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  memcpy(out, h->h_small, bytes * h->G);
+  return CRGC_OK;
+}
+
+// All-gather K host u64 per shard -> out[G*K] (host).
+static int ag_host(crgc_graph *h, const uint64_t *vals, uint32_t K, uint64_t *out) {
+  memcpy(h->h_small, vals, (size_t)K * 8);
+  if (h->x_small.ensure((size_t)K * 8 * (h->G + 2)) != hipSuccess) return CRGC_E_NOMEM;
+  char *tmp = (char *)h->x_small.ptr + (size_t)K * 8 * (h->G + 1);
+  HIP_TRY(hipMemcpyAsync(tmp, h->h_small, (size_t)K * 8, hipMemcpyHostToDevice, h->stream));
+  return ag_u64(h, {{tmp, K}}, out);
+}
+
+// Exchange by a count matrix M (M[r*G + d] = items r sends d, `elem` bytes
+// each): send holds this shard's items grouped by destination in shard order;
+// recv gets every source's items for this shard, in source order.
+// transpose = true runs the reverse direction (answers back to the askers).
+static int a2a(crgc_graph *h, const void *send, const uint64_t *M, size_t elem, Scratch &recv,
+               bool transpose, uint64_t *n_recv) {
+  const uint32_t G = h->G, me = h->shard;
+  auto cnt = [&](uint32_t from, uint32_t to) { return transpose ? M[to * G + from] : M[from * G + to]; };
+  size_t soff[MAX_SHARDS], sb[MAX_SHARDS], roff[MAX_SHARDS], rb[MAX_SHARDS];
+  size_t so = 0, ro = 0;
+  for (uint32_t r = 0; r < G; ++r) {
+    soff[r] = so;
+    sb[r] = cnt(me, r) * elem;
+    so += sb[r];
+    roff[r] = ro;
+    rb[r] = cnt(r, me) * elem;
+    ro += rb[r];
+  }
+  if (recv.ensure(ro + 8) != hipSuccess) return CRGC_E_NOMEM;
+  if (int rc = h->tp->alltoallv(h->shard, send, soff, sb, recv.ptr, roff, rb, h->stream)) {
+    h->poisoned = true;
+    return rc;
+  }
+  *n_recv = ro / elem;
+  return CRGC_OK;
+}
+
+// ---- batch packing (sharded merges all-gather the shards' batches) ----------
+struct Layout {
+  size_t off[11];
+  size_t size[11];
+  size_t total;
+};
+
+static Layout make_layout(std::initializer_list<size_t> sizes) {
+  Layout l{};
+  size_t o = 0;
+  int i = 0;
+  for (size_t s : sizes) {
+    o = (o + 255) & ~(size_t)255;
+    l.off[i] = o;
+    l.size[i] = s;
+    o += s;
+    ++i;
+  }
+  l.total = (o + 255) & ~(size_t)255;  // shards' blocks sit back to back: keep them aligned
+  return l;
+}
+
+static Layout entry_layout(uint64_t n, uint64_t C, uint64_t S, uint64_t U) {
+  return make_layout({n * 8, n * 2, n, (n + 1) * 4, C * 8, C * 8, (n + 1) * 4, S * 8, (n + 1) * 4,
+                      U * 8, U * 2});
+}
+
+static Layout delta_layout(uint64_t n, uint64_t nout) {
+  return make_layout({n * 8, n * 4, n * 8, n, (n + 1) * 4, nout * 8, nout * 4});
+}
+
+static int pack(crgc_graph *h, const Layout &l, const void *const *src, int narr, uint32_t memory,
+                char *dst) {
+  const hipMemcpyKind k = memory == CRGC_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  for (int i = 0; i < narr; ++i)
+    if (l.size[i]) HIP_TRY(hipMemcpyAsync(dst + l.off[i], src[i], l.size[i], k, h->stream));
+  return CRGC_OK;
+}
+
+// All-gather the shards' packed batches: vals = per-shard header (status
+// first), returns the G headers and the packed bytes of every shard, in shard
+// order, in x_pack_recv (offsets in roff).
+template <class LayoutOf>
+static int gather_batches(crgc_graph *h, const uint64_t *hdr, uint32_t K, const void *const *src,
+                          int narr, uint32_t memory, LayoutOf layout_of, std::vector<uint64_t> &H,
+                          std::vector<size_t> &roff) {
+  const uint32_t G = h->G;
+  H.assign((size_t)G * K, 0);
+  if (int rc = ag_host(h, hdr, K, H.data())) return rc;
+  // every shard learns every shard's validation verdict: all fail together
+  const int mine_rc = (int)(int64_t)H[(size_t)h->shard * K];
+  for (uint32_t r = 0; r < G; ++r)
+    if ((int64_t)H[(size_t)r * K] != 0) return mine_rc ? mine_rc : CRGC_E_INVAL;
+  const Layout mine = layout_of(&H[(size_t)h->shard * K]);
+  size_t soff[MAX_SHARDS], sb[MAX_SHARDS], rb[MAX_SHARDS];
+  roff.assign(G, 0);
+  size_t tot = 0;
+  for (uint32_t r = 0; r < G; ++r) {
+    soff[r] = 0;
+    sb[r] = mine.total;
+    roff[r] = tot;
+    rb[r] = layout_of(&H[(size_t)r * K]).total;
+    tot += rb[r];
+  }
+  if (h->x_pack.ensure(mine.total) != hipSuccess || h->x_pack_recv.ensure(tot) != hipSuccess)
+    return CRGC_E_NOMEM;
+  if (int rc = pack(h, mine, src, narr, memory, (char *)h->x_pack.ptr)) return rc;
+  if (int rc = h->tp->alltoallv(h->shard, h->x_pack.ptr, soff, sb, h->x_pack_recv.ptr, roff.data(), rb,
+                                h->stream)) {
+    h->poisoned = true;
+    return rc;
+  }
+  return CRGC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Validates an entry batch and learns its record counts (exact for host
+// batches; for device batches too when `exact`, by reading the last offsets).
+static int entry_counts(crgc_graph *h, const crgc_entry_batch *b, bool exact, uint64_t *C, uint64_t *S,
+                        uint64_t *U) {
   if (!b || b->memory > CRGC_MEM_DEVICE) return CRGC_E_INVAL;
   const uint64_t n = b->n_entries;
+  *C = *S = *U = 0;
   if (n == 0) return CRGC_OK;
   if (n >= (1ull << 31) / (h->F + 1)) return CRGC_E_INVAL;
-  if (!b->self || !b->recv_count || !b->flags || !b->created_off || !b->spawned_off ||
-      !b->updated_off)
+  if (!b->self || !b->recv_count || !b->flags || !b->created_off || !b->spawned_off || !b->updated_off)
     return CRGC_E_INVAL;
-  DeviceGuard dg(h->device);
-  uint64_t C, S, U;
   if (b->memory == CRGC_MEM_HOST) {
-    C = b->created_off[n];
-    S = b->spawned_off[n];
-    U = b->updated_off[n];
+    *C = b->created_off[n];
+    *S = b->spawned_off[n];
+    *U = b->updated_off[n];
     if (b->created_off[0] || b->spawned_off[0] || b->updated_off[0]) return CRGC_E_INVAL;
-    if (C > n * h->F || S > n * h->F || U > n * h->F) return CRGC_E_INVAL;
+  } else if (exact) {
+    uint32_t v[3] = {0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(&v[0], b->created_off + n, 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(&v[1], b->spawned_off + n, 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(&v[2], b->updated_off + n, 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    *C = v[0];
+    *S = v[1];
+    *U = v[2];
   } else {
-    C = S = U = n * h->F;  // bounds; kernels read the exact offsets
+    *C = *S = *U = n * h->F;  // bounds; kernels read the exact offsets
+    return CRGC_OK;
   }
+  if (*C > n * h->F || *S > n * h->F || *U > n * h->F) return CRGC_E_INVAL;
+  if ((*C && (!b->created_owner || !b->created_target)) || (*S && !b->spawned) ||
+      (*U && (!b->updated_ref || !b->updated_info)))
+    return CRGC_E_INVAL;
+  return CRGC_OK;
+}
+
+// One batch into this shard (every record applied by its home shard).
+static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t C, uint64_t S,
+                             uint64_t U) {
+  const uint64_t n = b->n_entries;
+  if (n == 0) return CRGC_OK;
   const uint64_t ids = n + 2 * C + S + U;
   const uint64_t max_atoms = n * 2 * (uint64_t)h->F;
   if (int rc = ensure_capacity(h, ids, C + U)) return rc;
 
   const size_t host_bytes =
       b->memory == CRGC_MEM_HOST
-          ? Carver::need({n * 8, n * 2, n, (n + 1) * 4, C * 8, C * 8, (n + 1) * 4, S * 8,
-                          (n + 1) * 4, U * 8, U * 2})
+          ? Carver::need({n * 8, n * 2, n, (n + 1) * 4, C * 8, C * 8, (n + 1) * 4, S * 8, (n + 1) * 4,
+                          U * 8, U * 2})
           : 0;
+  const bool sh = h->G > 1;
   const size_t work_bytes =
-      Carver::need({n * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4}) +
+      Carver::need({n * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4, sh ? n : 0,
+                    sh ? n * h->F * 8 : 0}) +
       edge_scratch(max_atoms);
   if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
     return CRGC_E_NOMEM;
@@ -491,6 +694,10 @@ int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
   a.ct_slot = wc.take<uint32_t>(n * h->F);
   a.co_slot = wc.take<uint32_t>(n * h->F);
   a.u_slot = wc.take<uint32_t>(n * h->F);
+  if (sh) {
+    a.self_need = wc.take<uint8_t>(n);
+    a.u_partner = wc.take<uint64_t>(n * h->F);
+  }
   a.atom_o = wc.take<uint32_t>(max_atoms);
   a.atom_t = wc.take<uint32_t>(max_atoms);
   a.atom_d = wc.take<int32_t>(max_atoms);
@@ -501,30 +708,80 @@ int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
   return CRGC_OK;
 }
 
-int crgc_merge_deltas(crgc_graph *h, const crgc_delta_batch *b) {
+int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
   if (int rc = check_graph(h)) return rc;
+  DeviceGuard dg(h->device);
+  uint64_t C = 0, S = 0, U = 0;
+  const int vrc = entry_counts(h, b, h->G > 1, &C, &S, &U);
+  if (h->G <= 1) return vrc ? vrc : merge_entries_one(h, b, C, S, U);
+  // Sharded: every shard applies its part of every shard's batch, in shard order.
+  const uint64_t n = vrc ? 0 : b->n_entries;
+  const uint64_t hdr[5] = {(uint64_t)(int64_t)vrc, n, C, S, U};
+  const void *arr[11] = {b ? b->self : nullptr,        b ? b->recv_count : nullptr,
+                         b ? b->flags : nullptr,       b ? b->created_off : nullptr,
+                         b ? b->created_owner : nullptr, b ? b->created_target : nullptr,
+                         b ? b->spawned_off : nullptr, b ? b->spawned : nullptr,
+                         b ? b->updated_off : nullptr, b ? b->updated_ref : nullptr,
+                         b ? b->updated_info : nullptr};
+  std::vector<uint64_t> H;
+  std::vector<size_t> roff;
+  auto lay = [](const uint64_t *x) { return entry_layout(x[1], x[2], x[3], x[4]); };
+  if (int rc = gather_batches(h, hdr, 5, arr, n ? 11 : 0, b ? b->memory : CRGC_MEM_HOST, lay, H, roff))
+    return rc;
+  for (uint32_t r = 0; r < h->G; ++r) {
+    const uint64_t *x = &H[(size_t)r * 5];
+    if (!x[1]) continue;
+    const Layout l = lay(x);
+    char *base = (char *)h->x_pack_recv.ptr + roff[r];
+    crgc_entry_batch v{};
+    v.n_entries = x[1];
+    v.self = (const uint64_t *)(base + l.off[0]);
+    v.recv_count = (const int16_t *)(base + l.off[1]);
+    v.flags = (const uint8_t *)(base + l.off[2]);
+    v.created_off = (const uint32_t *)(base + l.off[3]);
+    v.created_owner = (const uint64_t *)(base + l.off[4]);
+    v.created_target = (const uint64_t *)(base + l.off[5]);
+    v.spawned_off = (const uint32_t *)(base + l.off[6]);
+    v.spawned = (const uint64_t *)(base + l.off[7]);
+    v.updated_off = (const uint32_t *)(base + l.off[8]);
+    v.updated_ref = (const uint64_t *)(base + l.off[9]);
+    v.updated_info = (const int16_t *)(base + l.off[10]);
+    v.memory = CRGC_MEM_DEVICE;
+    if (int rc = merge_entries_one(h, &v, x[2], x[3], x[4])) return rc;
+  }
+  return CRGC_OK;
+}
+
+static int delta_counts(crgc_graph *h, const crgc_delta_batch *b, uint64_t *nout) {
   if (!b || b->memory > CRGC_MEM_DEVICE) return CRGC_E_INVAL;
   const uint64_t n = b->n_shadows;
+  *nout = 0;
   if (n == 0) return CRGC_OK;
   if (!b->id || !b->recv_count || !b->supervisor || !b->flags || !b->out_off) return CRGC_E_INVAL;
-  DeviceGuard dg(h->device);
-  uint64_t nout;
   if (b->memory == CRGC_MEM_HOST) {
     if (b->out_off[0]) return CRGC_E_INVAL;
-    nout = b->out_off[n];
+    *nout = b->out_off[n];
   } else {
     uint32_t v = 0;
     HIP_TRY(hipMemcpy(&v, b->out_off + n, 4, hipMemcpyDeviceToHost));
-    nout = v;
+    *nout = v;
   }
+  if (*nout && (!b->out_target || !b->out_count)) return CRGC_E_INVAL;
+  return CRGC_OK;
+}
+
+static int merge_deltas_one(crgc_graph *h, const crgc_delta_batch *b, uint64_t nout) {
+  const uint64_t n = b->n_shadows;
+  if (n == 0) return CRGC_OK;
   const uint64_t ids = 2 * n + nout;
   if (int rc = ensure_capacity(h, ids, nout)) return rc;
   const size_t host_bytes =
-      b->memory == CRGC_MEM_HOST
-          ? Carver::need({n * 8, n * 4, n * 8, n, (n + 1) * 4, nout * 8, nout * 4})
-          : 0;
+      b->memory == CRGC_MEM_HOST ? Carver::need({n * 8, n * 4, n * 8, n, (n + 1) * 4, nout * 8, nout * 4})
+                                 : 0;
+  const bool sh = h->G > 1;
   const size_t work_bytes =
-      Carver::need({n * 4, n * 4, std::max<uint64_t>(nout, 1) * 4}) + edge_scratch(nout);
+      Carver::need({n * 4, n * 4, std::max<uint64_t>(nout, 1) * 4, sh ? std::max<uint64_t>(nout, 1) * 8 : 0}) +
+      edge_scratch(nout);
   if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
     return CRGC_E_NOMEM;
   Carver sc(h->stage.ptr), wc(h->work.ptr);
@@ -541,6 +798,7 @@ int crgc_merge_deltas(crgc_graph *h, const crgc_delta_batch *b) {
   a.self_slot = wc.take<uint32_t>(n);
   a.sup_slot = wc.take<uint32_t>(n);
   a.ot_slot = wc.take<uint32_t>(std::max<uint64_t>(nout, 1));
+  if (sh) a.o_partner = wc.take<uint64_t>(std::max<uint64_t>(nout, 1));
   a.atom_o = wc.take<uint32_t>(std::max<uint64_t>(nout, 1));
   a.atom_t = wc.take<uint32_t>(std::max<uint64_t>(nout, 1));
   a.atom_d = wc.take<int32_t>(std::max<uint64_t>(nout, 1));
@@ -550,65 +808,153 @@ int crgc_merge_deltas(crgc_graph *h, const crgc_delta_batch *b) {
   return CRGC_OK;
 }
 
+int crgc_merge_deltas(crgc_graph *h, const crgc_delta_batch *b) {
+  if (int rc = check_graph(h)) return rc;
+  DeviceGuard dg(h->device);
+  uint64_t nout = 0;
+  const int vrc = delta_counts(h, b, &nout);
+  if (h->G <= 1) return vrc ? vrc : merge_deltas_one(h, b, nout);
+  const uint64_t n = vrc ? 0 : b->n_shadows;
+  const uint64_t hdr[3] = {(uint64_t)(int64_t)vrc, n, nout};
+  const void *arr[7] = {b ? b->id : nullptr,      b ? b->recv_count : nullptr, b ? b->supervisor : nullptr,
+                        b ? b->flags : nullptr,   b ? b->out_off : nullptr,    b ? b->out_target : nullptr,
+                        b ? b->out_count : nullptr};
+  std::vector<uint64_t> H;
+  std::vector<size_t> roff;
+  auto lay = [](const uint64_t *x) { return delta_layout(x[1], x[2]); };
+  if (int rc = gather_batches(h, hdr, 3, arr, n ? 7 : 0, b ? b->memory : CRGC_MEM_HOST, lay, H, roff))
+    return rc;
+  for (uint32_t r = 0; r < h->G; ++r) {
+    const uint64_t *x = &H[(size_t)r * 3];
+    if (!x[1]) continue;
+    const Layout l = lay(x);
+    char *base = (char *)h->x_pack_recv.ptr + roff[r];
+    crgc_delta_batch v{};
+    v.n_shadows = x[1];
+    v.id = (const uint64_t *)(base + l.off[0]);
+    v.recv_count = (const int32_t *)(base + l.off[1]);
+    v.supervisor = (const uint64_t *)(base + l.off[2]);
+    v.flags = (const uint8_t *)(base + l.off[3]);
+    v.out_off = (const uint32_t *)(base + l.off[4]);
+    v.out_target = (const uint64_t *)(base + l.off[5]);
+    v.out_count = (const int32_t *)(base + l.off[6]);
+    v.memory = CRGC_MEM_DEVICE;
+    if (int rc = merge_deltas_one(h, &v, x[2])) return rc;
+  }
+  return CRGC_OK;
+}
+
+// mergeUndoLog.  Sharded graphs: collective, every shard passes the same log.
 int crgc_merge_undo(crgc_graph *h, const crgc_undo_log *log) {
   if (int rc = check_graph(h)) return rc;
-  if (!log || log->memory != CRGC_MEM_HOST) return CRGC_E_INVAL;
-  const uint64_t n = log->n_fields;
-  if (n && (!log->actor || !log->message_count || !log->created_off)) return CRGC_E_INVAL;
-  if (n && log->created_off[0]) return CRGC_E_INVAL;
   DeviceGuard dg(h->device);
-  const uint64_t nc = n ? log->created_off[n] : 0;
-  {
-    // UndoLog.admitted is a map: one field per actor.
-    std::vector<uint64_t> ids(log->actor, log->actor + n);
-    std::sort(ids.begin(), ids.end());
-    if (std::adjacent_find(ids.begin(), ids.end()) != ids.end()) return CRGC_E_INVAL;
+  int vrc = CRGC_OK;
+  uint64_t n = 0, nc = 0;
+  if (!log || log->memory != CRGC_MEM_HOST) {
+    vrc = CRGC_E_INVAL;
+  } else {
+    n = log->n_fields;
+    if (n && (!log->actor || !log->message_count || !log->created_off)) vrc = CRGC_E_INVAL;
+    else if (n && log->created_off[0]) vrc = CRGC_E_INVAL;
+    else {
+      nc = n ? log->created_off[n] : 0;
+      if (nc && (!log->created_target || !log->created_count)) vrc = CRGC_E_INVAL;
+      // UndoLog.admitted is a map: one field per actor.
+      std::vector<uint64_t> ids(log->actor, log->actor + n);
+      std::sort(ids.begin(), ids.end());
+      if (std::adjacent_find(ids.begin(), ids.end()) != ids.end()) vrc = CRGC_E_INVAL;
+    }
   }
-  if (int rc = ensure_capacity(h, 0, nc)) return rc;
-  const size_t host_bytes = Carver::need({n * 8, n * 4, (n + 1) * 4, nc * 8, nc * 4});
-  const size_t work_bytes = edge_scratch(nc);
+  if (h->G > 1) {  // agree on validity before any collective work
+    const uint64_t st = (uint64_t)(int64_t)vrc;
+    std::vector<uint64_t> all(h->G);
+    if (int rc = ag_host(h, &st, 1, all.data())) return rc;
+    for (uint64_t v : all)
+      if (v) return vrc ? vrc : CRGC_E_INVAL;
+  } else if (vrc) {
+    return vrc;
+  }
+  if (int rc = ensure_capacity(h, nc, nc)) return rc;
+  std::vector<uint64_t> c_actor(nc);
+  for (uint64_t i = 0; i < n; ++i)
+    for (uint32_t k = log->created_off[i]; k < log->created_off[i + 1]; ++k) c_actor[k] = log->actor[i];
+  const size_t host_bytes = Carver::need({n * 8, n * 4, (n + 1) * 4, nc * 8, nc * 4, nc * 8});
+  const size_t work_bytes = edge_scratch(nc) + Carver::need({n + nc + 8});
   if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
     return CRGC_E_NOMEM;
   Carver sc(h->stage.ptr), wc(h->work.ptr);
   UndoArgs a{};
   a.n = n;
+  a.nc = nc;
   a.location = log->node_location;
   a.actor = stage(h, sc, log->actor, n, CRGC_MEM_HOST);
   a.msg = stage(h, sc, log->message_count, n, CRGC_MEM_HOST);
   a.c_off = stage(h, sc, log->created_off, n + 1, CRGC_MEM_HOST);
   a.c_target = stage(h, sc, log->created_target, nc, CRGC_MEM_HOST);
   a.c_count = stage(h, sc, log->created_count, nc, CRGC_MEM_HOST);
+  a.c_actor = stage(h, sc, c_actor.data(), nc, CRGC_MEM_HOST);
+  a.exists = wc.take<uint8_t>(n + nc + 8);
   a.atom_o = wc.take<uint32_t>(std::max<uint64_t>(nc, 1));
   a.atom_t = wc.take<uint32_t>(std::max<uint64_t>(nc, 1));
   a.atom_d = wc.take<int32_t>(std::max<uint64_t>(nc, 1));
-  // Detect the reference's ConcurrentModificationException before mutating.
-  HIP_TRY(launch_undo_check(h->g.d, a, h->stream));
-  HIP_TRY(sync_counters(h));
-  if (h->hctr->err & ERR_UNDO_NEW) {
-    const unsigned long long clear = 0;
-    // leave the graph usable: clear only the undo bit
-    h->hctr->err &= ~(unsigned long long)ERR_UNDO_NEW;
-    HIP_TRY(hipMemcpyAsync((char *)h->ctr + CTR_OFF(err), &h->hctr->err, 8, hipMemcpyHostToDevice,
-                           h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    (void)clear;
-    return CRGC_E_UNDO_NEW_SHADOW;
+  // The reference's ConcurrentModificationException, detected
+  // before any mutation: an admitted actor in the graph names a target that is not.
+  std::vector<uint8_t> ex(n + nc, 0);
+  if (n + nc) {
+    HIP_TRY(launch_undo_check(h->g.d, a, h->stream));
+    if (h->G > 1) {
+      const size_t words = (n + nc + 7) / 8;
+      std::vector<uint64_t> all(words * h->G);
+      if (h->x_ans.ensure(words * 8) != hipSuccess) return CRGC_E_NOMEM;
+      HIP_TRY(hipMemsetAsync(h->x_ans.ptr, 0, words * 8, h->stream));
+      HIP_TRY(hipMemcpyAsync(h->x_ans.ptr, a.exists, n + nc, hipMemcpyDeviceToDevice, h->stream));
+      if (words > MAX_SHARDS + 8) {  // beyond the small-gather staging: a direct exchange
+        if (h->x_ans_back.ensure(words * 8 * h->G) != hipSuccess) return CRGC_E_NOMEM;
+        if (int rc = h->tp->allgather(h->shard, h->x_ans.ptr, h->x_ans_back.ptr, words * 8, h->stream)) {
+          h->poisoned = true;
+          return rc;
+        }
+        HIP_TRY(hipMemcpy(all.data(), h->x_ans_back.ptr, words * 8 * h->G, hipMemcpyDeviceToHost));
+      } else if (int rc = ag_u64(h, {{h->x_ans.ptr, (uint32_t)words}}, all.data())) {
+        return rc;
+      }
+      for (uint32_t r = 0; r < h->G; ++r) {
+        const uint8_t *p = (const uint8_t *)&all[(size_t)r * words];
+        for (uint64_t i = 0; i < n + nc; ++i) ex[i] |= p[i];
+      }
+    } else {
+      HIP_TRY(hipMemcpyAsync(ex.data(), a.exists, n + nc, hipMemcpyDeviceToHost, h->stream));
+      HIP_TRY(hipStreamSynchronize(h->stream));
+    }
   }
+  for (uint64_t i = 0; i < n; ++i) {
+    if (!ex[i]) continue;  // field ignored (:166-167)
+    for (uint32_t k = log->created_off[i]; k < log->created_off[i + 1]; ++k)
+      if (!ex[n + k]) return CRGC_E_UNDO_NEW_SHADOW;
+  }
+  HIP_TRY(sync_counters(h));
   if (int rc = device_error(h)) return rc;
   HIP_TRY(launch_undo_apply(h->g.d, a, h->slot_top, h->stream));
   if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, nc, wc)) return rc;
-  note_merge(h, 0, nc);
+  note_merge(h, nc, nc);
   return CRGC_OK;
 }
 
-// BFS driver shared by trace and count_reachable_from.  Every level kernel is
-// bracketed by its own event pair, so `kernel_ms` is device time of the level
-// kernels only (no host round-trip gaps).  Levels are enqueued in chunks; the
-// first chunk is as deep as the previous trace, so a steady-state wakeup needs
-// one host synchronisation.
-static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64_t top,
-                      uint64_t *levels, uint64_t *roots, double *kernel_ms, uint64_t *launches,
-                      uint64_t *depth = nullptr) {
+// ---- mark ---------------------------------------------------------------------
+struct LevelRun {
+  uint64_t levels = 0, roots = 0, launches = 0, depth = 0;
+  double ms = 0, ms_f = 0, ms_t = 0, ms_e = 0;
+};
+
+// Level-synchronous BFS from the pseudo-roots (roots = true, start = 0) or
+// from candidates of level `start` (sharded rounds), until a level is empty.
+// Every level is bracketed by events between its three kernels, so the
+// timings are device time of each level kernel.  Levels are enqueued in
+// chunks; the first chunk of a trace is as deep as the previous trace, so a
+// steady-state wakeup needs one host synchronisation.  *end = the first empty
+// level (levels start .. *end-1 were non-empty).
+static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64_t top, bool roots,
+                      int start, LevelRun &lr, int *end) {
   LevelArgs la{};
   la.location = location;
   // Tuning switch for A/B runs (results are identical either way).
@@ -644,28 +990,26 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   la.tail_max = std::min<uint32_t>(std::max(la.tail_max, 1u), TAIL_QCAP);
   size_t nl = 0;
   auto launch = [&](int level, bool rootk) -> hipError_t {
-    if (h->lvl_ev.size() < 2 * (nl + 1)) {
-      for (int k = 0; k < 2; ++k) {
-        hipEvent_t e;
-        hipError_t r = hipEventCreate(&e);
-        if (r != hipSuccess) return r;
-        h->lvl_ev.push_back(e);
-      }
+    while (h->lvl_ev.size() < 4 * (nl + 1)) {
+      hipEvent_t e;
+      hipError_t r = hipEventCreate(&e);
+      if (r != hipSuccess) return r;
+      h->lvl_ev.push_back(e);
     }
-    hipError_t r = hipEventRecord(h->lvl_ev[2 * nl], h->stream);
-    if (r != hipSuccess) return r;
     la.level = level;
-    r = launch_level(h->g.d, la, rootk, investigate, top, h->stream);
-    if (r != hipSuccess) return r;
-    r = hipEventRecord(h->lvl_ev[2 * nl + 1], h->stream);
+    hipError_t r = launch_level(h->g.d, la, rootk, investigate, top, h->stream, &h->lvl_ev[4 * nl]);
     ++nl;
     return r;
   };
-  HIP_TRY(launch(0, true));
-  int L = 1;
-  int chunk = (int)std::min<uint64_t>(std::max<uint64_t>(4, h->last_levels + 1), 512);
+  int L = start;
+  if (roots) {
+    HIP_TRY(launch(0, true));
+    L = 1;
+  }
+  int chunk = roots ? (int)std::min<uint64_t>(std::max<uint64_t>(4, h->last_levels + 1), 512) : 4;
   std::vector<unsigned long long> ring(LEVEL_RING);
   unsigned long long tail[3] = {0, 0, 0};
+  const bool log = getenv("CRGC_LEVEL_LOG") != nullptr;
   for (;;) {
     for (int k = 0; k < chunk; ++k) HIP_TRY(launch(L + k, false));
     // counts of levels L-1 .. L+chunk-1
@@ -680,7 +1024,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
     HIP_TRY(hipMemcpyAsync(tail, (char *)h->ctr + CTR_OFF(tail_state), 24, hipMemcpyDeviceToHost,
                            h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
-    if (first == 0) *roots = ring[0];
+    if (roots && first == 0) lr.roots = ring[0];
     if (tail[0] == TAIL_BAILED) {  // k_tail handed a wide frontier back: resume there
       HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(tail_state), 0, 8, h->stream));
       L = (int)tail[1];
@@ -688,46 +1032,91 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
     }
     for (int lv = first; lv <= last; ++lv) {
       if (tail[0] == TAIL_DONE || ring[lv % LEVEL_RING] == 0) {
-        // levels 0 .. lv-1 were non-empty
-        *levels = tail[0] == TAIL_DONE ? (uint64_t)tail[1] : (uint64_t)lv;
+        const int e = tail[0] == TAIL_DONE ? (int)tail[1] : lv;
+        *end = e;
+        lr.levels += (uint64_t)std::max(0, e - (roots ? 0 : start));
         // level launches that did work: the first chunk of the next trace
-        if (depth) *depth = tail[0] == TAIL_DONE ? (uint64_t)tail[2] + 1 : (uint64_t)lv;
-        double ms = 0;
-        const bool log = getenv("CRGC_LEVEL_LOG") != nullptr;
+        if (roots) lr.depth = tail[0] == TAIL_DONE ? (uint64_t)tail[2] + 1 : (uint64_t)lv;
         for (size_t i = 0; i < nl; ++i) {
-          float t = 0;
-          hipEventElapsedTime(&t, h->lvl_ev[2 * i], h->lvl_ev[2 * i + 1]);
-          ms += t;
+          float t[3] = {0, 0, 0};
+          for (int k = 0; k < 3; ++k) hipEventElapsedTime(&t[k], h->lvl_ev[4 * i + k], h->lvl_ev[4 * i + k + 1]);
+          lr.ms_f += t[0];
+          lr.ms_t += t[1];
+          lr.ms_e += t[2];
+          lr.ms += t[0] + t[1] + t[2];
           if (log)
-            fprintf(stderr, "[crgc] level %zu frontier %llu  %.1f us%s\n", i,
-                    i <= (size_t)last ? ring[i % LEVEL_RING] : 0ull, t * 1e3,
-                    (la.flags & LV_PULL) && i >= 1 && i <= (size_t)last &&
-                            ring[(i - 1) % LEVEL_RING] * std::max<uint64_t>(la.pull_div, 1) >=
-                                (la.pull_div ? h->slot_top : la.pull_thresh)
-                        ? " (pull?)"
-                        : "");
+            fprintf(stderr, "[crgc] level %zu frontier %llu  %.1f us (frontier %.1f tail %.1f expand %.1f)\n",
+                    (roots ? 0 : (size_t)start) + i,
+                    (roots ? 0 : (size_t)start) + i <= (size_t)last
+                        ? ring[((roots ? 0 : (size_t)start) + i) % LEVEL_RING]
+                        : 0ull,
+                    (t[0] + t[1] + t[2]) * 1e3, t[0] * 1e3, t[1] * 1e3, t[2] * 1e3);
         }
-        *kernel_ms = ms;
-        *launches = nl;
+        lr.launches += nl;
         return CRGC_OK;
       }
     }
     L += chunk;
     chunk = std::min(chunk * 2, 512);
-    if ((uint64_t)L > (1ull << 40)) return CRGC_E_TIMEOUT;
+    if ((uint64_t)L > (1ull << 19)) return CRGC_E_TIMEOUT;  // (level + 1) << 12 tags are 32-bit
   }
 }
 
 static void reset_trace_counters(crgc_graph *h) {
-  // marked .. n_out, and the level ring
+  // marked .. the level ring
   const size_t a = CTR_OFF(marked), b = sizeof(Counters);
   hipMemsetAsync((char *)h->ctr + a, 0, b - a, h->stream);
   const uint64_t top = h->slot_top + h->ids_since;
+  const uint64_t nblk = round_up(std::min<uint64_t>(top, h->g.caps.scap), BLK_SLOTS) / BLK_SLOTS;
   hipMemsetAsync(h->g.d.blkstat, 0, (size_t)STAT_WG * 4 * 8, h->stream);
   hipMemsetAsync(h->g.d.qn_tag, 0, h->g.caps.scap / BLK_SLOTS * 4, h->stream);
   hipMemsetAsync(h->g.d.tl_tag, 0, h->g.caps.scap / BLK_SLOTS * 4, h->stream);
-  hipMemsetAsync(h->g.d.vis, 0, round_up(std::min<uint64_t>(top, h->g.caps.scap), BLK_SLOTS) / 8,
-                 h->stream);
+  hipMemsetAsync(h->g.d.vis, 0, nblk * BLK_SLOTS / 8, h->stream);
+  if (h->G > 1) hipMemsetAsync(h->g.d.xp_cnt, 0, nblk * 4, h->stream);
+}
+
+// Mark to the global fixpoint: local levels, then (sharded graphs) rounds of
+// exporting newly marked proxies to their home shards and continuing from
+// what arrives, until no shard has anything to send.
+static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t top, LevelRun &lr,
+                    uint64_t *rounds, uint64_t *ids_sent, double *ms_x) {
+  int end = 0;
+  if (int rc = run_levels(h, investigate, location, top, true, 0, lr, &end)) return rc;
+  *rounds = 1;
+  if (h->G <= 1) return CRGC_OK;
+  const uint32_t G = h->G, me = h->shard;
+  const uint64_t nblk = round_up(std::min<uint64_t>(top, h->g.caps.scap), BLK_SLOTS) / BLK_SLOTS;
+  std::vector<uint64_t> M((size_t)G * G);
+  for (;;) {
+    const auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(xcnt), 0, 2 * MAX_SHARDS * 8, h->stream));
+    HIP_TRY(launch_list(h->g.d, 0, false, h->g.d.xp_buf, h->g.d.xp_cnt, nblk, nullptr, nullptr, h->stream));
+    if (int rc = ag_u64(h, {{(char *)h->ctr + CTR_OFF(xcnt), G}}, M.data())) return rc;
+    uint64_t total = 0, nsend = 0;
+    for (uint64_t v : M) total += v;
+    for (uint32_t d = 0; d < G; ++d) nsend += M[(size_t)me * G + d];
+    if (total == 0) {
+      *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      return CRGC_OK;
+    }
+    if (h->x_send.ensure(nsend * 8 + 8) != hipSuccess) return CRGC_E_NOMEM;
+    HIP_TRY(launch_list(h->g.d, 0, true, h->g.d.xp_buf, h->g.d.xp_cnt, nblk, (uint64_t *)h->x_send.ptr,
+                        nullptr, h->stream));
+    HIP_TRY(hipMemsetAsync(h->g.d.xp_cnt, 0, nblk * 4, h->stream));
+    uint64_t nrecv = 0;
+    if (int rc = a2a(h, h->x_send.ptr, M.data(), 8, h->x_recv, false, &nrecv)) return rc;
+    *ids_sent += nsend;
+    // received ids are candidates of level L (a sparse level after an empty one)
+    const int L = end + 2;
+    HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(ring) + ((L - 2) % LEVEL_RING) * 8, 0, 8, h->stream));
+    HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(ring) + ((L - 1) % LEVEL_RING) * 8, 0, 8, h->stream));
+    HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(tail_state), 0, 8, h->stream));
+    HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(qh) + (L & 1) * 8, 0, 8, h->stream));
+    HIP_TRY(launch_import(h->g.d, (const uint64_t *)h->x_recv.ptr, nrecv, L, h->stream));
+    *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (int rc = run_levels(h, investigate, location, top, false, L, lr, &end)) return rc;
+    ++*rounds;
+  }
 }
 
 static int copy_lists(crgc_graph *h, crgc_trace_out *out) {
@@ -752,53 +1141,134 @@ static int copy_lists(crgc_graph *h, crgc_trace_out *out) {
   return big ? CRGC_E2BIG : CRGC_OK;
 }
 
+// Sharded sweep: garbage whose supervisor is a proxy asks the supervisor's
+// home for its mark; every shard learns the NPE verdict before committing;
+// committed garbage invalidates the other shards' proxies of it.
+static int sweep_sharded(crgc_graph *h, int should_kill, uint64_t top, double *ms_x) {
+  const uint32_t G = h->G, me = h->shard;
+  const uint64_t nblk = round_up(std::min<uint64_t>(top, h->g.caps.scap), BLK_SLOTS) / BLK_SLOTS;
+  HIP_TRY(launch_sweep(h->g.d, should_kill, top, h->stream, 1));
+  HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(xcnt), 0, 2 * MAX_SHARDS * 8, h->stream));
+  HIP_TRY(launch_list(h->g.d, 1, false, h->g.d.rq_buf, h->g.d.rq_cnt, nblk, nullptr, nullptr, h->stream));
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<uint64_t> V((size_t)G * (G + 1));
+  if (int rc = ag_u64(h, {{(char *)h->ctr + CTR_OFF(npe), 1}, {(char *)h->ctr + CTR_OFF(xcnt), G}}, V.data()))
+    return rc;
+  uint64_t npe = 0;
+  std::vector<uint64_t> R((size_t)G * G);
+  for (uint32_t r = 0; r < G; ++r) {
+    npe += V[(size_t)r * (G + 1)];
+    for (uint32_t d = 0; d < G; ++d) R[(size_t)r * G + d] = V[(size_t)r * (G + 1) + 1 + d];
+  }
+  if (npe) {  // the reference's NullPointerException on some shard: nobody commits
+    HIP_TRY(hipMemcpyAsync((char *)h->ctr + CTR_OFF(npe), &npe, 8, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(launch_sweep(h->g.d, should_kill, top, h->stream, 2));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return CRGC_OK;
+  }
+  uint64_t nreq = 0;
+  for (uint32_t d = 0; d < G; ++d) nreq += R[(size_t)me * G + d];
+  uint64_t total_req = 0;
+  for (uint64_t v : R) total_req += v;
+  if (total_req) {
+    if (h->x_send.ensure(nreq * 8 + 8) != hipSuccess || h->x_slot.ensure(nreq * 4 + 8) != hipSuccess)
+      return CRGC_E_NOMEM;
+    HIP_TRY(launch_list(h->g.d, 1, true, h->g.d.rq_buf, h->g.d.rq_cnt, nblk, (uint64_t *)h->x_send.ptr,
+                        (uint32_t *)h->x_slot.ptr, h->stream));
+    uint64_t nin = 0, nback = 0;
+    if (int rc = a2a(h, h->x_send.ptr, R.data(), 8, h->x_recv, false, &nin)) return rc;
+    if (h->x_ans.ensure(nin + 8) != hipSuccess) return CRGC_E_NOMEM;
+    HIP_TRY(launch_requests(h->g.d, 0, (const uint64_t *)h->x_recv.ptr, nin, (uint8_t *)h->x_ans.ptr,
+                            nullptr, h->stream));
+    if (int rc = a2a(h, h->x_ans.ptr, R.data(), 1, h->x_ans_back, true, &nback)) return rc;
+  }
+  HIP_TRY(launch_sweep(h->g.d, should_kill, top, h->stream, 2));  // ids + commit
+  if (nreq)
+    HIP_TRY(launch_requests(h->g.d, 1, nullptr, nreq, (uint8_t *)h->x_ans_back.ptr,
+                            (const uint32_t *)h->x_slot.ptr, h->stream));
+  // the other shards' proxies of this shard's garbage die with it
+  std::vector<uint64_t> NG(G);
+  if (int rc = ag_u64(h, {{(char *)h->ctr + CTR_OFF(n_garbage), 1}}, NG.data())) return rc;
+  uint64_t tg = 0;
+  for (uint64_t v : NG) tg += v;
+  if (tg) {
+    size_t soff[MAX_SHARDS], sb[MAX_SHARDS], roff[MAX_SHARDS], rb[MAX_SHARDS];
+    size_t ro = 0;
+    for (uint32_t r = 0; r < G; ++r) {
+      soff[r] = 0;
+      sb[r] = NG[me] * 8;
+      roff[r] = ro;
+      rb[r] = NG[r] * 8;
+      ro += rb[r];
+    }
+    if (h->x_recv.ensure(ro + 8) != hipSuccess) return CRGC_E_NOMEM;
+    if (int rc = h->tp->alltoallv(me, h->g.d.out_ids, soff, sb, h->x_recv.ptr, roff, rb, h->stream)) {
+      h->poisoned = true;
+      return rc;
+    }
+    HIP_TRY(launch_invalidate(h->g.d, (const uint64_t *)h->x_recv.ptr, tg, h->stream));
+  }
+  *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return CRGC_OK;
+}
+
 int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   if (int rc = check_graph(h)) return rc;
   if (!out) return CRGC_E_INVAL;
   DeviceGuard dg(h->device);
   const auto t0 = std::chrono::steady_clock::now();
-  // Surface merge-time device errors before tracing.
   // Grids are sized from an upper bound of slot_top; the kernels read the
   // exact value from the device counters, so no synchronisation is needed here.
   const uint64_t top = h->slot_top + h->ids_since;
   reset_trace_counters(h);
-  uint64_t levels = 0, roots = 0, launches = 0, depth = 0;
-  double mark_ms = 0;
-  if (int rc = run_levels(h, false, 0, top, &levels, &roots, &mark_ms, &launches, &depth)) return rc;
+  LevelRun lr;
+  uint64_t rounds = 0, ids_sent = 0;
+  double ms_x = 0;
+  if (int rc = mark_all(h, false, 0, top, lr, &rounds, &ids_sent, &ms_x)) return rc;
   HIP_TRY(hipEventRecord(h->ev[1], h->stream));
   HIP_TRY(launch_trace_stats(h->g.d, h->stream));
-  HIP_TRY(launch_sweep(h->g.d, should_kill ? 1 : 0, top, h->stream));
-
+  if (h->G <= 1) {
+    HIP_TRY(launch_sweep(h->g.d, should_kill ? 1 : 0, top, h->stream));
+  } else if (int rc = sweep_sharded(h, should_kill ? 1 : 0, top, &ms_x)) {
+    return rc;
+  }
   HIP_TRY(hipEventRecord(h->ev[2], h->stream));
   HIP_TRY(sync_counters(h));
   const Counters &c = *h->hctr;
   if (c.npe) return CRGC_E_NULL_SUPERVISOR;  // commit skipped: graph unchanged
   if (int rc = device_error(h)) return rc;
   crgc_trace_stats st{};
-  st.pseudo_roots = 0;
   st.edges_scanned = c.edges_scanned;
   st.sup_edges = c.sup_edges;
-  st.levels = levels;
-  st.launches = launches;
-  st.ms_mark = mark_ms;
+  st.levels = lr.levels;
+  st.launches = lr.launches;
+  st.ms_mark = lr.ms;
+  st.ms_frontier = lr.ms_f;
+  st.ms_tail = lr.ms_t;
+  st.ms_expand = lr.ms_e;
+  st.rounds = rounds;
+  st.ids_sent = ids_sent;
+  st.ms_exchange = ms_x;
   float ms = 0;
   hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
   st.ms_sweep = ms;
-  st.pseudo_roots = roots;
+  st.pseudo_roots = lr.roots;
   h->last_garbage = c.n_garbage;
   h->last_kill = c.n_kill;
   h->last_live = c.n_live;
   h->live = c.n_live;
+  h->n_proxy = c.n_proxy;
   h->inserted_at_trace = c.inserted;
   h->have_last = true;
-  h->last_levels = depth;
+  h->last_levels = lr.depth;
   const int rc = copy_lists(h, out);
   st.ms_total =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   h->last_stats = st;
   out->stats = st;
   // Keep the slot space dense: rebuild once dead slots outnumber live ones.
-  if (rc == CRGC_OK && h->slot_top > 65536 && h->slot_top > 2 * h->live) {
+  if (rc == CRGC_OK && h->slot_top > 65536 && h->slot_top > 2 * (h->live + h->n_proxy)) {
     if (int r2 = rebuild(h, 0, 0)) return r2;
   }
   return rc;
@@ -845,16 +1315,28 @@ int crgc_count_reachable_from(crgc_graph *h, uint16_t location, int64_t *out) {
   HIP_TRY(sync_counters(h));
   if (int rc = device_error(h)) return rc;
   reset_trace_counters(h);
-  uint64_t levels = 0, roots = 0, launches = 0;
-  double ms = 0;
+  LevelRun lr;
+  uint64_t rounds = 0, sent = 0;
+  double ms_x = 0;
   const uint64_t saved = h->last_levels;
-  const int rl = run_levels(h, true, location, h->slot_top, &levels, &roots, &ms, &launches);
+  const int rl = mark_all(h, true, location, h->slot_top, lr, &rounds, &sent, &ms_x);
   h->last_levels = saved;
   if (rl) return rl;
-  HIP_TRY(sync_counters(h));
-  *out = (int64_t)h->hctr->marked;
+  if (h->G <= 1) {
+    HIP_TRY(sync_counters(h));
+    *out = (int64_t)h->hctr->marked;
+    return CRGC_OK;
+  }
+  HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(n_out), 0, 8, h->stream));
+  HIP_TRY(launch_count_marked(h->g.d, h->slot_top, h->stream));
+  std::vector<uint64_t> all(h->G);
+  if (int rc = ag_u64(h, {{(char *)h->ctr + CTR_OFF(n_out), 1}}, all.data())) return rc;
+  int64_t sum = 0;
+  for (uint64_t v : all) sum += (int64_t)v;
+  *out = sum;
   return CRGC_OK;
 }
+
 
 int crgc_total_actors_seen(crgc_graph *h, uint64_t *out) {
   if (!h || !out) return CRGC_E_INVAL;
@@ -873,8 +1355,8 @@ int crgc_live_count(crgc_graph *h, uint64_t *out) {
   std::vector<uint8_t> fl(h->slot_top);
   if (h->slot_top)
     HIP_TRY(hipMemcpy(fl.data(), h->g.d.flags, h->slot_top, hipMemcpyDeviceToHost));
-  uint64_t k = 0;
-  for (uint8_t f : fl) k += (f & FL_ALIVE) ? 1 : 0;
+  uint64_t k = 0;  // proxies stand for other shards' shadows
+  for (uint8_t f : fl) k += (f & (FL_ALIVE | FL_PROXY)) == FL_ALIVE ? 1 : 0;
   *out = k;
   return CRGC_OK;
 }
@@ -904,7 +1386,7 @@ int crgc_export(crgc_graph *h, crgc_graph_export *out) {
   uint64_t nv = 0, ne = 0;
   bool big = false;
   for (uint64_t v = 0; v < top; ++v) {
-    if (!(fl[v] & FL_ALIVE)) continue;
+    if ((fl[v] & (FL_ALIVE | FL_PROXY)) != FL_ALIVE) continue;  // this shard's shadows only
     if (out->id) {
       if (nv < out->vertex_cap) {
         out->id[nv] = vid[v];

@@ -59,6 +59,12 @@ struct IdSeg {
   uint64_t n;              // bound (grid sizing)
   const uint32_t *n_dev;   // exact count on the device (an offsets array's last entry), or null
   bool none_ok;            // CRGC_NO_ACTOR means "none" here (SLOT_INVALID, no error)
+  // Sharded graphs: an id is resolved on this shard when it is home here, or
+  // when partner[r] (an aligned id, CRGC_NO_ACTOR = none) is home here (the
+  // id is then the far end of a local edge / supervisor: a proxy), or when
+  // need[r] is set.  Both null: home only.
+  const uint64_t *partner;
+  const uint8_t *need;
 };
 struct IdArgs {
   IdSeg seg[5];
@@ -89,6 +95,9 @@ struct EntryArgs {
   uint32_t *atom_o;      // [2*n*F]: created atoms, then updated atoms
   uint32_t *atom_t;
   int32_t *atom_d;
+  // sharded graphs: filled by k_entries_shard_prep
+  uint8_t *self_need;    // [n]   self is home here or supervises a child homed here
+  uint64_t *u_partner;   // [n*F] self for a deactivating update, else CRGC_NO_ACTOR
 };
 
 struct DeltaArgs {
@@ -107,16 +116,19 @@ struct DeltaArgs {
   uint32_t *atom_o;
   uint32_t *atom_t;
   int32_t *atom_d;
+  uint64_t *o_partner;   // sharded graphs: [nout] owning delta shadow of each outgoing entry
 };
 
 struct UndoArgs {
-  uint64_t n;
+  uint64_t n, nc;
   uint16_t location;
   const uint64_t *actor;
   const int32_t *msg;
   const uint32_t *c_off;
   const uint64_t *c_target;
   const int32_t *c_count;
+  const uint64_t *c_actor;  // [nc] the admitted actor each created-ref entry belongs to
+  uint8_t *exists;          // [n + nc] existence of each actor / target at its home shard
   uint32_t *atom_o;
   uint32_t *atom_t;
   int32_t *atom_d;
@@ -164,12 +176,24 @@ hipError_t launch_undo_apply(const DevGraph &g, const UndoArgs &a, uint64_t slot
                              hipStream_t s);
 hipError_t launch_edges(const DevGraph &g, const EdgeArgs &a, hipStream_t s);
 
+// ev: null, or 4 events recorded before k_frontier, k_tail, k_expand and after
 hipError_t launch_level(const DevGraph &g, const LevelArgs &a, bool roots, bool investigate,
-                        uint64_t slot_top, hipStream_t s);
+                        uint64_t slot_top, hipStream_t s, hipEvent_t *ev = nullptr);
 hipError_t launch_trace_stats(const DevGraph &g, hipStream_t s);
 // sweep + id compaction + removal of the garbage (skipped on a reference NPE)
-hipError_t launch_sweep(const DevGraph &g, int should_kill, uint64_t slot_top, hipStream_t s);
+// phase 1: classify + counts (k_sweep, k_sweep_scan); phase 2: ids + commit
+// (k_sweep_gather); 3: both
+hipError_t launch_sweep(const DevGraph &g, int should_kill, uint64_t slot_top, hipStream_t s,
+                        int phase = 3);
 int level_grid(uint64_t slot_top);
+// sharded graphs
+hipError_t launch_list(const DevGraph &g, int mode, bool scatter, uint32_t *buf, uint32_t *cnt,
+                       uint64_t nblk, uint64_t *send, uint32_t *send_slot, hipStream_t s);
+hipError_t launch_import(const DevGraph &g, const uint64_t *ids, uint64_t n, int level, hipStream_t s);
+hipError_t launch_requests(const DevGraph &g, int phase, const uint64_t *ids, uint64_t n, uint8_t *ans,
+                           const uint32_t *slots, hipStream_t s);
+hipError_t launch_invalidate(const DevGraph &g, const uint64_t *ids, uint64_t n, hipStream_t s);
+hipError_t launch_count_marked(const DevGraph &g, uint64_t slot_top, hipStream_t s);
 hipError_t launch_local_roots(const DevGraph &g, uint64_t slot_top, hipStream_t s);
 
 // rebuild: compact `src` (live vertices only, purged edges) into `dst`,

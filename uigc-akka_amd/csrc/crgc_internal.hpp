@@ -33,6 +33,11 @@ constexpr uint32_t RC_POS = 0x80000000u;     // reverse candidate: the edge's co
 // flags bits: ALIVE is internal; the rest equal CRGC_F_* of include/crgc.h
 constexpr uint8_t FL_ALIVE = 0x01, FL_INTERNED = 0x02, FL_LOCAL = 0x04, FL_BUSY = 0x08,
                   FL_ROOT = 0x10, FL_HALTED = 0x20;
+// Sharded graphs only: a proxy slot stands for an actor whose home is another
+// shard.  It carries the id (the edge / supervisor endpoint of a local owner)
+// and nothing else: never a pseudo-root, never live or garbage, no out-edges.
+constexpr uint8_t FL_PROXY = 0x40;
+constexpr uint32_t MAX_SHARDS = 64;
 
 // device error bits (Counters::err)
 constexpr uint32_t ERR_RESERVED_ID = 1u << 0;
@@ -79,6 +84,11 @@ struct Counters {
   unsigned long long tail_level;     // DONE: levels traced; BAILED: level to resume at
   unsigned long long tail_from;      // level at which k_tail took over
   unsigned long long qn[2], qh[2];   // per-level edge-range queue lengths
+  // sharded graphs
+  unsigned long long n_proxy;        // alive proxy slots seen by the last sweep
+  unsigned long long n_req;          // kill requests (garbage with a remote supervisor)
+  unsigned long long xcnt[MAX_SHARDS];  // ids to send per destination shard
+  unsigned long long xpos[MAX_SHARDS];  // scatter cursors
   unsigned long long ring[LEVEL_RING];
 };
 
@@ -148,6 +158,12 @@ struct DevGraph {
   uint64_t *out_b;    // per-block regions: kill slots (u32)
   uint64_t *out_ids;  // dense garbage ids
   uint64_t *out_kill; // dense kill ids
+  // sharded graphs (n_shards > 1)
+  uint32_t n_shards, shard;
+  uint32_t *xp_buf;   // per-block regions: proxy slots marked since the last export
+  uint32_t *xp_cnt;   // per block: listed proxies
+  uint32_t *rq_buf;   // per-block regions: garbage slots whose kill waits on a remote mark
+  uint32_t *rq_cnt;   // per block: listed requests
   Counters *ctr;
 };
 
@@ -159,6 +175,18 @@ __host__ __device__ inline uint64_t mix64(uint64_t x) {
   x *= 0x94d049bb133111ebull;
   x ^= x >> 31;
   return x;
+}
+
+// Home shard of an actor id.  Independent of the id-table hash (mix64(id) &
+// mask): with a power-of-two shard count a shared hash would leave each
+// shard's table using 1/G of its buckets.
+__host__ __device__ inline uint32_t shard_of(uint64_t id, uint32_t n_shards) {
+  const uint64_t h = mix64(id ^ 0x6a09e667f3bcc909ull);
+  return (uint32_t)(((h >> 32) * (uint64_t)n_shards) >> 32);
+}
+
+__device__ inline bool is_home(const DevGraph &g, uint64_t id) {
+  return g.n_shards <= 1 || shard_of(id, g.n_shards) == g.shard;
 }
 
 __host__ __device__ inline bool reserved_id(uint64_t id) {
@@ -291,8 +319,9 @@ __device__ inline int id_probe(const DevGraph &g, uint64_t id, uint64_t &bucket,
 __device__ inline uint32_t id_settle(const DevGraph &g, uint64_t id, uint64_t bucket,
                                      uint32_t slot, int state) {
   const bool ins = state == RS_INSERTED;
+  const bool home = ins && is_home(g, id);
   const unsigned long long s = wave_append(&g.ctr->slot_top, ins);
-  const uint64_t ball = __ballot(ins);
+  const uint64_t ball = __ballot(home);
   if (lane_id() == 0 && ball) atomicAdd(&g.ctr->inserted, (unsigned long long)__popcll(ball));
   if (ins) {
     if (s >= g.scap) {
@@ -301,7 +330,7 @@ __device__ inline uint32_t id_settle(const DevGraph &g, uint64_t id, uint64_t bu
     } else {
       slot = (uint32_t)s;
       g.vid[s] = id;
-      g.flags[s] = FL_ALIVE;
+      g.flags[s] = home ? FL_ALIVE : (FL_ALIVE | FL_PROXY);
     }
     atomicExch(&g.htab[bucket].val, slot);
   }
@@ -326,8 +355,9 @@ __device__ inline uint32_t id_settle(const DevGraph &g, uint64_t id, uint64_t bu
 __device__ inline uint32_t id_settle_block(const DevGraph &g, uint64_t id, uint64_t bucket,
                                            uint32_t slot, int state) {
   const bool ins = state == RS_INSERTED;
+  const bool home = ins && is_home(g, id);
   unsigned long long *const ctrs[2] = {&g.ctr->slot_top, &g.ctr->inserted};
-  const uint32_t v[2] = {ins ? 1u : 0u, ins ? 1u : 0u};
+  const uint32_t v[2] = {ins ? 1u : 0u, home ? 1u : 0u};
   unsigned long long base[2];
   block_append<2>(ctrs, v, base);
   if (ins) {
@@ -338,7 +368,7 @@ __device__ inline uint32_t id_settle_block(const DevGraph &g, uint64_t id, uint6
     } else {
       slot = (uint32_t)s;
       g.vid[s] = id;
-      g.flags[s] = FL_ALIVE;
+      g.flags[s] = home ? FL_ALIVE : (FL_ALIVE | FL_PROXY);
     }
     atomicExch(&g.htab[bucket].val, slot);
   }

@@ -48,6 +48,16 @@ __global__ __launch_bounds__(IDS_THREADS) void k_ids(DevGraph g, IdArgs a) {
       set_err(g.ctr, ERR_RESERVED_ID);
       has = false;
     }
+    if (has && g.n_shards > 1 && !is_home(g, id)) {
+      // not home here: resolve only as the far end of a local edge / supervisor
+      bool want = false;
+      if (sg.partner) {
+        const uint64_t p = sg.partner[r];
+        want = p != CRGC_NO_ACTOR && is_home(g, p);
+      }
+      if (!want && sg.need) want = sg.need[r] != 0;
+      has = want;
+    }
     uint64_t bucket = 0;
     uint32_t slot = SLOT_INVALID;
     int st = RS_NONE;
@@ -89,8 +99,14 @@ __global__ __launch_bounds__(256) void k_entries_apply(DevGraph g, EntryArgs a) 
   if (!ok) a.self_slot[i] = SLOT_INVALID;
   const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
   const int16_t rc = a.recv[i];
+  // Sharded graphs: every record is applied by the home shard of the shadow
+  // it writes (self, edge owner, spawned child, updated target).  k_ids only
+  // resolved the ids this shard needs, so a valid slot of a child / owner is
+  // a home slot; self may be a proxy (the supervisor of a child homed here).
+  const bool sh = g.n_shards > 1;
+  const bool self_home = !sh || is_home(g, a.self[i]);
   // Local information (:77-82): recv delta and the busy/root LWW tag.
-  if (vs(me)) {
+  if (vs(me) && self_home) {
     if (rc != 0) atomicAdd(&g.recv[me], (int32_t)rc);
     atomicMax(&g.vseq[me], tag);
   }
@@ -101,7 +117,7 @@ __global__ __launch_bounds__(256) void k_entries_apply(DevGraph g, EntryArgs a) 
     const uint32_t os = a.co_slot[k], ts = a.ct_slot[k];
     a.atom_o[k] = os;
     a.atom_t[k] = ts;
-    a.atom_d[k] = (vs(me) && vs(os) && vs(ts)) ? 1 : 0;
+    a.atom_d[k] = ((sh || vs(me)) && vs(os) && vs(ts)) ? 1 : 0;
   }
   // Spawned actors (:96-104): child.supervisor = self, last write wins.
   for (uint32_t k = s0; k < s1; ++k) {
@@ -116,11 +132,12 @@ __global__ __launch_bounds__(256) void k_entries_apply(DevGraph g, EntryArgs a) 
     const int16_t info = a.u_info[k];
     const bool good = vs(ts) && vs(me);
     const int32_t cnt = refob_count(info);
-    if (good && cnt > 0) atomicAdd(&g.recv[ts], -cnt);
+    const bool tgt_ok = sh ? (vs(ts) && is_home(g, a.u_ref[k])) : good;
+    if (tgt_ok && cnt > 0) atomicAdd(&g.recv[ts], -cnt);
     const uint64_t at = (uint64_t)ctot + k;
     a.atom_o[at] = me;
     a.atom_t[at] = ts;
-    a.atom_d[at] = (good && refob_deactivated(info)) ? -1 : 0;
+    a.atom_d[at] = (good && self_home && refob_deactivated(info)) ? -1 : 0;
   }
 }
 
@@ -146,18 +163,38 @@ __global__ __launch_bounds__(256) void k_entries_lww(DevGraph g, EntryArgs a) {
   }
 }
 
+// Sharded graphs: which shards need an entry's self (its home, and the homes
+// of its spawned children, where it becomes their supervisor), and which
+// updated refs are the far end of a deactivation edge owned by self.
+__global__ __launch_bounds__(256) void k_entries_shard_prep(DevGraph g, EntryArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const uint64_t cmax = a.n * a.F;
+  const uint64_t self = a.self[i];
+  bool need = is_home(g, self);
+  const uint32_t s0 = a.s_off[i], s1 = min((uint64_t)a.s_off[i + 1], cmax);
+  for (uint32_t k = s0; k < s1 && k < s0 + a.F; ++k) need |= is_home(g, a.spawned[k]);
+  a.self_need[i] = need;
+  const uint32_t u0 = a.u_off[i], u1 = min((uint64_t)a.u_off[i + 1], cmax);
+  for (uint32_t k = u0; k < u1 && k < u0 + a.F; ++k)
+    a.u_partner[k] = refob_deactivated(a.u_info[k]) ? self : CRGC_NO_ACTOR;
+}
+
 hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   const uint64_t nf = a.n * a.F;
+  const int blocks = (int)((a.n + 255) / 256);
+  const bool sh = g.n_shards > 1;
+  if (sh) hipLaunchKernelGGL(k_entries_shard_prep, dim3(blocks), dim3(256), 0, s, g, a);
   IdArgs ia{};
   ia.nseg = 5;
-  ia.seg[0] = IdSeg{a.self, a.self_slot, a.n, nullptr, false};
-  ia.seg[1] = IdSeg{a.c_target, a.ct_slot, nf, a.c_off + a.n, false};
-  ia.seg[2] = IdSeg{a.c_owner, a.co_slot, nf, a.c_off + a.n, false};
-  ia.seg[3] = IdSeg{a.spawned, a.spawn_slot, nf, a.s_off + a.n, false};
-  ia.seg[4] = IdSeg{a.u_ref, a.u_slot, nf, a.u_off + a.n, false};
+  ia.seg[0] = IdSeg{a.self, a.self_slot, a.n, nullptr, false, nullptr, sh ? a.self_need : nullptr};
+  ia.seg[1] = IdSeg{a.c_target, a.ct_slot, nf, a.c_off + a.n, false, a.c_owner, nullptr};
+  ia.seg[2] = IdSeg{a.c_owner, a.co_slot, nf, a.c_off + a.n, false, nullptr, nullptr};
+  ia.seg[3] = IdSeg{a.spawned, a.spawn_slot, nf, a.s_off + a.n, false, nullptr, nullptr};
+  ia.seg[4] = IdSeg{a.u_ref, a.u_slot, nf, a.u_off + a.n, false, sh ? a.u_partner : nullptr,
+                    nullptr};
   if (hipError_t e = launch_ids(g, ia, s)) return e;
-  const int blocks = (int)((a.n + 255) / 256);
   hipLaunchKernelGGL(k_entries_apply, dim3(blocks), dim3(256), 0, s, g, a);
   hipLaunchKernelGGL(k_entries_lww, dim3(blocks), dim3(256), 0, s, g, a);
   return hipGetLastError();
@@ -217,15 +254,29 @@ __global__ __launch_bounds__(256) void k_deltas_lww(DevGraph g, DeltaArgs a) {
   if (vs(ss) && g.sseq[me] == tag) g.sup[me] = ss;
 }
 
+// Sharded graphs: the owning delta shadow of every outgoing entry.
+__global__ __launch_bounds__(256) void k_deltas_shard_prep(DeltaArgs a, uint64_t n_out) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const uint32_t o0 = a.out_off[i], o1 = min((uint64_t)a.out_off[i + 1], n_out);
+  for (uint32_t k = o0; k < o1; ++k) a.o_partner[k] = a.id[i];
+}
+
 hipError_t launch_deltas(const DevGraph &g, const DeltaArgs &a, uint64_t n_out, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
+  const int blocks = (int)((a.n + 255) / 256);
+  const bool sh = g.n_shards > 1;
+  if (sh && n_out)
+    hipLaunchKernelGGL(k_deltas_shard_prep, dim3(blocks), dim3(256), 0, s, a, n_out);
+  // A delta shadow's own fields, supervisor and out-edges all live with it, so
+  // its id is resolved at home only; supervisor and targets also as proxies.
   IdArgs ia{};
   ia.nseg = 3;
-  ia.seg[0] = IdSeg{a.id, a.self_slot, a.n, nullptr, false};
-  ia.seg[1] = IdSeg{a.sup, a.sup_slot, a.n, nullptr, true};
-  ia.seg[2] = IdSeg{a.out_target, a.ot_slot, n_out, a.out_off + a.n, false};
+  ia.seg[0] = IdSeg{a.id, a.self_slot, a.n, nullptr, false, nullptr, nullptr};
+  ia.seg[1] = IdSeg{a.sup, a.sup_slot, a.n, nullptr, true, a.id, nullptr};
+  ia.seg[2] = IdSeg{a.out_target, a.ot_slot, n_out, a.out_off + a.n, false,
+                    sh ? a.o_partner : nullptr, nullptr};
   if (hipError_t e = launch_ids(g, ia, s)) return e;
-  const int blocks = (int)((a.n + 255) / 256);
   hipLaunchKernelGGL(k_deltas_apply, dim3(blocks), dim3(256), 0, s, g, a);
   hipLaunchKernelGGL(k_deltas_lww, dim3(blocks), dim3(256), 0, s, g, a);
   return hipGetLastError();
@@ -234,14 +285,16 @@ hipError_t launch_deltas(const DevGraph &g, const DeltaArgs &a, uint64_t n_out, 
 // ---------------------------------------------------------------------------
 // Undo logs — ShadowGraph.mergeUndoLog, ShadowGraph.java:158-174.
 // ---------------------------------------------------------------------------
-// The reference throws ConcurrentModificationException when a created-ref
-// target of an admitted actor is not yet in the graph: detect it.
-__global__ __launch_bounds__(256) void k_undo_check(DevGraph g, UndoArgs a) {
+// Existence of every admitted actor and created-ref target, looked up at its
+// home shard (exists[0..n) actors, exists[n..n+nc) targets).  The host ORs the
+// shards' answers and reports the reference's ConcurrentModificationException
+// (a target of an admitted actor not in the graph) before any
+// mutation.
+__global__ __launch_bounds__(256) void k_undo_exist(DevGraph g, UndoArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.n) return;
-  if (id_find(g, a.actor[i]) == SLOT_NONE) return;  // field ignored (:166-167)
-  for (uint32_t k = a.c_off[i]; k < a.c_off[i + 1]; ++k)
-    if (id_find(g, a.c_target[k]) == SLOT_NONE) set_err(g.ctr, ERR_UNDO_NEW);
+  if (i >= a.n + a.nc) return;
+  const uint64_t id = i < a.n ? a.actor[i] : a.c_target[i - a.n];
+  a.exists[i] = (is_home(g, id) && id_find(g, id) != SLOT_NONE) ? 1 : 0;
 }
 
 // 1. every shadow at the downed location becomes halted (:163-165)
@@ -249,27 +302,36 @@ __global__ __launch_bounds__(256) void k_undo_halt(DevGraph g, uint16_t loc, uin
   const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (v >= slot_top) return;
   const uint8_t f = g.flags[v];
-  if ((f & FL_ALIVE) && (uint16_t)(g.vid[v] >> 48) == loc) g.flags[v] = f | FL_HALTED;
+  if ((f & FL_ALIVE) && !(f & FL_PROXY) && (uint16_t)(g.vid[v] >> 48) == loc)
+    g.flags[v] = f | FL_HALTED;
 }
 
-// 2./3. undelivered messages and created refs of admitted actors (:166-172)
-__global__ __launch_bounds__(256) void k_undo_fields(DevGraph g, UndoArgs a) {
+// 2. undelivered messages of admitted actors (:166-169), at their home
+__global__ __launch_bounds__(256) void k_undo_recv(DevGraph g, UndoArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.n) return;
+  if (i >= a.n || a.msg[i] == 0 || !is_home(g, a.actor[i])) return;
   const uint32_t s = id_find(g, a.actor[i]);
-  const bool ok = s != SLOT_NONE;
-  if (ok && a.msg[i] != 0) atomicAdd(&g.recv[s], a.msg[i]);
-  for (uint32_t k = a.c_off[i]; k < a.c_off[i + 1]; ++k) {
-    const uint32_t t = ok ? id_find(g, a.c_target[k]) : SLOT_NONE;
-    a.atom_o[k] = s;
-    a.atom_t[k] = t;
-    a.atom_d[k] = (ok && t != SLOT_NONE) ? a.c_count[k] : 0;
-  }
+  if (s != SLOT_NONE) atomicAdd(&g.recv[s], a.msg[i]);
+}
+
+// 3. created refs of admitted actors (:170-172), one thread per entry, at the
+//    owner's home; a target homed elsewhere gets a proxy slot here.
+__global__ __launch_bounds__(256) void k_undo_edges(DevGraph g, UndoArgs a) {
+  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // every lane reaches id_resolve
+  const bool valid = k < a.nc;
+  const uint64_t owner = valid ? a.c_actor[k] : 0;
+  const uint32_t s = (valid && is_home(g, owner)) ? id_find(g, owner) : SLOT_NONE;
+  const bool has = s != SLOT_NONE;
+  const uint32_t t = id_resolve(g, has, has ? a.c_target[k] : 0);
+  if (!valid) return;
+  a.atom_o[k] = s;
+  a.atom_t[k] = t;
+  a.atom_d[k] = (has && vs(t)) ? a.c_count[k] : 0;
 }
 
 hipError_t launch_undo_check(const DevGraph &g, const UndoArgs &a, hipStream_t s) {
-  if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_undo_check, dim3((a.n + 255) / 256), dim3(256), 0, s, g, a);
+  if (a.n + a.nc == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_undo_exist, dim3((a.n + a.nc + 255) / 256), dim3(256), 0, s, g, a);
   return hipGetLastError();
 }
 
@@ -278,8 +340,8 @@ hipError_t launch_undo_apply(const DevGraph &g, const UndoArgs &a, uint64_t slot
   if (slot_top)
     hipLaunchKernelGGL(k_undo_halt, dim3((slot_top + 255) / 256), dim3(256), 0, s, g,
                        a.location, slot_top);
-  if (a.n)
-    hipLaunchKernelGGL(k_undo_fields, dim3((a.n + 255) / 256), dim3(256), 0, s, g, a);
+  if (a.n) hipLaunchKernelGGL(k_undo_recv, dim3((a.n + 255) / 256), dim3(256), 0, s, g, a);
+  if (a.nc) hipLaunchKernelGGL(k_undo_edges, dim3((a.nc + 255) / 256), dim3(256), 0, s, g, a);
   return hipGetLastError();
 }
 

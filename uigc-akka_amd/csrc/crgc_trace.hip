@@ -119,6 +119,7 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
   const bool bitmode = a.flags & LV_BITMAP_FRONT;
   const bool pull = !ROOTS && pull_level(c, L, a);
   const bool listing = !ROOTS && listing_level(c, L, a);
+  const bool sharded = !ROOTS && g.n_shards > 1;
   uint32_t n_front = 0, n_sup = 0, n_edges = 0;
 
   for (uint32_t blk = gw; blk < nblk; blk += nw) {
@@ -133,7 +134,9 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
         // investigateRemotelyHeldActors: every shadow at `location` (:305-310)
 #pragma unroll
         for (int j = 0; j < 32; ++j)
-          if ((fb[j] & FL_ALIVE) && (uint16_t)(g.vid[base + j] >> 48) == a.location) m |= 1u << j;
+          if ((fb[j] & (FL_ALIVE | FL_PROXY)) == FL_ALIVE &&
+              (uint16_t)(g.vid[base + j] >> 48) == a.location)
+            m |= 1u << j;
       } else {
         // isPseudoRoot (:201-203): 32 flag bytes + 32 receive counts per lane
         int4 r4[8];
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
           const uint8_t f = fb[j];
-          const bool root = (f & FL_ALIVE) && !(f & FL_HALTED) &&
+          const bool root = (f & (FL_ALIVE | FL_HALTED | FL_PROXY)) == FL_ALIVE &&
                             ((f & (FL_ROOT | FL_BUSY)) || !(f & FL_INTERNED) || rb[j] != 0);
           m |= root ? (1u << j) : 0u;
         }
@@ -205,11 +208,17 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
     // Frontier shadows -> supervisor marks + edge ranges (push levels).
     uint32_t nlight = 0;
     uint2 *region = g.qn_buf + (uint64_t)blk * BLK_SLOTS;
+    uint32_t nprox = sharded ? g.xp_cnt[blk] : 0;
     for (uint32_t c0 = 0; c0 < total; c0 += 64) {
       const uint32_t idx = c0 + lane;
       const bool valid = idx < total;
       const uint32_t v = valid ? s_front[wv][idx] : 0;
       const uint8_t f = valid ? g.flags[v] : 0;
+      if (sharded) {  // newly marked proxies: exported to their home shard after the round
+        const uint64_t pb = __ballot(f & FL_PROXY);
+        if (f & FL_PROXY) g.xp_buf[(uint64_t)blk * BLK_SLOTS + nprox + __popcll(pb & lanemask_lt())] = v;
+        nprox += __popcll(pb);
+      }
       const bool expand = valid && !(f & FL_HALTED);  // halted: marked, not expanded (:226)
       // traced edges = nonzero out-edges of expanded shadows (:231)
       if (expand) n_edges += g.nzdeg[v];
@@ -237,6 +246,7 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
       }
     }
     if (lane == 0 && nlight) g.qn_tag[blk] = tag | nlight;
+    if (sharded && lane == 0) g.xp_cnt[blk] = nprox;
     wave_lds_fence();
   }
   const uint64_t tf = block_sum4(n_front);
@@ -496,6 +506,10 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
       const uint32_t v = valid ? cur[i] : 0;
       const uint8_t f = valid ? g.flags[v] : 0;
       const bool expand = valid && !(f & FL_HALTED);  // (:226-229)
+      if (!first && (f & FL_PROXY)) {  // level L's were listed by k_frontier
+        const uint32_t pos = atomicAdd(&g.xp_cnt[v >> 11], 1u);
+        g.xp_buf[(uint64_t)(v >> 11) * BLK_SLOTS + pos] = v;
+      }
       uint2 ad = make_uint2(0, 0);
       if (expand) {
         ad = g.adj[v];
@@ -589,12 +603,13 @@ int level_grid(uint64_t slot_top) {
 }
 
 hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool investigate,
-                        uint64_t slot_top, hipStream_t s) {
+                        uint64_t slot_top, hipStream_t s, hipEvent_t *ev) {
   LevelArgs a = a0;
   const int grid = level_grid(slot_top);
   a.frontier_grid = grid;
   if (investigate) a.flags |= LV_INVESTIGATE;
   if (roots) a.flags |= LV_ROOTS;
+  if (ev) hipEventRecord(ev[0], s);
   if (roots && investigate)
     hipLaunchKernelGGL((k_frontier<true, true>), dim3(grid), dim3(256), 0, s, g, a);
   else if (roots)
@@ -604,8 +619,11 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
   else
     hipLaunchKernelGGL((k_frontier<false, false>), dim3(grid), dim3(256), 0, s, g, a);
   // level controller: the level count, and the narrow-frontier takeover
+  if (ev) hipEventRecord(ev[1], s);
   hipLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, g, a);
+  if (ev) hipEventRecord(ev[2], s);
   hipLaunchKernelGGL(k_expand, dim3(STAT_WG), dim3(256), 0, s, g, a);  // 8 WGs of 4 waves per CU
+  if (ev) hipEventRecord(ev[3], s);
   return hipGetLastError();
 }
 
@@ -656,17 +674,21 @@ __global__ __launch_bounds__(256) void k_sweep(DevGraph g, int should_kill) {
   const int lane = lane_id();
   const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const uint32_t nw = gridDim.x * 4;
-  uint32_t n_live = 0, n_npe = 0;
+  uint32_t n_live = 0, n_npe = 0, n_prox = 0, n_req = 0;
   for (uint32_t blk = gw; blk < nblk; blk += nw) {
     const uint64_t base = (uint64_t)blk * BLK_SLOTS + (uint64_t)lane * 32;
     const uint32_t word = g.vis[(uint64_t)blk * 64 + lane];
     const uint4 f4[2] = {*(const uint4 *)(g.flags + base), *(const uint4 *)(g.flags + base + 16)};
     const uint8_t *fb = (const uint8_t *)f4;
-    uint32_t alive = 0, kill = 0;
+    uint32_t alive = 0, kill = 0, req = 0, prox = 0;
 #pragma unroll
-    for (int j = 0; j < 32; ++j) alive |= (fb[j] & FL_ALIVE) ? (1u << j) : 0u;
+    for (int j = 0; j < 32; ++j) {
+      alive |= ((fb[j] & (FL_ALIVE | FL_PROXY)) == FL_ALIVE) ? (1u << j) : 0u;
+      prox |= ((fb[j] & (FL_ALIVE | FL_PROXY)) == (FL_ALIVE | FL_PROXY)) ? (1u << j) : 0u;
+    }
     const uint32_t garbage = alive & ~word;
     n_live += __popc(alive & word);
+    n_prox += __popc(prox);
     uint32_t gm = garbage;
     while (gm) {
       const int j = __ffs(gm) - 1;
@@ -676,11 +698,27 @@ __global__ __launch_bounds__(256) void k_sweep(DevGraph g, int should_kill) {
         const uint32_t s = g.sup[base + j];
         if (s == SLOT_NONE) {
           n_npe++;
-        } else if (should_kill && !(f & FL_HALTED) && s < 0xFFFFFFF0u &&
-                   ((g.vis[s >> 5] >> (s & 31)) & 1u)) {
-          kill |= 1u << j;
+        } else if (should_kill && !(f & FL_HALTED) && s < 0xFFFFFFF0u) {
+          if ((g.vis[s >> 5] >> (s & 31)) & 1u) {
+            kill |= 1u << j;
+          } else if ((g.flags[s] & (FL_ALIVE | FL_PROXY)) == (FL_ALIVE | FL_PROXY)) {
+            // an unmarked proxy says nothing: its home shard knows the mark
+            req |= 1u << j;
+          }
         }
       }
+    }
+    if (g.n_shards > 1) {
+      const uint32_t rc = __popc(req), ri = wave_incl_scan(rc);
+      uint32_t rp = ri - rc;
+      uint32_t *ra = g.rq_buf + (uint64_t)blk * BLK_SLOTS;
+      while (req) {
+        const int j = __ffs(req) - 1;
+        req &= req - 1;
+        ra[rp++] = (uint32_t)(base + j);
+      }
+      if (lane == 63) g.rq_cnt[blk] = ri;
+      n_req += rc;
     }
     const uint32_t gc = __popc(garbage), kc = __popc(kill);
     const uint32_t gi = wave_incl_scan(gc), ki = wave_incl_scan(kc);
@@ -706,9 +744,13 @@ __global__ __launch_bounds__(256) void k_sweep(DevGraph g, int should_kill) {
   }
   const uint64_t tl = block_sum4(n_live);
   const uint64_t tn = block_sum4(n_npe);
+  const uint64_t tp = block_sum4(n_prox);
+  const uint64_t tr = block_sum4(n_req);
   if (threadIdx.x == 0) {
     g.blkstat[(uint64_t)blockIdx.x * 4 + STAT_LIVE] = tl;
     if (tn) atomicAdd(&c->npe, (unsigned long long)tn);
+    if (tp) atomicAdd(&c->n_proxy, (unsigned long long)tp);
+    if (tr) atomicAdd(&c->n_req, (unsigned long long)tr);
   }
 }
 
@@ -793,11 +835,203 @@ __global__ __launch_bounds__(256) void k_sweep_gather(DevGraph g) {
   }
 }
 
-hipError_t launch_sweep(const DevGraph &g, int should_kill, uint64_t slot_top, hipStream_t s) {
+hipError_t launch_sweep(const DevGraph &g, int should_kill, uint64_t slot_top, hipStream_t s,
+                        int phase) {
   const int grid = level_grid(slot_top);
-  hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(256), 0, s, g, should_kill);
-  hipLaunchKernelGGL(k_sweep_scan, dim3(1), dim3(1024), 0, s, g, (uint32_t)grid);
-  hipLaunchKernelGGL(k_sweep_gather, dim3(grid), dim3(256), 0, s, g);
+  if (phase & 1) {
+    hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(256), 0, s, g, should_kill);
+    hipLaunchKernelGGL(k_sweep_scan, dim3(1), dim3(1024), 0, s, g, (uint32_t)grid);
+  }
+  if (phase & 2) hipLaunchKernelGGL(k_sweep_gather, dim3(grid), dim3(256), 0, s, g);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Sharded graphs: exchange lists.  A shard lists slots per
+// 2048-slot block (newly marked proxies during the mark, garbage whose kill
+// waits on a remote supervisor mark during the sweep); these kernels turn a
+// listing into actor ids packed by destination shard, one region per shard
+// in shard order, ready for the all-to-all.
+//   k_list_count    per-destination counts (LDS histogram, one atomic per
+//                   destination per workgroup) -> Counters::xcnt
+//   k_list_scatter  ids (and the listed slot, for requests) into
+//                   send[off(d) + ...]; off = exclusive scan of xcnt
+// MODE 0: export (id of the listed proxy);  MODE 1: request (id of the
+// listed garbage shadow's supervisor, plus the garbage slot).
+// ---------------------------------------------------------------------------
+template <int MODE>
+__device__ inline uint64_t listed_id(const DevGraph &g, uint32_t v) {
+  return MODE == 0 ? g.vid[v] : g.vid[g.sup[v]];
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_list_count(DevGraph g, const uint32_t *buf, const uint32_t *cnt,
+                                                    uint64_t nblk) {
+  __shared__ uint32_t hist[MAX_SHARDS];
+  for (uint32_t d = threadIdx.x; d < MAX_SHARDS; d += 256) hist[d] = 0;
+  __syncthreads();
+  const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t blk = gw; blk < nblk; blk += nw) {
+    const uint32_t n = cnt[blk];
+    for (uint32_t i = lane_id(); i < n; i += 64)
+      atomicAdd(&hist[shard_of(listed_id<MODE>(g, buf[blk * BLK_SLOTS + i]), g.n_shards)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < g.n_shards; d += 256)
+    if (hist[d]) atomicAdd(&g.ctr->xcnt[d], (unsigned long long)hist[d]);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_list_scatter(DevGraph g, uint32_t *buf, uint32_t *cnt,
+                                                      uint64_t nblk, uint64_t *send, uint32_t *send_slot) {
+  __shared__ uint32_t hist[MAX_SHARDS];
+  __shared__ unsigned long long base[MAX_SHARDS];
+  for (uint32_t d = threadIdx.x; d < MAX_SHARDS; d += 256) hist[d] = 0;
+  __syncthreads();
+  const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t blk = gw; blk < nblk; blk += nw) {
+    const uint32_t n = cnt[blk];
+    for (uint32_t i = lane_id(); i < n; i += 64)
+      atomicAdd(&hist[shard_of(listed_id<MODE>(g, buf[blk * BLK_SLOTS + i]), g.n_shards)], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < g.n_shards) {
+    const uint32_t d = threadIdx.x;
+    unsigned long long off = 0;
+    for (uint32_t e = 0; e < d; ++e) off += g.ctr->xcnt[e];
+    base[d] = off + (hist[d] ? atomicAdd(&g.ctr->xpos[d], (unsigned long long)hist[d]) : 0ull);
+    hist[d] = 0;
+  }
+  __syncthreads();
+  for (uint64_t blk = gw; blk < nblk; blk += nw) {
+    const uint32_t n = cnt[blk];
+    for (uint32_t i = lane_id(); i < n; i += 64) {
+      const uint32_t v = buf[blk * BLK_SLOTS + i];
+      const uint64_t id = listed_id<MODE>(g, v);
+      const uint32_t d = shard_of(id, g.n_shards);
+      const uint64_t at = base[d] + atomicAdd(&hist[d], 1u);
+      send[at] = id;
+      if (MODE == 1) send_slot[at] = v;
+    }
+  }
+}
+
+hipError_t launch_list(const DevGraph &g, int mode, bool scatter, uint32_t *buf, uint32_t *cnt,
+                       uint64_t nblk, uint64_t *send, uint32_t *send_slot, hipStream_t s) {
+  if (nblk == 0) return hipSuccess;
+  const int grid = (int)((nblk + 3) / 4);
+  if (!scatter) {
+    if (mode == 0) hipLaunchKernelGGL(k_list_count<0>, dim3(grid), dim3(256), 0, s, g, buf, cnt, nblk);
+    else hipLaunchKernelGGL(k_list_count<1>, dim3(grid), dim3(256), 0, s, g, buf, cnt, nblk);
+  } else {
+    if (mode == 0)
+      hipLaunchKernelGGL(k_list_scatter<0>, dim3(grid), dim3(256), 0, s, g, buf, cnt, nblk, send, send_slot);
+    else
+      hipLaunchKernelGGL(k_list_scatter<1>, dim3(grid), dim3(256), 0, s, g, buf, cnt, nblk, send, send_slot);
+  }
+  return hipGetLastError();
+}
+
+// Ids received from other shards' marked proxies become candidates of level
+// L (a sparse level: the dirty map names their blocks).  ring[L-1] gets the
+// number of candidates so the level kernels run.
+__global__ __launch_bounds__(256) void k_import(DevGraph g, const uint64_t *ids, uint64_t n, int L) {
+  uint8_t *Fc = g.front[L & 1];
+  uint8_t *Dc = g.dirty[L & 1];
+  uint32_t found = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const uint32_t v = id_find(g, ids[i]);
+    if (v >= 0xFFFFFFF0u) continue;  // collected since (cannot happen while proxies are purged)
+    if ((g.flags[v] & (FL_ALIVE | FL_PROXY)) != FL_ALIVE) continue;
+    if ((g.vis[v >> 5] >> (v & 31)) & 1u) continue;
+    Fc[v] = 1;
+    Dc[v >> 11] = 1;
+    ++found;
+  }
+  const uint64_t t = block_sum4(found);
+  if (threadIdx.x == 0 && t) atomicAdd(&g.ctr->ring[(L - 1) % LEVEL_RING], (unsigned long long)t);
+}
+
+hipError_t launch_import(const DevGraph &g, const uint64_t *ids, uint64_t n, int level, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_import, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, g, ids, n, level);
+  return hipGetLastError();
+}
+
+// Kill requests answered at the supervisor's home: is it marked?
+__global__ __launch_bounds__(256) void k_req_answer(DevGraph g, const uint64_t *ids, uint64_t n,
+                                                    uint8_t *ans) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const uint32_t v = id_find(g, ids[i]);
+    ans[i] = (v < 0xFFFFFFF0u && ((g.vis[v >> 5] >> (v & 31)) & 1u)) ? 1 : 0;
+  }
+}
+
+// Requests whose supervisor is marked join the kill list (after the gather).
+__global__ __launch_bounds__(256) void k_kill_fix(DevGraph g, const uint32_t *slots, const uint8_t *ans,
+                                                  uint64_t n) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t b = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); b < n; b += stride) {
+    const uint64_t i = b + lane_id();
+    const bool k = i < n && ans[i];
+    const unsigned long long at = wave_append(&g.ctr->n_kill, k);
+    if (k) g.out_kill[at] = g.vid[slots[i]];
+  }
+}
+
+hipError_t launch_requests(const DevGraph &g, int phase, const uint64_t *ids, uint64_t n, uint8_t *ans,
+                           const uint32_t *slots, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const int grid = grid_for(n, 256, 4096);
+  if (phase == 0) hipLaunchKernelGGL(k_req_answer, dim3(grid), dim3(256), 0, s, g, ids, n, ans);
+  else hipLaunchKernelGGL(k_kill_fix, dim3(grid), dim3(256), 0, s, g, slots, ans, n);
+  return hipGetLastError();
+}
+
+// Other shards' garbage: this shard's proxies of it die with it (their ids
+// will name a new incarnation if they ever reappear — SURVEY E9).
+__global__ __launch_bounds__(256) void k_invalidate(DevGraph g, const uint64_t *ids, uint64_t n) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    uint64_t bucket = KEY_EMPTY;
+    const uint32_t v = id_find(g, ids[i], &bucket);
+    if (v >= 0xFFFFFFF0u || bucket == KEY_EMPTY) continue;
+    if ((g.flags[v] & (FL_ALIVE | FL_PROXY)) != (FL_ALIVE | FL_PROXY)) continue;
+    g.htab[bucket].key = KEY_TOMB;
+    g.flags[v] = 0;
+  }
+}
+
+hipError_t launch_invalidate(const DevGraph &g, const uint64_t *ids, uint64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_invalidate, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, g, ids, n);
+  return hipGetLastError();
+}
+
+// Marked home shadows (investigateRemotelyHeldActors' to.size(), :329) -> n_out.
+__global__ __launch_bounds__(256) void k_count_marked(DevGraph g) {
+  const uint64_t nblk = (g.ctr->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
+  const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
+  uint32_t k = 0;
+  for (uint64_t blk = gw; blk < nblk; blk += nw) {
+    const uint64_t base = blk * BLK_SLOTS + (uint64_t)lane_id() * 32;
+    const uint32_t word = g.vis[blk * 64 + lane_id()];
+    if (!word) continue;
+    const uint4 f4[2] = {*(const uint4 *)(g.flags + base), *(const uint4 *)(g.flags + base + 16)};
+    const uint8_t *fb = (const uint8_t *)f4;
+    uint32_t home = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) home |= ((fb[j] & (FL_ALIVE | FL_PROXY)) == FL_ALIVE) ? (1u << j) : 0u;
+    k += __popc(word & home);
+  }
+  const uint64_t t = block_sum4(k);
+  if (threadIdx.x == 0 && t) atomicAdd(&g.ctr->n_out, (unsigned long long)t);
+}
+
+hipError_t launch_count_marked(const DevGraph &g, uint64_t slot_top, hipStream_t s) {
+  hipLaunchKernelGGL(k_count_marked, dim3(level_grid(slot_top)), dim3(256), 0, s, g);
   return hipGetLastError();
 }
 

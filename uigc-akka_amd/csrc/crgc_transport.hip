@@ -1,0 +1,166 @@
+// crgc_transport.hip — shard-to-shard exchange: RCCL over xGMI, or in-process
+// device copies for G logical shards on one GPU (see crgc_transport.hpp).
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cstring>
+#include <new>
+
+#include "../../include/crgc.h"
+#include "crgc_internal.hpp"
+#include "crgc_transport.hpp"
+
+namespace crgc {
+
+// ---- LocalTransport ----------------------------------------------------------
+// A generation barrier with a bound: a shard that never arrives (its caller
+// failed before the collective) breaks the transport instead of hanging the
+// others forever.
+int LocalTransport::barrier() {
+  std::unique_lock<std::mutex> lk(m);
+  if (broken) return CRGC_E_TIMEOUT;
+  const uint64_t gen = generation;
+  if (++arrived == n_shards) {
+    arrived = 0;
+    ++generation;
+    cv.notify_all();
+    return CRGC_OK;
+  }
+  if (!cv.wait_for(lk, std::chrono::seconds(300), [&] { return generation != gen || broken; })) {
+    broken = true;
+    cv.notify_all();
+  }
+  return broken ? CRGC_E_TIMEOUT : CRGC_OK;
+}
+
+int LocalTransport::allgather(uint32_t shard, const void *send, void *recv, size_t bytes,
+                              hipStream_t s) {
+  if (hipStreamSynchronize(s) != hipSuccess) return CRGC_E_DEVICE;  // send is complete
+  post[shard].ptr = send;
+  if (int rc = barrier()) return rc;
+  for (uint32_t r = 0; r < n_shards; ++r)
+    if (bytes && hipMemcpyAsync((char *)recv + (size_t)r * bytes, post[r].ptr, bytes, hipMemcpyDefault,
+                                s) != hipSuccess)
+      return CRGC_E_DEVICE;
+  if (hipStreamSynchronize(s) != hipSuccess) return CRGC_E_DEVICE;
+  return barrier();  // nobody reuses its send buffer before every peer has copied it
+}
+
+int LocalTransport::alltoallv(uint32_t shard, const void *send, const size_t *soff, const size_t *sbytes,
+                              void *recv, const size_t *roff, const size_t *rbytes, hipStream_t s) {
+  (void)sbytes;
+  if (hipStreamSynchronize(s) != hipSuccess) return CRGC_E_DEVICE;
+  post[shard].ptr = send;
+  post[shard].soff = soff;
+  if (int rc = barrier()) return rc;
+  for (uint32_t r = 0; r < n_shards; ++r) {
+    if (!rbytes[r]) continue;
+    const char *src = (const char *)post[r].ptr + post[r].soff[shard];
+    if (hipMemcpyAsync((char *)recv + roff[r], src, rbytes[r], hipMemcpyDefault, s) != hipSuccess)
+      return CRGC_E_DEVICE;
+  }
+  if (hipStreamSynchronize(s) != hipSuccess) return CRGC_E_DEVICE;
+  return barrier();
+}
+
+// ---- RcclTransport -------------------------------------------------------------
+struct RcclTransport final : crgc_transport {
+  ncclComm_t comm = nullptr;
+  uint32_t rank = 0;
+  int device = 0;
+  ~RcclTransport() override {
+    if (comm) ncclCommDestroy(comm);
+  }
+  bool accepts(uint32_t shard, int dev) const override { return shard == rank && dev == device; }
+  int allgather(uint32_t, const void *send, void *recv, size_t bytes, hipStream_t s) override {
+    if (!bytes) return CRGC_OK;
+    return ncclAllGather(send, recv, bytes, ncclUint8, comm, s) == ncclSuccess ? CRGC_OK
+                                                                               : CRGC_E_DEVICE;
+  }
+  int alltoallv(uint32_t, const void *send, const size_t *soff, const size_t *sbytes, void *recv,
+                const size_t *roff, const size_t *rbytes, hipStream_t s) override {
+    // own block: a device copy; peers: one grouped send/recv per direction
+    if (rbytes[rank] &&
+        hipMemcpyAsync((char *)recv + roff[rank], (const char *)send + soff[rank], rbytes[rank],
+                       hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return CRGC_E_DEVICE;
+    if (ncclGroupStart() != ncclSuccess) return CRGC_E_DEVICE;
+    for (uint32_t r = 0; r < n_shards; ++r) {
+      if (r == rank) continue;
+      if (sbytes[r] && ncclSend((const char *)send + soff[r], sbytes[r], ncclUint8, (int)r, comm, s) !=
+                           ncclSuccess)
+        return CRGC_E_DEVICE;
+      if (rbytes[r] &&
+          ncclRecv((char *)recv + roff[r], rbytes[r], ncclUint8, (int)r, comm, s) != ncclSuccess)
+        return CRGC_E_DEVICE;
+    }
+    return ncclGroupEnd() == ncclSuccess ? CRGC_OK : CRGC_E_DEVICE;
+  }
+};
+
+int rccl_unique_id(uint8_t id[128]) {
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return CRGC_E_DEVICE;
+  memcpy(id, &u, 128);
+  return CRGC_OK;
+}
+
+crgc_transport *make_rccl_transport(const uint8_t id[128], uint32_t n_shards, uint32_t shard, int device,
+                                    int *rc) {
+  RcclTransport *t = new (std::nothrow) RcclTransport();
+  if (!t) {
+    *rc = CRGC_E_NOMEM;
+    return nullptr;
+  }
+  t->n_shards = n_shards;
+  t->rank = shard;
+  t->device = device;
+  int prev = 0;
+  hipGetDevice(&prev);
+  hipSetDevice(device);
+  ncclUniqueId u;
+  memcpy(&u, id, 128);
+  const ncclResult_t r = ncclCommInitRank(&t->comm, (int)n_shards, u, (int)shard);
+  hipSetDevice(prev);
+  if (r != ncclSuccess) {
+    t->comm = nullptr;
+    delete t;
+    *rc = CRGC_E_DEVICE;
+    return nullptr;
+  }
+  *rc = CRGC_OK;
+  return t;
+}
+
+}  // namespace crgc
+
+extern "C" {
+
+int crgc_transport_local(uint32_t n_shards, crgc_transport **out) {
+  if (!out || n_shards < 1 || n_shards > crgc::TRANSPORT_MAX_SHARDS) return CRGC_E_INVAL;
+  *out = new (std::nothrow) crgc::LocalTransport(n_shards);
+  return *out ? CRGC_OK : CRGC_E_NOMEM;
+}
+
+int crgc_transport_rccl_id(uint8_t id[128]) {
+  if (!id) return CRGC_E_INVAL;
+  return crgc::rccl_unique_id(id);
+}
+
+int crgc_transport_rccl(const uint8_t id[128], uint32_t n_shards, uint32_t shard, int32_t device,
+                        crgc_transport **out) {
+  if (!out || !id || n_shards < 1 || n_shards > crgc::TRANSPORT_MAX_SHARDS || shard >= n_shards)
+    return CRGC_E_INVAL;
+  int rc = CRGC_OK;
+  *out = crgc::make_rccl_transport(id, n_shards, shard, device, &rc);
+  return rc;
+}
+
+void crgc_transport_destroy(crgc_transport *t) { delete t; }
+
+uint32_t crgc_shard_of(uint64_t id, uint32_t n_shards) {
+  return n_shards <= 1 ? 0u : crgc::shard_of(id, n_shards);
+}
+
+}  // extern "C"

@@ -1,0 +1,67 @@
+// crgc_transport.hpp — the data-movement layer between the shards of a
+// hash-partitioned shadow graph.
+//
+// Two implementations behind one interface:
+//   RcclTransport   one process per GPU, RCCL over xGMI (ncclAllGather and
+//                   grouped ncclSend/ncclRecv), stream-ordered on the graph's
+//                   stream.  This is the production transport.
+//   LocalTransport  the G shards live in one process, each driven by its own
+//                   host thread; the exchange is device-to-device copies
+//                   through a shared rendezvous.  It lets G logical shards run
+//                   on one GPU, which is how the sharded protocol is
+//                   parity-tested on a single-GPU box.
+// Every call is collective: all G shards make the same calls in the same
+// order.  Buffers are device buffers; sizes are bytes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <cstddef>
+#include <cstdint>
+#include <mutex>
+
+struct crgc_transport {
+  uint32_t n_shards = 1;
+  virtual ~crgc_transport() = default;
+  // Whether `shard` may be driven through this transport (RCCL: its own rank).
+  virtual bool accepts(uint32_t shard, int device) const = 0;
+  // recv[r*bytes .. (r+1)*bytes) = shard r's send[0 .. bytes)
+  virtual int allgather(uint32_t shard, const void *send, void *recv, size_t bytes, hipStream_t s) = 0;
+  // shard me sends send[soff[r] .. +sbytes[r]) to r and receives r's block
+  // for it into recv[roff[r] .. +rbytes[r]).  rbytes[r] must equal r's sbytes[me].
+  virtual int alltoallv(uint32_t shard, const void *send, const size_t *soff, const size_t *sbytes,
+                        void *recv, const size_t *roff, const size_t *rbytes, hipStream_t s) = 0;
+};
+
+namespace crgc {
+
+constexpr uint32_t TRANSPORT_MAX_SHARDS = 64;
+
+// One process, one host thread per shard.
+struct LocalTransport final : crgc_transport {
+  struct Post {
+    const void *ptr = nullptr;
+    const size_t *soff = nullptr;
+  };
+  std::mutex m;
+  std::condition_variable cv;
+  uint32_t arrived = 0;
+  uint64_t generation = 0;
+  bool broken = false;
+  Post post[TRANSPORT_MAX_SHARDS];
+
+  explicit LocalTransport(uint32_t g) { n_shards = g; }
+  bool accepts(uint32_t shard, int) const override { return shard < n_shards; }
+  int barrier();
+  int allgather(uint32_t shard, const void *send, void *recv, size_t bytes, hipStream_t s) override;
+  int alltoallv(uint32_t shard, const void *send, const size_t *soff, const size_t *sbytes, void *recv,
+                const size_t *roff, const size_t *rbytes, hipStream_t s) override;
+};
+
+// Created by crgc_transport_rccl (crgc_transport.hip); RCCL types stay there.
+crgc_transport *make_rccl_transport(const uint8_t id[128], uint32_t n_shards, uint32_t shard,
+                                    int device, int *rc);
+int rccl_unique_id(uint8_t id[128]);
+
+}  // namespace crgc
