@@ -183,3 +183,41 @@ def test_device_resident_batches_sharded(sharded, oracle_mod):
         h._all(lambda s, b: s.merge_entries(b.to_device()), [(p,) for p in parts])
         o.merge_entries(batch)
         _same(h.trace(True), o.trace(True))
+
+
+def test_one_shard_protocol_matches_oracle(sharded, oracle_mod):
+    """G = 1 with a transport runs every collective step of the sharded protocol."""
+    h, o = sharded(1), oracle_mod.OracleGraph()
+    fz = fuzz.Fuzz(21)
+    for step in range(8):
+        eb = fz.entries(300)
+        h.merge_entries(eb); o.merge_entries(eb)
+        if step % 2:
+            db = fz.deltas(4)
+            h.merge_deltas(db); o.merge_deltas(db)
+        assert h.export() == o.export()
+        _same(h.trace(True), o.trace(True))
+        fz.sync(o.export())
+
+
+def test_rccl_transport_single_rank(hip_mod, oracle_mod):
+    """The RCCL transport (ncclCommInitRank, ncclAllGather, grouped send/recv
+    around the self copy) on a one-rank communicator: RCCL refuses two ranks
+    on one GPU, and the test box has one.  The 2/4/8-rank exchange is the same
+    code with peers (covered by the in-process transport above)."""
+    uid = hip_mod.Transport.rccl_unique_id()
+    t = hip_mod.Transport.rccl(uid, 1, 0, 0)
+    try:
+        h = hip_mod.ShadowGraph(n_shards=1, shard=0, transport=t)
+        o = oracle_mod.OracleGraph()
+        w = kats.RandomWorld(seed=5, max_actors=300, wake_every=11)
+        for batch in w.steps():
+            h.merge_entries(batch)
+            o.merge_entries(batch)
+            rh, ro = h.trace(True), o.trace(True)
+            _same(rh, ro)
+            w.kill(ro.kill_set())
+        assert h.export() == o.export()
+        h.close()
+    finally:
+        t.close()

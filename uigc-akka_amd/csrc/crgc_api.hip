@@ -55,7 +55,7 @@ void free_arrays(Arrays &a) {
 }
 
 hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, uint32_t n_shards,
-                        uint32_t shard) {
+                        uint32_t shard, bool sharded) {
   a.caps = c;
   DevGraph &d = a.d;
   d = DevGraph{};
@@ -121,7 +121,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   A(dmalloc(&d.tq, 2 * (uint64_t)TAIL_QCAP));
   A(dmalloc(&d.tl_buf, c.scap));
   A(dmalloc(&d.tl_tag, c.scap / BLK_SLOTS));
-  if (n_shards > 1) {
+  if (sharded) {
     A(dmalloc(&d.xp_buf, c.scap));
     A(dmalloc(&d.xp_cnt, c.scap / BLK_SLOTS));
     A(dmalloc(&d.rq_buf, c.scap));
@@ -153,7 +153,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   hipMemsetAsync(d.rcap, 0, c.scap * 4, s);
   hipMemsetAsync(d.rnew, 0, c.scap * 4, s);
   hipMemsetAsync(d.fx, 0, c.scap / 8, s);
-  if (n_shards > 1) {
+  if (sharded) {
     hipMemsetAsync(d.xp_cnt, 0, c.scap / BLK_SLOTS * 4, s);
     hipMemsetAsync(d.rq_cnt, 0, c.scap / BLK_SLOTS * 4, s);
   }
@@ -269,7 +269,7 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms) {
       std::min<uint64_t>(src_top, h->live + (h->hctr->inserted - h->inserted_at_trace));
   Caps c = caps_for(std::max<uint64_t>(live_ub, 1), h->etab_used, ids, atoms);
   Arrays dst;
-  HIP_TRY(alloc_arrays(dst, c, h->ctr, h->stream, h->G, h->shard));
+  HIP_TRY(alloc_arrays(dst, c, h->ctr, h->stream, h->G, h->shard, h->tp != nullptr));
   Scratch tmp;
   const size_t need = Carver::need({src_top * 4 + 4, c.scap * 8, rebuild_scan_tmp_bytes(c.scap)});
   if (tmp.ensure(need) != hipSuccess) {
@@ -373,8 +373,10 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
   h->device = cfg ? cfg->device : 0;
   h->F = (cfg && cfg->entry_field_size) ? cfg->entry_field_size : 4;
   h->DGS = (cfg && cfg->delta_graph_size) ? cfg->delta_graph_size : 64;
-  if (cfg && cfg->n_shards > 1) {
-    if (cfg->n_shards > MAX_SHARDS || cfg->shard >= cfg->n_shards || !cfg->transport ||
+  // A transport makes the handle a shard (a transport with n_shards == 1 runs
+  // the sharded protocol on one shard: a self-check of the transport).
+  if (cfg && (cfg->n_shards > 1 || cfg->transport)) {
+    if (cfg->n_shards < 1 || cfg->n_shards > MAX_SHARDS || cfg->shard >= cfg->n_shards || !cfg->transport ||
         cfg->transport->n_shards != cfg->n_shards ||
         !cfg->transport->accepts(cfg->shard, cfg->device)) {
       delete h;
@@ -411,7 +413,7 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     const uint64_t v0 = cfg && cfg->vertex_capacity ? cfg->vertex_capacity : (1u << 16);
     const uint64_t e0 = cfg && cfg->edge_capacity ? cfg->edge_capacity : 8 * v0;
     Caps c = caps_for(v0, e0, v0, e0);
-    if (hipError_t e = alloc_arrays(h->g, c, h->ctr, h->stream, h->G, h->shard)) {
+    if (hipError_t e = alloc_arrays(h->g, c, h->ctr, h->stream, h->G, h->shard, h->tp != nullptr)) {
       rc = map_hip(e);
       break;
     }
@@ -666,7 +668,7 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
           ? Carver::need({n * 8, n * 2, n, (n + 1) * 4, C * 8, C * 8, (n + 1) * 4, S * 8, (n + 1) * 4,
                           U * 8, U * 2})
           : 0;
-  const bool sh = h->G > 1;
+  const bool sh = h->tp;
   const size_t work_bytes =
       Carver::need({n * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4, sh ? n : 0,
                     sh ? n * h->F * 8 : 0}) +
@@ -712,8 +714,8 @@ int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
   if (int rc = check_graph(h)) return rc;
   DeviceGuard dg(h->device);
   uint64_t C = 0, S = 0, U = 0;
-  const int vrc = entry_counts(h, b, h->G > 1, &C, &S, &U);
-  if (h->G <= 1) return vrc ? vrc : merge_entries_one(h, b, C, S, U);
+  const int vrc = entry_counts(h, b, h->tp, &C, &S, &U);
+  if (!h->tp) return vrc ? vrc : merge_entries_one(h, b, C, S, U);
   // Sharded: every shard applies its part of every shard's batch, in shard order.
   const uint64_t n = vrc ? 0 : b->n_entries;
   const uint64_t hdr[5] = {(uint64_t)(int64_t)vrc, n, C, S, U};
@@ -778,7 +780,7 @@ static int merge_deltas_one(crgc_graph *h, const crgc_delta_batch *b, uint64_t n
   const size_t host_bytes =
       b->memory == CRGC_MEM_HOST ? Carver::need({n * 8, n * 4, n * 8, n, (n + 1) * 4, nout * 8, nout * 4})
                                  : 0;
-  const bool sh = h->G > 1;
+  const bool sh = h->tp;
   const size_t work_bytes =
       Carver::need({n * 4, n * 4, std::max<uint64_t>(nout, 1) * 4, sh ? std::max<uint64_t>(nout, 1) * 8 : 0}) +
       edge_scratch(nout);
@@ -813,7 +815,7 @@ int crgc_merge_deltas(crgc_graph *h, const crgc_delta_batch *b) {
   DeviceGuard dg(h->device);
   uint64_t nout = 0;
   const int vrc = delta_counts(h, b, &nout);
-  if (h->G <= 1) return vrc ? vrc : merge_deltas_one(h, b, nout);
+  if (!h->tp) return vrc ? vrc : merge_deltas_one(h, b, nout);
   const uint64_t n = vrc ? 0 : b->n_shadows;
   const uint64_t hdr[3] = {(uint64_t)(int64_t)vrc, n, nout};
   const void *arr[7] = {b ? b->id : nullptr,      b ? b->recv_count : nullptr, b ? b->supervisor : nullptr,
@@ -865,7 +867,7 @@ int crgc_merge_undo(crgc_graph *h, const crgc_undo_log *log) {
       if (std::adjacent_find(ids.begin(), ids.end()) != ids.end()) vrc = CRGC_E_INVAL;
     }
   }
-  if (h->G > 1) {  // agree on validity before any collective work
+  if (h->tp) {  // agree on validity before any collective work
     const uint64_t st = (uint64_t)(int64_t)vrc;
     std::vector<uint64_t> all(h->G);
     if (int rc = ag_host(h, &st, 1, all.data())) return rc;
@@ -902,7 +904,7 @@ int crgc_merge_undo(crgc_graph *h, const crgc_undo_log *log) {
   std::vector<uint8_t> ex(n + nc, 0);
   if (n + nc) {
     HIP_TRY(launch_undo_check(h->g.d, a, h->stream));
-    if (h->G > 1) {
+    if (h->tp) {
       const size_t words = (n + nc + 7) / 8;
       std::vector<uint64_t> all(words * h->G);
       if (h->x_ans.ensure(words * 8) != hipSuccess) return CRGC_E_NOMEM;
@@ -1072,7 +1074,7 @@ static void reset_trace_counters(crgc_graph *h) {
   hipMemsetAsync(h->g.d.qn_tag, 0, h->g.caps.scap / BLK_SLOTS * 4, h->stream);
   hipMemsetAsync(h->g.d.tl_tag, 0, h->g.caps.scap / BLK_SLOTS * 4, h->stream);
   hipMemsetAsync(h->g.d.vis, 0, nblk * BLK_SLOTS / 8, h->stream);
-  if (h->G > 1) hipMemsetAsync(h->g.d.xp_cnt, 0, nblk * 4, h->stream);
+  if (h->tp) hipMemsetAsync(h->g.d.xp_cnt, 0, nblk * 4, h->stream);
 }
 
 // Mark to the global fixpoint: local levels, then (sharded graphs) rounds of
@@ -1083,7 +1085,7 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
   int end = 0;
   if (int rc = run_levels(h, investigate, location, top, true, 0, lr, &end)) return rc;
   *rounds = 1;
-  if (h->G <= 1) return CRGC_OK;
+  if (!h->tp) return CRGC_OK;
   const uint32_t G = h->G, me = h->shard;
   const uint64_t nblk = round_up(std::min<uint64_t>(top, h->g.caps.scap), BLK_SLOTS) / BLK_SLOTS;
   std::vector<uint64_t> M((size_t)G * G);
@@ -1228,7 +1230,7 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   if (int rc = mark_all(h, false, 0, top, lr, &rounds, &ids_sent, &ms_x)) return rc;
   HIP_TRY(hipEventRecord(h->ev[1], h->stream));
   HIP_TRY(launch_trace_stats(h->g.d, h->stream));
-  if (h->G <= 1) {
+  if (!h->tp) {
     HIP_TRY(launch_sweep(h->g.d, should_kill ? 1 : 0, top, h->stream));
   } else if (int rc = sweep_sharded(h, should_kill ? 1 : 0, top, &ms_x)) {
     return rc;
@@ -1322,7 +1324,7 @@ int crgc_count_reachable_from(crgc_graph *h, uint16_t location, int64_t *out) {
   const int rl = mark_all(h, true, location, h->slot_top, lr, &rounds, &sent, &ms_x);
   h->last_levels = saved;
   if (rl) return rl;
-  if (h->G <= 1) {
+  if (!h->tp) {
     HIP_TRY(sync_counters(h));
     *out = (int64_t)h->hctr->marked;
     return CRGC_OK;
