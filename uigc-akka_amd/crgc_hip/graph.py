@@ -31,6 +31,18 @@ from .batch import (Entry, EntryBatch, DeltaBatch, UndoBatch, TraceResult, Graph
                     export_to_state)
 
 
+def _host_ids(n: int) -> np.ndarray:
+    """A host id buffer for trace results: page-locked when torch can provide
+    it (the device copies into it directly), else ordinary memory."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return torch.empty(n, dtype=torch.int64, pin_memory=True).numpy().view(np.uint64)
+    except Exception:
+        pass
+    return np.zeros(n, np.uint64)
+
+
 class ShadowGraph:
     def __init__(self, entry_field_size: int = 4, delta_graph_size: int = 64,
                  device: int = 0, vertex_capacity: int = 0, edge_capacity: int = 0,
@@ -134,14 +146,14 @@ class ShadowGraph:
         """trace() into reusable host buffers: (result with buffer views, n_garbage, n_kill)."""
         self.flush()
         if getattr(self, "_gbuf", None) is None:
-            self._gbuf = np.zeros(1 << 16, np.uint64)
-            self._kbuf = np.zeros(1 << 16, np.uint64)
+            self._gbuf = _host_ids(1 << 16)
+            self._kbuf = _host_ids(1 << 16)
         rc, out = self._trace_into(shouldKill, self._gbuf, self._kbuf)
         if rc == abi.E2BIG:
             if out.n_garbage > len(self._gbuf):
-                self._gbuf = np.zeros(int(out.n_garbage) * 2, np.uint64)
+                self._gbuf = _host_ids(int(out.n_garbage) * 2)
             if out.n_kill > len(self._kbuf):
-                self._kbuf = np.zeros(int(out.n_kill) * 2, np.uint64)
+                self._kbuf = _host_ids(int(out.n_kill) * 2)
             out.garbage_ids, out.garbage_cap = _ptr(self._gbuf), len(self._gbuf)
             out.kill_ids, out.kill_cap = _ptr(self._kbuf), len(self._kbuf)
             rc = self.lib.crgc_last_trace(self.h, C.byref(out))

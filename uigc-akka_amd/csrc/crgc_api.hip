@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <functional>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -196,7 +197,8 @@ struct crgc_graph {
   crgc_trace_stats last_stats{};
   bool have_last = false;
   uint64_t last_levels = 0;
-  std::vector<hipEvent_t> lvl_ev;  // 4 per level launch: k_frontier | k_tail | k_expand |
+  std::vector<hipEvent_t> lvl_ev;  // 6 per level launch: start / stop of its 3 kernels
+  std::vector<hipEvent_t> chunk_ev;  // start / stop of every chunk of level launches
   uint64_t *roots_buf = nullptr;
   uint64_t roots_cap = 0;
   // sharded graphs (G > 1): transport and exchange buffers
@@ -234,6 +236,8 @@ struct DeviceGuard {
   }
 };
 
+void absorb_counters(crgc_graph *h);
+
 // Read back the small counters (blocking).
 hipError_t sync_counters(crgc_graph *h) {
   hipError_t e = hipMemcpyAsync(h->hctr, h->ctr, offsetof(Counters, ring), hipMemcpyDeviceToHost,
@@ -241,12 +245,17 @@ hipError_t sync_counters(crgc_graph *h) {
   if (e != hipSuccess) return e;
   e = hipStreamSynchronize(h->stream);
   if (e != hipSuccess) return e;
+  absorb_counters(h);
+  return hipSuccess;
+}
+
+// Bookkeeping from a fresh host copy of the counters.
+void absorb_counters(crgc_graph *h) {
   h->slot_top = h->hctr->slot_top;
   h->pool_top = h->hctr->pool_top;
   h->rpool_top = h->hctr->rpool_top;
   h->etab_used = h->hctr->etab_used;
   h->ids_since = h->atoms_since = 0;
-  return hipSuccess;
 }
 
 int device_error(crgc_graph *h) {
@@ -444,6 +453,7 @@ void crgc_destroy(crgc_graph *h) {
   for (auto &e : h->ev)
     if (e) hipEventDestroy(e);
   for (auto &e : h->lvl_ev) hipEventDestroy(e);
+  for (auto &e : h->chunk_ev) hipEventDestroy(e);
   if (h->own_stream && h->stream) hipStreamDestroy(h->stream);
   delete h;
 }
@@ -946,7 +956,12 @@ int crgc_merge_undo(crgc_graph *h, const crgc_undo_log *log) {
 struct LevelRun {
   uint64_t levels = 0, roots = 0, launches = 0, depth = 0;
   double ms = 0, ms_f = 0, ms_t = 0, ms_e = 0;
+  bool defer = false;                  // leave the event queries to the caller (pending)
+  std::function<void()> pending;
 };
+
+static void collect_times(crgc_graph *h, LevelRun &lr, size_t nl, size_t nc, int timing, bool log,
+                          size_t first_level, size_t last, const std::vector<unsigned long long> &ring);
 
 // Level-synchronous BFS from the pseudo-roots (roots = true, start = 0) or
 // from candidates of level `start` (sharded rounds), until a level is empty.
@@ -956,7 +971,8 @@ struct LevelRun {
 // steady-state wakeup needs one host synchronisation.  *end = the first empty
 // level (levels start .. *end-1 were non-empty).
 static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64_t top, bool roots,
-                      int start, LevelRun &lr, int *end) {
+                      int start, LevelRun &lr, int *end,
+                      const std::function<hipError_t()> &after_chunk = nullptr) {
   LevelArgs la{};
   la.location = location;
   // Tuning switch for A/B runs (results are identical either way).
@@ -990,19 +1006,39 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   if (const char *m = getenv("CRGC_TAIL_MAX")) la.tail_max = (uint32_t)strtoul(m, nullptr, 10);
   la.tail_start = std::min<uint32_t>(la.tail_start, TAIL_QCAP);
   la.tail_max = std::min<uint32_t>(std::max(la.tail_max, 1u), TAIL_QCAP);
-  size_t nl = 0;
-  auto launch = [&](int level, bool rootk) -> hipError_t {
-    while (h->lvl_ev.size() < 4 * (nl + 1)) {
+  // Device times, from timing-only events (no system-scope fence):
+  //   every chunk of levels: an event pair around it (ms_mark, dispatch gaps included);
+  //   CRGC_KERNEL_TIMING=1 (default): k_expand's start / stop carried by its dispatch;
+  //   CRGC_KERNEL_TIMING=2: all three level kernels (each timed dispatch costs a few us);
+  //   CRGC_KERNEL_TIMING=0: chunks only.
+  const char *kt = getenv("CRGC_KERNEL_TIMING");
+  const int timing = kt ? atoi(kt) : 1;
+  auto new_event = [&](std::vector<hipEvent_t> &v, size_t n) -> hipError_t {
+    while (v.size() < n) {
       hipEvent_t e;
-      hipError_t r = hipEventCreate(&e);
+      hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
       if (r != hipSuccess) return r;
-      h->lvl_ev.push_back(e);
+      v.push_back(e);
+    }
+    return hipSuccess;
+  };
+  size_t nl = 0, nc = 0;
+  auto launch = [&](int level, bool rootk) -> hipError_t {
+    hipEvent_t ev[6] = {};
+    if (timing) {
+      if (hipError_t r = new_event(h->lvl_ev, 6 * (nl + 1))) return r;
+      for (int k = timing >= 2 ? 0 : 4; k < 6; ++k) ev[k] = h->lvl_ev[6 * nl + k];
     }
     la.level = level;
-    hipError_t r = launch_level(h->g.d, la, rootk, investigate, top, h->stream, &h->lvl_ev[4 * nl]);
+    hipError_t r = launch_level(h->g.d, la, rootk, investigate, top, h->stream, ev);
     ++nl;
     return r;
   };
+  auto chunk_event = [&]() -> hipError_t {
+    if (hipError_t r = new_event(h->chunk_ev, nc + 1)) return r;
+    return hipEventRecord(h->chunk_ev[nc++], h->stream);
+  };
+  HIP_TRY(chunk_event());
   int L = start;
   if (roots) {
     HIP_TRY(launch(0, true));
@@ -1013,7 +1049,11 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   unsigned long long tail[3] = {0, 0, 0};
   const bool log = getenv("CRGC_LEVEL_LOG") != nullptr;
   for (;;) {
+    if (nc % 2 == 0) HIP_TRY(chunk_event());
     for (int k = 0; k < chunk; ++k) HIP_TRY(launch(L + k, false));
+    HIP_TRY(chunk_event());
+    // work that runs only if this chunk finished the mark (its kernels check mark_done)
+    if (after_chunk) HIP_TRY(after_chunk());
     // counts of levels L-1 .. L+chunk-1
     const int first = L - 1, last = L + chunk - 1;
     for (int lv = first; lv <= last;) {
@@ -1039,22 +1079,14 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
         lr.levels += (uint64_t)std::max(0, e - (roots ? 0 : start));
         // level launches that did work: the first chunk of the next trace
         if (roots) lr.depth = tail[0] == TAIL_DONE ? (uint64_t)tail[2] + 1 : (uint64_t)lv;
-        for (size_t i = 0; i < nl; ++i) {
-          float t[3] = {0, 0, 0};
-          for (int k = 0; k < 3; ++k) hipEventElapsedTime(&t[k], h->lvl_ev[4 * i + k], h->lvl_ev[4 * i + k + 1]);
-          lr.ms_f += t[0];
-          lr.ms_t += t[1];
-          lr.ms_e += t[2];
-          lr.ms += t[0] + t[1] + t[2];
-          if (log)
-            fprintf(stderr, "[crgc] level %zu frontier %llu  %.1f us (frontier %.1f tail %.1f expand %.1f)\n",
-                    (roots ? 0 : (size_t)start) + i,
-                    (roots ? 0 : (size_t)start) + i <= (size_t)last
-                        ? ring[((roots ? 0 : (size_t)start) + i) % LEVEL_RING]
-                        : 0ull,
-                    (t[0] + t[1] + t[2]) * 1e3, t[0] * 1e3, t[1] * 1e3, t[2] * 1e3);
-        }
         lr.launches += nl;
+        lr.pending = [h, nl, nc, timing, log, roots, start, last, ring, &lr]() {
+          collect_times(h, lr, nl, nc, timing, log, roots ? 0 : (size_t)start, (size_t)last, ring);
+        };
+        if (!lr.defer) {
+          lr.pending();
+          lr.pending = nullptr;
+        }
         return CRGC_OK;
       }
     }
@@ -1064,17 +1096,41 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   }
 }
 
+// Device times of one run_levels call, from its events (host-side queries,
+// deferred by crgc_trace until the result copies are in flight).
+static void collect_times(crgc_graph *h, LevelRun &lr, size_t nl, size_t nc, int timing, bool log,
+                          size_t first_level, size_t last, const std::vector<unsigned long long> &ring) {
+  {
+    {
+      {
+        for (size_t i = 0; i + 1 < nc; i += 2) {
+          float t = 0;
+          hipEventElapsedTime(&t, h->chunk_ev[i], h->chunk_ev[i + 1]);
+          lr.ms += t;
+        }
+        for (size_t i = 0; i < (timing ? nl : 0); ++i) {
+          float t[3] = {0, 0, 0};
+          for (int k = timing >= 2 ? 0 : 2; k < 3; ++k)
+            hipEventElapsedTime(&t[k], h->lvl_ev[6 * i + 2 * k], h->lvl_ev[6 * i + 2 * k + 1]);
+          lr.ms_f += t[0];
+          lr.ms_t += t[1];
+          lr.ms_e += t[2];
+          if (log)
+            fprintf(stderr, "[crgc] level %zu frontier %llu  %.1f us (frontier %.1f tail %.1f expand %.1f)\n",
+                    first_level + i, first_level + i <= last ? ring[(first_level + i) % LEVEL_RING] : 0ull,
+                    (t[0] + t[1] + t[2]) * 1e3, t[0] * 1e3, t[1] * 1e3, t[2] * 1e3);
+        }
+      }
+    }
+  }
+}
+
 static void reset_trace_counters(crgc_graph *h) {
-  // marked .. the level ring
+  // marked .. the level ring, and the per-block state of the blocks this trace can touch
   const size_t a = CTR_OFF(marked), b = sizeof(Counters);
-  hipMemsetAsync((char *)h->ctr + a, 0, b - a, h->stream);
   const uint64_t top = h->slot_top + h->ids_since;
   const uint64_t nblk = round_up(std::min<uint64_t>(top, h->g.caps.scap), BLK_SLOTS) / BLK_SLOTS;
-  hipMemsetAsync(h->g.d.blkstat, 0, (size_t)STAT_WG * 4 * 8, h->stream);
-  hipMemsetAsync(h->g.d.qn_tag, 0, h->g.caps.scap / BLK_SLOTS * 4, h->stream);
-  hipMemsetAsync(h->g.d.tl_tag, 0, h->g.caps.scap / BLK_SLOTS * 4, h->stream);
-  hipMemsetAsync(h->g.d.vis, 0, nblk * BLK_SLOTS / 8, h->stream);
-  if (h->tp) hipMemsetAsync(h->g.d.xp_cnt, 0, nblk * 4, h->stream);
+  launch_trace_reset(h->g.d, nblk, (uint32_t)(a / 8), (uint32_t)((b - a) / 8), h->stream);
 }
 
 // Mark to the global fixpoint: local levels, then (sharded graphs) rounds of
@@ -1121,7 +1177,7 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
   }
 }
 
-static int copy_lists(crgc_graph *h, crgc_trace_out *out) {
+static int copy_lists(crgc_graph *h, crgc_trace_out *out, bool sync = true) {
   bool big = false;
   out->n_garbage = h->last_garbage;
   out->n_kill = h->last_kill;
@@ -1139,7 +1195,7 @@ static int copy_lists(crgc_graph *h, crgc_trace_out *out) {
       HIP_TRY(hipMemcpyAsync(out->kill_ids, h->g.d.out_kill, h->last_kill * 8, hipMemcpyDeviceToHost,
                              h->stream));
   }
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  if (sync) HIP_TRY(hipStreamSynchronize(h->stream));
   return big ? CRGC_E2BIG : CRGC_OK;
 }
 
@@ -1227,19 +1283,45 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   LevelRun lr;
   uint64_t rounds = 0, ids_sent = 0;
   double ms_x = 0;
-  if (int rc = mark_all(h, false, 0, top, lr, &rounds, &ids_sent, &ms_x)) return rc;
-  HIP_TRY(hipEventRecord(h->ev[1], h->stream));
-  HIP_TRY(launch_trace_stats(h->g.d, h->stream));
   if (!h->tp) {
-    HIP_TRY(launch_sweep(h->g.d, should_kill ? 1 : 0, top, h->stream));
-  } else if (int rc = sweep_sharded(h, should_kill ? 1 : 0, top, &ms_x)) {
-    return rc;
+    // The sweep is enqueued behind every level chunk and runs only once the
+    // mark is done (mark_done), together with the counter read-back, so a
+    // steady-state wakeup has one host synchronisation for mark + sweep.
+    auto sweep = [&]() -> hipError_t {
+      hipError_t e = hipEventRecord(h->ev[1], h->stream);
+      if (e == hipSuccess) e = launch_trace_stats(h->g.d, h->stream);
+      if (e == hipSuccess) e = launch_sweep(h->g.d, should_kill ? 1 : 0, top, h->stream);
+      if (e == hipSuccess) e = hipEventRecord(h->ev[2], h->stream);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(h->hctr, h->ctr, offsetof(Counters, ring), hipMemcpyDeviceToHost, h->stream);
+      return e;
+    };
+    int end = 0;
+    rounds = 1;
+    lr.defer = true;
+    if (int rc = run_levels(h, false, 0, top, true, 0, lr, &end, sweep)) return rc;
+    absorb_counters(h);  // read back with the last chunk's level counts
+  } else {
+    if (int rc = mark_all(h, false, 0, top, lr, &rounds, &ids_sent, &ms_x)) return rc;
+    HIP_TRY(hipEventRecord(h->ev[1], h->stream));
+    HIP_TRY(launch_trace_stats(h->g.d, h->stream));
+    if (int rc = sweep_sharded(h, should_kill ? 1 : 0, top, &ms_x)) return rc;
+    HIP_TRY(hipEventRecord(h->ev[2], h->stream));
+    HIP_TRY(sync_counters(h));
   }
-  HIP_TRY(hipEventRecord(h->ev[2], h->stream));
-  HIP_TRY(sync_counters(h));
   const Counters &c = *h->hctr;
   if (c.npe) return CRGC_E_NULL_SUPERVISOR;  // commit skipped: graph unchanged
   if (int rc = device_error(h)) return rc;
+  h->last_garbage = c.n_garbage;
+  h->last_kill = c.n_kill;
+  h->last_live = c.n_live;
+  // result copies first; the event queries overlap them
+  const int rc = copy_lists(h, out, /*sync=*/false);
+  if (lr.pending) {
+    lr.pending();
+    lr.pending = nullptr;
+  }
+  HIP_TRY(hipStreamSynchronize(h->stream));
   crgc_trace_stats st{};
   st.edges_scanned = c.edges_scanned;
   st.sup_edges = c.sup_edges;
@@ -1256,15 +1338,11 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
   st.ms_sweep = ms;
   st.pseudo_roots = lr.roots;
-  h->last_garbage = c.n_garbage;
-  h->last_kill = c.n_kill;
-  h->last_live = c.n_live;
   h->live = c.n_live;
   h->n_proxy = c.n_proxy;
   h->inserted_at_trace = c.inserted;
   h->have_last = true;
   h->last_levels = lr.depth;
-  const int rc = copy_lists(h, out);
   st.ms_total =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   h->last_stats = st;

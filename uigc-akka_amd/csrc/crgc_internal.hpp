@@ -80,6 +80,8 @@ struct Counters {
   unsigned long long n_live;
   unsigned long long npe;
   unsigned long long n_out;          // generic output counter (local roots)
+  unsigned long long mark_done;      // set by k_tail at the first empty level (or its own finish):
+                                     // the sweep kernels enqueued behind the level chunk run
   unsigned long long tail_state;     // narrow-frontier kernel: 0 idle, TAIL_DONE, TAIL_BAILED
   unsigned long long tail_level;     // DONE: levels traced; BAILED: level to resume at
   unsigned long long tail_from;      // level at which k_tail took over

@@ -17,6 +17,8 @@
 // No hot global counters either (one word saturates at ~88 atomics/us on
 // MI355X): frontier ranges go to per-block regions with level-tagged counts,
 // statistics to per-workgroup partials reduced by a single block.
+#include <hip/hip_ext.h>
+
 #include "crgc_host.hpp"
 
 namespace crgc {
@@ -467,6 +469,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
       c->ring[L % LEVEL_RING] = n0;
       c->marked += n0;
       c->qh[(L + 1) & 1] = 0;  // next level's hub queue (last read by k_expand(L-1))
+      if (n0 == 0) c->mark_done = 1;
     }
     return;
   }
@@ -590,6 +593,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
     } else {
       c->tail_level = L + rounds;  // levels 0 .. L+rounds-1 were non-empty
       c->tail_state = TAIL_DONE;
+      c->mark_done = 1;
     }
   }
 }
@@ -609,27 +613,55 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
   a.frontier_grid = grid;
   if (investigate) a.flags |= LV_INVESTIGATE;
   if (roots) a.flags |= LV_ROOTS;
-  if (ev) hipEventRecord(ev[0], s);
-  if (roots && investigate)
-    hipLaunchKernelGGL((k_frontier<true, true>), dim3(grid), dim3(256), 0, s, g, a);
-  else if (roots)
-    hipLaunchKernelGGL((k_frontier<true, false>), dim3(grid), dim3(256), 0, s, g, a);
-  else if (investigate)
-    hipLaunchKernelGGL((k_frontier<false, true>), dim3(grid), dim3(256), 0, s, g, a);
-  else
-    hipLaunchKernelGGL((k_frontier<false, false>), dim3(grid), dim3(256), 0, s, g, a);
+  // Timed launches carry their start / stop events in the dispatch itself
+  // (hipExtLaunchKernelGGL): no separate event packets between the kernels.
+  hipEvent_t e[6] = {};
+  if (ev)
+    for (int k = 0; k < 6; ++k) e[k] = ev[k];
+  auto frontier = [&](auto kern) {
+    hipExtLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, e[0], e[1], 0, g, a);
+  };
+  if (roots && investigate) frontier(k_frontier<true, true>);
+  else if (roots) frontier(k_frontier<true, false>);
+  else if (investigate) frontier(k_frontier<false, true>);
+  else frontier(k_frontier<false, false>);
   // level controller: the level count, and the narrow-frontier takeover
-  if (ev) hipEventRecord(ev[1], s);
-  hipLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, g, a);
-  if (ev) hipEventRecord(ev[2], s);
-  hipLaunchKernelGGL(k_expand, dim3(STAT_WG), dim3(256), 0, s, g, a);  // 8 WGs of 4 waves per CU
-  if (ev) hipEventRecord(ev[3], s);
+  hipExtLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, e[2], e[3], 0, g, a);
+  // 8 WGs of 4 waves per CU
+  hipExtLaunchKernelGGL(k_expand, dim3(STAT_WG), dim3(256), 0, s, e[4], e[5], 0, g, a);
+  return hipGetLastError();
+}
+
+// Per-trace reset in one launch: the marked bitmap, the per-block level tags
+// and proxy listings of the blocks this trace can touch, the per-workgroup
+// statistics, and the trace counters (marked .. the end of the level ring).
+__global__ __launch_bounds__(256) void k_trace_reset(DevGraph g, uint64_t nblk, uint32_t ctr_from,
+                                                     uint32_t ctr_words) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  const uint64_t t0 = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  uint4 *vis4 = reinterpret_cast<uint4 *>(g.vis);  // 2048 slots = 64 words = 16 uint4 per block
+  for (uint64_t i = t0; i < nblk * 16; i += stride) vis4[i] = make_uint4(0, 0, 0, 0);
+  for (uint64_t i = t0; i < nblk; i += stride) {
+    g.qn_tag[i] = 0;
+    g.tl_tag[i] = 0;
+    if (g.xp_cnt) g.xp_cnt[i] = 0;
+  }
+  for (uint64_t i = t0; i < (uint64_t)STAT_WG * 4; i += stride) g.blkstat[i] = 0;
+  unsigned long long *cw = reinterpret_cast<unsigned long long *>(g.ctr) + ctr_from;
+  for (uint64_t i = t0; i < ctr_words; i += stride) cw[i] = 0;
+}
+
+hipError_t launch_trace_reset(const DevGraph &g, uint64_t nblk, uint32_t ctr_from, uint32_t ctr_words,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(k_trace_reset, dim3(grid_for(std::max<uint64_t>(nblk * 16, ctr_words), 256, 2048)),
+                     dim3(256), 0, s, g, nblk, ctr_from, ctr_words);
   return hipGetLastError();
 }
 
 // Sum of the per-workgroup sup/edge partials into the counters (once per trace).
 __global__ __launch_bounds__(256) void k_trace_stats(DevGraph g) {
   __shared__ uint64_t red[2][256];
+  if (!g.ctr->mark_done) return;  // enqueued behind a level chunk that did not finish the mark
   uint64_t su = 0, ed = 0;
   for (uint32_t b = threadIdx.x; b < STAT_WG; b += 256) {
     su += g.blkstat[b * 4 + STAT_SUP];
@@ -669,6 +701,7 @@ hipError_t launch_trace_stats(const DevGraph &g, hipStream_t s) {
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_sweep(DevGraph g, int should_kill) {
   Counters *c = g.ctr;
+  if (!c->mark_done) return;
   const uint64_t slot_top = c->slot_top;
   const uint32_t nblk = (uint32_t)((slot_top + BLK_SLOTS - 1) / BLK_SLOTS);
   const int lane = lane_id();
@@ -760,6 +793,7 @@ __global__ __launch_bounds__(1024) void k_sweep_scan(DevGraph g, uint32_t sweep_
   __shared__ uint64_t wsum[2][16];
   __shared__ uint64_t carry[2];
   Counters *c = g.ctr;
+  if (!c->mark_done) return;
   const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
   const int lane = lane_id(), wv = threadIdx.x >> 6;
   if (threadIdx.x == 0) carry[0] = carry[1] = 0;
@@ -810,6 +844,7 @@ __global__ __launch_bounds__(1024) void k_sweep_scan(DevGraph g, uint32_t sweep_
 
 __global__ __launch_bounds__(256) void k_sweep_gather(DevGraph g) {
   Counters *c = g.ctr;
+  if (!c->mark_done) return;
   const bool commit = c->npe == 0;
   const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
   const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);

@@ -21,11 +21,18 @@ class WlBatch(C.Structure):
                                    "s_off", "spawned", "u_off", "u_ref", "u_info")]
 
 
+class WlDeltas(C.Structure):
+    _fields_ = [("n_graphs", C.c_uint64), ("n_shadows", C.c_uint64), ("n_out", C.c_uint64)] + \
+        [(k, C.c_void_p) for k in ("graph_off", "id", "recv", "sup", "flags", "out_off",
+                                   "out_target", "out_count")]
+
+
 def build(force=False) -> str:
-    src = os.path.join(_HERE, "world.cpp")
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("world.cpp", "deltas.cpp")]
+    if force or not os.path.exists(LIB) or \
+            any(os.path.getmtime(LIB) < os.path.getmtime(s) for s in srcs):
         os.makedirs(os.path.dirname(LIB), exist_ok=True)
-        subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", LIB, src])
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", LIB, *srcs])
     return LIB
 
 
@@ -50,6 +57,10 @@ def _load():
             getattr(lib, f).argtypes = [C.c_void_p]
         lib.wl_take.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(WlBatch)]
         lib.wl_compact.argtypes = [C.c_void_p]
+        lib.wl_deltas_create.restype = C.c_void_p
+        lib.wl_deltas_destroy.argtypes = [C.c_void_p]
+        lib.wl_deltas_build.argtypes = [C.c_void_p, C.POINTER(WlBatch), C.c_uint32, C.c_uint32,
+                                        C.POINTER(WlDeltas)]
         _lib = lib
     return _lib
 
@@ -127,3 +138,58 @@ class World:
         if need > 0:
             self.simulate(need)
         return self.take(n_entries)
+
+
+def deltas_of(batch: EntryBatch, F: int = 4, dgs: int = 64):
+    """A remote node's drained entries folded into DeltaGraphs
+    (LocalGC.scala:159-177 over DeltaGraph.java:73-180; workload/deltas.cpp):
+    returns (DeltaBatch of the decoded shadows in graph order, graph offsets)."""
+    from crgc_hip.batch import DeltaBatch
+    lib = _load()
+    wb = WlBatch()
+    wb.n = batch.n_entries
+    keep = []
+    for k, name in (("self", "self"), ("recv", "recv_count"), ("flags", "flags"),
+                    ("c_off", "created_off"), ("c_owner", "created_owner"),
+                    ("c_target", "created_target"), ("s_off", "spawned_off"),
+                    ("spawned", "spawned"), ("u_off", "updated_off"), ("u_ref", "updated_ref"),
+                    ("u_info", "updated_info")):
+        a = np.ascontiguousarray(getattr(batch, name))
+        keep.append(a)
+        setattr(wb, k, a.ctypes.data)
+    b = lib.wl_deltas_create()
+    try:
+        d = WlDeltas()
+        lib.wl_deltas_build(b, C.byref(wb), F, dgs, C.byref(d))
+        ns, no = d.n_shadows, d.n_out
+        out = DeltaBatch(_arr(d.id, ns, np.uint64), _arr(d.recv, ns, np.int32),
+                         _arr(d.sup, ns, np.uint64), _arr(d.flags, ns, np.uint8),
+                         _arr(d.out_off, ns + 1, np.uint32), _arr(d.out_target, no, np.uint64),
+                         _arr(d.out_count, no, np.int32))
+        return out, _arr(d.graph_off, d.n_graphs + 1, np.uint32)
+    finally:
+        lib.wl_deltas_destroy(b)
+
+
+def undo_of(deltas, location: int):
+    """UndoLog.mergeDeltaGraph (UndoLog.java:39-67) over a downed node's merged
+    deltas: every shadow the node did not own (not interned) gives back its
+    receive count and its created refs.  Fields with nothing left to undo are
+    kept, as the reference's admitted map keeps them.  Returns an UndoBatch."""
+    from crgc_hip import abi
+    from crgc_hip.batch import UndoBatch
+    fields = {}
+    ext = np.nonzero((deltas.flags & abi.DELTA_INTERNED) == 0)[0]
+    for r in ext.tolist():
+        a = int(deltas.id[r])
+        f = fields.setdefault(a, [0, {}])
+        f[0] -= int(deltas.recv_count[r])
+        for k in range(int(deltas.out_off[r]), int(deltas.out_off[r + 1])):
+            t = int(deltas.out_target[k])
+            c = f[1].get(t, 0) - int(deltas.out_count[k])
+            if c:
+                f[1][t] = c
+            else:
+                f[1].pop(t, None)
+    return UndoBatch.from_fields(location, [(a, m, list(refs.items()))
+                                            for a, (m, refs) in fields.items()])
