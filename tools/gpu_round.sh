@@ -19,6 +19,7 @@ fi
 cd /tmp
 timeout -k 10 420 python3 "$ROOT/bench.py" > "$O/bench.json" 2> "$O/bench.err"
 timeout -k 10 300 python3 "$ROOT/bench.py" --workload c3 --steps 3 --warmup 1 > "$O/c3.json" 2> "$O/c3.err"
+timeout -k 10 420 python3 "$ROOT/bench.py" --workload c5 --steps 5 --warmup 1 > "$O/c5.json" 2> "$O/c5.err"
 timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o kt -- \
   python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$O/bench_kt.json" 2> "$O/bench_kt.err"
 if [ "${3:-}" = "pmc" ]; then
