@@ -400,12 +400,21 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
 // ---------------------------------------------------------------------------
 // k_tail: one workgroup finishes the mark once a sparse level's frontier is
 // narrow (deep chains and rings, the last levels of a wide trace): rounds over
-// a queue in place of kernel pairs, a claim = atomicOr on `vis`.  It replaces
-// k_expand of the level it starts at (the frontier listed by k_frontier), and
-// hands back to the level kernels when a round discovers more than tail_max
-// shadows: the pending ones become candidate bytes of level L+2.
+// a queue in place of level-kernel triples.  It replaces k_expand of the level
+// it starts at (the frontier listed by k_frontier), and hands back to the level
+// kernels when a round discovers more than tail_max shadows: the pending ones
+// become candidate bytes of level L+2.
+// A round is latency-bound (one chain link per round), so its state stays on
+// chip: the first TAIL_LQ entries of both queues live in LDS (the rest spill to
+// g.tq), and for graphs of up to TAIL_LVIS_WORDS x 32 slots so does the marked
+// bitmap (claims are LDS atomics; written back before the kernel ends).  A
+// shadow with at most TAIL_LIGHT out-edges is walked by its own thread, so a
+// round over light shadows needs no workgroup scan.
 // ---------------------------------------------------------------------------
 constexpr int TAIL_THREADS = 1024;
+constexpr uint32_t TAIL_LQ = 1024;
+constexpr uint32_t TAIL_LIGHT = 16;
+constexpr uint32_t TAIL_LVIS_WORDS = 32 * 1024;  // 128 KiB: graphs of up to 1,048,576 slots
 
 // Exclusive scan over the workgroup; `total` gets the sum.
 __device__ inline uint32_t tail_scan(uint32_t v, uint32_t *s_w, uint32_t &total) {
@@ -426,22 +435,141 @@ __device__ inline uint32_t tail_scan(uint32_t v, uint32_t *s_w, uint32_t &total)
   return r;
 }
 
+// A queue whose first TAIL_LQ entries are in LDS.
+struct TailQ {
+  uint32_t *l, *g;
+  __device__ uint32_t get(uint32_t i) const { return i < TAIL_LQ ? l[i] : g[i]; }
+  __device__ void put(uint32_t i, uint32_t v) const {
+    if (i < TAIL_LQ) l[i] = v;
+    else g[i] = v;
+  }
+};
+
+struct TailLds {
+  uint32_t *start, *off, *w, *next, *vis;
+};
+
+struct TailOut {
+  uint32_t n_sup = 0, n_edges = 0, rounds = 0, n = 0;
+  int32_t claims = 0;
+  bool bailed = false;
+};
+
 // Claim t for the next round; without queue room it becomes a candidate byte
 // of the resume level instead (and the round ends in a bail).
-__device__ inline void tail_claim(const DevGraph &g, uint32_t t, uint32_t *nxt, uint32_t *s_next,
+template <bool LV>
+__device__ inline void tail_claim(const DevGraph &g, const TailLds &sh, uint32_t t, const TailQ &nxt,
                                   uint8_t *Fb, uint8_t *Db, int32_t &claims) {
   const uint32_t bit = 1u << (t & 31);
-  if (g.vis[t >> 5] & bit) return;
-  if (atomicOr(&g.vis[t >> 5], bit) & bit) return;
-  const uint32_t pos = atomicAdd(s_next, 1u);
+  uint32_t *w = LV ? &sh.vis[t >> 5] : &g.vis[t >> 5];
+  if (*w & bit) return;
+  if (atomicOr(w, bit) & bit) return;
+  const uint32_t pos = atomicAdd(sh.next, 1u);
   if (pos < TAIL_QCAP) {
-    nxt[pos] = t;
+    nxt.put(pos, t);
     ++claims;
   } else {
-    atomicAnd(&g.vis[t >> 5], ~bit);
+    atomicAnd(w, ~bit);
     Fb[t] = 1;
     Db[t >> 11] = 1;
   }
+}
+
+template <bool LV>
+__device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const TailLds &sh, TailQ cur,
+                                   TailQ nxt, uint32_t n, TailOut &o) {
+  const int L = a.level;
+  const bool investigate = a.flags & LV_INVESTIGATE;
+  uint8_t *Fn = g.front[(L + 1) & 1];  // k_frontier(L)'s supervisor pushes, redone here
+  uint8_t *Dn = g.dirty[(L + 1) & 1];
+  uint8_t *Fb = g.front[L & 1];        // bail: candidates of level L+2
+  uint8_t *Db = g.dirty[L & 1];
+  bool first = true;
+  for (;;) {
+    if (threadIdx.x == 0) *sh.next = 0;
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < n; c0 += TAIL_THREADS) {
+      const uint32_t i = c0 + threadIdx.x;
+      const bool valid = i < n;
+      const uint32_t v = valid ? cur.get(i) : 0;
+      const uint8_t f = valid ? g.flags[v] : 0;
+      const bool expand = valid && !(f & FL_HALTED);  // (:226-229)
+      if (!first && (f & FL_PROXY)) {  // level L's were listed by k_frontier
+        const uint32_t pos = atomicAdd(&g.xp_cnt[v >> 11], 1u);
+        g.xp_buf[(uint64_t)(v >> 11) * BLK_SLOTS + pos] = v;
+      }
+      uint2 ad = make_uint2(0, 0);
+      if (expand) {
+        ad = g.adj[v];
+        if (!first) o.n_edges += g.nzdeg[v];  // level L's were counted by k_frontier
+        if (!investigate) {
+          const uint32_t s = g.sup[v];  // (:258-267)
+          if (s < 0xFFFFFFF0u) {
+            if (first) {
+              Fn[s] = 0;
+              Dn[s >> 11] = 0;
+            } else {
+              ++o.n_sup;
+            }
+            tail_claim<LV>(g, sh, s, nxt, Fb, Db, o.claims);
+          }
+        }
+      }
+      const bool heavy = ad.y > TAIL_LIGHT;
+      if (!heavy) {  // this thread walks its shadow's out-edges (:231-241)
+        for (uint32_t e = 0; e < ad.y; e += 4) {
+          uint64_t ed[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) ed[u] = e + u < ad.y ? g.pool[(uint64_t)ad.x + e + u] : 0;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (edge_count(ed[u]) > 0) tail_claim<LV>(g, sh, edge_target(ed[u]), nxt, Fb, Db, o.claims);
+        }
+      }
+      if (__syncthreads_or(heavy)) {  // heavy shadows: the workgroup shares their edges
+        uint32_t total;
+        const uint32_t st = tail_scan(heavy ? ad.y : 0u, sh.w, total);
+        sh.start[threadIdx.x] = st;
+        sh.off[threadIdx.x] = ad.x;
+        __syncthreads();
+        for (uint32_t e = threadIdx.x; e < total; e += TAIL_THREADS) {
+          int lo = 0, hi = TAIL_THREADS - 1;  // last item whose start <= e
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (sh.start[mid] <= e) lo = mid;
+            else hi = mid - 1;
+          }
+          const uint64_t ed = g.pool[(uint64_t)sh.off[lo] + (e - sh.start[lo])];
+          if (edge_count(ed) > 0) tail_claim<LV>(g, sh, edge_target(ed), nxt, Fb, Db, o.claims);
+        }
+        __syncthreads();
+      }
+    }
+    __syncthreads();
+    const uint32_t nn = *sh.next;
+    first = false;
+    ++o.rounds;
+    if (nn == 0) break;
+    if (nn > a.tail_max) {
+      // hand the pending shadows to the level kernels as level L+2 candidates
+      const uint32_t m = min(nn, (uint32_t)TAIL_QCAP);
+      for (uint32_t i = threadIdx.x; i < m; i += TAIL_THREADS) {
+        const uint32_t t = nxt.get(i);
+        atomicAnd(LV ? &sh.vis[t >> 5] : &g.vis[t >> 5], ~(1u << (t & 31)));
+        Fb[t] = 1;
+        Db[t >> 11] = 1;
+      }
+      o.bailed = true;
+      n = m;
+      break;
+    }
+    const TailQ tmp = cur;
+    cur = nxt;
+    nxt = tmp;
+    n = nn;
+    __syncthreads();
+  }
+  o.n = n;
 }
 
 __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) {
@@ -450,6 +578,8 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
   __shared__ uint32_t s_w[40];
   __shared__ uint32_t s_next;
   __shared__ unsigned long long s_red[TAIL_THREADS];
+  __shared__ uint32_t s_q[2][TAIL_LQ];
+  __shared__ uint32_t s_vis[TAIL_LVIS_WORDS];
   Counters *c = g.ctr;
   const int L = a.level;
   if (c->tail_state) return;
@@ -474,9 +604,10 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
     return;
   }
   // Take over: gather the listed frontier from the per-block regions.
-  uint32_t *cur = g.tq, *nxt = g.tq + TAIL_QCAP;
+  TailQ cur{s_q[0], g.tq}, nxt{s_q[1], g.tq + TAIL_QCAP};
+  const uint64_t top = c->slot_top;
   {
-    const uint32_t nblk = (uint32_t)((c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS);
+    const uint32_t nblk = (uint32_t)((top + BLK_SLOTS - 1) / BLK_SLOTS);
     const uint32_t want = (uint32_t)(L + 1);
     uint32_t base = 0;
     for (uint32_t b0 = 0; b0 < nblk; b0 += TAIL_THREADS) {
@@ -486,112 +617,42 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
       uint32_t tot;
       const uint32_t off = base + tail_scan(cnt, s_w, tot);
       for (uint32_t i = 0; i < cnt; ++i)
-        if (off + i < TAIL_QCAP) cur[off + i] = g.tl_buf[(uint64_t)b * BLK_SLOTS + i];
+        if (off + i < TAIL_QCAP) cur.put(off + i, g.tl_buf[(uint64_t)b * BLK_SLOTS + i]);
       base += tot;
     }
-    __syncthreads();
   }
-  const bool investigate = a.flags & LV_INVESTIGATE;
-  uint8_t *Fn = g.front[(L + 1) & 1];  // k_frontier(L)'s supervisor pushes, redone here
-  uint8_t *Dn = g.dirty[(L + 1) & 1];
-  uint8_t *Fb = g.front[L & 1];        // bail: candidates of level L+2
-  uint8_t *Db = g.dirty[L & 1];
-  uint32_t n = (uint32_t)n0;
-  uint32_t n_sup = 0, n_edges = 0, rounds = 0;
-  int32_t claims = 0;
-  bool first = true, bailed = false;
-  for (;;) {
-    if (threadIdx.x == 0) s_next = 0;
-    __syncthreads();
-    for (uint32_t c0 = 0; c0 < n; c0 += TAIL_THREADS) {
-      const uint32_t i = c0 + threadIdx.x;
-      const bool valid = i < n;
-      const uint32_t v = valid ? cur[i] : 0;
-      const uint8_t f = valid ? g.flags[v] : 0;
-      const bool expand = valid && !(f & FL_HALTED);  // (:226-229)
-      if (!first && (f & FL_PROXY)) {  // level L's were listed by k_frontier
-        const uint32_t pos = atomicAdd(&g.xp_cnt[v >> 11], 1u);
-        g.xp_buf[(uint64_t)(v >> 11) * BLK_SLOTS + pos] = v;
-      }
-      uint2 ad = make_uint2(0, 0);
-      if (expand) {
-        ad = g.adj[v];
-        if (!first) n_edges += g.nzdeg[v];  // level L's were counted by k_frontier
-        if (!investigate) {
-          const uint32_t s = g.sup[v];  // (:258-267)
-          if (s < 0xFFFFFFF0u) {
-            if (first) {
-              Fn[s] = 0;
-              Dn[s >> 11] = 0;
-            } else {
-              ++n_sup;
-            }
-            tail_claim(g, s, nxt, &s_next, Fb, Db, claims);
-          }
-        }
-      }
-      uint32_t total;
-      const uint32_t st = tail_scan(ad.y, s_w, total);
-      s_start[threadIdx.x] = st;
-      s_off[threadIdx.x] = ad.x;
-      if (threadIdx.x == 0) s_start[TAIL_THREADS] = total;
-      __syncthreads();
-      for (uint32_t e = threadIdx.x; e < total; e += TAIL_THREADS) {
-        int lo = 0, hi = TAIL_THREADS - 1;  // last item whose start <= e
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (s_start[mid] <= e) lo = mid;
-          else hi = mid - 1;
-        }
-        const uint64_t ed = g.pool[(uint64_t)s_off[lo] + (e - s_start[lo])];
-        if (edge_count(ed) > 0) tail_claim(g, edge_target(ed), nxt, &s_next, Fb, Db, claims);
-      }
-      __syncthreads();
-    }
-    __syncthreads();
-    const uint32_t nn = s_next;
-    first = false;
-    ++rounds;
-    if (nn == 0) break;
-    if (nn > a.tail_max) {
-      // hand the pending shadows to the level kernels as level L+2 candidates
-      const uint32_t m = min(nn, (uint32_t)TAIL_QCAP);
-      for (uint32_t i = threadIdx.x; i < m; i += TAIL_THREADS) {
-        const uint32_t t = nxt[i];
-        atomicAnd(&g.vis[t >> 5], ~(1u << (t & 31)));
-        Fb[t] = 1;
-        Db[t >> 11] = 1;
-      }
-      bailed = true;
-      n = m;
-      break;
-    }
-    uint32_t *tmp = cur;
-    cur = nxt;
-    nxt = tmp;
-    n = nn;
-    __syncthreads();
-  }
+  const bool lv = top <= (uint64_t)TAIL_LVIS_WORDS * 32;
+  const uint32_t nw = (uint32_t)((top + 31) / 32);
+  if (lv)
+    for (uint32_t k = threadIdx.x; k < nw; k += TAIL_THREADS) s_vis[k] = g.vis[k];
+  __syncthreads();
+  const TailLds sh{s_start, s_off, s_w, &s_next, s_vis};
+  TailOut o;
+  if (lv) tail_rounds<true>(g, a, sh, cur, nxt, (uint32_t)n0, o);
+  else tail_rounds<false>(g, a, sh, cur, nxt, (uint32_t)n0, o);
+  __syncthreads();
+  if (lv)
+    for (uint32_t k = threadIdx.x; k < nw; k += TAIL_THREADS) g.vis[k] = s_vis[k];
   // statistics: claims became marked shadows (k_frontier(L) counted level L)
   uint32_t tot_claims, tot_sup, tot_edges;
-  tail_scan((uint32_t)claims, s_w, tot_claims);
-  tail_scan(n_sup, s_w, tot_sup);
-  tail_scan(n_edges, s_w, tot_edges);
+  tail_scan((uint32_t)o.claims, s_w, tot_claims);
+  tail_scan(o.n_sup, s_w, tot_sup);
+  tail_scan(o.n_edges, s_w, tot_edges);
   if (threadIdx.x == 0) {
-    const uint64_t marked_new = (uint64_t)tot_claims - (bailed ? n : 0);  // queued claims undone
+    const uint64_t marked_new = (uint64_t)tot_claims - (o.bailed ? o.n : 0);  // queued claims undone
     c->ring[L % LEVEL_RING] = n0;
     c->marked += n0 + marked_new;
     g.blkstat[STAT_SUP] += tot_sup;
     g.blkstat[STAT_EDGES] += tot_edges;
     c->tail_from = L;
-    if (bailed) {
+    if (o.bailed) {
       c->ring[L % LEVEL_RING] = 1;  // level L+2 runs sparse over the dirty blocks
-      c->ring[(L + 1) % LEVEL_RING] = n;
+      c->ring[(L + 1) % LEVEL_RING] = o.n;
       c->qh[L & 1] = 0;
       c->tail_level = L + 2;
       c->tail_state = TAIL_BAILED;
     } else {
-      c->tail_level = L + rounds;  // levels 0 .. L+rounds-1 were non-empty
+      c->tail_level = L + o.rounds;  // levels 0 .. L+rounds-1 were non-empty
       c->tail_state = TAIL_DONE;
       c->mark_done = 1;
     }
