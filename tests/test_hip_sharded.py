@@ -98,6 +98,60 @@ def test_fuzz_sharded(sharded, oracle_mod, G, seed, cap):
     assert h.export() == o.export()
 
 
+def test_allgather_merge_form_matches_oracle(sharded, oracle_mod, monkeypatch):
+    """CRGC_ROUTE=0: every shard applies its part of every shard's whole batch
+    (the form above 16 shards) instead of receiving routed parts."""
+    monkeypatch.setenv("CRGC_ROUTE", "0")
+    h, o = sharded(3), oracle_mod.OracleGraph()
+    fz = fuzz.Fuzz(17)
+    for step in range(8):
+        eb = fz.entries(400)
+        h.merge_entries(eb, split=True)
+        o.merge_entries(eb)
+        assert h.export() == o.export()
+        _same(h.trace(True), o.trace(True))
+        fz.sync(o.export())
+
+
+def test_routed_and_allgather_forms_agree(sharded, hip_mod, monkeypatch):
+    """The same split batches through both merge forms give the same shards."""
+    w = world.World(seed=0x5EED + 7)
+    w.bulk_graph(20_000, 200_000, alpha=2.1, n_roots=200)
+    batches = list(w.batches(1 << 16)) + [w.wakeup_batch(5_000) for _ in range(2)]
+    routed = sharded(4)
+    monkeypatch.setenv("CRGC_ROUTE", "0")
+    gathered = sharded(4)
+    for b in batches:
+        routed.merge_entries(b, split=True)
+        gathered.merge_entries(b, split=True)
+    for a, c in zip(routed.shards, gathered.shards):
+        assert a.export() == c.export()
+    _same(routed.trace(True), gathered.trace(True))
+
+
+def test_malformed_offsets_fail_every_shard(sharded):
+    """A device batch whose offsets run backwards, contributed by one shard,
+    is refused by every shard (the sender's route count flags it)."""
+    from crgc_hip import EntryBatch
+    h = sharded(2)
+    a, b = (1 << 48) | 5, (1 << 48) | 6
+    u8, i16, u32, u64 = np.uint8, np.int16, np.uint32, np.uint64
+    bad = EntryBatch(np.array([a, b], u64), np.zeros(2, i16), np.array([2, 0], u8),
+                     np.array([0, 2, 1], u32), np.array([a, a], u64), np.array([b, b], u64),
+                     np.zeros(3, u32), np.zeros(0, u64), np.zeros(3, u32), np.zeros(0, u64),
+                     np.zeros(0, i16)).to_device()
+    empty = EntryBatch.from_entries([]).to_device()
+    codes = []
+
+    def go(s, batch):
+        try:
+            s.merge_entries(batch)
+        except abi.CrgcError as e:
+            codes.append(e.code)
+    h._all(go, [(bad,), (empty,)])
+    assert codes == [abi.E_INVAL, abi.E_INVAL]
+
+
 def test_power_law_c1_sharded(sharded, oracle_mod):
     w = world.World(seed=0x5EED + 1)
     w.bulk_graph(100_000, 1_000_000, alpha=2.1, n_roots=1000)

@@ -206,7 +206,10 @@ struct crgc_graph {
   uint32_t G = 1, shard = 0;
   uint64_t n_proxy = 0;              // alive proxy slots at the last sweep
   Scratch x_send, x_slot, x_recv, x_ans, x_ans_back, x_small, x_pack, x_pack_recv;
+  Scratch x_route, x_route_send, x_cat;  // routed entry merges
   uint64_t *h_small = nullptr;       // pinned host staging for small all-gathers
+  char *h_route = nullptr;           // pinned RoutePart / ConcatPart tables
+  bool route = true;                 // CRGC_ROUTE=0: all-gather every batch instead
 };
 
 namespace {
@@ -394,6 +397,7 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     h->G = cfg->n_shards;
     h->shard = cfg->shard;
     h->tp = cfg->transport;
+    if (const char *m = getenv("CRGC_ROUTE")) h->route = atoi(m) != 0;
   }
   DeviceGuard dg(h->device);
   int rc = CRGC_OK;
@@ -413,7 +417,8 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     if (hipMalloc(&h->ctr, sizeof(Counters)) != hipSuccess ||
         hipHostMalloc(&h->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&h->h_small, 8 * (size_t)MAX_SHARDS * (MAX_SHARDS + 8), hipHostMallocDefault) !=
-            hipSuccess) {
+            hipSuccess ||
+        hipHostMalloc(&h->h_route, ROUTE_TABLE_BYTES, hipHostMallocDefault) != hipSuccess) {
       rc = CRGC_E_NOMEM;
       break;
     }
@@ -444,11 +449,12 @@ void crgc_destroy(crgc_graph *h) {
   h->stage.release();
   h->work.release();
   for (Scratch *x : {&h->x_send, &h->x_slot, &h->x_recv, &h->x_ans, &h->x_ans_back, &h->x_small,
-                     &h->x_pack, &h->x_pack_recv})
+                     &h->x_pack, &h->x_pack_recv, &h->x_route, &h->x_route_send, &h->x_cat})
     x->release();
   if (h->ctr) hipFree(h->ctr);
   if (h->hctr) hipHostFree(h->hctr);
   if (h->h_small) hipHostFree(h->h_small);
+  if (h->h_route) hipHostFree(h->h_route);
   if (h->roots_buf) hipFree(h->roots_buf);
   for (auto &e : h->ev)
     if (e) hipEventDestroy(e);
@@ -720,12 +726,181 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   return CRGC_OK;
 }
 
+static size_t part_bytes(uint64_t n, uint64_t C, uint64_t S, uint64_t U) {
+  return n ? entry_layout(n, C, S, U).total : 0;
+}
+
+static RoutePart part_at(char *base, uint64_t n, uint64_t C, uint64_t S, uint64_t U) {
+  const Layout l = entry_layout(n, C, S, U);
+  RoutePart p;
+  p.self = (uint64_t *)(base + l.off[0]);
+  p.recv = (int16_t *)(base + l.off[1]);
+  p.flags = (uint8_t *)(base + l.off[2]);
+  p.c_off = (uint32_t *)(base + l.off[3]);
+  p.c_owner = (uint64_t *)(base + l.off[4]);
+  p.c_target = (uint64_t *)(base + l.off[5]);
+  p.s_off = (uint32_t *)(base + l.off[6]);
+  p.spawned = (uint64_t *)(base + l.off[7]);
+  p.u_off = (uint32_t *)(base + l.off[8]);
+  p.u_ref = (uint64_t *)(base + l.off[9]);
+  p.u_info = (int16_t *)(base + l.off[10]);
+  return p;
+}
+
+static crgc_entry_batch batch_of(const RoutePart &p, uint64_t n) {
+  crgc_entry_batch v{};
+  v.n_entries = n;
+  v.self = p.self;
+  v.recv_count = p.recv;
+  v.flags = p.flags;
+  v.created_off = p.c_off;
+  v.created_owner = p.c_owner;
+  v.created_target = p.c_target;
+  v.spawned_off = p.s_off;
+  v.spawned = p.spawned;
+  v.updated_off = p.u_off;
+  v.updated_ref = p.u_ref;
+  v.updated_info = p.u_info;
+  v.memory = CRGC_MEM_DEVICE;
+  return v;
+}
+
+// Sharded, routed (crgc_route.hip): every shard cuts its batch into one part
+// per destination shard, one all-to-all moves the parts, and every shard
+// merges what it received, concatenated in shard order, as one batch.
+static int merge_entries_routed(crgc_graph *h, const crgc_entry_batch *b, int vrc, uint64_t C, uint64_t S,
+                                uint64_t U) {
+  const uint32_t G = h->G, me = h->shard;
+  const uint64_t n = vrc ? 0 : b->n_entries;
+  const uint64_t nblk = (n + RT_THREADS - 1) / RT_THREADS;
+  const size_t need = Carver::need({8, (size_t)G * 32, (size_t)G * nblk * 8, (size_t)G * nblk * 32,
+                                    sizeof(RoutePart) * ROUTE_MAX_SHARDS, sizeof(ConcatPart) * ROUTE_MAX_SHARDS});
+  if (h->x_route.ensure(need) != hipSuccess) return CRGC_E_NOMEM;
+  Carver rv(h->x_route.ptr);
+  RouteArgs a{};
+  a.err = rv.take<unsigned long long>(1);
+  a.totals = rv.take<uint64_t>((size_t)G * 4);
+  a.blk_tot = rv.take<uint64_t>((size_t)G * nblk);
+  a.blk_pre = rv.take<uint64_t>((size_t)G * nblk * 4);
+  RoutePart *d_parts = rv.take<RoutePart>(ROUTE_MAX_SHARDS);
+  ConcatPart *d_cat = rv.take<ConcatPart>(ROUTE_MAX_SHARDS);
+  HIP_TRY(hipMemsetAsync(a.err, 0, 8, h->stream));
+  HIP_TRY(hipMemsetAsync(a.totals, 0, (size_t)G * 32, h->stream));
+  if (n) {
+    const void *src[11] = {b->self,    b->recv_count, b->flags,       b->created_off, b->created_owner,
+                           b->created_target, b->spawned_off, b->spawned, b->updated_off, b->updated_ref,
+                           b->updated_info};
+    const void *p[11];
+    if (b->memory == CRGC_MEM_HOST) {  // one staging copy per array, then every part from HBM
+      const Layout l = entry_layout(n, C, S, U);
+      if (h->x_pack.ensure(l.total) != hipSuccess) return CRGC_E_NOMEM;
+      if (int rc = pack(h, l, src, 11, CRGC_MEM_HOST, (char *)h->x_pack.ptr)) return rc;
+      for (int i = 0; i < 11; ++i) p[i] = (char *)h->x_pack.ptr + l.off[i];
+    } else {
+      for (int i = 0; i < 11; ++i) p[i] = src[i];
+    }
+    a.n = n;
+    a.nblk = nblk;
+    a.G = G;
+    a.F = h->F;
+    a.C = C;
+    a.S = S;
+    a.U = U;
+    a.self = (const uint64_t *)p[0];
+    a.recv = (const int16_t *)p[1];
+    a.flags = (const uint8_t *)p[2];
+    a.c_off = (const uint32_t *)p[3];
+    a.c_owner = (const uint64_t *)p[4];
+    a.c_target = (const uint64_t *)p[5];
+    a.s_off = (const uint32_t *)p[6];
+    a.spawned = (const uint64_t *)p[7];
+    a.u_off = (const uint32_t *)p[8];
+    a.u_ref = (const uint64_t *)p[9];
+    a.u_info = (const int16_t *)p[10];
+    HIP_TRY(launch_route(a, 0, nullptr, h->stream));
+  }
+  // every shard's validation status, malformed-offset word and per-destination counts
+  const uint32_t K = 2 + 4 * G;
+  std::vector<uint64_t> H((size_t)G * K);
+  h->h_small[0] = (uint64_t)(int64_t)vrc;
+  if (int rc = ag_u64(h, {{h->h_small, 1}, {a.err, 1}, {a.totals, 4 * G}}, H.data())) return rc;
+  bool bad = false;
+  for (uint32_t r = 0; r < G; ++r) bad |= H[(size_t)r * K] != 0 || H[(size_t)r * K + 1] != 0;
+  if (bad) {  // all fail together; malformed offsets would have poisoned every shard
+    if (vrc) return vrc;
+    for (uint32_t r = 0; r < G; ++r)
+      if (H[(size_t)r * K + 1]) h->poisoned = true;
+    return CRGC_E_INVAL;
+  }
+  auto tot = [&](uint32_t from, uint32_t to, int q) { return H[(size_t)from * K + 2 + to * 4 + q]; };
+  size_t soff[MAX_SHARDS], sb[MAX_SHARDS], roff[MAX_SHARDS], rb[MAX_SHARDS];
+  size_t so = 0, ro = 0;
+  for (uint32_t r = 0; r < G; ++r) {
+    soff[r] = so;
+    sb[r] = part_bytes(tot(me, r, 0), tot(me, r, 1), tot(me, r, 2), tot(me, r, 3));
+    so += sb[r];
+    roff[r] = ro;
+    rb[r] = part_bytes(tot(r, me, 0), tot(r, me, 1), tot(r, me, 2), tot(r, me, 3));
+    ro += rb[r];
+  }
+  if (h->x_route_send.ensure(so + 256) != hipSuccess || h->x_pack_recv.ensure(ro + 256) != hipSuccess)
+    return CRGC_E_NOMEM;
+  if (n) {
+    RoutePart *tab = (RoutePart *)h->h_route;
+    for (uint32_t d = 0; d < G; ++d)
+      tab[d] = part_at((char *)h->x_route_send.ptr + soff[d], tot(me, d, 0), tot(me, d, 1), tot(me, d, 2),
+                       tot(me, d, 3));
+    HIP_TRY(hipMemcpyAsync(d_parts, tab, sizeof(RoutePart) * G, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(launch_route(a, 1, d_parts, h->stream));
+  }
+  if (int rc = h->tp->alltoallv(me, h->x_route_send.ptr, soff, sb, h->x_pack_recv.ptr, roff, rb, h->stream)) {
+    h->poisoned = true;
+    return rc;
+  }
+  // the received parts, in shard order, as one batch
+  uint64_t N = 0, Ct = 0, St = 0, Ut = 0;
+  uint32_t sources = 0, last = 0;
+  ConcatPart *cat = (ConcatPart *)(h->h_route + 4096);
+  for (uint32_t r = 0; r < G; ++r) {
+    const uint64_t rn = tot(r, me, 0);
+    const Layout l = entry_layout(rn, tot(r, me, 1), tot(r, me, 2), tot(r, me, 3));
+    cat[r].base = (const char *)h->x_pack_recv.ptr + roff[r];
+    for (int i = 0; i < 11; ++i) cat[r].off[i] = l.off[i];
+    cat[r].pn = N;
+    cat[r].pC = Ct;
+    cat[r].pS = St;
+    cat[r].pU = Ut;
+    N += rn;
+    Ct += tot(r, me, 1);
+    St += tot(r, me, 2);
+    Ut += tot(r, me, 3);
+    if (rn) {
+      ++sources;
+      last = r;
+    }
+  }
+  if (N == 0) return CRGC_OK;
+  crgc_entry_batch v;
+  if (sources == 1) {  // one sender: its part is the batch
+    v = batch_of(part_at((char *)h->x_pack_recv.ptr + roff[last], N, Ct, St, Ut), N);
+  } else {
+    if (h->x_cat.ensure(part_bytes(N, Ct, St, Ut) + 256) != hipSuccess) return CRGC_E_NOMEM;
+    const RoutePart dst = part_at((char *)h->x_cat.ptr, N, Ct, St, Ut);
+    HIP_TRY(hipMemcpyAsync(d_cat, cat, sizeof(ConcatPart) * G, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(launch_concat(d_cat, G, dst, N, Ct, St, Ut, h->stream));
+    v = batch_of(dst, N);
+  }
+  return merge_entries_one(h, &v, Ct, St, Ut);
+}
+
 int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
   if (int rc = check_graph(h)) return rc;
   DeviceGuard dg(h->device);
   uint64_t C = 0, S = 0, U = 0;
   const int vrc = entry_counts(h, b, h->tp, &C, &S, &U);
   if (!h->tp) return vrc ? vrc : merge_entries_one(h, b, C, S, U);
+  if (h->route && h->G <= ROUTE_MAX_SHARDS && h->F <= ROUTE_MAX_F)
+    return merge_entries_routed(h, b, vrc, C, S, U);
   // Sharded: every shard applies its part of every shard's batch, in shard order.
   const uint64_t n = vrc ? 0 : b->n_entries;
   const uint64_t hdr[5] = {(uint64_t)(int64_t)vrc, n, C, S, U};

@@ -206,6 +206,61 @@ hipError_t launch_rebuild(const DevGraph &src, uint64_t src_slot_top, const DevG
                           hipStream_t s);
 size_t rebuild_scan_tmp_bytes(uint64_t n);
 
+// routed sharded entry merges (crgc_route.hip)
+constexpr int RT_THREADS = 256;
+constexpr uint32_t ROUTE_MAX_SHARDS = 16;  // above: the all-gather form
+constexpr uint32_t ROUTE_MAX_F = 255;      // per-block counts packed in 16 bits
+constexpr size_t ROUTE_TABLE_BYTES = 8192; // pinned RoutePart[16] at 0, ConcatPart[16] at 4096
+
+struct RouteArgs {
+  uint64_t n, nblk;
+  uint32_t G, F;
+  uint64_t C, S, U;  // record counts of the batch (offset bounds)
+  const uint64_t *self;
+  const int16_t *recv;
+  const uint8_t *flags;
+  const uint32_t *c_off;
+  const uint64_t *c_owner;
+  const uint64_t *c_target;
+  const uint32_t *s_off;
+  const uint64_t *spawned;
+  const uint32_t *u_off;
+  const uint64_t *u_ref;
+  const int16_t *u_info;
+  unsigned long long *err;  // malformed offsets (set by k_route_count)
+  uint64_t *blk_tot;        // [G * nblk] packed per-block counts
+  uint64_t *blk_pre;        // [G * nblk * 4] exclusive block prefixes
+  uint64_t *totals;         // [G * 4] entries, created, spawned, updated per destination
+};
+
+// One destination's part: an entry batch in device memory.
+struct RoutePart {
+  uint64_t *self;
+  int16_t *recv;
+  uint8_t *flags;
+  uint32_t *c_off;
+  uint64_t *c_owner;
+  uint64_t *c_target;
+  uint32_t *s_off;
+  uint64_t *spawned;
+  uint32_t *u_off;
+  uint64_t *u_ref;
+  int16_t *u_info;
+};
+
+// One received part (entry_layout offsets from base) and where it lands in
+// the concatenated batch.
+struct ConcatPart {
+  const char *base;
+  uint64_t off[11];
+  uint64_t pn, pC, pS, pU;
+};
+
+// phase 0: k_route_count + k_route_scan; phase 1: k_route_scatter (parts on the device)
+hipError_t launch_route(const RouteArgs &a, int phase, const RoutePart *parts, hipStream_t s);
+hipError_t launch_concat(const ConcatPart *parts, uint32_t G, const RoutePart &dst, uint64_t N, uint64_t C,
+                         uint64_t S, uint64_t U, hipStream_t s);
+
 int grid_for(uint64_t threads, int block = 256, int cap = 4096);
 
 }  // namespace crgc
