@@ -1154,6 +1154,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   la.flags = LV_CHECK_BEFORE_STORE;
   if (const char *m = getenv("CRGC_MARK_CHECK")) la.flags = atoi(m) ? LV_CHECK_BEFORE_STORE : 0;
   if (const char *m = getenv("CRGC_MARK_BITS")) la.flags |= atoi(m) ? LV_BITMAP_FRONT : 0;
+  if (const char *m = getenv("CRGC_EXP8")) la.flags |= atoi(m) ? LV_EXP8 : 0;
   la.sparse_thresh = (uint32_t)std::max<uint64_t>(64, (top / BLK_SLOTS) / 4);
   // Direction optimisation: dense levels after a frontier of >= top/div shadows pull.
   uint64_t pull_div = 16;

@@ -155,6 +155,7 @@ constexpr uint32_t LV_PULL = 4;                // dense levels scan in-candidate
 constexpr uint32_t LV_TAIL = 8;                // narrow frontiers go to one workgroup (k_tail)
 constexpr uint32_t LV_INVESTIGATE = 16;        // set by launch_level: no supervisor edges
 constexpr uint32_t LV_ROOTS = 32;              // set by launch_level: the pseudo-root level
+constexpr uint32_t LV_EXP8 = 64;               // k_expand: 8 edges per lane per step (else 4)
 
 struct LevelArgs {
   int level;

@@ -24,7 +24,6 @@
 namespace crgc {
 
 constexpr uint32_t RANGE_MAX = 256;  // longer segments (hubs) are cut into pieces
-constexpr int EXP_UNROLL = 4;        // independent edge loads in flight per lane
 constexpr int STAT_FRONT = 0, STAT_SUP = 1, STAT_EDGES = 2, STAT_LIVE = 3;
 
 __device__ inline bool sparse_level(const Counters *c, int L, uint32_t thr) {
@@ -261,20 +260,54 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
   }
 }
 
-__device__ inline void expand_edge(const DevGraph &g, uint8_t *Fn, uint8_t *Dn, bool sp_next, bool check,
-                                   uint64_t ed, uint32_t *Fbits) {
-  const int32_t cntv = edge_count(ed);
-  if (cntv > 0) {  // (:231-241)
-    if (Fbits) mark_target_bits(g, Fbits, Dn, sp_next, edge_target(ed));
-    else mark_target(g, Fn, Dn, sp_next, edge_target(ed), check);
+// U edges of one lane (:231-241).  Each phase issues all its loads
+// before any is waited on: the vis words, then the candidate bytes of the
+// targets still unmarked, then the stores — two dependent round trips per
+// group of edges instead of two per edge (a byte store may alias any load, so
+// per-edge marking would serialise them).
+template <int U>
+__device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn, bool sp_next, bool check,
+                                    const uint64_t (&ed)[U], uint32_t *Fbits) {
+  uint32_t t[U];
+  bool go[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    go[u] = edge_count(ed[u]) > 0;
+    t[u] = edge_target(ed[u]);
+  }
+  if (Fbits) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (go[u]) mark_target_bits(g, Fbits, Dn, sp_next, t[u]);
+    return;
+  }
+  uint32_t w[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) w[u] = go[u] ? g.vis[t[u] >> 5] : ~0u;
+#pragma unroll
+  for (int u = 0; u < U; ++u) go[u] = !((w[u] >> (t[u] & 31)) & 1u);
+  uint8_t fb[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) fb[u] = (go[u] && check) ? Fn[t[u]] : 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (go[u] && fb[u] == 0) Fn[t[u]] = 1;
+  if (sp_next) {
+    uint8_t db[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) db[u] = go[u] ? Dn[t[u] >> 11] : 1;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (db[u] == 0) Dn[t[u] >> 11] = 1;
   }
 }
 
 // ---------------------------------------------------------------------------
 // k_expand: every wave of the grid walks the level's ranges, 64 light ranges
 // per step (degree scan + binary search in LDS assigns edges to lanes) or one
-// hub piece per step, EXP_UNROLL independent edge loads per lane.
+// hub piece per step, U independent edge loads per lane.
 // ---------------------------------------------------------------------------
+template <int U>
 __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   __shared__ uint32_t s_start[4][65];
   __shared__ uint32_t s_off[4][64];
@@ -357,10 +390,10 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
     s_start[wv][lane] = incl - r.y;
     s_off[wv][lane] = r.x;
     wave_lds_fence();
-    for (uint32_t e0 = 0; e0 < dtot; e0 += 64 * EXP_UNROLL) {
-      uint64_t ed[EXP_UNROLL];
+    for (uint32_t e0 = 0; e0 < dtot; e0 += 64 * U) {
+      uint64_t ed[U];
 #pragma unroll
-      for (int u = 0; u < EXP_UNROLL; ++u) {
+      for (int u = 0; u < U; ++u) {
         const uint32_t e = e0 + u * 64 + lane;
         ed[u] = 0;  // count 0: neither traced nor counted
         if (e < dtot) {
@@ -373,25 +406,21 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
           ed[u] = g.pool[(uint64_t)s_off[wv][lo] + (e - s_start[wv][lo])];
         }
       }
-#pragma unroll
-      for (int u = 0; u < EXP_UNROLL; ++u)
-        expand_edge(g, Fn, Dn, sp_next, check, ed[u], Fbits);
+      expand_edges(g, Fn, Dn, sp_next, check, ed, Fbits);
     }
     wave_lds_fence();
   }
   // hub pieces: one per step
   for (uint64_t hi = gw; hi < nh; hi += nw) {
     const uint2 r = g.qh_buf[hi];
-    for (uint32_t e0 = 0; e0 < r.y; e0 += 64 * EXP_UNROLL) {
-      uint64_t ed[EXP_UNROLL];
+    for (uint32_t e0 = 0; e0 < r.y; e0 += 64 * U) {
+      uint64_t ed[U];
 #pragma unroll
-      for (int u = 0; u < EXP_UNROLL; ++u) {
+      for (int u = 0; u < U; ++u) {
         const uint32_t e = e0 + u * 64 + lane;
         ed[u] = e < r.y ? g.pool[(uint64_t)r.x + e] : 0;
       }
-#pragma unroll
-      for (int u = 0; u < EXP_UNROLL; ++u)
-        expand_edge(g, Fn, Dn, sp_next, check, ed[u], Fbits);
+      expand_edges(g, Fn, Dn, sp_next, check, ed, Fbits);
     }
   }
 }
@@ -689,7 +718,10 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
   // level controller: the level count, and the narrow-frontier takeover
   hipExtLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, e[2], e[3], 0, g, a);
   // 8 WGs of 4 waves per CU
-  hipExtLaunchKernelGGL(k_expand, dim3(STAT_WG), dim3(256), 0, s, e[4], e[5], 0, g, a);
+  if (a.flags & LV_EXP8)
+    hipExtLaunchKernelGGL(k_expand<8>, dim3(STAT_WG), dim3(256), 0, s, e[4], e[5], 0, g, a);
+  else
+    hipExtLaunchKernelGGL(k_expand<4>, dim3(STAT_WG), dim3(256), 0, s, e[4], e[5], 0, g, a);
   return hipGetLastError();
 }
 
