@@ -201,6 +201,50 @@ typedef struct crgc_trace_out {
   crgc_trace_stats stats;
 } crgc_trace_out;
 
+/*
+ * DeltaGraphs of one wakeup's entries, built on the device:
+ * what LocalGC does per entry when num-nodes > 1 (LocalGC.scala:159-177) —
+ * fold the entries, in queue order, into DeltaGraph.mergeEntry
+ * (DeltaGraph.java:73-125), finalize the graph whenever isFull() holds after
+ * an entry (:174-180) and finalize the last non-empty one at the end.
+ *
+ * Outputs, per graph g, shadows in compressed-id order:
+ *   - the decoded shadows as one crgc_delta_batch (graphs back to back,
+ *     outgoing entries in Java iteration order), ready for crgc_merge_deltas
+ *     on a remote node's graph;
+ *   - the DataOutput bytes DeltaGraph.serialize writes between the address
+ *     object and the compression table (DeltaGraph.java:196-200): big-endian
+ *     writeShort(size), then DeltaShadow.serialize of every shadow
+ *     (DeltaShadow.java:57-69) with the outgoing map in java.util.HashMap
+ *     iteration order.  The JVM writes the address, these bytes
+ *     (ObjectOutputStream.write: the same block-data stream as the field
+ *     writes), then the compression table from decoder ids.
+ * All arrays are caller buffers in `memory`; graph_off / wire_off /
+ * out_off hold one more element than their counts.  Pass NULL arrays to learn
+ * the sizes; CRGC_E2BIG when a capacity is short (the counts hold the sizes).
+ * Requires delta_graph_size <= 64 and delta_graph_size > 4*F + 1.
+ */
+typedef struct crgc_delta_graphs {
+  uint32_t memory;         /* CRGC_MEM_HOST / CRGC_MEM_DEVICE                  */
+  uint32_t _pad;
+  uint64_t graph_cap, n_graphs;
+  uint32_t *graph_off;     /* [n_graphs+1] first shadow of each graph          */
+  uint64_t *wire_off;      /* [n_graphs+1] first wire byte of each graph       */
+  uint64_t shadow_cap, n_shadows;
+  uint64_t *id;            /* [n_shadows] decoder[cid]                         */
+  int32_t *recv_count;
+  uint64_t *supervisor;    /* decoder[supervisor] or CRGC_NO_ACTOR             */
+  uint8_t *flags;          /* CRGC_DELTA_*                                     */
+  uint32_t *out_off;       /* [n_shadows+1]                                    */
+  uint64_t out_cap, n_out;
+  uint64_t *out_target;
+  int32_t *out_count;
+  uint64_t wire_cap, wire_bytes;
+  uint8_t *wire;
+} crgc_delta_graphs;
+
+int crgc_build_delta_graphs(crgc_graph *g, const crgc_entry_batch *batch, crgc_delta_graphs *out);
+
 /* Full graph state, for parity tests and debugging (the reference's
  * ShadowGraph.assertEquals / Shadow.assertEquals, ShadowGraph.java:176-199).
  * Two-phase: call with NULL arrays to learn n_vertices / n_edges. */

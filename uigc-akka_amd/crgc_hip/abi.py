@@ -152,6 +152,31 @@ class CrgcGraphExport(C.Structure):
     ]
 
 
+class CrgcDeltaGraphs(C.Structure):
+    _fields_ = [
+        ("memory", C.c_uint32),
+        ("_pad", C.c_uint32),
+        ("graph_cap", _U64),
+        ("n_graphs", _U64),
+        ("graph_off", _P),
+        ("wire_off", _P),
+        ("shadow_cap", _U64),
+        ("n_shadows", _U64),
+        ("id", _P),
+        ("recv_count", _P),
+        ("supervisor", _P),
+        ("flags", _P),
+        ("out_off", _P),
+        ("out_cap", _U64),
+        ("n_out", _U64),
+        ("out_target", _P),
+        ("out_count", _P),
+        ("wire_cap", _U64),
+        ("wire_bytes", _U64),
+        ("wire", _P),
+    ]
+
+
 # Entry points declared in include/crgc.h — every one must be exported.
 EXPORTED_SYMBOLS = (
     "crgc_create",
@@ -166,6 +191,7 @@ EXPORTED_SYMBOLS = (
     "crgc_total_actors_seen",
     "crgc_live_count",
     "crgc_export",
+    "crgc_build_delta_graphs",
     "crgc_strerror",
     "crgc_transport_rccl_id",
     "crgc_transport_rccl",
@@ -232,6 +258,8 @@ def load_library(path: str | None = None) -> C.CDLL:
     lib.crgc_transport_destroy.argtypes = [_P]
     lib.crgc_shard_of.restype = C.c_uint32
     lib.crgc_shard_of.argtypes = [_U64, C.c_uint32]
+    lib.crgc_build_delta_graphs.restype = C.c_int
+    lib.crgc_build_delta_graphs.argtypes = [_P, C.POINTER(CrgcEntryBatch), C.POINTER(CrgcDeltaGraphs)]
     _declare(lib, "crgc_")
     if path is None:
         _lib = lib

@@ -69,6 +69,8 @@ class ShadowGraph:
         self._chk(self.lib.crgc_create(C.byref(cfg), C.byref(h)), "crgc_create")
         self.h = h
         self.F = entry_field_size
+        self.DGS = delta_graph_size
+        self.device = device
         self._pending: List[Entry] = []
 
     # -- lifecycle ------------------------------------------------------------
@@ -209,6 +211,49 @@ class ShadowGraph:
     def export(self):
         self.flush()
         return export_to_state(self.lib.crgc_export, self.h)
+
+    # -- DeltaGraph production (num-nodes > 1, LocalGC.scala:159-177) --------------
+    def build_delta_graphs(self, batch: EntryBatch, device_out: bool = False):
+        """The wakeup's entries folded into DeltaGraphs on the device
+        (DeltaGraph.java:73-180).  Returns (DeltaBatch of the decoded shadows,
+        graph_off, wire bytes, wire_off): graph g is shadows
+        graph_off[g]:graph_off[g+1] and payload bytes wire[wire_off[g]:wire_off[g+1]]
+        (writeShort(size) + DeltaShadow.serialize per shadow).  device_out: the
+        arrays are torch tensors on the graph's device."""
+        s = batch.struct()
+        q = abi.CrgcDeltaGraphs()
+        q.memory = abi.MEM_DEVICE if device_out else abi.MEM_HOST
+        self._chk(self.lib.crgc_build_delta_graphs(self.h, C.byref(s), C.byref(q)),
+                  "crgc_build_delta_graphs")
+        G, NS, NO, NW = q.n_graphs, q.n_shadows, q.n_out, q.wire_bytes
+        if device_out:
+            import torch
+            dev = f"cuda:{self.device}"
+            mk = lambda n, dt: torch.empty(max(n, 1), dtype=dt, device=dev)  # noqa: E731
+            u32, u64 = torch.uint32, torch.uint64
+            arrs = dict(graph_off=mk(G + 1, u32), wire_off=mk(G + 1, u64), id=mk(NS, u64),
+                        recv_count=mk(NS, torch.int32), supervisor=mk(NS, u64),
+                        flags=mk(NS, torch.uint8), out_off=mk(NS + 1, u32),
+                        out_target=mk(NO, u64), out_count=mk(NO, torch.int32),
+                        wire=mk(NW, torch.uint8))
+        else:
+            mk = lambda n, dt: np.zeros(max(n, 1), dtype=dt)  # noqa: E731
+            arrs = dict(graph_off=mk(G + 1, np.uint32), wire_off=mk(G + 1, np.uint64),
+                        id=mk(NS, np.uint64), recv_count=mk(NS, np.int32),
+                        supervisor=mk(NS, np.uint64), flags=mk(NS, np.uint8),
+                        out_off=mk(NS + 1, np.uint32), out_target=mk(NO, np.uint64),
+                        out_count=mk(NO, np.int32), wire=mk(NW, np.uint8))
+        for k, v in arrs.items():
+            setattr(q, k, _ptr(v))
+        q.graph_cap, q.shadow_cap, q.out_cap, q.wire_cap = G, NS, NO, NW
+        self._chk(self.lib.crgc_build_delta_graphs(self.h, C.byref(s), C.byref(q)),
+                  "crgc_build_delta_graphs")
+        cut = lambda k, n: arrs[k][:n]  # noqa: E731
+        mem = abi.MEM_DEVICE if device_out else abi.MEM_HOST
+        deltas = DeltaBatch(cut("id", NS), cut("recv_count", NS), cut("supervisor", NS),
+                            cut("flags", NS), cut("out_off", NS + 1), cut("out_target", NO),
+                            cut("out_count", NO), memory=mem)
+        return deltas, cut("graph_off", G + 1), cut("wire", NW), cut("wire_off", G + 1)
 
 
 class Transport:

@@ -207,6 +207,7 @@ struct crgc_graph {
   uint64_t n_proxy = 0;              // alive proxy slots at the last sweep
   Scratch x_send, x_slot, x_recv, x_ans, x_ans_back, x_small, x_pack, x_pack_recv;
   Scratch x_route, x_route_send, x_cat;  // routed entry merges
+  Scratch x_dg, x_dg_store, x_dg_out;    // DeltaGraph production
   uint64_t *h_small = nullptr;       // pinned host staging for small all-gathers
   char *h_route = nullptr;           // pinned RoutePart / ConcatPart tables
   bool route = true;                 // CRGC_ROUTE=0: all-gather every batch instead
@@ -449,7 +450,8 @@ void crgc_destroy(crgc_graph *h) {
   h->stage.release();
   h->work.release();
   for (Scratch *x : {&h->x_send, &h->x_slot, &h->x_recv, &h->x_ans, &h->x_ans_back, &h->x_small,
-                     &h->x_pack, &h->x_pack_recv, &h->x_route, &h->x_route_send, &h->x_cat})
+                     &h->x_pack, &h->x_pack_recv, &h->x_route, &h->x_route_send, &h->x_cat,
+                     &h->x_dg, &h->x_dg_store, &h->x_dg_out})
     x->release();
   if (h->ctr) hipFree(h->ctr);
   if (h->hctr) hipHostFree(h->hctr);
@@ -1535,6 +1537,163 @@ int crgc_last_trace(crgc_graph *h, crgc_trace_out *out) {
   if (!out || !h->have_last) return CRGC_E_INVAL;
   DeviceGuard dg(h->device);
   return copy_lists(h, out);
+}
+
+// DeltaGraphs of one wakeup (crgc_delta.hip): the chain of graph starts,
+// then a count pass, scans, and a write pass over the graphs.
+int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta_graphs *out) {
+  if (int rc = check_graph(h)) return rc;
+  if (!out || out->memory > CRGC_MEM_DEVICE) return CRGC_E_INVAL;
+  if (h->DGS > DG_MAX || h->DGS <= 4 * h->F + 1) return CRGC_E_INVAL;
+  DeviceGuard dg(h->device);
+  uint64_t C = 0, S = 0, U = 0;
+  if (int rc = entry_counts(h, b, true, &C, &S, &U)) return rc;
+  const uint64_t n = b->n_entries;
+  if (n >= (1ull << 31)) return CRGC_E_INVAL;
+  const size_t nh_bytes =
+      b->memory == CRGC_MEM_HOST
+          ? Carver::need({n * 8, n * 2, n, (n + 1) * 4, C * 8, C * 8, (n + 1) * 4, S * 8, (n + 1) * 4, U * 8,
+                          U * 2})
+          : 0;
+  uint32_t levels = 1;
+  while ((1ull << (levels - 1)) < n + 1) ++levels;
+  const uint64_t N = n + 1, nblk = (n + 1023) / 1024, nbs = 4 * ((N + 1023) / 1024) + 8;
+  const size_t need = Carver::need({sizeof(DgCounters), (size_t)levels * N * 4, N, N, nblk * 4 + 4,
+                                    nblk * 8 + 8, nbs * 8, N * 4, N * 4, N * 4, N * 4, N * 4, N * 8, N * 8,
+                                    N * 8, N * 8});
+  if (h->stage.ensure(nh_bytes + 256) != hipSuccess || h->x_dg.ensure(need) != hipSuccess)
+    return CRGC_E_NOMEM;
+  Carver sc(h->stage.ptr), dc(h->x_dg.ptr);
+  DgArgs a{};
+  a.n = n;
+  a.F = h->F;
+  a.DGS = h->DGS;
+  a.T = h->DGS - 4 * h->F - 1;
+  a.C = C;
+  a.S = S;
+  a.U = U;
+  if (n) {
+    a.self = stage(h, sc, b->self, n, b->memory);
+    a.recv = stage(h, sc, b->recv_count, n, b->memory);
+    a.flags = stage(h, sc, b->flags, n, b->memory);
+    a.c_off = stage(h, sc, b->created_off, n + 1, b->memory);
+    a.c_owner = stage(h, sc, b->created_owner, C, b->memory);
+    a.c_target = stage(h, sc, b->created_target, C, b->memory);
+    a.s_off = stage(h, sc, b->spawned_off, n + 1, b->memory);
+    a.spawned = stage(h, sc, b->spawned, S, b->memory);
+    a.u_off = stage(h, sc, b->updated_off, n + 1, b->memory);
+    a.u_ref = stage(h, sc, b->updated_ref, U, b->memory);
+    a.u_info = stage(h, sc, b->updated_info, U, b->memory);
+  }
+  a.ctr = dc.take<DgCounters>(1);
+  a.J = dc.take<uint32_t>((size_t)levels * N);
+  a.levels = levels;
+  a.mark = dc.take<uint8_t>(N);
+  a.lng = dc.take<uint8_t>(N);
+  a.blk = dc.take<uint32_t>(nblk + 1);
+  a.blk_off = dc.take<uint64_t>(nblk + 1);
+  a.bsum = dc.take<uint64_t>(nbs);
+  a.starts = dc.take<uint32_t>(N);
+  a.g_size = dc.take<uint32_t>(N);
+  a.g_nout = dc.take<uint32_t>(N);
+  a.g_bytes = dc.take<uint32_t>(N);
+  a.g_big = dc.take<uint32_t>(N);
+  a.g_shadow = dc.take<uint64_t>(N);
+  a.g_out = dc.take<uint64_t>(N);
+  a.g_wire = dc.take<uint64_t>(N);
+  a.g_bigrank = dc.take<uint64_t>(N);
+  HIP_TRY(hipMemsetAsync(a.ctr, 0, sizeof(DgCounters), h->stream));
+  DgCounters hc{};
+  auto fetch = [&]() -> int {
+    HIP_TRY(hipMemcpyAsync(&hc, a.ctr, sizeof(DgCounters), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return CRGC_OK;
+  };
+  uint64_t G = 0;
+  if (n) {
+    HIP_TRY(launch_dg_chain(a, 0, h->stream));
+    if (int rc = fetch()) return rc;
+    if (hc.err) return CRGC_E_INVAL;  // malformed offsets or reserved ids: nothing was built
+    while (hc.first_long != ~0u) {  // a chain start whose graph runs past DG_SPAN_CAP entries
+      HIP_TRY(launch_dg_chain(a, 1, h->stream));
+      if (int rc = fetch()) return rc;
+    }
+    G = hc.n_graphs;
+    DgOut none{};
+    HIP_TRY(launch_dg_build(a, G, false, false, 0, none, h->stream));
+    HIP_TRY(launch_dg_scans(a, G, false, h->stream));
+    if (int rc = fetch()) return rc;
+    if (hc.n_big) {  // graphs with more outgoing records than LDS holds
+      a.store_words = dg_store_words(h->DGS);
+      const uint64_t win = std::min<uint64_t>(hc.n_big, DG_BIG_WINDOW);
+      if (h->x_dg_store.ensure(win * a.store_words * 8) != hipSuccess) return CRGC_E_NOMEM;
+      a.store = (uint64_t *)h->x_dg_store.ptr;
+      for (uint64_t r0 = 0; r0 < hc.n_big; r0 += DG_BIG_WINDOW)
+        HIP_TRY(launch_dg_build(a, G, false, true, r0, none, h->stream));
+      HIP_TRY(launch_dg_scans(a, G, true, h->stream));
+      if (int rc = fetch()) return rc;
+    }
+  }
+  const uint64_t NS = n ? hc.n_shadows : 0, NO = n ? hc.n_out : 0, NW = n ? hc.wire : 0;
+  out->n_graphs = G;
+  out->n_shadows = NS;
+  out->n_out = NO;
+  out->wire_bytes = NW;
+  const bool any = out->graph_off || out->wire_off || out->id || out->recv_count || out->supervisor ||
+                   out->flags || out->out_off || out->out_target || out->out_count || out->wire;
+  if (!any) return CRGC_OK;  // sizes only
+  if (!out->graph_off || !out->wire_off || !out->id || !out->recv_count || !out->supervisor || !out->flags ||
+      !out->out_off || (NO && (!out->out_target || !out->out_count)) || !out->wire)
+    return CRGC_E_INVAL;
+  if (out->graph_cap < G || out->shadow_cap < NS || out->out_cap < NO || out->wire_cap < NW) return CRGC_E2BIG;
+  DgOut o{};
+  const bool dev = out->memory == CRGC_MEM_DEVICE;
+  if (dev) {
+    o = DgOut{out->graph_off, out->wire_off, out->id, out->recv_count, out->supervisor, out->flags,
+              out->out_off, out->out_target, out->out_count, out->wire};
+  } else {
+    const size_t ob = Carver::need({(G + 1) * 4, (G + 1) * 8, NS * 8, NS * 4, NS * 8, NS, (NS + 1) * 4, NO * 8,
+                                    NO * 4, NW});
+    if (h->x_dg_out.ensure(ob) != hipSuccess) return CRGC_E_NOMEM;
+    Carver oc(h->x_dg_out.ptr);
+    o.graph_off = oc.take<uint32_t>(G + 1);
+    o.wire_off = oc.take<uint64_t>(G + 1);
+    o.id = oc.take<uint64_t>(NS);
+    o.recv = oc.take<int32_t>(NS);
+    o.sup = oc.take<uint64_t>(NS);
+    o.flags = oc.take<uint8_t>(NS);
+    o.out_off = oc.take<uint32_t>(NS + 1);
+    o.out_target = oc.take<uint64_t>(NO);
+    o.out_count = oc.take<int32_t>(NO);
+    o.wire = oc.take<uint8_t>(NW);
+  }
+  if (G) {
+    HIP_TRY(launch_dg_build(a, G, true, false, 0, o, h->stream));
+    for (uint64_t r0 = 0; r0 < hc.n_big; r0 += DG_BIG_WINDOW)
+      HIP_TRY(launch_dg_build(a, G, true, true, r0, o, h->stream));
+    HIP_TRY(launch_dg_offsets(a, G, o, h->stream));
+  } else {  // no graphs: the closing offsets only
+    HIP_TRY(hipMemsetAsync(o.graph_off, 0, 4, h->stream));
+    HIP_TRY(hipMemsetAsync(o.wire_off, 0, 8, h->stream));
+    HIP_TRY(hipMemsetAsync(o.out_off, 0, 4, h->stream));
+  }
+  if (!dev) {
+    auto d2h = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
+      return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream) : hipSuccess;
+    };
+    HIP_TRY(d2h(out->graph_off, o.graph_off, (G + 1) * 4));
+    HIP_TRY(d2h(out->wire_off, o.wire_off, (G + 1) * 8));
+    HIP_TRY(d2h(out->id, o.id, NS * 8));
+    HIP_TRY(d2h(out->recv_count, o.recv, NS * 4));
+    HIP_TRY(d2h(out->supervisor, o.sup, NS * 8));
+    HIP_TRY(d2h(out->flags, o.flags, NS));
+    HIP_TRY(d2h(out->out_off, o.out_off, (NS + 1) * 4));
+    HIP_TRY(d2h(out->out_target, o.out_target, NO * 8));
+    HIP_TRY(d2h(out->out_count, o.out_count, NO * 4));
+    HIP_TRY(d2h(out->wire, o.wire, NW));
+  }
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return CRGC_OK;
 }
 
 int crgc_local_roots(crgc_graph *h, uint64_t *out, uint64_t cap, uint64_t *n) {
