@@ -219,41 +219,51 @@ class ShadowGraph:
         graph_off, wire bytes, wire_off): graph g is shadows
         graph_off[g]:graph_off[g+1] and payload bytes wire[wire_off[g]:wire_off[g+1]]
         (writeShort(size) + DeltaShadow.serialize per shadow).  device_out: the
-        arrays are torch tensors on the graph's device."""
+        arrays are torch tensors on the graph's device.  The returned arrays are
+        views of buffers reused by the next call with the same device_out."""
         s = batch.struct()
+        key = "_dg_dev" if device_out else "_dg_host"
+        bufs = getattr(self, key, None)
         q = abi.CrgcDeltaGraphs()
-        q.memory = abi.MEM_DEVICE if device_out else abi.MEM_HOST
-        self._chk(self.lib.crgc_build_delta_graphs(self.h, C.byref(s), C.byref(q)),
-                  "crgc_build_delta_graphs")
-        G, NS, NO, NW = q.n_graphs, q.n_shadows, q.n_out, q.wire_bytes
-        if device_out:
-            import torch
-            dev = f"cuda:{self.device}"
-            mk = lambda n, dt: torch.empty(max(n, 1), dtype=dt, device=dev)  # noqa: E731
-            u32, u64 = torch.uint32, torch.uint64
-            arrs = dict(graph_off=mk(G + 1, u32), wire_off=mk(G + 1, u64), id=mk(NS, u64),
-                        recv_count=mk(NS, torch.int32), supervisor=mk(NS, u64),
-                        flags=mk(NS, torch.uint8), out_off=mk(NS + 1, u32),
-                        out_target=mk(NO, u64), out_count=mk(NO, torch.int32),
-                        wire=mk(NW, torch.uint8))
+        for attempt in range(2):
+            q.memory = abi.MEM_DEVICE if device_out else abi.MEM_HOST
+            if bufs is not None:
+                arrs, caps = bufs
+                for k, v in arrs.items():
+                    setattr(q, k, _ptr(v))
+                q.graph_cap, q.shadow_cap, q.out_cap, q.wire_cap = caps
+            rc = self.lib.crgc_build_delta_graphs(self.h, C.byref(s), C.byref(q))
+            if rc == abi.OK and bufs is not None:
+                break
+            if rc not in (abi.OK, abi.E2BIG):
+                self._chk(rc, "crgc_build_delta_graphs")
+            caps = tuple(int(x * 1.25) + 16 for x in (q.n_graphs, q.n_shadows, q.n_out, q.wire_bytes))
+            bufs = (self._dg_buffers(device_out, *caps), caps)
+            setattr(self, key, bufs)
         else:
-            mk = lambda n, dt: np.zeros(max(n, 1), dtype=dt)  # noqa: E731
-            arrs = dict(graph_off=mk(G + 1, np.uint32), wire_off=mk(G + 1, np.uint64),
-                        id=mk(NS, np.uint64), recv_count=mk(NS, np.int32),
-                        supervisor=mk(NS, np.uint64), flags=mk(NS, np.uint8),
-                        out_off=mk(NS + 1, np.uint32), out_target=mk(NO, np.uint64),
-                        out_count=mk(NO, np.int32), wire=mk(NW, np.uint8))
-        for k, v in arrs.items():
-            setattr(q, k, _ptr(v))
-        q.graph_cap, q.shadow_cap, q.out_cap, q.wire_cap = G, NS, NO, NW
-        self._chk(self.lib.crgc_build_delta_graphs(self.h, C.byref(s), C.byref(q)),
-                  "crgc_build_delta_graphs")
+            self._chk(rc, "crgc_build_delta_graphs")
+        arrs = bufs[0]
+        G, NS, NO, NW = q.n_graphs, q.n_shadows, q.n_out, q.wire_bytes
         cut = lambda k, n: arrs[k][:n]  # noqa: E731
         mem = abi.MEM_DEVICE if device_out else abi.MEM_HOST
         deltas = DeltaBatch(cut("id", NS), cut("recv_count", NS), cut("supervisor", NS),
                             cut("flags", NS), cut("out_off", NS + 1), cut("out_target", NO),
                             cut("out_count", NO), memory=mem)
         return deltas, cut("graph_off", G + 1), cut("wire", NW), cut("wire_off", G + 1)
+
+    def _dg_buffers(self, device_out, G, NS, NO, NW):
+        if device_out:
+            import torch
+            dev = f"cuda:{self.device}"
+            mk = lambda n, dt: torch.empty(n, dtype=dt, device=dev)  # noqa: E731
+            u8, i32, u32, u64 = torch.uint8, torch.int32, torch.uint32, torch.uint64
+        else:
+            mk = lambda n, dt: np.zeros(n, dtype=dt)  # noqa: E731
+            u8, i32, u32, u64 = np.uint8, np.int32, np.uint32, np.uint64
+        return dict(graph_off=mk(G + 1, u32), wire_off=mk(G + 1, u64), id=mk(NS, u64),
+                    recv_count=mk(NS, i32), supervisor=mk(NS, u64), flags=mk(NS, u8),
+                    out_off=mk(NS + 1, u32), out_target=mk(NO, u64), out_count=mk(NO, i32),
+                    wire=mk(NW, u8))
 
 
 class Transport:
