@@ -207,7 +207,7 @@ struct crgc_graph {
   uint64_t n_proxy = 0;              // alive proxy slots at the last sweep
   Scratch x_send, x_slot, x_recv, x_ans, x_ans_back, x_small, x_pack, x_pack_recv;
   Scratch x_route, x_route_send, x_cat;  // routed entry merges
-  Scratch x_dg, x_dg_store, x_dg_out;    // DeltaGraph production
+  Scratch x_dg, x_dg_out;    // DeltaGraph production
   uint64_t *h_small = nullptr;       // pinned host staging for small all-gathers
   char *h_route = nullptr;           // pinned RoutePart / ConcatPart tables
   bool route = true;                 // CRGC_ROUTE=0: all-gather every batch instead
@@ -451,7 +451,7 @@ void crgc_destroy(crgc_graph *h) {
   h->work.release();
   for (Scratch *x : {&h->x_send, &h->x_slot, &h->x_recv, &h->x_ans, &h->x_ans_back, &h->x_small,
                      &h->x_pack, &h->x_pack_recv, &h->x_route, &h->x_route_send, &h->x_cat,
-                     &h->x_dg, &h->x_dg_store, &h->x_dg_out})
+                     &h->x_dg, &h->x_dg_out})
     x->release();
   if (h->ctr) hipFree(h->ctr);
   if (h->hctr) hipHostFree(h->hctr);
@@ -1559,8 +1559,7 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
   while ((1ull << (levels - 1)) < n + 1) ++levels;
   const uint64_t N = n + 1, nblk = (n + 1023) / 1024, nbs = 4 * ((N + 1023) / 1024) + 8;
   const size_t need = Carver::need({sizeof(DgCounters), (size_t)levels * N * 4, N, N, nblk * 4 + 4,
-                                    nblk * 8 + 8, nbs * 8, N * 4, N * 4, N * 4, N * 4, N * 4, N * 8, N * 8,
-                                    N * 8, N * 8});
+                                    nblk * 8 + 8, nbs * 8, N * 4, N * 4, N * 4, N * 4, N * 8, N * 8, N * 8});
   if (h->stage.ensure(nh_bytes + 256) != hipSuccess || h->x_dg.ensure(need) != hipSuccess)
     return CRGC_E_NOMEM;
   Carver sc(h->stage.ptr), dc(h->x_dg.ptr);
@@ -1597,11 +1596,9 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
   a.g_size = dc.take<uint32_t>(N);
   a.g_nout = dc.take<uint32_t>(N);
   a.g_bytes = dc.take<uint32_t>(N);
-  a.g_big = dc.take<uint32_t>(N);
   a.g_shadow = dc.take<uint64_t>(N);
   a.g_out = dc.take<uint64_t>(N);
   a.g_wire = dc.take<uint64_t>(N);
-  a.g_bigrank = dc.take<uint64_t>(N);
   HIP_TRY(hipMemsetAsync(a.ctr, 0, sizeof(DgCounters), h->stream));
   DgCounters hc{};
   auto fetch = [&]() -> int {
@@ -1614,25 +1611,15 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
     HIP_TRY(launch_dg_chain(a, 0, h->stream));
     if (int rc = fetch()) return rc;
     if (hc.err) return CRGC_E_INVAL;  // malformed offsets or reserved ids: nothing was built
-    while (hc.first_long != ~0u) {  // a chain start whose graph runs past DG_SPAN_CAP entries
+    while (hc.first_long != ~0u) {  // a chain start whose graph runs past the span window
       HIP_TRY(launch_dg_chain(a, 1, h->stream));
       if (int rc = fetch()) return rc;
     }
     G = hc.n_graphs;
     DgOut none{};
-    HIP_TRY(launch_dg_build(a, G, false, false, 0, none, h->stream));
-    HIP_TRY(launch_dg_scans(a, G, false, h->stream));
+    HIP_TRY(launch_dg_build(a, G, false, none, h->stream));
+    HIP_TRY(launch_dg_scans(a, G, h->stream));
     if (int rc = fetch()) return rc;
-    if (hc.n_big) {  // graphs with more outgoing records than LDS holds
-      a.store_words = dg_store_words(h->DGS);
-      const uint64_t win = std::min<uint64_t>(hc.n_big, DG_BIG_WINDOW);
-      if (h->x_dg_store.ensure(win * a.store_words * 8) != hipSuccess) return CRGC_E_NOMEM;
-      a.store = (uint64_t *)h->x_dg_store.ptr;
-      for (uint64_t r0 = 0; r0 < hc.n_big; r0 += DG_BIG_WINDOW)
-        HIP_TRY(launch_dg_build(a, G, false, true, r0, none, h->stream));
-      HIP_TRY(launch_dg_scans(a, G, true, h->stream));
-      if (int rc = fetch()) return rc;
-    }
   }
   const uint64_t NS = n ? hc.n_shadows : 0, NO = n ? hc.n_out : 0, NW = n ? hc.wire : 0;
   out->n_graphs = G;
@@ -1668,9 +1655,7 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
     o.wire = oc.take<uint8_t>(NW);
   }
   if (G) {
-    HIP_TRY(launch_dg_build(a, G, true, false, 0, o, h->stream));
-    for (uint64_t r0 = 0; r0 < hc.n_big; r0 += DG_BIG_WINDOW)
-      HIP_TRY(launch_dg_build(a, G, true, true, r0, o, h->stream));
+    HIP_TRY(launch_dg_build(a, G, true, o, h->stream));
     HIP_TRY(launch_dg_offsets(a, G, o, h->stream));
   } else {  // no graphs: the closing offsets only
     HIP_TRY(hipMemsetAsync(o.graph_off, 0, 4, h->stream));

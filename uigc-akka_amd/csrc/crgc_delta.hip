@@ -5,25 +5,22 @@
 // more at the end of the wakeup (LocalGC.scala:159-177; DeltaGraph.java:73-180).
 // Where one graph ends depends on where it started — a graph is full once it
 // holds T = DGS - 4F - 1 distinct actors — so the cut is a chain:
-//   k_dg_span     thread per entry s: the end of a graph that would start at
-//                 s (per-thread id set in LDS, at most DG_SPAN_CAP entries;
-//                 longer ones are deferred)
+//   k_dg_span     for every entry s, the end of a graph that would start at
+//                 s (one wave streams the entries past 64 starts through a
+//                 last-seen table; graphs longer than its window are deferred)
 //   k_dg_double   J_{k+1} = J_k o J_k (pointer doubling)
 //   k_dg_mark     starts reachable from entry 0, top level down
 //   k_dg_long     one workgroup resolves the first deferred start on the
 //                 chain, 64 entries per step
 //   k_dg_count / k_dg_scatter   the starts, compacted
-// Then one thread per graph replays DeltaGraph.mergeEntry over its entries
-// (k_dg_build: state in LDS, or in a global store for graphs with more than
-// DG_RCAP outgoing records) — once to size the outputs, once to write them:
+// Then one wave per graph replays DeltaGraph.mergeEntry over its entries
+// (k_dg_build, state in LDS) — once to size the outputs, once to write them:
 // the decoded shadows and the DataOutput bytes of DeltaShadow.serialize, the
 // outgoing map in java.util.HashMap iteration order.
 #include "crgc_host.hpp"
 
 namespace crgc {
 
-constexpr uint32_t DG_P = 128;     // per-thread hash slots (2 x DG_MAX)
-constexpr uint32_t DG_T = 64;      // threads per workgroup of the per-thread kernels
 constexpr uint32_t DG_LONG_P = 8192;  // k_dg_long: the set plus one step's new ids
 constexpr uint32_t SCAN_B = 1024;
 constexpr uint8_t NONE8 = 0xFF;
@@ -71,55 +68,90 @@ __device__ inline void dg_ids(const DgArgs &a, uint64_t e, const DgRange &r, Fn 
 }
 
 // ---- the chain of graph starts ----------------------------------------------
-__global__ __launch_bounds__(DG_T) void k_dg_span(DgArgs a) {
-  __shared__ uint64_t tab[DG_P * DG_T];
-  const uint32_t t = threadIdx.x;
-  const uint64_t s = (uint64_t)blockIdx.x * DG_T + t;
+// One wave per 64 consecutive starts (lane l: start s0 + l).  The wave streams
+// entries from s0 through one table of the ids seen so far, each with the last
+// entry it was seen in; an occurrence is new to lane l's graph iff that entry
+// is before s0 + l.  So every entry is read once per wave and no lane keeps a
+// set of its own.  Lanes still short of T after SPAN_WIN entries (or when the
+// table is 3/4 full) are deferred.
+constexpr uint32_t SPAN_P = 1024;    // ids per wave table
+constexpr uint32_t SPAN_WIN = 192;   // entries a wave streams past s0
+
+__global__ __launch_bounds__(256) void k_dg_span(DgArgs a) {
+  __shared__ uint64_t key[4][SPAN_P];
+  __shared__ uint32_t last[4][SPAN_P];
+  const int w = threadIdx.x >> 6, lane = lane_id();
+  const uint64_t s0 = ((uint64_t)blockIdx.x * 4 + w) * 64;
+  if (s0 > a.n) return;
+  uint64_t *K = key[w];
+  uint32_t *Ls = last[w];
+  for (uint32_t k = lane; k < SPAN_P; k += 64) K[k] = CRGC_NO_ACTOR;
+  wave_lds_fence();
+  const uint64_t s = s0 + lane;
+  uint32_t cnt = 0;
+  bool done = s >= a.n, bad = false;
+  uint64_t end = s >= a.n ? a.n : s;
+  uint32_t used = 0;
+  uint64_t e = s0;
+  const uint64_t stop = min(a.n, s0 + SPAN_WIN);
+  for (; e < stop; ++e) {
+    if (__ballot(!done) == 0) break;
+    if (used > SPAN_P - SPAN_P / 4) break;
+    const DgRange r = dg_range(a, e);
+    bad |= r.bad;
+    const uint32_t nc = r.c1 - r.c0, ns = r.s1 - r.s0, nu = r.u1 - r.u0;
+    const uint32_t m = 1 + 2 * nc + ns + nu;  // <= 1 + 4F <= 64 ids, in encode order
+    uint64_t myid = 0;
+    if ((uint32_t)lane < m) {
+      const uint32_t k = lane;
+      if (k == 0) myid = a.self[e];
+      else if (k < 1 + 2 * nc) myid = ((k - 1) & 1) ? a.c_owner[r.c0 + (k - 1) / 2] : a.c_target[r.c0 + (k - 1) / 2];
+      else if (k < 1 + 2 * nc + ns) myid = a.spawned[r.s0 + (k - 1 - 2 * nc)];
+      else myid = a.u_ref[r.u0 + (k - 1 - 2 * nc - ns)];
+      bad |= dg_reserved(myid);
+    }
+    const bool in = !done && e >= s;
+    for (uint32_t k = 0; k < m; ++k) {
+      const uint64_t x = __shfl(myid, k);
+      uint32_t h = dg_hash(x, 10);
+      int64_t prev = -1;
+      for (;;) {  // every lane walks the same probe sequence (broadcast reads)
+        const uint64_t y = K[h];
+        if (y == x) {
+          prev = Ls[h];
+          break;
+        }
+        if (y == CRGC_NO_ACTOR) {
+          if (lane == 0) K[h] = x;
+          ++used;
+          break;
+        }
+        h = (h + 1) & (SPAN_P - 1);
+      }
+      if (lane == 0) Ls[h] = (uint32_t)e;
+      wave_lds_fence();
+      if (in && prev < (int64_t)s) ++cnt;
+    }
+    if (in && cnt >= a.T) {  // isFull after entry e (:174-180)
+      done = true;
+      end = e + 1;
+    }
+  }
+  if (!done && e == a.n) {  // the last graph of the wakeup (LocalGC.scala:174-177)
+    done = true;
+    end = a.n;
+  }
+  if (__ballot(bad) && lane == 0) atomicOr(&a.ctr->err, 1ull);
   if (s > a.n) return;
   if (s == a.n) {
     a.J[s] = (uint32_t)a.n;
     a.lng[s] = 0;
     return;
   }
-  uint64_t *tb = tab + t;
-  for (uint32_t k = 0; k < DG_P; ++k) tb[k * DG_T] = CRGC_NO_ACTOR;
-  uint32_t size = 0;
-  bool bad = false;
-  auto ins = [&](uint64_t id) {
-    bad |= dg_reserved(id);
-    uint32_t h = dg_hash(id, 7);
-    for (;;) {  // never full: at most DGS - 1 < DG_P ids
-      const uint64_t k = tb[h * DG_T];
-      if (k == id) return;
-      if (k == CRGC_NO_ACTOR) {
-        tb[h * DG_T] = id;
-        ++size;
-        return;
-      }
-      h = (h + 1) & (DG_P - 1);
-    }
-  };
-  uint64_t end = s;
-  bool deferred = true;
-  uint64_t e = s;
-  for (; e < a.n && e < s + DG_SPAN_CAP; ++e) {
-    const DgRange r = dg_range(a, e);
-    bad |= r.bad;
-    dg_ids(a, e, r, ins);
-    if (size >= a.T) {  // isFull after this entry (:174-180)
-      end = e + 1;
-      deferred = false;
-      break;
-    }
-  }
-  if (deferred && e == a.n) {  // the last graph of the wakeup (LocalGC.scala:174-177)
-    end = a.n;
-    deferred = false;
-  }
-  if (bad) atomicOr(&a.ctr->err, 1ull);
-  a.J[s] = (uint32_t)end;  // a deferred start points at itself until k_dg_long resolves it
-  a.lng[s] = deferred;
-  if (deferred) atomicAdd(&a.ctr->n_long, 1u);
+  a.J[s] = (uint32_t)(done ? end : s);  // a deferred start points at itself until k_dg_long
+  a.lng[s] = !done;
+  const uint64_t dl = __ballot(!done);
+  if (lane == 0 && dl) atomicAdd(&a.ctr->n_long, (unsigned)__popcll(dl));
 }
 
 __global__ __launch_bounds__(256) void k_dg_double(DgArgs a, uint32_t k) {
@@ -325,7 +357,7 @@ static int dg_grid(uint64_t n) { return (int)std::min<uint64_t>((n + 255) / 256,
 hipError_t launch_dg_chain(const DgArgs &a, int phase, hipStream_t s) {
   const uint64_t N = a.n + 1;
   if (phase == 0) {
-    hipLaunchKernelGGL(k_dg_span, dim3((N + DG_T - 1) / DG_T), dim3(DG_T), 0, s, a);
+    hipLaunchKernelGGL(k_dg_span, dim3((N + 255) / 256), dim3(256), 0, s, a);
     for (uint32_t k = 0; k + 1 < a.levels; ++k)
       hipLaunchKernelGGL(k_dg_double, dim3(dg_grid(N)), dim3(256), 0, s, a, k);
     hipMemsetAsync(a.mark, 0, N, s);
@@ -353,271 +385,257 @@ hipError_t launch_dg_chain(const DgArgs &a, int phase, hipStream_t s) {
   return hipGetLastError();
 }
 
-// ---- one graph: DeltaGraph.mergeEntry replayed by one thread -----------------
-// Element i of a per-thread array X is X[i * st] (st = DG_T in LDS, 1 in a
-// global store).
-struct DgStore {
-  uint8_t *tab;    // [DG_P] cid per hash slot (NONE8: empty)
-  uint64_t *dec;   // [DGS] decoder: id per cid (DeltaGraph.java:162-169)
-  int32_t *recv;   // [DGS] DeltaShadow.recvCount
-  uint8_t *sup;    // [DGS] supervisor cid (NONE8: -1)
-  uint8_t *fl;     // [DGS] CRGC_DELTA_*
-  uint8_t *osz;    // [DGS] outgoing.size()
-  uint8_t *omax;   // [DGS] largest outgoing.size() so far: the HashMap's capacity
-  uint64_t *rec;   // [rcap] owner | target << 8 | (u32)count << 32; count 0: key absent
-  uint32_t *rins;  // [rcap] time of the key's last insertion (HashMap bin order)
-  uint32_t st, rcap;
-};
+// ---- one graph: DeltaGraph.mergeEntry replayed by one wave ------------------
+// The wave loads the graph's entries a batch at a time (whole entries, at most
+// 64 ids: one id per lane), encodes the ids in order against an LDS table
+// (DeltaGraph.encode, :148-156) and applies each entry's effects in order.
+// Outgoing maps are one 64 x 64 count matrix: cnt[o][t] and the time of the
+// key's last insertion, plus each owner's size and largest size — all that
+// java.util.HashMap iteration order depends on.
+constexpr uint32_t DGW_P = 128;  // id -> cid hash slots
 
-__device__ inline DgStore dg_global_store(uint64_t *base, uint32_t dgs) {
-  DgStore S;
-  char *p = (char *)base;
-  S.dec = (uint64_t *)p;
-  p += DG_MAX * 8;
-  S.rec = (uint64_t *)p;
-  p += (size_t)dgs * dgs * 8;
-  S.rins = (uint32_t *)p;
-  p += (size_t)dgs * dgs * 4;
-  S.recv = (int32_t *)p;
-  p += DG_MAX * 4;
-  S.tab = (uint8_t *)p;
-  p += DG_P;
-  S.sup = (uint8_t *)p;
-  p += DG_MAX;
-  S.fl = (uint8_t *)p;
-  p += DG_MAX;
-  S.osz = (uint8_t *)p;
-  p += DG_MAX;
-  S.omax = (uint8_t *)p;
-  S.st = 1;
-  S.rcap = dgs * dgs;  // distinct (owner, target) pairs never exceed DGS^2
-  return S;
-}
-
-uint64_t dg_store_words(uint32_t dgs) {
-  const uint64_t bytes = DG_MAX * 8 + (uint64_t)dgs * dgs * 12 + DG_MAX * 4 + DG_P + 4 * DG_MAX;
-  return (bytes + 63) / 64 * 8;
-}
-
-struct DgGraph {
-  uint32_t size, nrec;
-  bool ok;
+struct DgWave {
+  uint64_t key[DGW_P];
+  uint64_t dec[DG_MAX];      // decoder: id per cid (DeltaGraph.java:162-169)
+  int32_t cnt[DG_MAX * DG_MAX];   // outgoing[o][t] (0: absent)
+  uint32_t ins[DG_MAX * DG_MAX];  // op time of the key's last insertion
+  int32_t recv[DG_MAX];
+  uint8_t tabc[DGW_P];       // cid per hash slot
+  uint8_t sup[DG_MAX];       // supervisor cid, NONE8: -1
+  uint8_t fl[DG_MAX];        // CRGC_DELTA_*
+  uint8_t osz[DG_MAX];       // outgoing.size()
+  uint8_t omax[DG_MAX];      // largest outgoing.size(): the HashMap's capacity
 };
 
 // Replays DeltaGraph.mergeEntry (DeltaGraph.java:73-125) over entries
-// [starts[g], starts[g+1]).  ok = false: more than rcap outgoing records.
-__device__ DgGraph dg_replay(const DgArgs &a, uint64_t g, const DgStore &S) {
-  const uint32_t st = S.st;
-  for (uint32_t k = 0; k < DG_P; ++k) S.tab[k * st] = NONE8;
-  DgGraph G{0, 0, true};
-  uint32_t clock = 0;
-  auto enc = [&](uint64_t id) -> uint32_t {  // encode (:148-156)
-    uint32_t h = dg_hash(id, 7);
-    for (;;) {
-      const uint32_t c = S.tab[h * st];
-      if (c == NONE8) {
-        const uint32_t n = G.size++;
-        S.tab[h * st] = (uint8_t)n;
-        S.dec[n * st] = id;
-        S.recv[n * st] = 0;
-        S.sup[n * st] = NONE8;
-        S.fl[n * st] = 0;
-        S.osz[n * st] = 0;
-        S.omax[n * st] = 0;
-        return n;
-      }
-      if (S.dec[c * st] == id) return c;
-      h = (h + 1) & (DG_P - 1);
-    }
-  };
-  auto upd = [&](uint32_t o, uint32_t t, int32_t d) {  // updateOutgoing (:127-136)
-    const uint64_t key = (uint64_t)o | ((uint64_t)t << 8);
-    uint32_t k = 0;
-    for (; k < G.nrec; ++k)
-      if ((S.rec[k * st] & 0xFFFFull) == key) break;
-    int32_t cnt;
-    if (k == G.nrec) {
-      if (G.nrec == S.rcap) {
-        G.ok = false;
-        return;
-      }
-      ++G.nrec;
-      cnt = 0;
-    } else {
-      cnt = (int32_t)(uint32_t)(S.rec[k * st] >> 32);
-    }
-    const int32_t nc = (int32_t)((uint32_t)cnt + (uint32_t)d);
-    if (cnt == 0) {  // put of an absent key: appended to its bin
-      S.rins[k * st] = clock;
-      const uint32_t sz = S.osz[o * st] + 1u;
-      S.osz[o * st] = (uint8_t)sz;
-      if (sz > S.omax[o * st]) S.omax[o * st] = (uint8_t)sz;
-    } else if (nc == 0) {  // remove
-      S.osz[o * st] = (uint8_t)(S.osz[o * st] - 1u);
-    }
-    S.rec[k * st] = key | ((uint64_t)(uint32_t)nc << 32);
-    ++clock;
-  };
+// [starts[g], starts[g+1]); returns the number of shadows.  Lane-uniform
+// control flow; lane 0 performs the LDS writes of the serial steps.
+__device__ uint32_t dg_replay(const DgArgs &a, uint64_t g, DgWave &W) {
+  const int lane = lane_id();
+  for (uint32_t k = lane; k < DGW_P; k += 64) W.tabc[k] = NONE8;
+  for (uint32_t k = lane; k < DG_MAX * DG_MAX; k += 64) W.cnt[k] = 0;
+  wave_lds_fence();
+  uint32_t size = 0, clock = 0;
   const uint64_t e0 = a.starts[g], e1 = a.starts[g + 1];
-  for (uint64_t e = e0; e < e1 && G.ok; ++e) {
-    const DgRange r = dg_range(a, e);
-    const uint32_t me = enc(a.self[e]);  // local information (:75-80)
-    const uint8_t ef = a.flags[e];
-    S.fl[me * st] = (uint8_t)(CRGC_DELTA_INTERNED | ((ef & CRGC_ENTRY_ROOT) ? CRGC_DELTA_ROOT : 0) |
-                              ((ef & CRGC_ENTRY_BUSY) ? CRGC_DELTA_BUSY : 0));
-    S.recv[me * st] = (int32_t)((uint32_t)S.recv[me * st] + (uint32_t)(int32_t)a.recv[e]);
-    for (uint32_t k = r.c0; k < r.c1; ++k) {  // created refs (:83-92): target, then owner
-      const uint32_t t = enc(a.c_target[k]);
-      const uint32_t o = enc(a.c_owner[k]);
-      upd(o, t, 1);
+  auto op = [&](uint32_t o, uint32_t t, int32_t d) {  // updateOutgoing (:127-136)
+    const uint32_t k = o * DG_MAX + t;
+    const int32_t c = W.cnt[k];
+    const int32_t nc = (int32_t)((uint32_t)c + (uint32_t)d);
+    if (lane == 0) {
+      W.cnt[k] = nc;
+      if (c == 0) {  // put of an absent key: appended to its bin
+        W.ins[k] = clock;
+        const uint32_t sz = W.osz[o] + 1u;
+        W.osz[o] = (uint8_t)sz;
+        if (sz > W.omax[o]) W.omax[o] = (uint8_t)sz;
+      } else if (nc == 0) {  // remove
+        W.osz[o] = (uint8_t)(W.osz[o] - 1u);
+      }
     }
-    for (uint32_t k = r.s0; k < r.s1; ++k) S.sup[enc(a.spawned[k]) * st] = (uint8_t)me;  // (:95-104)
-    for (uint32_t k = r.u0; k < r.u1; ++k) {  // updated refs (:107-124)
-      const uint32_t t = enc(a.u_ref[k]);
-      const int16_t info = a.u_info[k];
-      const int32_t sc = refob_count(info);
-      if (sc > 0) S.recv[t * st] = (int32_t)((uint32_t)S.recv[t * st] - (uint32_t)sc);
-      if (refob_deactivated(info)) upd(me, t, -1);
+    ++clock;
+    wave_lds_fence();
+  };
+  for (uint64_t eb = e0; eb < e1;) {
+    // a batch of whole entries with at most 64 ids: lane l holds entry eb+l's ranges
+    const uint64_t el = eb + lane;
+    DgRange r{};
+    uint32_t m = 0;
+    if (el < e1) {
+      r = dg_range(a, el);
+      m = 1 + 2 * (r.c1 - r.c0) + (r.s1 - r.s0) + (r.u1 - r.u0);
     }
+    const uint32_t incl = wave_incl_scan(m);
+    const uint64_t fits = __ballot(el < e1 && incl <= 64);
+    const uint32_t ne = fits ? (uint32_t)__popcll(fits) : 1;  // entries of this batch (m <= 63)
+    const uint32_t mt = __shfl(incl, ne - 1);
+    // lane k: the k-th id of the batch, in encode order
+    uint64_t myid = 0;
+    int16_t myinfo = 0;
+    uint32_t my_e = 0;  // entry of id `lane`: the number of entries ending at or before it
+    for (uint32_t q = 0; q < ne; ++q)
+      if (__shfl(incl, q) <= (uint32_t)lane) my_e = q + 1;
+    if (my_e >= ne) my_e = ne - 1;
+    const uint8_t myflags = el < e1 ? a.flags[el] : 0;
+    const int16_t myrecv = el < e1 ? a.recv[el] : 0;
+    {
+      // every lane needs the ranges of the entry its id belongs to
+      const uint32_t c0 = __shfl(r.c0, my_e), c1 = __shfl(r.c1, my_e);
+      const uint32_t s0 = __shfl(r.s0, my_e), s1 = __shfl(r.s1, my_e), u0 = __shfl(r.u0, my_e);
+      const uint32_t base = __shfl(incl - m, my_e);
+      if ((uint32_t)lane < mt) {
+        const uint32_t k = lane - base, nc = c1 - c0, ns = s1 - s0;
+        if (k == 0) myid = a.self[eb + my_e];
+        else if (k < 1 + 2 * nc) myid = ((k - 1) & 1) ? a.c_owner[c0 + (k - 1) / 2] : a.c_target[c0 + (k - 1) / 2];
+        else if (k < 1 + 2 * nc + ns) myid = a.spawned[s0 + (k - 1 - 2 * nc)];
+        else {
+          myid = a.u_ref[u0 + (k - 1 - 2 * nc - ns)];
+          myinfo = a.u_info[u0 + (k - 1 - 2 * nc - ns)];
+        }
+      }
+    }
+    // encode, in order (:148-156)
+    uint32_t mycid = 0;
+    for (uint32_t k = 0; k < mt; ++k) {
+      const uint64_t x = __shfl(myid, k);
+      uint32_t h = dg_hash(x, 7);
+      uint32_t c;
+      for (;;) {
+        c = W.tabc[h];
+        if (c == NONE8) {
+          c = size++;
+          if (lane == 0) {
+            W.tabc[h] = (uint8_t)c;
+            W.key[h] = x;
+            W.dec[c] = x;
+            W.recv[c] = 0;
+            W.sup[c] = NONE8;
+            W.fl[c] = 0;
+            W.osz[c] = 0;
+            W.omax[c] = 0;
+          }
+          wave_lds_fence();
+          break;
+        }
+        if (W.key[h] == x) break;
+        h = (h + 1) & (DGW_P - 1);
+      }
+      if ((uint32_t)lane == k) mycid = c;
+    }
+    // effects, entry by entry
+    for (uint32_t q = 0; q < ne; ++q) {
+      const uint32_t base = __shfl(incl - m, q);
+      const uint32_t c0 = __shfl(r.c0, q), c1 = __shfl(r.c1, q), s0 = __shfl(r.s0, q),
+                     s1 = __shfl(r.s1, q), u0 = __shfl(r.u0, q), u1 = __shfl(r.u1, q);
+      (void)c0;
+      (void)s0;
+      (void)u0;
+      const uint32_t nc = c1 - c0, ns = s1 - s0, nu = u1 - u0;
+      const uint32_t me = __shfl(mycid, base);
+      const uint8_t ef = (uint8_t)__shfl((uint32_t)myflags, q);
+      const int32_t erecv = __shfl((int32_t)myrecv, q);
+      if (lane == 0) {  // local information (:75-80)
+        W.fl[me] = (uint8_t)(CRGC_DELTA_INTERNED | ((ef & CRGC_ENTRY_ROOT) ? CRGC_DELTA_ROOT : 0) |
+                             ((ef & CRGC_ENTRY_BUSY) ? CRGC_DELTA_BUSY : 0));
+        W.recv[me] = (int32_t)((uint32_t)W.recv[me] + (uint32_t)erecv);
+      }
+      wave_lds_fence();
+      for (uint32_t j = 0; j < nc; ++j)  // created refs (:83-92)
+        op(__shfl(mycid, base + 2 + 2 * j), __shfl(mycid, base + 1 + 2 * j), 1);
+      for (uint32_t j = 0; j < ns; ++j) {  // spawned actors (:95-104)
+        const uint32_t ch = __shfl(mycid, base + 1 + 2 * nc + j);
+        if (lane == 0) W.sup[ch] = (uint8_t)me;
+      }
+      for (uint32_t j = 0; j < nu; ++j) {  // updated refs (:107-124)
+        const uint32_t t = __shfl(mycid, base + 1 + 2 * nc + ns + j);
+        const int16_t info = (int16_t)__shfl((int32_t)myinfo, base + 1 + 2 * nc + ns + j);
+        const int32_t sc = refob_count(info);
+        if (sc > 0 && lane == 0) W.recv[t] = (int32_t)((uint32_t)W.recv[t] - (uint32_t)sc);
+        wave_lds_fence();
+        if (refob_deactivated(info)) op(me, t, -1);
+      }
+      wave_lds_fence();
+    }
+    eb += ne;
   }
-  return G;
-}
-
-__device__ inline uint32_t dg_nout(const DgStore &S, const DgGraph &G) {
-  uint32_t n = 0;
-  for (uint32_t k = 0; k < G.nrec; ++k) n += (S.rec[k * S.st] >> 32) ? 1u : 0u;
-  return n;
+  return size;
 }
 
 __device__ inline void put_be(uint8_t *p, uint32_t v, int bytes) {
   for (int i = 0; i < bytes; ++i) p[i] = (uint8_t)(v >> (8 * (bytes - 1 - i)));
 }
 
-// The graph's shadows in compressed-id order: decoded rows, and the bytes of
-// writeShort(size) + DeltaShadow.serialize each (DeltaShadow.java:57-69).  A
-// DeltaShadow.outgoing is a HashMap<Short,Integer> built by the default
-// constructor: 16 bins, doubling whenever its size passes 3/4 of them, so its
-// capacity follows from the largest size it ever had; iteration walks bins in
-// order (bin = key & (capacity - 1): Short.hashCode is the value) and each bin
-// in insertion order (a removed key re-put goes to the tail; resizes keep the
-// order).  Keys < DGS <= 64 never fill a bin to the treeify threshold.
-__device__ void dg_emit(const DgArgs &a, uint64_t g, const DgStore &S, const DgGraph &G, const DgOut &o) {
-  const uint32_t st = S.st;
-  const uint64_t sb = a.g_shadow[g];
-  uint64_t ob = a.g_out[g];
-  uint8_t *w = o.wire + a.g_wire[g];
-  put_be(w, G.size, 2);
-  w += 2;
-  for (uint32_t c = 0; c < G.size; ++c) {
-    const uint64_t row = sb + c;
-    const uint8_t sp = S.sup[c * st], f = S.fl[c * st];
-    const int32_t rc = S.recv[c * st];
-    const uint32_t nk = S.osz[c * st];
-    o.id[row] = S.dec[c * st];
-    o.recv[row] = rc;
-    o.sup[row] = sp == NONE8 ? CRGC_NO_ACTOR : S.dec[sp * st];
-    o.flags[row] = f;
-    o.out_off[row] = (uint32_t)ob;
-    put_be(w, (uint32_t)rc, 4);
-    put_be(w + 4, sp == NONE8 ? 0xFFFFu : sp, 2);
-    w[6] = (f & CRGC_DELTA_INTERNED) ? 1 : 0;
-    w[7] = (f & CRGC_DELTA_ROOT) ? 1 : 0;
-    w[8] = (f & CRGC_DELTA_BUSY) ? 1 : 0;
-    put_be(w + 9, nk, 4);
-    w += 13;
-    uint32_t cap = 16;
-    while (S.omax[c * st] > cap - cap / 4) cap <<= 1;
-    uint64_t last = 0;
-    for (uint32_t j = 0; j < nk; ++j) {  // next key in iteration order
-      uint64_t best = ~0ull;
-      uint32_t bk = 0;
-      for (uint32_t k = 0; k < G.nrec; ++k) {
-        const uint64_t r = S.rec[k * st];
-        if ((r & 0xFF) != c || !(r >> 32)) continue;
-        const uint32_t t = (uint32_t)(r >> 8) & 0xFF;
-        const uint64_t ord = ((uint64_t)(t & (cap - 1)) << 32 | S.rins[k * st]) + 1;  // > 0
-        if (ord > last && ord < best) {
-          best = ord;
-          bk = k;
-        }
+// The graph's shadows in compressed-id order, lane c = shadow c: decoded rows,
+// and the bytes of writeShort(size) + DeltaShadow.serialize each
+// (DeltaShadow.java:57-69).  A DeltaShadow.outgoing is a HashMap<Short,
+// Integer> built by the default constructor: 16 bins, doubling whenever its
+// size passes 3/4 of them, so its capacity follows from the largest size it
+// ever had; iteration walks bins in order (bin = key & (capacity - 1):
+// Short.hashCode is the value) and each bin in insertion order (a removed key
+// re-put goes to the tail; resizes keep the order).  Keys < DGS <= 64 never
+// fill a bin to the treeify threshold.
+__device__ void dg_emit(const DgArgs &a, uint64_t g, const DgWave &W, uint32_t size, const DgOut &o) {
+  const uint32_t c = lane_id();
+  const bool on = c < size;
+  const uint32_t nk = on ? W.osz[c] : 0;
+  const uint32_t nb = on ? 13 + 6 * nk : 0;
+  const uint32_t oi = wave_incl_scan(nk), bi = wave_incl_scan(nb);
+  if (!on) return;
+  const uint64_t row = a.g_shadow[g] + c;
+  uint64_t ob = a.g_out[g] + oi - nk;
+  uint8_t *w = o.wire + a.g_wire[g] + 2 + bi - nb;
+  if (c == 0) put_be(o.wire + a.g_wire[g], size, 2);
+  const uint8_t sp = W.sup[c], f = W.fl[c];
+  const int32_t rc = W.recv[c];
+  o.id[row] = W.dec[c];
+  o.recv[row] = rc;
+  o.sup[row] = sp == NONE8 ? CRGC_NO_ACTOR : W.dec[sp];
+  o.flags[row] = f;
+  o.out_off[row] = (uint32_t)ob;
+  put_be(w, (uint32_t)rc, 4);
+  put_be(w + 4, sp == NONE8 ? 0xFFFFu : sp, 2);
+  w[6] = (f & CRGC_DELTA_INTERNED) ? 1 : 0;
+  w[7] = (f & CRGC_DELTA_ROOT) ? 1 : 0;
+  w[8] = (f & CRGC_DELTA_BUSY) ? 1 : 0;
+  put_be(w + 9, nk, 4);
+  w += 13;
+  uint32_t cap = 16;
+  while (W.omax[c] > cap - cap / 4) cap <<= 1;
+  const int32_t *row_cnt = W.cnt + c * DG_MAX;
+  const uint32_t *row_ins = W.ins + c * DG_MAX;
+  for (uint32_t bin = 0; bin < cap && bin < DG_MAX; ++bin) {
+    // the bin's keys (bin, bin + cap, ...) in insertion order: at most 4 (cap >= 16, keys < 64)
+    uint32_t ks[4], n = 0;
+    for (uint32_t t = bin; t < DG_MAX; t += cap) {
+      if (row_cnt[t] == 0) continue;
+      uint32_t i = n++;
+      while (i > 0 && row_ins[ks[i - 1]] > row_ins[t]) {
+        ks[i] = ks[i - 1];
+        --i;
       }
-      last = best;
-      const uint64_t r = S.rec[bk * st];
-      const uint32_t t = (uint32_t)(r >> 8) & 0xFF;
-      const int32_t cnt = (int32_t)(uint32_t)(r >> 32);
-      o.out_target[ob] = S.dec[t * st];
-      o.out_count[ob] = cnt;
+      ks[i] = t;
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t t = ks[i];
+      o.out_target[ob] = W.dec[t];
+      o.out_count[ob] = row_cnt[t];
       ++ob;
       put_be(w, t, 2);
-      put_be(w + 2, (uint32_t)cnt, 4);
+      put_be(w + 2, (uint32_t)row_cnt[t], 4);
       w += 6;
     }
   }
 }
 
-__device__ inline void dg_sizes(const DgArgs &a, uint64_t g, const DgStore &S, const DgGraph &G) {
-  const uint32_t nout = dg_nout(S, G);
-  a.g_size[g] = G.size;
-  a.g_nout[g] = nout;
-  a.g_bytes[g] = 2 + 13 * G.size + 6 * nout;
-}
-
 template <bool WRITE>
-__global__ __launch_bounds__(DG_T) void k_dg_build(DgArgs a, uint64_t ng, DgOut o) {
-  __shared__ uint64_t l_dec[DG_MAX * DG_T];
-  __shared__ uint64_t l_rec[DG_RCAP * DG_T];
-  __shared__ uint32_t l_rins[DG_RCAP * DG_T];
-  __shared__ int32_t l_recv[DG_MAX * DG_T];
-  __shared__ uint8_t l_tab[DG_P * DG_T];
-  __shared__ uint8_t l_sup[DG_MAX * DG_T], l_fl[DG_MAX * DG_T], l_osz[DG_MAX * DG_T], l_omax[DG_MAX * DG_T];
-  const uint32_t t = threadIdx.x;
-  const uint64_t g = (uint64_t)blockIdx.x * DG_T + t;
-  if (g >= ng) return;
-  if (WRITE && a.g_big[g]) return;
-  DgStore S{l_tab + t, l_dec + t, l_recv + t, l_sup + t, l_fl + t, l_osz + t, l_omax + t, l_rec + t,
-            l_rins + t, DG_T, DG_RCAP};
-  const DgGraph G = dg_replay(a, g, S);
-  if (WRITE) {
-    dg_emit(a, g, S, G, o);
-  } else if (G.ok) {
-    a.g_big[g] = 0;
-    dg_sizes(a, g, S, G);
-  } else {  // sized by the global-store pass
-    a.g_big[g] = 1;
-    a.g_size[g] = a.g_nout[g] = a.g_bytes[g] = 0;
+__global__ __launch_bounds__(64) void k_dg_build(DgArgs a, uint64_t ng, DgOut o) {
+  __shared__ DgWave W;
+  for (uint64_t g = blockIdx.x; g < ng; g += gridDim.x) {
+    const uint32_t size = dg_replay(a, g, W);
+    if (WRITE) {
+      dg_emit(a, g, W, size, o);
+    } else {
+      const uint32_t c = lane_id();
+      const uint32_t nk = c < size ? W.osz[c] : 0;
+      const uint32_t nout = __shfl(wave_incl_scan(nk), 63);
+      if (c == 0) {
+        a.g_size[g] = size;
+        a.g_nout[g] = nout;
+        a.g_bytes[g] = 2 + 13 * size + 6 * nout;
+      }
+    }
+    wave_lds_fence();
   }
 }
 
-// Graphs with more than DG_RCAP outgoing records: big ranks [r0, r0 + DG_BIG_WINDOW).
-template <bool WRITE>
-__global__ __launch_bounds__(64) void k_dg_build_big(DgArgs a, uint64_t ng, uint64_t r0, DgOut o) {
-  for (uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x; g < ng; g += (uint64_t)gridDim.x * 64) {
-    if (!a.g_big[g]) continue;
-    const uint64_t r = a.g_bigrank[g];
-    if (r < r0 || r >= r0 + DG_BIG_WINDOW) continue;
-    const DgStore S = dg_global_store(a.store + (r - r0) * a.store_words, a.DGS);
-    const DgGraph G = dg_replay(a, g, S);
-    if (WRITE) dg_emit(a, g, S, G, o);
-    else dg_sizes(a, g, S, G);
-  }
-}
-
-hipError_t launch_dg_build(const DgArgs &a, uint64_t ng, bool write, bool big, uint64_t r0, const DgOut &o,
-                           hipStream_t s) {
+hipError_t launch_dg_build(const DgArgs &a, uint64_t ng, bool write, const DgOut &o, hipStream_t s) {
   if (ng == 0) return hipSuccess;
-  if (big) {
-    const int grid = (int)std::min<uint64_t>((ng + 63) / 64, 4096);
-    if (write) hipLaunchKernelGGL(k_dg_build_big<true>, dim3(grid), dim3(64), 0, s, a, ng, r0, o);
-    else hipLaunchKernelGGL(k_dg_build_big<false>, dim3(grid), dim3(64), 0, s, a, ng, r0, o);
-  } else {
-    const dim3 grid((unsigned)((ng + DG_T - 1) / DG_T));
-    if (write) hipLaunchKernelGGL(k_dg_build<true>, grid, dim3(DG_T), 0, s, a, ng, o);
-    else hipLaunchKernelGGL(k_dg_build<false>, grid, dim3(DG_T), 0, s, a, ng, o);
-  }
+  const dim3 grid((unsigned)std::min<uint64_t>(ng, 4096));
+  if (write) hipLaunchKernelGGL(k_dg_build<true>, grid, dim3(64), 0, s, a, ng, o);
+  else hipLaunchKernelGGL(k_dg_build<false>, grid, dim3(64), 0, s, a, ng, o);
   return hipGetLastError();
 }
 
-hipError_t launch_dg_scans(const DgArgs &a, uint64_t ng, bool big_only, hipStream_t s) {
+hipError_t launch_dg_scans(const DgArgs &a, uint64_t ng, hipStream_t s) {
   ScanSet q{};
   q.n = ng;
   q.bsum = a.bsum;
@@ -631,12 +649,6 @@ hipError_t launch_dg_scans(const DgArgs &a, uint64_t ng, bool big_only, hipStrea
   q.out[2] = a.g_wire;
   q.total[2] = &a.ctr->wire;
   q.k = 3;
-  if (!big_only) {
-    q.in[3] = a.g_big;
-    q.out[3] = a.g_bigrank;
-    q.total[3] = &a.ctr->n_big;
-    q.k = 4;
-  }
   return run_scan(q, s);
 }
 

@@ -264,16 +264,12 @@ hipError_t launch_concat(const ConcatPart *parts, uint32_t G, const RoutePart &d
 
 // device DeltaGraph production (crgc_delta.hip)
 constexpr uint32_t DG_MAX = 64;         // delta_graph_size bound: per-thread state in LDS
-constexpr uint32_t DG_SPAN_CAP = 256;   // entries a span thread simulates before deferring
-constexpr uint32_t DG_RCAP = 64;        // outgoing (owner, target) records per graph in LDS
-constexpr uint32_t DG_BIG_WINDOW = 4096;  // graphs with more records per global-store launch
 
 struct DgCounters {
   unsigned long long err;       // malformed offsets / reserved ids
   unsigned int first_long;      // first graph start whose span was deferred (~0: none)
   unsigned int n_long;
   unsigned long long n_graphs;  // graph starts (exclusive-scan total)
-  unsigned long long n_big;     // graphs needing global stores
   unsigned long long n_shadows, n_out, wire;  // totals of the per-graph scans
 };
 
@@ -302,10 +298,8 @@ struct DgArgs {
   uint64_t *bsum;      // [4 * ceil(n / 1024)] block sums of the scans
   uint32_t *starts;    // [n_graphs+1]
   // per graph: sizes from the count pass, exclusive scans for the write pass
-  uint32_t *g_size, *g_nout, *g_bytes, *g_big;
-  uint64_t *g_shadow, *g_out, *g_wire, *g_bigrank;
-  uint64_t *store;     // global stores of the big graphs of one window
-  uint64_t store_words;  // words per big-graph store
+  uint32_t *g_size, *g_nout, *g_bytes;
+  uint64_t *g_shadow, *g_out, *g_wire;
 };
 
 struct DgOut {
@@ -321,15 +315,13 @@ struct DgOut {
   uint8_t *wire;
 };
 
-uint64_t dg_store_words(uint32_t dgs);
 // phase 0: spans + doubling + chain from entry 0; 1: chain from a resolved
 // deferred start (k_dg_long, then marking); 2: compaction of the starts.
 hipError_t launch_dg_chain(const DgArgs &a, int phase, hipStream_t s);
-// count (write = false) or write pass; big: the graphs of big-rank window [r0, r0 + DG_BIG_WINDOW)
-hipError_t launch_dg_build(const DgArgs &a, uint64_t n_graphs, bool write, bool big, uint64_t r0,
-                           const DgOut &o, hipStream_t s);
-// exclusive scans of the per-graph counts (after the count passes)
-hipError_t launch_dg_scans(const DgArgs &a, uint64_t n_graphs, bool big_only, hipStream_t s);
+// count (write = false) or write pass: one wave per graph
+hipError_t launch_dg_build(const DgArgs &a, uint64_t n_graphs, bool write, const DgOut &o, hipStream_t s);
+// exclusive scans of the per-graph counts (after the count pass)
+hipError_t launch_dg_scans(const DgArgs &a, uint64_t n_graphs, hipStream_t s);
 hipError_t launch_dg_offsets(const DgArgs &a, uint64_t n_graphs, const DgOut &o, hipStream_t s);
 
 int grid_for(uint64_t threads, int block = 256, int cap = 4096);

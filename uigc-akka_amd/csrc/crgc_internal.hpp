@@ -200,6 +200,12 @@ __device__ inline void set_err(Counters *c, uint32_t bit) {
 }
 
 __device__ inline int lane_id() { return threadIdx.x & 63; }
+// Orders one wave's LDS writes before its later LDS reads.
+__device__ inline void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 __device__ inline uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
 // Full-wave inclusive scan (all 64 lanes must be active).

@@ -48,11 +48,6 @@ __device__ inline bool listing_level(const Counters *c, int L, const LevelArgs &
   return sparse_level(c, L, a.sparse_thresh) || c->ring[(L - 1) % LEVEL_RING] <= a.tail_max;
 }
 
-__device__ inline void wave_lds_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 __device__ inline void mark_target(const DevGraph &g, uint8_t *Fn, uint8_t *Dn, bool sp_next,
                                    uint32_t t, bool check = false) {
