@@ -245,6 +245,41 @@ typedef struct crgc_delta_graphs {
 
 int crgc_build_delta_graphs(crgc_graph *g, const crgc_entry_batch *batch, crgc_delta_graphs *out);
 
+/*
+ * UndoLog folding on the device.  A collector folds every
+ * DeltaGraph it receives into the sender's UndoLog (LocalGC.scala:133,
+ * UndoLog.mergeDeltaGraph, UndoLog.java:39-67) and every IngressEntry into
+ * the log of its egress node (UndoLog.mergeIngressEntry, :69-93); when a node
+ * leaves, its log is merged (ShadowGraph.mergeUndoLog, :158-174).  A
+ * crgc_undo_acc is one such log, kept in HBM on its graph's device and
+ * stream; destroy it before the graph.
+ */
+typedef struct crgc_undo_acc crgc_undo_acc;
+
+typedef struct crgc_undo_log_out {
+  uint64_t field_cap, n_fields;
+  uint64_t *actor;             /* [n_fields] UndoLog.admitted keys             */
+  int32_t *message_count;      /* [n_fields] Field.messageCount                */
+  uint32_t *created_off;       /* [n_fields+1]                                 */
+  uint64_t created_cap, n_created;
+  uint64_t *created_target;    /* Field.createdRefs with nonzero counts        */
+  int32_t *created_count;
+} crgc_undo_log_out;
+
+int crgc_undo_acc_create(crgc_graph *g, uint16_t node_location, crgc_undo_acc **out);
+void crgc_undo_acc_destroy(crgc_undo_acc *u);
+/* UndoLog.mergeDeltaGraph for every DeltaGraph of the batch (graphs back to
+ * back, as crgc_merge_deltas takes them). */
+int crgc_undo_acc_fold_deltas(crgc_undo_acc *u, const crgc_delta_batch *deltas);
+/* UndoLog.mergeIngressEntry for the admitted fields of IngressEntries
+ * (IngressEntry.admitted flattened like an UndoLog; node_location unused). */
+int crgc_undo_acc_fold_ingress(crgc_undo_acc *u, const crgc_undo_log *fields);
+/* The accumulated log, host arrays; two-phase: NULL arrays give the sizes,
+ * CRGC_E2BIG when a capacity is short.  Field order unspecified. */
+int crgc_undo_acc_export(crgc_undo_acc *u, crgc_undo_log_out *out);
+/* ShadowGraph.mergeUndoLog with the accumulated log (crgc_merge_undo's rules). */
+int crgc_merge_undo_acc(crgc_graph *g, crgc_undo_acc *u);
+
 /* Full graph state, for parity tests and debugging (the reference's
  * ShadowGraph.assertEquals / Shadow.assertEquals, ShadowGraph.java:176-199).
  * Two-phase: call with NULL arrays to learn n_vertices / n_edges. */

@@ -6,7 +6,8 @@ ShadowGraph surface (ShadowGraph.java), bound through ctypes.
 """
 from . import abi
 from .batch import Entry, EntryBatch, DeltaBatch, UndoBatch, TraceResult, RefobInfo, GraphState
-from .graph import ShadowGraph, ShardedShadowGraph, Transport, shard_of
+from .graph import ShadowGraph, ShardedShadowGraph, Transport, UndoAccumulator, shard_of
 
 __all__ = ["abi", "Entry", "EntryBatch", "DeltaBatch", "UndoBatch", "TraceResult", "RefobInfo",
-           "GraphState", "ShadowGraph", "ShardedShadowGraph", "Transport", "shard_of"]
+           "GraphState", "ShadowGraph", "ShardedShadowGraph", "Transport", "UndoAccumulator",
+           "shard_of"]

@@ -177,6 +177,20 @@ class CrgcDeltaGraphs(C.Structure):
     ]
 
 
+class CrgcUndoLogOut(C.Structure):
+    _fields_ = [
+        ("field_cap", _U64),
+        ("n_fields", _U64),
+        ("actor", _P),
+        ("message_count", _P),
+        ("created_off", _P),
+        ("created_cap", _U64),
+        ("n_created", _U64),
+        ("created_target", _P),
+        ("created_count", _P),
+    ]
+
+
 # Entry points declared in include/crgc.h — every one must be exported.
 EXPORTED_SYMBOLS = (
     "crgc_create",
@@ -192,6 +206,12 @@ EXPORTED_SYMBOLS = (
     "crgc_live_count",
     "crgc_export",
     "crgc_build_delta_graphs",
+    "crgc_undo_acc_create",
+    "crgc_undo_acc_destroy",
+    "crgc_undo_acc_fold_deltas",
+    "crgc_undo_acc_fold_ingress",
+    "crgc_undo_acc_export",
+    "crgc_merge_undo_acc",
     "crgc_strerror",
     "crgc_transport_rccl_id",
     "crgc_transport_rccl",
@@ -258,6 +278,18 @@ def load_library(path: str | None = None) -> C.CDLL:
     lib.crgc_transport_destroy.argtypes = [_P]
     lib.crgc_shard_of.restype = C.c_uint32
     lib.crgc_shard_of.argtypes = [_U64, C.c_uint32]
+    lib.crgc_undo_acc_create.restype = C.c_int
+    lib.crgc_undo_acc_create.argtypes = [_P, C.c_uint16, C.POINTER(_P)]
+    lib.crgc_undo_acc_destroy.restype = None
+    lib.crgc_undo_acc_destroy.argtypes = [_P]
+    lib.crgc_undo_acc_fold_deltas.restype = C.c_int
+    lib.crgc_undo_acc_fold_deltas.argtypes = [_P, C.POINTER(CrgcDeltaBatch)]
+    lib.crgc_undo_acc_fold_ingress.restype = C.c_int
+    lib.crgc_undo_acc_fold_ingress.argtypes = [_P, C.POINTER(CrgcUndoLog)]
+    lib.crgc_undo_acc_export.restype = C.c_int
+    lib.crgc_undo_acc_export.argtypes = [_P, C.POINTER(CrgcUndoLogOut)]
+    lib.crgc_merge_undo_acc.restype = C.c_int
+    lib.crgc_merge_undo_acc.argtypes = [_P, _P]
     lib.crgc_build_delta_graphs.restype = C.c_int
     lib.crgc_build_delta_graphs.argtypes = [_P, C.POINTER(CrgcEntryBatch), C.POINTER(CrgcDeltaGraphs)]
     _declare(lib, "crgc_")

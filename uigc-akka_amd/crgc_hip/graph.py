@@ -212,6 +212,14 @@ class ShadowGraph:
         self.flush()
         return export_to_state(self.lib.crgc_export, self.h)
 
+    def undo_accumulator(self, node_location: int) -> "UndoAccumulator":
+        return UndoAccumulator(self, node_location)
+
+    def merge_undo_acc(self, acc: "UndoAccumulator"):
+        """ShadowGraph.mergeUndoLog(undoLogs(address)) with a device-folded log."""
+        self.flush()
+        self._chk(self.lib.crgc_merge_undo_acc(self.h, acc.h), "crgc_merge_undo_acc")
+
     # -- DeltaGraph production (num-nodes > 1, LocalGC.scala:159-177) --------------
     def build_delta_graphs(self, batch: EntryBatch, device_out: bool = False):
         """The wakeup's entries folded into DeltaGraphs on the device
@@ -264,6 +272,57 @@ class ShadowGraph:
                     recv_count=mk(NS, i32), supervisor=mk(NS, u64), flags=mk(NS, u8),
                     out_off=mk(NS + 1, u32), out_target=mk(NO, u64), out_count=mk(NO, i32),
                     wire=mk(NW, u8))
+
+
+class UndoAccumulator:
+    """UndoLog(nodeAddress) kept on the graph's device (UndoLog.java:16-104):
+    fold_deltas = mergeDeltaGraph (:39-67, called per DeltaMsg, LocalGC.scala:133),
+    fold_ingress = mergeIngressEntry (:69-93); graph.merge_undo_acc(acc) =
+    ShadowGraph.mergeUndoLog with it (:158-174).  Close before the graph."""
+
+    def __init__(self, graph: "ShadowGraph", node_location: int):
+        self.lib, self.graph = graph.lib, graph
+        self.location = node_location
+        h = C.c_void_p()
+        ShadowGraph._chk(self.lib.crgc_undo_acc_create(graph.h, node_location, C.byref(h)),
+                         "crgc_undo_acc_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.crgc_undo_acc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def fold_deltas(self, batch: DeltaBatch):
+        ShadowGraph._chk(self.lib.crgc_undo_acc_fold_deltas(self.h, C.byref(batch.struct())),
+                         "crgc_undo_acc_fold_deltas")
+
+    mergeDeltaGraph = fold_deltas
+
+    def fold_ingress(self, fields: UndoBatch):
+        ShadowGraph._chk(self.lib.crgc_undo_acc_fold_ingress(self.h, C.byref(fields.struct())),
+                         "crgc_undo_acc_fold_ingress")
+
+    mergeIngressEntry = fold_ingress
+
+    def export(self) -> UndoBatch:
+        q = abi.CrgcUndoLogOut()
+        ShadowGraph._chk(self.lib.crgc_undo_acc_export(self.h, C.byref(q)), "crgc_undo_acc_export")
+        nf, nc = int(q.n_fields), int(q.n_created)
+        actor, msg = np.zeros(nf + 1, np.uint64), np.zeros(nf + 1, np.int32)
+        off = np.zeros(nf + 1, np.uint32)
+        tgt, cnt = np.zeros(nc + 1, np.uint64), np.zeros(nc + 1, np.int32)
+        q.actor, q.message_count, q.created_off = _ptr(actor), _ptr(msg), _ptr(off)
+        q.created_target, q.created_count = _ptr(tgt), _ptr(cnt)
+        q.field_cap, q.created_cap = nf, nc
+        ShadowGraph._chk(self.lib.crgc_undo_acc_export(self.h, C.byref(q)), "crgc_undo_acc_export")
+        return UndoBatch(self.location, actor[:nf], msg[:nf], off, tgt[:nc], cnt[:nc])
 
 
 class Transport:

@@ -1681,6 +1681,261 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
   return CRGC_OK;
 }
 
+}  // extern "C"
+
+// ---- UndoLog folding on the device (crgc_undo.hip) ---------------------------
+struct crgc_undo_acc {
+  crgc_graph *h = nullptr;
+  uint16_t location = 0;
+  UndoAccDev d{};
+  void *mem = nullptr;                 // the tables
+  unsigned long long *ctr = nullptr;   // n_ids, n_pairs
+  uint64_t ids_ub = 0, pairs_ub = 0;   // upper bounds of the inserted keys
+  Scratch stage, exp;
+};
+
+namespace {
+
+static uint64_t pow2_at_least(uint64_t v) {
+  uint64_t p = 1024;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+static hipError_t ua_alloc(UndoAccDev &d, void **mem, uint64_t cap, uint64_t pcap, unsigned long long *ctr,
+                           hipStream_t s) {
+  const size_t bytes = Carver::need({cap * 8, cap, cap * 4, pcap * 8, pcap * 4});
+  if (hipError_t e = hipMalloc(mem, bytes)) return e;
+  Carver c(*mem);
+  d.keys = c.take<uint64_t>(cap);
+  d.adm = c.take<uint8_t>(cap);
+  d.msg = c.take<int32_t>(cap);
+  d.pkeys = c.take<uint64_t>(pcap);
+  d.pcnt = c.take<int32_t>(pcap);
+  d.cap = cap;
+  d.pcap = pcap;
+  d.n_ids = ctr;
+  d.n_pairs = ctr + 1;
+  return launch_ua_init(d, s);
+}
+
+// Room for `ids` / `pairs` more keys at load <= 1/2, rehashing into larger tables.
+static int ua_reserve(crgc_undo_acc *u, uint64_t ids, uint64_t pairs) {
+  crgc_graph *h = u->h;
+  if (u->ids_ub + ids <= u->d.cap / 2 && u->pairs_ub + pairs <= u->d.pcap / 2) return CRGC_OK;
+  unsigned long long c[2];
+  HIP_TRY(hipMemcpyAsync(c, u->ctr, 16, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  u->ids_ub = c[0];
+  u->pairs_ub = c[1];
+  const bool grow_ids = u->ids_ub + ids > u->d.cap / 2;
+  const bool grow_pairs = grow_ids || u->pairs_ub + pairs > u->d.pcap / 2;
+  if (!grow_pairs) return CRGC_OK;
+  const uint64_t cap = grow_ids ? pow2_at_least(4 * (u->ids_ub + ids)) : u->d.cap;
+  const uint64_t pcap = u->pairs_ub + pairs > u->d.pcap / 2 ? pow2_at_least(4 * (u->pairs_ub + pairs)) : u->d.pcap;
+  UndoAccDev n{};
+  void *mem = nullptr;
+  HIP_TRY(ua_alloc(n, &mem, cap, pcap, u->ctr, h->stream));
+  uint32_t *map = nullptr;  // the new tables are one allocation: ids move too
+  if (hipMalloc(&map, u->d.cap * 4) != hipSuccess) {
+    hipFree(mem);
+    return CRGC_E_NOMEM;
+  }
+  hipError_t e = launch_ua_rehash(u->d, n, map, true, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (map) hipFree(map);
+  if (e != hipSuccess) {
+    hipFree(mem);
+    return map_hip(e);
+  }
+  hipFree(u->mem);
+  u->mem = mem;
+  u->d = n;
+  return CRGC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int crgc_undo_acc_create(crgc_graph *h, uint16_t node_location, crgc_undo_acc **out) {
+  if (!out) return CRGC_E_INVAL;
+  *out = nullptr;
+  if (int rc = check_graph(h)) return rc;
+  DeviceGuard dg(h->device);
+  crgc_undo_acc *u = new (std::nothrow) crgc_undo_acc();
+  if (!u) return CRGC_E_NOMEM;
+  u->h = h;
+  u->location = node_location;
+  if (hipMalloc(&u->ctr, 16) != hipSuccess) {
+    delete u;
+    return CRGC_E_NOMEM;
+  }
+  hipError_t e = hipMemsetAsync(u->ctr, 0, 16, h->stream);
+  if (e == hipSuccess) e = ua_alloc(u->d, &u->mem, 1 << 12, 1 << 12, u->ctr, h->stream);
+  if (e != hipSuccess) {
+    crgc_undo_acc_destroy(u);
+    return map_hip(e);
+  }
+  *out = u;
+  return CRGC_OK;
+}
+
+void crgc_undo_acc_destroy(crgc_undo_acc *u) {
+  if (!u) return;
+  DeviceGuard dg(u->h->device);
+  hipStreamSynchronize(u->h->stream);
+  if (u->mem) hipFree(u->mem);
+  if (u->ctr) hipFree(u->ctr);
+  u->stage.release();
+  u->exp.release();
+  delete u;
+}
+
+int crgc_undo_acc_fold_deltas(crgc_undo_acc *u, const crgc_delta_batch *b) {
+  if (!u) return CRGC_E_INVAL;
+  crgc_graph *h = u->h;
+  if (int rc = check_graph(h)) return rc;
+  DeviceGuard dg(h->device);
+  uint64_t nout = 0;
+  if (int rc = delta_counts(h, b, &nout)) return rc;
+  const uint64_t n = b->n_shadows;
+  if (n == 0) return CRGC_OK;
+  if (int rc = ua_reserve(u, n + nout, nout)) return rc;
+  const size_t host_bytes =
+      b->memory == CRGC_MEM_HOST ? Carver::need({n * 8, n * 4, n, (n + 1) * 4, nout * 8, nout * 4}) : 0;
+  if (u->stage.ensure(host_bytes + 256) != hipSuccess) return CRGC_E_NOMEM;
+  Carver sc(u->stage.ptr);
+  UaDeltaArgs a{};
+  a.n = n;
+  a.nout = nout;
+  a.id = stage(h, sc, b->id, n, b->memory);
+  a.recv = stage(h, sc, b->recv_count, n, b->memory);
+  a.flags = stage(h, sc, b->flags, n, b->memory);
+  a.out_off = stage(h, sc, b->out_off, n + 1, b->memory);
+  a.out_target = stage(h, sc, b->out_target, nout, b->memory);
+  a.out_count = stage(h, sc, b->out_count, nout, b->memory);
+  HIP_TRY(launch_ua_fold_deltas(u->d, a, h->stream));
+  u->ids_ub += n + nout;
+  u->pairs_ub += nout;
+  return CRGC_OK;
+}
+
+int crgc_undo_acc_fold_ingress(crgc_undo_acc *u, const crgc_undo_log *f) {
+  if (!u || !f || f->memory > CRGC_MEM_DEVICE) return CRGC_E_INVAL;
+  crgc_graph *h = u->h;
+  if (int rc = check_graph(h)) return rc;
+  DeviceGuard dg(h->device);
+  const uint64_t n = f->n_fields;
+  if (n == 0) return CRGC_OK;
+  if (!f->actor || !f->message_count || !f->created_off) return CRGC_E_INVAL;
+  uint32_t nc32 = 0;
+  if (f->memory == CRGC_MEM_HOST) {
+    if (f->created_off[0]) return CRGC_E_INVAL;
+    nc32 = f->created_off[n];
+  } else {
+    HIP_TRY(hipMemcpy(&nc32, f->created_off + n, 4, hipMemcpyDeviceToHost));
+  }
+  const uint64_t nc = nc32;
+  if (nc && (!f->created_target || !f->created_count)) return CRGC_E_INVAL;
+  if (int rc = ua_reserve(u, n + nc, nc)) return rc;
+  const size_t host_bytes =
+      f->memory == CRGC_MEM_HOST ? Carver::need({n * 8, n * 4, (n + 1) * 4, nc * 8, nc * 4}) : 0;
+  if (u->stage.ensure(host_bytes + 256) != hipSuccess) return CRGC_E_NOMEM;
+  Carver sc(u->stage.ptr);
+  UaFieldArgs a{};
+  a.n = n;
+  a.nc = nc;
+  a.sign = 1;
+  a.actor = stage(h, sc, f->actor, n, f->memory);
+  a.msg = stage(h, sc, f->message_count, n, f->memory);
+  a.c_off = stage(h, sc, f->created_off, n + 1, f->memory);
+  a.c_target = stage(h, sc, f->created_target, nc, f->memory);
+  a.c_count = stage(h, sc, f->created_count, nc, f->memory);
+  HIP_TRY(launch_ua_fold_fields(u->d, a, h->stream));
+  u->ids_ub += n + nc;
+  u->pairs_ub += nc;
+  return CRGC_OK;
+}
+
+int crgc_undo_acc_export(crgc_undo_acc *u, crgc_undo_log_out *out) {
+  if (!u || !out) return CRGC_E_INVAL;
+  crgc_graph *h = u->h;
+  if (int rc = check_graph(h)) return rc;
+  DeviceGuard dg(h->device);
+  const uint64_t cap = u->d.cap, nbs = 4 * ((cap + 1023) / 1024) + 8;
+  const size_t need = Carver::need({16, cap * 4, cap * 4, cap * 8, cap * 8, nbs * 8});
+  if (u->exp.ensure(need) != hipSuccess) return CRGC_E_NOMEM;
+  Carver c(u->exp.ptr);
+  UaExportArgs x{};
+  x.n_fields = c.take<unsigned long long>(2);
+  x.n_created = x.n_fields + 1;
+  x.admf = c.take<uint32_t>(cap);
+  x.deg = c.take<uint32_t>(cap);
+  x.aidx = c.take<uint64_t>(cap);
+  x.roff = c.take<uint64_t>(cap);
+  x.bsum = c.take<uint64_t>(nbs);
+  HIP_TRY(launch_ua_export(u->d, x, 0, h->stream));
+  unsigned long long nn[2];
+  HIP_TRY(hipMemcpyAsync(nn, x.n_fields, 16, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  const uint64_t NF = nn[0], NC = nn[1];
+  out->n_fields = NF;
+  out->n_created = NC;
+  if (!out->actor && !out->message_count && !out->created_off && !out->created_target && !out->created_count)
+    return CRGC_OK;
+  if (!out->actor || !out->message_count || !out->created_off || (NC && (!out->created_target || !out->created_count)))
+    return CRGC_E_INVAL;
+  if (out->field_cap < NF || out->created_cap < NC) return CRGC_E2BIG;
+  Scratch o;
+  if (o.ensure(Carver::need({NF * 8, NF * 4, (NF + 1) * 4, NC * 8, NC * 4})) != hipSuccess) return CRGC_E_NOMEM;
+  Carver oc(o.ptr);
+  x.actor = oc.take<uint64_t>(NF);
+  x.msg = oc.take<int32_t>(NF);
+  x.c_off = oc.take<uint32_t>(NF + 1);
+  x.c_target = oc.take<uint64_t>(NC);
+  x.c_count = oc.take<int32_t>(NC);
+  hipError_t e = launch_ua_export(u->d, x, 1, h->stream);
+  auto d2h = [&](void *dst, const void *src, size_t bytes) {
+    if (e == hipSuccess && bytes) e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream);
+  };
+  d2h(out->actor, x.actor, NF * 8);
+  d2h(out->message_count, x.msg, NF * 4);
+  d2h(out->created_off, x.c_off, (NF + 1) * 4);
+  d2h(out->created_target, x.c_target, NC * 8);
+  d2h(out->created_count, x.c_count, NC * 4);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  o.release();
+  return map_hip(e);
+}
+
+int crgc_merge_undo_acc(crgc_graph *h, crgc_undo_acc *u) {
+  if (!u || u->h != h) return CRGC_E_INVAL;
+  crgc_undo_log_out q{};
+  if (int rc = crgc_undo_acc_export(u, &q)) return rc;
+  std::vector<uint64_t> actor(q.n_fields + 1), target(q.n_created + 1);
+  std::vector<int32_t> msg(q.n_fields + 1), count(q.n_created + 1);
+  std::vector<uint32_t> off(q.n_fields + 1);
+  q.field_cap = q.n_fields;
+  q.created_cap = q.n_created;
+  q.actor = actor.data();
+  q.message_count = msg.data();
+  q.created_off = off.data();
+  q.created_target = target.data();
+  q.created_count = count.data();
+  if (int rc = crgc_undo_acc_export(u, &q)) return rc;
+  crgc_undo_log log{};
+  log.node_location = u->location;
+  log.n_fields = q.n_fields;
+  log.actor = actor.data();
+  log.message_count = msg.data();
+  log.created_off = off.data();
+  log.created_target = target.data();
+  log.created_count = count.data();
+  log.memory = CRGC_MEM_HOST;
+  return crgc_merge_undo(h, &log);
+}
+
 int crgc_local_roots(crgc_graph *h, uint64_t *out, uint64_t cap, uint64_t *n) {
   if (int rc = check_graph(h)) return rc;
   if (!n) return CRGC_E_INVAL;

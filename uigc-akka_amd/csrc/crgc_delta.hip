@@ -284,14 +284,6 @@ __global__ __launch_bounds__(256) void k_dg_scatter(DgArgs a) {
 }
 
 // ---- exclusive scans of up to 4 u32 arrays (two levels of 1024) -------------
-struct ScanSet {
-  const uint32_t *in[4];
-  uint64_t *out[4];
-  unsigned long long *total[4];
-  int k;
-  uint64_t n, nb;
-  uint64_t *bsum;  // [4][nb]
-};
 
 __global__ __launch_bounds__(SCAN_B) void k_scan_sums(ScanSet q) {
   const uint64_t i = (uint64_t)blockIdx.x * SCAN_B + threadIdx.x;
@@ -340,7 +332,7 @@ __global__ __launch_bounds__(SCAN_B) void k_scan_apply(ScanSet q) {
   }
 }
 
-static hipError_t run_scan(ScanSet q, hipStream_t s) {
+hipError_t run_scan(ScanSet q, hipStream_t s) {
   if (q.n == 0) {
     for (int j = 0; j < q.k; ++j) hipMemsetAsync(q.total[j], 0, 8, s);
     return hipGetLastError();

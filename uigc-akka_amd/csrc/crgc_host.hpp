@@ -262,6 +262,18 @@ hipError_t launch_route(const RouteArgs &a, int phase, const RoutePart *parts, h
 hipError_t launch_concat(const ConcatPart *parts, uint32_t G, const RoutePart &dst, uint64_t N, uint64_t C,
                          uint64_t S, uint64_t U, hipStream_t s);
 
+// Exclusive scans of up to 4 u32 arrays of n elements (two levels of 1024,
+// crgc_delta.hip): out[j][i] = sum of in[j][0..i), *total[j] = the sum.
+struct ScanSet {
+  const uint32_t *in[4];
+  uint64_t *out[4];
+  unsigned long long *total[4];
+  int k;
+  uint64_t n, nb;
+  uint64_t *bsum;  // [4 * ceil(n / 1024)] scratch
+};
+hipError_t run_scan(ScanSet q, hipStream_t s);
+
 // device DeltaGraph production (crgc_delta.hip)
 constexpr uint32_t DG_MAX = 64;         // delta_graph_size bound: per-thread state in LDS
 
@@ -323,6 +335,53 @@ hipError_t launch_dg_build(const DgArgs &a, uint64_t n_graphs, bool write, const
 // exclusive scans of the per-graph counts (after the count pass)
 hipError_t launch_dg_scans(const DgArgs &a, uint64_t n_graphs, hipStream_t s);
 hipError_t launch_dg_offsets(const DgArgs &a, uint64_t n_graphs, const DgOut &o, hipStream_t s);
+
+// UndoLog folding on the device (crgc_undo.hip)
+struct UndoAccDev {
+  uint64_t *keys;   // [cap] ids (~0: empty); the bucket index is the id's slot
+  uint8_t *adm;     // [cap] UndoLog.admitted holds a Field for this id
+  int32_t *msg;     // [cap] Field.messageCount
+  uint64_t cap;
+  uint64_t *pkeys;  // [pcap] actor bucket << 32 | target bucket
+  int32_t *pcnt;    // [pcap] Field.createdRefs[target]
+  uint64_t pcap;
+  unsigned long long *n_ids, *n_pairs;  // keys inserted so far
+};
+struct UaDeltaArgs {
+  uint64_t n, nout;
+  const uint64_t *id;
+  const int32_t *recv;
+  const uint8_t *flags;
+  const uint32_t *out_off;
+  const uint64_t *out_target;
+  const int32_t *out_count;
+};
+struct UaFieldArgs {
+  uint64_t n, nc;
+  int32_t sign;
+  const uint64_t *actor;
+  const int32_t *msg;
+  const uint32_t *c_off;
+  const uint64_t *c_target;
+  const int32_t *c_count;
+};
+struct UaExportArgs {
+  uint32_t *admf, *deg;  // [cap]
+  uint64_t *aidx, *roff; // [cap] exclusive scans
+  uint64_t *bsum;
+  unsigned long long *n_fields, *n_created;
+  uint64_t *actor;
+  int32_t *msg;
+  uint32_t *c_off;
+  uint64_t *c_target;
+  int32_t *c_count;
+};
+hipError_t launch_ua_fold_deltas(const UndoAccDev &u, const UaDeltaArgs &a, hipStream_t s);
+hipError_t launch_ua_fold_fields(const UndoAccDev &u, const UaFieldArgs &a, hipStream_t s);
+hipError_t launch_ua_init(const UndoAccDev &u, hipStream_t s);
+hipError_t launch_ua_rehash(const UndoAccDev &o, const UndoAccDev &n, uint32_t *map, bool ids, hipStream_t s);
+// phase 0: counts and scans; 1: the arrays
+hipError_t launch_ua_export(const UndoAccDev &u, const UaExportArgs &x, int phase, hipStream_t s);
 
 int grid_for(uint64_t threads, int block = 256, int cap = 4096);
 
