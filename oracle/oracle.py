@@ -28,11 +28,14 @@ from crgc_hip.batch import TraceResult, export_to_state, _ptr  # noqa: E402
 LIB_PATH = os.path.join(_HERE, "_build", "libcrgc_oracle.so")
 
 
+OMP_LIB_PATH = os.path.join(_HERE, "_build", "libcrgc_omp.so")
+
+
 def build(force: bool = False) -> str:
-    """Compile the oracle with g++ (recipe also in oracle/Makefile)."""
-    src = os.path.join(_HERE, "crgc_oracle.cpp")
-    if not force and os.path.exists(LIB_PATH) and \
-            os.path.getmtime(LIB_PATH) >= os.path.getmtime(src):
+    """Compile the oracle (and the OpenMP bench baseline) with g++ (oracle/Makefile)."""
+    fresh = all(os.path.exists(lib) and os.path.getmtime(lib) >= os.path.getmtime(os.path.join(_HERE, src))
+                for lib, src in ((LIB_PATH, "crgc_oracle.cpp"), (OMP_LIB_PATH, "omp_baseline.cpp")))
+    if not force and fresh:
         return LIB_PATH
     os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
     subprocess.check_call(["make", "-s", "-C", _HERE])
@@ -125,3 +128,33 @@ class OracleGraph:
 
     def export(self):
         return export_to_state(self.lib.oracle_export, self.h)
+
+
+def omp_trace_baseline(g: "OracleGraph", threads: int, reps: int = 3) -> dict:
+    """BENCH ONLY: the OpenMP trace (oracle/omp_baseline.cpp) over a CSR snapshot
+    of the oracle's graph: best wall seconds of `reps` mark + sweep passes."""
+    lib = C.CDLL(OMP_LIB_PATH)
+    e = abi.CrgcGraphExport()
+    lib_o = g.lib
+    lib_o.oracle_export(g.h, C.byref(e))
+    nv, ne = int(e.n_vertices), int(e.n_edges)
+    ids, rc = np.zeros(nv, np.uint64), np.zeros(nv, np.int32)
+    fl, sup = np.zeros(nv, np.uint8), np.zeros(nv, np.uint64)
+    eo, et, ec = np.zeros(ne, np.uint64), np.zeros(ne, np.uint64), np.zeros(ne, np.int32)
+    e.vertex_cap, e.edge_cap = nv, ne
+    e.id, e.recv_count, e.flags, e.supervisor = _ptr(ids), _ptr(rc), _ptr(fl), _ptr(sup)
+    e.edge_owner, e.edge_target, e.edge_count = _ptr(eo), _ptr(et), _ptr(ec)
+    if lib_o.oracle_export(g.h, C.byref(e)) != abi.OK:
+        raise RuntimeError("oracle export failed")
+    best = C.c_double()
+    out = [C.c_uint64() for _ in range(4)]
+    P = C.c_void_p
+    lib.omp_trace_bench.argtypes = [C.c_uint64, P, P, P, P, C.c_uint64, P, P, P, C.c_int, C.c_int,
+                                    C.POINTER(C.c_double)] + [C.POINTER(C.c_uint64)] * 4
+    lib.omp_trace_bench.restype = C.c_int
+    if lib.omp_trace_bench(nv, _ptr(ids), _ptr(rc), _ptr(fl), _ptr(sup), ne, _ptr(eo), _ptr(et),
+                           _ptr(ec), threads, reps, C.byref(best), *[C.byref(x) for x in out]):
+        raise RuntimeError("omp baseline: malformed snapshot")
+    return {"seconds": best.value, "edges_scanned": out[0].value, "marked": out[1].value,
+            "garbage": out[2].value, "kill": out[3].value, "vertices": nv, "edges": ne}
+
