@@ -1152,11 +1152,16 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
                       const std::function<hipError_t()> &after_chunk = nullptr) {
   LevelArgs la{};
   la.location = location;
-  // Tuning switch for A/B runs (results are identical either way).
-  la.flags = LV_CHECK_BEFORE_STORE;
-  if (const char *m = getenv("CRGC_MARK_CHECK")) la.flags = atoi(m) ? LV_CHECK_BEFORE_STORE : 0;
+  // Tuning switches for A/B runs (results are identical either way).  Defaults
+  // from tools/ab_trace.py on C2 (profiles/r1h): plain candidate stores, the
+  // edge stream read non-temporal, no marked-word filter while < 1/16 is marked.
+  la.flags = LV_NT;
+  la.vis_skip_div = 16;
+  if (const char *m = getenv("CRGC_MARK_CHECK")) la.flags |= atoi(m) ? LV_CHECK_BEFORE_STORE : 0;
   if (const char *m = getenv("CRGC_MARK_BITS")) la.flags |= atoi(m) ? LV_BITMAP_FRONT : 0;
   if (const char *m = getenv("CRGC_EXP8")) la.flags |= atoi(m) ? LV_EXP8 : 0;
+  if (const char *m = getenv("CRGC_EXPAND_NT")) la.flags = atoi(m) ? la.flags | LV_NT : la.flags & ~LV_NT;
+  if (const char *m = getenv("CRGC_VIS_SKIP")) la.vis_skip_div = (uint32_t)strtoul(m, nullptr, 10);
   la.sparse_thresh = (uint32_t)std::max<uint64_t>(64, (top / BLK_SLOTS) / 4);
   // Direction optimisation: dense levels after a frontier of >= top/div shadows pull.
   uint64_t pull_div = 16;

@@ -156,6 +156,7 @@ constexpr uint32_t LV_TAIL = 8;                // narrow frontiers go to one wor
 constexpr uint32_t LV_INVESTIGATE = 16;        // set by launch_level: no supervisor edges
 constexpr uint32_t LV_ROOTS = 32;              // set by launch_level: the pseudo-root level
 constexpr uint32_t LV_EXP8 = 64;               // k_expand: 8 edges per lane per step (else 4)
+constexpr uint32_t LV_NT = 128;                // k_expand: edge stream read non-temporal
 
 struct LevelArgs {
   int level;
@@ -166,6 +167,7 @@ struct LevelArgs {
   uint32_t tail_max;       // ... whose candidates number <= this, and bails above it
   uint32_t frontier_grid;  // workgroups of k_frontier (set by launch_level)
   uint32_t flags;          // LV_*
+  uint32_t vis_skip_div;   // push levels skip the marked-word filter while marked * div < slot_top
   uint16_t location;
 };
 

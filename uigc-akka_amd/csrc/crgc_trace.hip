@@ -24,6 +24,8 @@
 namespace crgc {
 
 constexpr uint32_t RANGE_MAX = 256;  // longer segments (hubs) are cut into pieces
+constexpr int FB = 4;               // k_frontier: chunks of 64 frontier shadows per load group
+constexpr uint32_t NO_SLOT = ~0u;
 constexpr int STAT_FRONT = 0, STAT_SUP = 1, STAT_EDGES = 2, STAT_LIVE = 3;
 
 __device__ inline bool sparse_level(const Counters *c, int L, uint32_t thr) {
@@ -205,39 +207,71 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
     uint32_t nlight = 0;
     uint2 *region = g.qn_buf + (uint64_t)blk * BLK_SLOTS;
     uint32_t nprox = sharded ? g.xp_cnt[blk] : 0;
-    for (uint32_t c0 = 0; c0 < total; c0 += 64) {
-      const uint32_t idx = c0 + lane;
-      const bool valid = idx < total;
-      const uint32_t v = valid ? s_front[wv][idx] : 0;
-      const uint8_t f = valid ? g.flags[v] : 0;
-      if (sharded) {  // newly marked proxies: exported to their home shard after the round
-        const uint64_t pb = __ballot(f & FL_PROXY);
-        if (f & FL_PROXY) g.xp_buf[(uint64_t)blk * BLK_SLOTS + nprox + __popcll(pb & lanemask_lt())] = v;
-        nprox += __popcll(pb);
+    // FB chunks of 64 frontier shadows at a time: every per-shadow load of the
+    // group (flags, degree, segment, supervisor) is issued before any store,
+    // then the supervisors' marked words, so a dense block costs two memory
+    // round trips per 64*FB shadows instead of two per 64.
+    for (uint32_t c0 = 0; c0 < total; c0 += 64 * FB) {
+      uint32_t v[FB], nz[FB], sp[FB];
+      uint8_t f[FB];
+      uint2 ad[FB];
+#pragma unroll
+      for (int b = 0; b < FB; ++b) {
+        const uint32_t idx = c0 + b * 64 + lane;
+        v[b] = idx < total ? s_front[wv][idx] : NO_SLOT;
       }
-      const bool expand = valid && !(f & FL_HALTED);  // halted: marked, not expanded (:226)
-      // traced edges = nonzero out-edges of expanded shadows (:231)
-      if (expand) n_edges += g.nzdeg[v];
-      const uint2 ad = (expand && !pull) ? g.adj[v] : make_uint2(0, 0);
-      if (!INVESTIGATE && expand) {
-        const uint32_t s = g.sup[v];  // supervisor edge (:258-267)
-        if (s < 0xFFFFFFF0u) {         // not null, not collected
-          n_sup++;
-          if (bitmode) mark_target_bits(g, g.fbits[(L + 1) & 1], Dn, sp_next, s);
-          else mark_target(g, Fn, Dn, sp_next, s);
+#pragma unroll
+      for (int b = 0; b < FB; ++b) {
+        const bool valid = v[b] != NO_SLOT;
+        f[b] = valid ? g.flags[v[b]] : 0;
+        nz[b] = valid ? g.nzdeg[v[b]] : 0;
+        ad[b] = (valid && !pull) ? g.adj[v[b]] : make_uint2(0, 0);
+        sp[b] = (valid && !INVESTIGATE) ? g.sup[v[b]] : NO_SLOT;
+      }
+      uint32_t sw[FB];
+#pragma unroll
+      for (int b = 0; b < FB; ++b) {
+        // halted: marked, not expanded (:226); supervisor edge (:258-267) unless null / collected
+        if (v[b] == NO_SLOT || (f[b] & FL_HALTED)) {
+          nz[b] = 0;
+          ad[b] = make_uint2(0, 0);
+          sp[b] = NO_SLOT;
         }
+        if (sp[b] >= 0xFFFFFFF0u) sp[b] = NO_SLOT;
+        sw[b] = (sp[b] != NO_SLOT && !bitmode) ? g.vis[sp[b] >> 5] : ~0u;
       }
-      const bool light = ad.y > 0 && ad.y <= RANGE_MAX;
-      const uint64_t ball = __ballot(light);
-      if (light) region[nlight + __popcll(ball & lanemask_lt())] = ad;
-      nlight += __popcll(ball);
-      const uint32_t pieces = ad.y > RANGE_MAX ? (ad.y + RANGE_MAX - 1) / RANGE_MAX : 0;
-      if (__ballot(pieces != 0)) {  // hubs are rare: a wave-aggregated append
-        const unsigned long long hi = wave_atomic_add(qh_cnt, pieces);
-        for (uint32_t k = 0; k < pieces; ++k) {
-          const uint32_t len = min(RANGE_MAX, ad.y - k * RANGE_MAX);
-          if (hi + k < g.qh_cap) g.qh_buf[hi + k] = make_uint2(ad.x + k * RANGE_MAX, len);
-          else set_err(c, ERR_QUEUE_FULL);
+#pragma unroll
+      for (int b = 0; b < FB; ++b) {
+        if (sharded) {  // newly marked proxies: exported to their home shard after the round
+          const uint64_t pb = __ballot(f[b] & FL_PROXY);
+          if (f[b] & FL_PROXY)
+            g.xp_buf[(uint64_t)blk * BLK_SLOTS + nprox + __popcll(pb & lanemask_lt())] = v[b];
+          nprox += __popcll(pb);
+        }
+        n_edges += nz[b];  // traced edges = nonzero out-edges of expanded shadows (:231)
+        if (sp[b] != NO_SLOT) {
+          n_sup++;
+          const uint32_t s = sp[b];
+          if (bitmode) {
+            mark_target_bits(g, g.fbits[(L + 1) & 1], Dn, sp_next, s);
+          } else if (!((sw[b] >> (s & 31)) & 1u)) {
+            Fn[s] = 1;
+            if (sp_next && Dn[s >> 11] == 0) Dn[s >> 11] = 1;
+          }
+        }
+        const uint32_t len = ad[b].y;
+        const bool light = len > 0 && len <= RANGE_MAX;
+        const uint64_t ball = __ballot(light);
+        if (light) region[nlight + __popcll(ball & lanemask_lt())] = ad[b];
+        nlight += __popcll(ball);
+        const uint32_t pieces = len > RANGE_MAX ? (len + RANGE_MAX - 1) / RANGE_MAX : 0;
+        if (__ballot(pieces != 0)) {  // hubs are rare: a wave-aggregated append
+          const unsigned long long hi = wave_atomic_add(qh_cnt, pieces);
+          for (uint32_t k = 0; k < pieces; ++k) {
+            const uint32_t pl = min(RANGE_MAX, len - k * RANGE_MAX);
+            if (hi + k < g.qh_cap) g.qh_buf[hi + k] = make_uint2(ad[b].x + k * RANGE_MAX, pl);
+            else set_err(c, ERR_QUEUE_FULL);
+          }
         }
       }
     }
@@ -262,7 +296,7 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
 // per-edge marking would serialise them).
 template <int U>
 __device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn, bool sp_next, bool check,
-                                    const uint64_t (&ed)[U], uint32_t *Fbits) {
+                                    const uint64_t (&ed)[U], uint32_t *Fbits, bool skipvis) {
   uint32_t t[U];
   bool go[U];
 #pragma unroll
@@ -276,11 +310,13 @@ __device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn,
       if (go[u]) mark_target_bits(g, Fbits, Dn, sp_next, t[u]);
     return;
   }
-  uint32_t w[U];
+  if (!skipvis) {  // early levels mark few shadows: a store costs less than the filter
+    uint32_t w[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) w[u] = go[u] ? g.vis[t[u] >> 5] : ~0u;
+    for (int u = 0; u < U; ++u) w[u] = go[u] ? g.vis[t[u] >> 5] : ~0u;
 #pragma unroll
-  for (int u = 0; u < U; ++u) go[u] = !((w[u] >> (t[u] & 31)) & 1u);
+    for (int u = 0; u < U; ++u) go[u] = !((w[u] >> (t[u] & 31)) & 1u);
+  }
   uint8_t fb[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) fb[u] = (go[u] && check) ? Fn[t[u]] : 0;
@@ -302,7 +338,13 @@ __device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn,
 // per step (degree scan + binary search in LDS assigns edges to lanes) or one
 // hub piece per step, U independent edge loads per lane.
 // ---------------------------------------------------------------------------
-template <int U>
+template <bool NT>
+__device__ inline uint64_t pool_load(const uint64_t *p) {
+  if (NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+
+template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   __shared__ uint32_t s_start[4][65];
   __shared__ uint32_t s_off[4][64];
@@ -322,6 +364,9 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   const uint64_t nw = (uint64_t)gridDim.x * 4;
   const uint32_t want = (uint32_t)(L + 1);
   const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
+  // A candidate byte stored for an already-marked target is dropped by the next
+  // k_frontier (bits & ~vis), so the filter is an optimisation only.
+  const bool skipvis = !Fbits && a.vis_skip_div && c->marked * a.vis_skip_div < c->slot_top;
 
   if (pull_level(c, L, a)) {
     // Pull: each unmarked, not-yet-found shadow looks for an expandable
@@ -398,10 +443,10 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
             if (s_start[wv][mid] <= e) lo = mid;
             else hi = mid - 1;
           }
-          ed[u] = g.pool[(uint64_t)s_off[wv][lo] + (e - s_start[wv][lo])];
+          ed[u] = pool_load<NT>(&g.pool[(uint64_t)s_off[wv][lo] + (e - s_start[wv][lo])]);
         }
       }
-      expand_edges(g, Fn, Dn, sp_next, check, ed, Fbits);
+      expand_edges(g, Fn, Dn, sp_next, check, ed, Fbits, skipvis);
     }
     wave_lds_fence();
   }
@@ -413,9 +458,9 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t e = e0 + u * 64 + lane;
-        ed[u] = e < r.y ? g.pool[(uint64_t)r.x + e] : 0;
+        ed[u] = e < r.y ? pool_load<NT>(&g.pool[(uint64_t)r.x + e]) : 0;
       }
-      expand_edges(g, Fn, Dn, sp_next, check, ed, Fbits);
+      expand_edges(g, Fn, Dn, sp_next, check, ed, Fbits, skipvis);
     }
   }
 }
@@ -713,10 +758,12 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
   // level controller: the level count, and the narrow-frontier takeover
   hipExtLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, e[2], e[3], 0, g, a);
   // 8 WGs of 4 waves per CU
-  if (a.flags & LV_EXP8)
-    hipExtLaunchKernelGGL(k_expand<8>, dim3(STAT_WG), dim3(256), 0, s, e[4], e[5], 0, g, a);
-  else
-    hipExtLaunchKernelGGL(k_expand<4>, dim3(STAT_WG), dim3(256), 0, s, e[4], e[5], 0, g, a);
+  auto expand = [&](auto kern) {
+    hipExtLaunchKernelGGL(kern, dim3(STAT_WG), dim3(256), 0, s, e[4], e[5], 0, g, a);
+  };
+  if (a.flags & LV_EXP8) expand(k_expand<8, false>);
+  else if (a.flags & LV_NT) expand(k_expand<4, true>);
+  else expand(k_expand<4, false>);
   return hipGetLastError();
 }
 
