@@ -48,7 +48,7 @@ void free_arrays(Arrays &a) {
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill, d.fbits[0], d.fbits[1],
                 d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.fx, d.tq, d.tl_buf, d.tl_tag,
-                d.xp_buf, d.xp_cnt, d.rq_buf, d.rq_cnt, d.binq};
+                d.xp_buf, d.xp_cnt, d.rq_buf, d.rq_cnt};
   for (void *p : ps)
     if (p) hipFree(p);
   a.allocated = false;
@@ -119,8 +119,6 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   A(dmalloc(&d.rnew, c.scap));
   A(dmalloc(&d.rpool, d.rpcap));
   A(dmalloc(&d.fx, c.scap / 32));
-  d.binq_cap = std::max<uint64_t>(4096, c.pcap / 32);  // 64 bins: 2 x the edge pool
-  A(dmalloc(&d.binq, (uint64_t)PB_W * PB_B * d.binq_cap));
   A(dmalloc(&d.tq, 2 * (uint64_t)TAIL_QCAP));
   A(dmalloc(&d.tl_buf, c.scap));
   A(dmalloc(&d.tl_tag, c.scap / BLK_SLOTS));
@@ -1164,10 +1162,6 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   if (const char *m = getenv("CRGC_EXP8")) la.flags |= atoi(m) ? LV_EXP8 : 0;
   if (const char *m = getenv("CRGC_EXPAND_NT")) la.flags = atoi(m) ? la.flags | LV_NT : la.flags & ~LV_NT;
   if (const char *m = getenv("CRGC_VIS_SKIP")) la.vis_skip_div = (uint32_t)strtoul(m, nullptr, 10);
-  // Propagation blocking: push levels whose frontier has >= pb_min shadows bin
-  // their candidates by XCD-affine slot block; k_bin_apply stores them.
-  la.pb_min = 0;
-  if (const char *m = getenv("CRGC_PB")) la.pb_min = (uint32_t)strtoul(m, nullptr, 10);
   la.sparse_thresh = (uint32_t)std::max<uint64_t>(64, (top / BLK_SLOTS) / 4);
   // Direction optimisation: dense levels after a frontier of >= top/div shadows pull.
   uint64_t pull_div = 16;

@@ -168,7 +168,6 @@ struct LevelArgs {
   uint32_t frontier_grid;  // workgroups of k_frontier (set by launch_level)
   uint32_t flags;          // LV_*
   uint32_t vis_skip_div;   // push levels skip the marked-word filter while marked * div < slot_top
-  uint32_t pb_min;         // push levels with a frontier of >= pb_min (> 0) shadows bin their candidates
   uint16_t location;
 };
 

@@ -53,8 +53,6 @@ constexpr uint32_t ERR_QUEUE_FULL = 1u << 9;
 
 constexpr int WAVE = 64;
 constexpr int BLK_SLOTS = 2048;          // slots per wave-block (64 lanes x 32)
-constexpr int PB_B = 8;                 // candidate bins: (slot >> 11) & 7, one per XCD under round-robin placement
-constexpr int PB_W = 8;                 // writer groups (blockIdx % 8): spreads the bins' append counters
 constexpr int LEVEL_RING = 4096;         // ring of per-level frontier counts
 constexpr int STAT_WG = 2048;            // max workgroups of the level / sweep kernels
 constexpr int TAIL_QCAP = 1 << 16;       // narrow-frontier queue capacity (per buffer)
@@ -93,9 +91,6 @@ struct Counters {
   unsigned long long n_req;          // kill requests (garbage with a remote supervisor)
   unsigned long long xcnt[MAX_SHARDS];  // ids to send per destination shard
   unsigned long long xpos[MAX_SHARDS];  // scatter cursors
-  // propagation-blocking bins of push levels (k_expand -> k_bin_apply), by level
-  // parity; [writer group * PB_B + bin].  Zeroed by k_frontier of their level.
-  unsigned int binctr[2][PB_W * PB_B];
   unsigned long long ring[LEVEL_RING];
 };
 
@@ -140,8 +135,6 @@ struct DevGraph {
   uint32_t *rpool;           // owner slot | RC_POS while count(owner -> slot) > 0
   uint64_t rpcap;
   uint32_t *fx;              // expandable frontier bitmap (frontier & !halted)
-  uint32_t *binq;            // [PB_W * PB_B][binq_cap] candidate slots of a push level, binned
-  uint64_t binq_cap;
   uint32_t *tq;              // narrow-frontier queues, 2 x TAIL_QCAP slots
   uint32_t *tl_buf;          // per-block regions: a listed level's frontier slots
   uint32_t *tl_tag;          // per block: (level+1) << 12 | listed slots

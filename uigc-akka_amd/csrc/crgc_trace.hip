@@ -93,8 +93,6 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
   __shared__ uint32_t s_front[4][BLK_SLOTS];
   Counters *c = g.ctr;
   const int L = a.level;
-  // this level's bins: k_bin_apply(L-2) has read them, k_expand(L) fills them
-  if (blockIdx.x == 0 && threadIdx.x < PB_W * PB_B) c->binctr[L & 1][threadIdx.x] = 0;
   if (c->tail_state) return;  // k_tail finished the mark (or bailed to a later level)
   if (blockIdx.x == 0 && threadIdx.x == 0) c->ring[(L + 1) % LEVEL_RING] = 0;
   uint64_t *stat = g.blkstat + (uint64_t)blockIdx.x * 4;
@@ -291,67 +289,6 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// Propagation blocking (wide push levels).  The candidate byte map is 10 MB at
-// C2, larger than one XCD's L2, so direct stores from every XCD miss to the
-// Infinity Cache.  Instead each wave bins its candidates by (slot >> 11) & 7
-// in an LDS ring per bin and appends full groups of 64 to the bin's queue
-// (one counter add per group); k_bin_apply then stores bin j from workgroups
-// with blockIdx % 8 == j, which round-robin placement puts on one XCD, so the
-// bin's 1.25 MB of candidate bytes stays in that L2.  Placement affects speed
-// only: every bin is applied whichever XCD runs it.
-// ---------------------------------------------------------------------------
-constexpr uint32_t PB_RING = 128;  // per wave and bin; < 64 pending between pushes
-
-struct PbWave {
-  uint32_t *ring;  // LDS [PB_B][PB_RING]
-  uint32_t fill[PB_B], done[PB_B];
-  uint32_t wgrp;
-};
-
-__device__ inline void pb_flush(const DevGraph &g, PbWave &pw, int j, uint32_t n, int L, uint8_t *Fn,
-                                uint8_t *Dn, bool sp_next) {
-  const int lane = lane_id();
-  const uint32_t q = pw.wgrp * PB_B + j;
-  uint32_t base = 0;
-  if (lane == 0) base = atomicAdd(&g.ctr->binctr[L & 1][q], n);
-  base = __shfl(base, 0);
-  if ((uint32_t)lane < n) {
-    const uint32_t t = pw.ring[j * PB_RING + ((pw.done[j] + lane) & (PB_RING - 1))];
-    if (t >= g.ctr->slot_top) {
-      set_err(g.ctr, ERR_QUEUE_FULL);  // never: a binned candidate is an edge target
-    } else if ((uint64_t)base + lane < g.binq_cap) {
-      g.binq[(uint64_t)q * g.binq_cap + base + lane] = t;
-    } else {  // bin full: a direct store, as without binning
-      Fn[t] = 1;
-      if (sp_next && Dn[t >> 11] == 0) Dn[t >> 11] = 1;
-    }
-  }
-  pw.done[j] = __builtin_amdgcn_readfirstlane(pw.done[j] + n);
-}
-
-template <int U>
-__device__ inline void pb_push(const DevGraph &g, PbWave &pw, const bool (&go)[U], const uint32_t (&t)[U],
-                               int L, uint8_t *Fn, uint8_t *Dn, bool sp_next) {
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int mine = go[u] ? (int)((t[u] >> 11) & (PB_B - 1)) : -1;
-    if (!__ballot(mine >= 0)) continue;
-#pragma unroll
-    for (int j = 0; j < PB_B; ++j) {
-      const uint64_t m = __ballot(mine == j);
-      if (!m) continue;
-      if (mine == j) pw.ring[j * PB_RING + ((pw.fill[j] + __popcll(m & lanemask_lt())) & (PB_RING - 1))] = t[u];
-      pw.fill[j] = __builtin_amdgcn_readfirstlane(pw.fill[j] + (uint32_t)__popcll(m));  // uniform: SGPR
-    }
-    wave_lds_fence();
-#pragma unroll
-    for (int j = 0; j < PB_B; ++j)
-      if (pw.fill[j] - pw.done[j] >= 64) pb_flush(g, pw, j, 64, L, Fn, Dn, sp_next);
-    wave_lds_fence();  // ring slots read by the flush are rewritten by later pushes
-  }
-}
-
 // U edges of one lane (:231-241).  Each phase issues all its loads
 // before any is waited on: the vis words, then the candidate bytes of the
 // targets still unmarked, then the stores — two dependent round trips per
@@ -359,8 +296,7 @@ __device__ inline void pb_push(const DevGraph &g, PbWave &pw, const bool (&go)[U
 // per-edge marking would serialise them).
 template <int U>
 __device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn, bool sp_next, bool check,
-                                    const uint64_t (&ed)[U], uint32_t *Fbits, bool skipvis, bool pb,
-                                    PbWave &pw, int L) {
+                                    const uint64_t (&ed)[U], uint32_t *Fbits, bool skipvis) {
   uint32_t t[U];
   bool go[U];
 #pragma unroll
@@ -379,11 +315,7 @@ __device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn,
 #pragma unroll
     for (int u = 0; u < U; ++u) w[u] = go[u] ? g.vis[t[u] >> 5] : ~0u;
 #pragma unroll
-    for (int u = 0; u < U; ++u) go[u] = go[u] && !((w[u] >> (t[u] & 31)) & 1u);
-  }
-  if (pb) {
-    pb_push<U>(g, pw, go, t, L, Fn, Dn, sp_next);
-    return;
+    for (int u = 0; u < U; ++u) go[u] = !((w[u] >> (t[u] & 31)) & 1u);
   }
   uint8_t fb[U];
 #pragma unroll
@@ -412,7 +344,7 @@ __device__ inline uint64_t pool_load(const uint64_t *p) {
   return *p;
 }
 
-template <int U, bool NT, bool PBK>
+template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   __shared__ uint32_t s_start[4][65];
   __shared__ uint32_t s_off[4][64];
@@ -435,13 +367,6 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   // A candidate byte stored for an already-marked target is dropped by the next
   // k_frontier (bits & ~vis), so the filter is an optimisation only.
   const bool skipvis = !Fbits && a.vis_skip_div && c->marked * a.vis_skip_div < c->slot_top;
-  __shared__ uint32_t s_ring[4][PB_B * PB_RING];
-  PbWave pw;
-  pw.ring = s_ring[wv];
-  pw.wgrp = blockIdx.x % PB_W;
-#pragma unroll
-  for (int j = 0; j < PB_B; ++j) pw.fill[j] = pw.done[j] = 0;
-  const bool pb = PBK && !Fbits && a.pb_min && g.binq && c->ring[L % LEVEL_RING] >= a.pb_min;
 
   if (pull_level(c, L, a)) {
     // Pull: each unmarked, not-yet-found shadow looks for an expandable
@@ -521,7 +446,7 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
           ed[u] = pool_load<NT>(&g.pool[(uint64_t)s_off[wv][lo] + (e - s_start[wv][lo])]);
         }
       }
-      expand_edges(g, Fn, Dn, sp_next, check, ed, Fbits, skipvis, pb, pw, L);
+      expand_edges(g, Fn, Dn, sp_next, check, ed, Fbits, skipvis);
     }
     wave_lds_fence();
   }
@@ -535,51 +460,7 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
         const uint32_t e = e0 + u * 64 + lane;
         ed[u] = e < r.y ? pool_load<NT>(&g.pool[(uint64_t)r.x + e]) : 0;
       }
-      expand_edges(g, Fn, Dn, sp_next, check, ed, Fbits, skipvis, pb, pw, L);
-    }
-  }
-  if (pb) {  // partial groups
-#pragma unroll
-    for (int j = 0; j < PB_B; ++j)
-      if (pw.fill[j] != pw.done[j]) pb_flush(g, pw, j, pw.fill[j] - pw.done[j], L, Fn, Dn, sp_next);
-  }
-}
-
-// Candidate stores of a binned push level: bin j from workgroups b % 8 == j.
-__global__ __launch_bounds__(256) void k_bin_apply(DevGraph g, LevelArgs a) {
-  const Counters *c = g.ctr;
-  const int L = a.level;
-  const int j = blockIdx.x % PB_B;
-  const uint32_t part = blockIdx.x / PB_B, nparts = gridDim.x / PB_B;
-  const bool sp_next = sparse_level(c, L + 1, a.sparse_thresh);
-  const uint64_t top = c->slot_top;
-  uint8_t *Fn = g.front[(L + 1) & 1];
-  uint8_t *Dn = g.dirty[(L + 1) & 1];
-  for (int w = 0; w < PB_W; ++w) {
-    const uint32_t q = w * PB_B + j;
-    const uint64_t n = min((uint64_t)c->binctr[L & 1][q], g.binq_cap);
-    const uint32_t *qb = g.binq + (uint64_t)q * g.binq_cap;
-    for (uint64_t i0 = (uint64_t)part * 1024; i0 < n; i0 += (uint64_t)nparts * 1024) {
-      uint32_t t[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint64_t i = i0 + k * 256 + threadIdx.x;
-        t[k] = i < n ? qb[i] : NO_SLOT;
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (t[k] != NO_SLOT && t[k] >= top) {
-          set_err(g.ctr, ERR_QUEUE_FULL);  // never: queues hold edge targets
-          t[k] = NO_SLOT;
-        }
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (t[k] != NO_SLOT) Fn[t[k]] = 1;
-      if (sp_next) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (t[k] != NO_SLOT && Dn[t[k] >> 11] == 0) Dn[t[k] >> 11] = 1;
-      }
+      expand_edges(g, Fn, Dn, sp_next, check, ed, Fbits, skipvis);
     }
   }
 }
@@ -877,15 +758,12 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
   // level controller: the level count, and the narrow-frontier takeover
   hipExtLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, e[2], e[3], 0, g, a);
   // 8 WGs of 4 waves per CU
-  const bool pb = a.pb_min && g.binq && !(a.flags & LV_BITMAP_FRONT);
-  auto expand = [&](auto kern) {  // with binning, its stop event is k_bin_apply's
-    hipExtLaunchKernelGGL(kern, dim3(STAT_WG), dim3(256), 0, s, e[4], pb ? nullptr : e[5], 0, g, a);
+  auto expand = [&](auto kern) {
+    hipExtLaunchKernelGGL(kern, dim3(STAT_WG), dim3(256), 0, s, e[4], e[5], 0, g, a);
   };
-  if (a.flags & LV_EXP8) expand(k_expand<8, false, false>);
-  else if (pb) expand(k_expand<4, true, true>);
-  else if (a.flags & LV_NT) expand(k_expand<4, true, false>);
-  else expand(k_expand<4, false, false>);
-  if (pb) hipExtLaunchKernelGGL(k_bin_apply, dim3(STAT_WG), dim3(256), 0, s, nullptr, e[5], 0, g, a);
+  if (a.flags & LV_EXP8) expand(k_expand<8, false>);
+  else if (a.flags & LV_NT) expand(k_expand<4, true>);
+  else expand(k_expand<4, false>);
   return hipGetLastError();
 }
 
