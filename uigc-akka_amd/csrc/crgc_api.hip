@@ -1153,11 +1153,13 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   LevelArgs la{};
   la.location = location;
   // Tuning switches for A/B runs (results are identical either way).  Defaults
-  // from tools/ab_trace.py on C2 (profiles/r1h): plain candidate stores, the
-  // edge stream read non-temporal, no marked-word filter while < 1/16 is marked.
-  la.flags = LV_NT;
+  // from tools/ab_trace.py on the bench's C2 graph after 12 wakeups
+  // (profiles/r1n): candidate byte read before its store, the edge stream read
+  // non-temporal, no marked-word filter while < 1/16 of the slots is marked.
+  la.flags = LV_NT | LV_CHECK_BEFORE_STORE;
   la.vis_skip_div = 16;
-  if (const char *m = getenv("CRGC_MARK_CHECK")) la.flags |= atoi(m) ? LV_CHECK_BEFORE_STORE : 0;
+  if (const char *m = getenv("CRGC_MARK_CHECK"))
+    la.flags = atoi(m) ? la.flags | LV_CHECK_BEFORE_STORE : la.flags & ~LV_CHECK_BEFORE_STORE;
   if (const char *m = getenv("CRGC_MARK_BITS")) la.flags |= atoi(m) ? LV_BITMAP_FRONT : 0;
   if (const char *m = getenv("CRGC_EXP8")) la.flags |= atoi(m) ? LV_EXP8 : 0;
   if (const char *m = getenv("CRGC_EXPAND_NT")) la.flags = atoi(m) ? la.flags | LV_NT : la.flags & ~LV_NT;

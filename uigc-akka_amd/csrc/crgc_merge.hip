@@ -472,17 +472,41 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_seg_plan(Seg<T> s, Counters *c
   }
 }
 
+// Most touched owners keep their segment: each lane tests one owner's plan, a
+// segment of <= SEG_LANE_COPY entries is copied by its own lane, longer ones by
+// the whole wave one after another (a wave per owner made every wave walk its
+// share of the touched list one dependent load at a time).
+constexpr uint32_t SEG_LANE_COPY = 8;
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_seg_move(Seg<T> s) {
   const uint64_t n = *s.ntouched;
   const uint64_t nw = (uint64_t)gridDim.x * 4;
-  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += nw) {
-    const uint32_t r = s.reloc[i];
-    if (r >= 0xFFFFFFFEu) continue;
-    const uint32_t o = s.touched[i];
-    const uint2 ad = s.adj[o];
-    for (uint32_t e = lane_id(); e < ad.y; e += 64) s.pool[(uint64_t)r + e] = s.pool[(uint64_t)ad.x + e];
-    if (lane_id() == 0) {
+  const int lane = lane_id();
+  for (uint64_t b = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; b < n; b += nw * 64) {
+    const uint64_t i = b + lane;
+    const uint32_t r = i < n ? s.reloc[i] : 0xFFFFFFFFu;
+    const bool mv = r < 0xFFFFFFFEu;
+    const uint32_t o = mv ? s.touched[i] : 0;
+    const uint2 ad = mv ? s.adj[o] : make_uint2(0, 0);
+    const bool small = mv && ad.y <= SEG_LANE_COPY;
+    if (small) {
+      T x[SEG_LANE_COPY];
+#pragma unroll
+      for (uint32_t e = 0; e < SEG_LANE_COPY; ++e)
+        if (e < ad.y) x[e] = s.pool[(uint64_t)ad.x + e];
+#pragma unroll
+      for (uint32_t e = 0; e < SEG_LANE_COPY; ++e)
+        if (e < ad.y) s.pool[(uint64_t)r + e] = x[e];
+    }
+    uint64_t big = __ballot(mv && !small);
+    while (big) {
+      const int k = __ffsll((unsigned long long)big) - 1;
+      big &= big - 1;
+      const uint32_t rk = __shfl(r, k), xk = __shfl(ad.x, k), yk = __shfl(ad.y, k);
+      for (uint32_t e = lane; e < yk; e += 64) s.pool[(uint64_t)rk + e] = s.pool[(uint64_t)xk + e];
+    }
+    if (mv) {
       s.adj[o].x = r;
       s.cap[o] = seg_cap(ad.y + s.nnew[o]);
     }
