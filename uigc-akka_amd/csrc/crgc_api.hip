@@ -1173,6 +1173,8 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   }
   if (const char *m = getenv("CRGC_PULL_DIV")) pull_div = std::max<uint64_t>(1, strtoull(m, nullptr, 10));
   la.pull_div = (uint32_t)pull_div;  // against the exact slot count, on the device
+  la.pull_cur_div = 4;
+  if (const char *m = getenv("CRGC_PULL_CUR_DIV")) la.pull_cur_div = (uint32_t)strtoul(m, nullptr, 10);
   la.pull_thresh = 0;
   // Test hooks: absolute thresholds (0 disables sparse levels entirely).
   if (const char *m = getenv("CRGC_PULL_THRESH")) {

@@ -168,6 +168,7 @@ struct LevelArgs {
   uint32_t frontier_grid;  // workgroups of k_frontier (set by launch_level)
   uint32_t flags;          // LV_*
   uint32_t vis_skip_div;   // push levels skip the marked-word filter while marked * div < slot_top
+  uint32_t pull_cur_div;   // k_expand also pulls once the current frontier is >= slot_top / div
   uint16_t location;
 };
 

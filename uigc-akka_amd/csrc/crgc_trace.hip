@@ -43,6 +43,19 @@ __device__ inline bool pull_level(const Counters *c, int L, const LevelArgs &a) 
   return a.pull_div ? prev * a.pull_div >= c->slot_top : prev >= a.pull_thresh;
 }
 
+// Levels whose k_frontier scans every block write `fx`, so k_expand can still
+// pull when the frontier it finds is large although the previous one was not
+// (the decision above is made before the level's own frontier is counted).
+__device__ inline bool fx_level(const Counters *c, int L, const LevelArgs &a) {
+  if (!(a.flags & LV_PULL) || (a.flags & LV_BITMAP_FRONT) || L < 1 || !a.pull_cur_div) return false;
+  return !sparse_level(c, L, a.sparse_thresh) && !sparse_level(c, L + 1, a.sparse_thresh);
+}
+
+__device__ inline bool pull_now(const Counters *c, int L, const LevelArgs &a) {
+  if (pull_level(c, L, a)) return true;
+  return fx_level(c, L, a) && c->ring[L % LEVEL_RING] * a.pull_cur_div >= c->slot_top;
+}
+
 // Whether level L lists its frontier for k_tail (same answer in k_frontier and
 // k_tail): the level may be narrow (sparse, or after a narrow level).
 __device__ inline bool listing_level(const Counters *c, int L, const LevelArgs &a) {
@@ -116,6 +129,7 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
   const uint32_t tag = (uint32_t)(L + 1) << 12;
   const bool bitmode = a.flags & LV_BITMAP_FRONT;
   const bool pull = !ROOTS && pull_level(c, L, a);
+  const bool write_fx = !ROOTS && (pull || fx_level(c, L, a));
   const bool listing = !ROOTS && listing_level(c, L, a);
   const bool sharded = !ROOTS && g.n_shards > 1;
   uint32_t n_front = 0, n_sup = 0, n_edges = 0;
@@ -182,13 +196,15 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
     const uint32_t incl = wave_incl_scan(cnt);
     const uint32_t total = __shfl(incl, 63);
     uint32_t pos = incl - cnt;
-    if (pull) {
+    if (write_fx) {
       // expandable frontier = frontier minus halted shadows (this wave owns the words)
-      const uint4 f4[2] = {*(const uint4 *)(g.flags + base), *(const uint4 *)(g.flags + base + 16)};
-      const uint8_t *fb = (const uint8_t *)f4;
       uint32_t halted = 0;
+      if (m) {
+        const uint4 f4[2] = {*(const uint4 *)(g.flags + base), *(const uint4 *)(g.flags + base + 16)};
+        const uint8_t *fb = (const uint8_t *)f4;
 #pragma unroll
-      for (int j = 0; j < 32; ++j) halted |= (fb[j] & FL_HALTED) ? (1u << j) : 0u;
+        for (int j = 0; j < 32; ++j) halted |= (fb[j] & FL_HALTED) ? (1u << j) : 0u;
+      }
       g.fx[(uint64_t)blk * 64 + lane] = m & ~halted;
     }
     while (m) {
@@ -368,7 +384,7 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   // k_frontier (bits & ~vis), so the filter is an optimisation only.
   const bool skipvis = !Fbits && a.vis_skip_div && c->marked * a.vis_skip_div < c->slot_top;
 
-  if (pull_level(c, L, a)) {
+  if (pull_now(c, L, a)) {
     // Pull: each unmarked, not-yet-found shadow looks for an expandable
     // frontier shadow among its in-candidates whose edge to it has a
     // positive count (RC_POS), and stops at the first.  A thread owns 4
