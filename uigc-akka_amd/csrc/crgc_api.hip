@@ -1163,6 +1163,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   if (const char *m = getenv("CRGC_MARK_BITS")) la.flags |= atoi(m) ? LV_BITMAP_FRONT : 0;
   if (const char *m = getenv("CRGC_EXP8")) la.flags |= atoi(m) ? LV_EXP8 : 0;
   if (const char *m = getenv("CRGC_EXPAND_NT")) la.flags = atoi(m) ? la.flags | LV_NT : la.flags & ~LV_NT;
+  if (const char *m = getenv("CRGC_PULL_SEQ")) la.flags |= atoi(m) ? LV_PULL_SEQ : 0;
   if (const char *m = getenv("CRGC_VIS_SKIP")) la.vis_skip_div = (uint32_t)strtoul(m, nullptr, 10);
   la.sparse_thresh = (uint32_t)std::max<uint64_t>(64, (top / BLK_SLOTS) / 4);
   // Direction optimisation: dense levels after a frontier of >= top/div shadows pull.

@@ -157,6 +157,7 @@ constexpr uint32_t LV_INVESTIGATE = 16;        // set by launch_level: no superv
 constexpr uint32_t LV_ROOTS = 32;              // set by launch_level: the pseudo-root level
 constexpr uint32_t LV_EXP8 = 64;               // k_expand: 8 edges per lane per step (else 4)
 constexpr uint32_t LV_NT = 128;                // k_expand: edge stream read non-temporal
+constexpr uint32_t LV_PULL_SEQ = 256;          // pull: a thread's in-candidate lists one after another
 
 struct LevelArgs {
   int level;

@@ -26,6 +26,7 @@ namespace crgc {
 constexpr uint32_t RANGE_MAX = 256;  // longer segments (hubs) are cut into pieces
 constexpr int FB = 4;               // k_frontier: chunks of 64 frontier shadows per load group
 constexpr uint32_t NO_SLOT = ~0u;
+constexpr uint32_t PULL_K = 4;      // pull: in-candidates per list per round
 constexpr int STAT_FRONT = 0, STAT_SUP = 1, STAT_EDGES = 2, STAT_LIVE = 3;
 
 __device__ inline bool sparse_level(const Counters *c, int L, uint32_t thr) {
@@ -407,23 +408,54 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
       const uint4 r23 = *(const uint4 *)(g.radj + v0 + 2);
       const uint32_t ro[4] = {r01.x, r01.z, r23.x, r23.z};
       const uint32_t rl[4] = {r01.y, r01.w, r23.y, r23.w};
-      uint32_t found = 0;
-      for (int j = 0; j < 4; ++j) {
-        if (!((todo >> j) & 1u)) continue;
-        const uint32_t *rp = g.rpool + ro[j];
-        const uint32_t n = rl[j];
-        bool hit = false;
-        for (uint32_t i = 0; i < n && !hit; i += 4) {
-          uint32_t u[4];
+      // The thread's (up to) 4 lists are walked together, PULL_K candidates of
+      // each per round: one round trip for the candidates, one for their
+      // frontier bits, until every list has a hit or is exhausted.
+      uint32_t found = 0, live = todo, pos = 0;
+      if (a.flags & LV_PULL_SEQ) {  // A/B: one list after another
+        live = 0;
+        for (int j = 0; j < 4; ++j) {
+          if (!((todo >> j) & 1u)) continue;
+          const uint32_t *rp = g.rpool + ro[j];
+          const uint32_t n = rl[j];
+          bool hit = false;
+          for (uint32_t i = 0; i < n && !hit; i += 4) {
+            uint32_t uu[4];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) u[k] = i + k < n ? rp[i + k] : 0u;  // 0: no RC_POS
+            for (int k = 0; k < 4; ++k) uu[k] = i + k < n ? rp[i + k] : 0u;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const uint32_t sl = u[k] & ~RC_POS;
-            if ((u[k] & RC_POS) && ((g.fx[sl >> 5] >> (sl & 31)) & 1u)) hit = true;
+            for (int k = 0; k < 4; ++k) {
+              const uint32_t sl = uu[k] & ~RC_POS;
+              if ((uu[k] & RC_POS) && ((g.fx[sl >> 5] >> (sl & 31)) & 1u)) hit = true;
+            }
           }
+          if (hit) found |= 1u << (8 * j);
         }
-        if (hit) found |= 1u << (8 * j);
+      }
+      while (live) {
+        uint32_t u[4][PULL_K];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int k = 0; k < PULL_K; ++k)
+            u[j][k] = ((live >> j) & 1u) && pos + k < rl[j] ? g.rpool[(uint64_t)ro[j] + pos + k] : 0u;
+        uint32_t w[4][PULL_K];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int k = 0; k < PULL_K; ++k) {
+            const uint32_t sl = u[j][k] & ~RC_POS;
+            w[j][k] = (u[j][k] & RC_POS) ? g.fx[sl >> 5] >> (sl & 31) : 0u;  // 0: no RC_POS
+          }
+        pos += PULL_K;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          bool hit = false;
+#pragma unroll
+          for (int k = 0; k < PULL_K; ++k) hit |= (w[j][k] & 1u) != 0;
+          if (hit && ((live >> j) & 1u)) found |= 1u << (8 * j);
+          if (hit || pos >= rl[j]) live &= ~(1u << j);
+        }
       }
       if (found) *(uint32_t *)(Fn + v0) = cand | found;
     }
