@@ -255,7 +255,7 @@ def load_library(path: str | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("CRGC_LIB_AB") or LIB_PATH  # CRGC_LIB_AB: A/B of two builds
     if not os.path.exists(p):
         raise RuntimeError(
             f"libcrgc_hip.so not found at {p}; build it with "

@@ -103,8 +103,8 @@ __device__ inline uint64_t block_sum4(uint64_t v) {
 // of `qn` (light) or, cut into RANGE_MAX pieces, to `qh` (hubs).
 // ---------------------------------------------------------------------------
 template <bool ROOTS, bool INVESTIGATE>
-__global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
-  __shared__ uint32_t s_front[4][BLK_SLOTS];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_frontier(DevGraph g, LevelArgs a) {
+  __shared__ uint16_t s_front[4][BLK_SLOTS];  // offsets in the block: 16 KiB, so LDS allows 8 waves/SIMD
   Counters *c = g.ctr;
   const int L = a.level;
   if (c->tail_state) return;  // k_tail finished the mark (or bailed to a later level)
@@ -211,12 +211,13 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
     while (m) {
       const int j = __ffs(m) - 1;
       m &= m - 1;
-      s_front[wv][pos++] = (uint32_t)(base + j);
+      s_front[wv][pos++] = (uint16_t)(lane * 32 + j);
     }
     n_front += cnt;
     wave_lds_fence();
     if (listing && total) {  // into the block's own region: no shared counter
-      for (uint32_t i = lane; i < total; i += 64) g.tl_buf[(uint64_t)blk * BLK_SLOTS + i] = s_front[wv][i];
+      for (uint32_t i = lane; i < total; i += 64)
+        g.tl_buf[(uint64_t)blk * BLK_SLOTS + i] = blk * BLK_SLOTS + s_front[wv][i];
       if (lane == 0) g.tl_tag[blk] = tag | total;
     }
 
@@ -235,7 +236,7 @@ __global__ __launch_bounds__(256) void k_frontier(DevGraph g, LevelArgs a) {
 #pragma unroll
       for (int b = 0; b < FB; ++b) {
         const uint32_t idx = c0 + b * 64 + lane;
-        v[b] = idx < total ? s_front[wv][idx] : NO_SLOT;
+        v[b] = idx < total ? blk * BLK_SLOTS + s_front[wv][idx] : NO_SLOT;
       }
 #pragma unroll
       for (int b = 0; b < FB; ++b) {
