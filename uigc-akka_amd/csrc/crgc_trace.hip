@@ -593,6 +593,39 @@ __device__ inline void tail_claim(const DevGraph &g, const TailLds &sh, uint32_t
   }
 }
 
+// Walks: a thread keeps the first shadow it claims while processing one and
+// processes it next itself, in the same round (a chain link per step instead
+// of per round); any further claim goes to the next round's queue.
+template <bool LV>
+__device__ inline void tail_claim_keep(const DevGraph &g, const TailLds &sh, uint32_t t, const TailQ &nxt,
+                                       uint8_t *Fb, uint8_t *Db, int32_t &claims, uint32_t &keep) {
+  if (keep != NO_SLOT) {
+    tail_claim<LV>(g, sh, t, nxt, Fb, Db, claims);
+    return;
+  }
+  const uint32_t bit = 1u << (t & 31);
+  uint32_t *w = LV ? &sh.vis[t >> 5] : &g.vis[t >> 5];
+  if (*w & bit) return;
+  if (atomicOr(w, bit) & bit) return;
+  keep = t;
+  ++claims;
+}
+
+// A kept shadow that is not walked after all (a hub): queued like a claim.
+template <bool LV>
+__device__ inline void tail_enqueue_claimed(const DevGraph &g, const TailLds &sh, uint32_t t, const TailQ &nxt,
+                                            uint8_t *Fb, uint8_t *Db, int32_t &claims) {
+  const uint32_t pos = atomicAdd(sh.next, 1u);
+  if (pos < TAIL_QCAP) {
+    nxt.put(pos, t);
+  } else {
+    atomicAnd(LV ? &sh.vis[t >> 5] : &g.vis[t >> 5], ~(1u << (t & 31)));
+    Fb[t] = 1;
+    Db[t >> 11] = 1;
+    --claims;
+  }
+}
+
 template <bool LV>
 __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const TailLds &sh, TailQ cur,
                                    TailQ nxt, uint32_t n, TailOut &o) {
@@ -608,42 +641,58 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
     __syncthreads();
     for (uint32_t c0 = 0; c0 < n; c0 += TAIL_THREADS) {
       const uint32_t i = c0 + threadIdx.x;
-      const bool valid = i < n;
-      const uint32_t v = valid ? cur.get(i) : 0;
-      const uint8_t f = valid ? g.flags[v] : 0;
-      const bool expand = valid && !(f & FL_HALTED);  // (:226-229)
-      if (!first && (f & FL_PROXY)) {  // level L's were listed by k_frontier
-        const uint32_t pos = atomicAdd(&g.xp_cnt[v >> 11], 1u);
-        g.xp_buf[(uint64_t)(v >> 11) * BLK_SLOTS + pos] = v;
-      }
+      bool have = i < n;
+      uint32_t v = have ? cur.get(i) : 0;
+      bool vfirst = first;
       uint2 ad = make_uint2(0, 0);
-      if (expand) {
-        ad = g.adj[v];
-        if (!first) o.n_edges += g.nzdeg[v];  // level L's were counted by k_frontier
-        if (!investigate) {
-          const uint32_t s = g.sup[v];  // (:258-267)
-          if (s < 0xFFFFFFF0u) {
-            if (first) {
-              Fn[s] = 0;
-              Dn[s >> 11] = 0;
-            } else {
-              ++o.n_sup;
+      while (have) {
+        have = false;
+        const uint8_t f = g.flags[v];
+        const bool expand = !(f & FL_HALTED);  // (:226-229)
+        if (!vfirst && (f & FL_PROXY)) {  // level L's were listed by k_frontier
+          const uint32_t pos = atomicAdd(&g.xp_cnt[v >> 11], 1u);
+          g.xp_buf[(uint64_t)(v >> 11) * BLK_SLOTS + pos] = v;
+        }
+        ad = make_uint2(0, 0);
+        uint32_t keep = NO_SLOT;
+        if (expand) {
+          ad = g.adj[v];
+          if (!vfirst) o.n_edges += g.nzdeg[v];  // level L's were counted by k_frontier
+          if (!investigate) {
+            const uint32_t s = g.sup[v];  // (:258-267)
+            if (s < 0xFFFFFFF0u) {
+              if (vfirst) {
+                Fn[s] = 0;
+                Dn[s >> 11] = 0;
+              } else {
+                ++o.n_sup;
+              }
+              tail_claim_keep<LV>(g, sh, s, nxt, Fb, Db, o.claims, keep);
             }
-            tail_claim<LV>(g, sh, s, nxt, Fb, Db, o.claims);
+          }
+        }
+        if (ad.y <= TAIL_LIGHT) {  // this thread walks its shadow's out-edges (:231-241)
+          for (uint32_t e = 0; e < ad.y; e += 4) {
+            uint64_t ed[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) ed[u] = e + u < ad.y ? g.pool[(uint64_t)ad.x + e + u] : 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (edge_count(ed[u]) > 0)
+                tail_claim_keep<LV>(g, sh, edge_target(ed[u]), nxt, Fb, Db, o.claims, keep);
+          }
+        }
+        if (keep != NO_SLOT) {
+          if (ad.y <= TAIL_LIGHT) {  // walk on
+            v = keep;
+            vfirst = false;
+            have = true;
+          } else {  // this shadow's edges go to the workgroup pass below: queue the kept one
+            tail_enqueue_claimed<LV>(g, sh, keep, nxt, Fb, Db, o.claims);
           }
         }
       }
       const bool heavy = ad.y > TAIL_LIGHT;
-      if (!heavy) {  // this thread walks its shadow's out-edges (:231-241)
-        for (uint32_t e = 0; e < ad.y; e += 4) {
-          uint64_t ed[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) ed[u] = e + u < ad.y ? g.pool[(uint64_t)ad.x + e + u] : 0;
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (edge_count(ed[u]) > 0) tail_claim<LV>(g, sh, edge_target(ed[u]), nxt, Fb, Db, o.claims);
-        }
-      }
       if (__syncthreads_or(heavy)) {  // heavy shadows: the workgroup shares their edges
         uint32_t total;
         const uint32_t st = tail_scan(heavy ? ad.y : 0u, sh.w, total);
