@@ -647,7 +647,11 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
       uint2 ad = make_uint2(0, 0);
       while (have) {
         have = false;
+        // every per-shadow field in one round trip (a walk step is one chain link)
         const uint8_t f = g.flags[v];
+        const uint2 adv = g.adj[v];
+        const uint32_t nzv = g.nzdeg[v];
+        const uint32_t supv = investigate ? NO_SLOT : g.sup[v];
         const bool expand = !(f & FL_HALTED);  // (:226-229)
         if (!vfirst && (f & FL_PROXY)) {  // level L's were listed by k_frontier
           const uint32_t pos = atomicAdd(&g.xp_cnt[v >> 11], 1u);
@@ -656,10 +660,10 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
         ad = make_uint2(0, 0);
         uint32_t keep = NO_SLOT;
         if (expand) {
-          ad = g.adj[v];
-          if (!vfirst) o.n_edges += g.nzdeg[v];  // level L's were counted by k_frontier
+          ad = adv;
+          if (!vfirst) o.n_edges += nzv;  // level L's were counted by k_frontier
           if (!investigate) {
-            const uint32_t s = g.sup[v];  // (:258-267)
+            const uint32_t s = supv;  // (:258-267)
             if (s < 0xFFFFFFF0u) {
               if (vfirst) {
                 Fn[s] = 0;
