@@ -1,0 +1,67 @@
+"""Every trace tuning switch gives the oracle's result (HIP vs oracle).
+
+The level kernels read A/B switches per trace (CRGC_* in crgc_api.hip
+run_levels).  They change how the mark is computed — push or pull per level,
+the marked-word filter, check-before-store, the non-temporal edge stream, the
+pull walk, the narrow-frontier takeover — never what is marked.  Each variant
+replays the same seeded stream (a C1-sized power-law graph, then mutator
+wakeups) into a fresh graph and must match the oracle wakeup by wakeup.
+"""
+import pytest
+
+import world
+
+pytestmark = pytest.mark.gpu
+
+ACTORS, EDGES, BATCH, WAKEUPS = 100_000, 1_000_000, 10_000, 3
+
+VARIANTS = [
+    {},
+    {"CRGC_PULL_CUR_DIV": "0"},           # direction from the previous frontier only
+    {"CRGC_PULL_CUR_DIV": "1000000"},     # pull on every dense level with a frontier
+    {"CRGC_PULL": "0"},                   # push only
+    {"CRGC_VIS_SKIP": "0"},               # always filter by the marked words
+    {"CRGC_VIS_SKIP": "1000000"},         # almost never filter
+    {"CRGC_MARK_CHECK": "0"},             # plain candidate stores
+    {"CRGC_EXPAND_NT": "0"},              # default-policy edge stream
+    {"CRGC_PULL_SEQ": "1"},               # one in-candidate list after another
+    {"CRGC_TAIL": "0"},                   # no narrow-frontier takeover
+    {"CRGC_TAIL_START": "1000000", "CRGC_TAIL_MAX": "64"},  # early takeover, frequent bails
+]
+
+
+def _stream():
+    w = world.World(seed=0x5EED + 11)
+    w.bulk_graph(ACTORS, EDGES, alpha=2.1, n_roots=ACTORS // 100)
+    return w
+
+
+def _key(r):
+    return (r.garbage_set(), r.kill_set(), r.n_live, r.pseudo_roots, r.sup_edges)
+
+
+@pytest.fixture(scope="module")
+def oracle_results(oracle_mod):
+    w = _stream()
+    o = oracle_mod.OracleGraph()
+    for b in w.batches(1 << 20):
+        o.merge_entries(b)
+    out = [_key(o.trace(True))]
+    for _ in range(WAKEUPS):
+        o.merge_entries(w.wakeup_batch(BATCH))
+        out.append(_key(o.trace(True)))
+    return out
+
+
+@pytest.mark.parametrize("env", VARIANTS, ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()) or "defaults")
+def test_trace_switches_match_oracle(hip_mod, oracle_results, monkeypatch, env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    w = _stream()
+    h = hip_mod.ShadowGraph(vertex_capacity=ACTORS * 2, edge_capacity=EDGES * 2)
+    for b in w.batches(1 << 20):
+        h.merge_entries(b)
+    assert _key(h.trace(True)) == oracle_results[0]
+    for i in range(WAKEUPS):
+        h.merge_entries(w.wakeup_batch(BATCH).to_device())
+        assert _key(h.trace(True)) == oracle_results[i + 1], f"wakeup {i}"
