@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define CRGC_ABI_VERSION 1u
+#define CRGC_ABI_VERSION 2u  /* 2: crgc_trace_stats.expand_launches / expand_bytes */
 
 /* ---- status codes ------------------------------------------------------- */
 #define CRGC_OK 0
@@ -188,6 +188,9 @@ typedef struct crgc_trace_stats {
   uint64_t rounds;         /* exchange rounds (1 + frontier all-to-alls)    */
   uint64_t ids_sent;       /* frontier ids sent to other shards             */
   double ms_exchange;      /* host wall time spent in exchanges             */
+  /* the k_expand roofline */
+  uint64_t expand_launches;/* k_expand dispatches of this trace             */
+  uint64_t expand_bytes;   /* bytes k_expand read + wrote, by element width  */
 } crgc_trace_stats;
 
 typedef struct crgc_trace_out {

@@ -45,8 +45,12 @@ def test_library_loads_and_exports_every_declared_symbol():
     assert lib.crgc_strerror(abi.E_NULL_SUPERVISOR).startswith(b"local garbage")
 
 
-def test_library_is_gfx950_only():
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", abi.LIB_PATH],
+def test_library_is_gfx950_only(tmp_path):
+    # --offloading extracts the code objects next to its input: work on a copy
+    import shutil
+    lib = tmp_path / "libcrgc_hip.so"
+    shutil.copy(abi.LIB_PATH, lib)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)],
                          capture_output=True, text=True).stdout
     arches = set(re.findall(r"gfx\d+", out))
     assert arches == {"gfx950"}, arches

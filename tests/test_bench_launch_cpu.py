@@ -1,0 +1,35 @@
+"""bench.py's own multi-rank launcher on the CPU (gloo): `--gpus N` with no
+launcher around it starts N ranks through torch.distributed.run, each checks
+its world size, and rank 0 reports the max-over-ranks wall time (--dry-run:
+the same rendezvous, barriers and reductions, no GPU work)."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(REPO, "bench.py")
+
+
+def _run(args, env=None):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True,
+                          timeout=300, cwd=REPO, env=e)
+
+
+def test_bench_starts_its_own_ranks():
+    p = _run(["--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout              # rank 0 only
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["ranks_reported"] == 2 and out["dry_run"]
+    assert out["steps"] == 3 and out["ms_per_step"] > 0
+
+
+def test_bench_refuses_a_world_size_other_than_gpus():
+    p = _run(["--gpus", "2", "--dry-run"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode == 2 and "world size 1 != --gpus 2" in p.stderr

@@ -1,5 +1,8 @@
 """HIP vs oracle on the BASELINE.json configurations (C1, C2 scaled, C3, C5).
 
+C1 / C2 wakeups follow SURVEY §8d: about 9 % of the actors busy and 1 % with
+mail in flight when LocalGC drains the queue (workload/world.cpp wl_wakeup).
+
 Bit-exact parity is checked on garbage and kill *sets*, live counts and the
 exported graph state, wakeup by wakeup, at sizes the oracle finishes in
 seconds.  The full-size C2 graph is checked by size-independent properties
@@ -28,9 +31,69 @@ def _load(g, w, batch):
         g.merge_entries(b)
 
 
+def c1_world(actors=100_000, seed=0x5EED + 1):
+    """C1 as BASELINE.json / SURVEY §8d state it: 1e5 actors, uniform 1 + Poisson
+    acquaintances (~1e6 refs, counts 1 / 2 / -1), 1 % roots, 5 % planted dead
+    components, RandomSpec's op mix (RandomSpec.scala:69-87)."""
+    w = world.World(seed=seed)
+    w.set_mix(send=0.2, share=0.2, release=0.2, spawn=0.2, actions_per_msg=2.0)
+    w.uniform_graph(actors, mean_acq=8.0, n_roots=actors // 100, dead_frac=0.05)
+    return w
+
+
+def busy_wakeup(w, actors, batch):
+    """A wakeup with 9 % of the actors busy and 1 % with mail in flight at the cut."""
+    return w.wakeup(batch, busy=actors * 9 // 100, pending=actors // 100)
+
+
+def test_c1_spec_wakeups_match_oracle(hip_mod, oracle_mod):
+    actors = 100_000
+    w = c1_world(actors)
+    h = hip_mod.ShadowGraph(vertex_capacity=actors, edge_capacity=10 * actors)
+    o = oracle_mod.OracleGraph()
+    for b in w.batches(1 << 20):
+        h.merge_entries(b)
+        o.merge_entries(b)
+    r0 = o.trace(True)
+    _same(h.trace(True), r0)
+    assert len(r0.garbage) == actors // 20            # the planted dead components
+    for k in range(6):
+        b = busy_wakeup(w, actors, 10_000)
+        h.merge_entries(b.to_device())
+        o.merge_entries(b)
+        rh, ro = h.trace(True), o.trace(True)
+        _same(rh, ro)
+        if k >= 1:                                     # roots + busy + mail in flight ~ 11 %
+            assert 0.09 * ro.n_live < ro.pseudo_roots < 0.13 * ro.n_live
+    assert h.export() == o.export()
+    assert h.total_actors_seen() == o.total_actors_seen()
+
+
+def test_c2_shape_busy_wakeups_match_oracle(hip_mod, oracle_mod):
+    """C2 at 1/10 scale with the §8d wakeup: 10 % busy / in flight at every cut."""
+    actors = 1_000_000
+    w = world.World(seed=0x5EED + 2)
+    w.bulk_graph(actors, 10 * actors, alpha=2.1, n_roots=actors // 1000, cap=100000)
+    h = hip_mod.ShadowGraph(vertex_capacity=actors, edge_capacity=12 * actors)
+    o = oracle_mod.OracleGraph()
+    for b in w.batches(1 << 20):
+        h.merge_entries(b)
+        o.merge_entries(b)
+    _same(h.trace(True), o.trace(True))
+    for k in range(3):
+        b = busy_wakeup(w, actors, actors // 10)
+        h.merge_entries(b.to_device())
+        o.merge_entries(b)
+        rh, ro = h.trace(True), o.trace(True)
+        _same(rh, ro)
+        assert rh.edges_scanned == ro.edges_scanned
+    assert ro.pseudo_roots > 0.09 * ro.n_live
+    assert h.total_actors_seen() == o.total_actors_seen()
+
+
 @pytest.mark.parametrize("actors,edges,batch,wakeups", [
-    (100_000, 1_000_000, 10_000, 6),       # C1: the reference's CPU-runnable case
-    (1_000_000, 10_000_000, 100_000, 2),   # C2 shape at 1/10 scale
+    (100_000, 1_000_000, 10_000, 6),       # power law at C1 size, quiet wakeups
+    (1_000_000, 10_000_000, 100_000, 2),   # C2 shape at 1/10 scale, quiet wakeups
 ])
 def test_power_law_wakeups_match_oracle(hip_mod, oracle_mod, actors, edges, batch, wakeups):
     w = world.World(seed=0x5EED + 1)
@@ -107,7 +170,7 @@ def test_c2_full_size_properties(hip_mod):
     r0 = h.trace(True)
     assert r0.n_live + len(r0.garbage) == seen          # every shadow is live or garbage
     for _ in range(2):
-        b = w.wakeup_batch(1_000_000)
+        b = busy_wakeup(w, 10_000_000, 1_000_000)
         h.merge_entries(b.to_device())
         pre = h.live_count()
         r = h.trace(True)

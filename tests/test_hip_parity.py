@@ -167,3 +167,33 @@ def test_empty_graph_and_empty_batches(hip_mod, oracle_mod):
     h.merge_deltas(DeltaBatch.from_rows([])); o.merge_deltas(DeltaBatch.from_rows([]))
     _same_trace(h.trace(True), o.trace(True))
     assert h.live_count() == 0
+
+
+def test_last_trace_survives_the_compaction_after_a_trace(hip_mod, oracle_mod):
+    """Two-phase trace: crgc_trace with no buffers, then
+    crgc_last_trace.  A trace that leaves dead slots outnumbering live ones
+    compacts the graph before it returns; the retained lists must survive it."""
+    import world
+    w = world.World(seed=0x5EED + 21)
+    # 1 live chain, 800 dead rings of 100: slot_top > 65536 and dead >> live
+    w.chain_graph(n_chains=1, chain_len=1000, n_sup_chains=0, sup_depth=0,
+                  n_rings=800, ring_len=100)
+    h, o = _pair(hip_mod, oracle_mod)
+    for b in w.batches(1 << 20):
+        h.merge_entries(b)
+        o.merge_entries(b)
+    r, ng, nk = h.trace_counts(True)          # no id buffers: counts only
+    ro = o.trace(True)
+    assert ng == len(ro.garbage) == 80_000 and nk == len(ro.kill)
+    assert h.live_count() == ro.n_live         # the compaction ran
+    g, k = h.last_trace()
+    assert set(g.tolist()) == ro.garbage_set() and len(g) == ng
+    assert set(k.tolist()) == ro.kill_set() and len(k) == nk
+    # and once more after a merge that grows the graph past its capacity
+    w.chain_graph(n_chains=1, chain_len=200_000, n_sup_chains=0, sup_depth=0, n_rings=0, ring_len=0)
+    for b in w.batches(1 << 20):
+        h.merge_entries(b)
+        o.merge_entries(b)
+    g2, k2 = h.last_trace()
+    assert set(g2.tolist()) == ro.garbage_set() and set(k2.tolist()) == ro.kill_set()
+    _same_trace(h.trace(True), o.trace(True))

@@ -275,3 +275,26 @@ def test_rccl_transport_single_rank(hip_mod, oracle_mod):
         h.close()
     finally:
         t.close()
+
+
+def test_c4_shape_eight_shards(sharded, oracle_mod):
+    """G = 8 logical shards (the 8-GPU layout of C4) on a scaled C2/C4-shaped
+    power-law graph with §8d wakeups (9 % busy, 1 % in flight), split batches:
+    bit-exact against the unsharded oracle at every wakeup."""
+    V = 200_000
+    w = world.World(seed=0x5EED + 4)
+    w.bulk_graph(V, 10 * V, alpha=2.1, n_roots=V // 1000, cap=100000)
+    h, o = sharded(8), oracle_mod.OracleGraph()
+    for b in w.batches(1 << 18):
+        h.merge_entries(b, split=True)
+        o.merge_entries(b)
+    _same(h.trace(True), o.trace(True))
+    for _ in range(3):
+        b = w.wakeup(V // 10, busy=V * 9 // 100, pending=V // 100)
+        h.merge_entries(b, split=True)
+        o.merge_entries(b)
+        rh = h.trace(True)
+        _same(rh, o.trace(True))
+        assert rh.rounds >= 2 and rh.ids_sent > 0  # marks crossed shards
+    assert h.export() == o.export()
+    assert h.total_actors_seen() == o.total_actors_seen()

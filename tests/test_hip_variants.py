@@ -2,8 +2,8 @@
 
 The level kernels read A/B switches per trace (CRGC_* in crgc_api.hip
 run_levels).  They change how the mark is computed — push or pull per level,
-the marked-word filter, check-before-store, the non-temporal edge stream, the
-pull walk, the narrow-frontier takeover — never what is marked.  Each variant
+the narrow-frontier takeover — never what is marked.  (Round 1's losing
+variants were removed from the product; profiles/r1h, r1n, r1r keep their A/B.)  Each variant
 replays the same seeded stream (a C1-sized power-law graph, then mutator
 wakeups) into a fresh graph and must match the oracle wakeup by wakeup.
 """
@@ -20,11 +20,6 @@ VARIANTS = [
     {"CRGC_PULL_CUR_DIV": "0"},           # direction from the previous frontier only
     {"CRGC_PULL_CUR_DIV": "1000000"},     # pull on every dense level with a frontier
     {"CRGC_PULL": "0"},                   # push only
-    {"CRGC_VIS_SKIP": "0"},               # always filter by the marked words
-    {"CRGC_VIS_SKIP": "1000000"},         # almost never filter
-    {"CRGC_MARK_CHECK": "0"},             # plain candidate stores
-    {"CRGC_EXPAND_NT": "0"},              # default-policy edge stream
-    {"CRGC_PULL_SEQ": "1"},               # one in-candidate list after another
     {"CRGC_TAIL": "0"},                   # no narrow-frontier takeover
     {"CRGC_TAIL_START": "1000000", "CRGC_TAIL_MAX": "64"},  # early takeover, frequent bails
 ]

@@ -43,3 +43,30 @@ def test_undo_of_matches_python_undo_log():
         for g in delta.deltas_from_entries(b.to_entries(), address=2):
             log.mergeDeltaGraph(g)
         assert _canon(world.undo_of(d, 2)) == _canon(log.to_batch())
+
+
+def test_c1_generator_has_the_stated_shape(oracle_mod):
+    """C1 (BASELINE.json config 1): ~1e6 refs over 1e5 actors, counts
+    1 / 2 / -1 at 90 / 8 / 2 %, 5 % dead components, and at every wakeup ~1 %
+    roots + 9 % busy + 1 % with mail in flight."""
+    from collections import Counter
+    V = 100_000
+    w = world.World(seed=0x5EED + 1)
+    w.set_mix(send=0.2, share=0.2, release=0.2, spawn=0.2, actions_per_msg=2.0)
+    w.uniform_graph(V, mean_acq=8.0, n_roots=V // 100, dead_frac=0.05)
+    o = oracle_mod.OracleGraph()
+    for b in w.batches(1 << 20):
+        o.merge_entries(b)
+    st = o.export()
+    n_edges = len(st.edges)
+    assert 0.9e6 < n_edges < 1.2e6
+    acq = Counter(c for (a, t), c in st.edges.items() if a != t)
+    tot = sum(acq.values())
+    assert acq[-1] / tot > 0.01 and acq[2] / tot > 0.05 and acq[1] / tot > 0.85
+    r = o.trace(True)
+    assert len(r.garbage) == V // 20 and len(r.kill) == V // 20
+    for _ in range(3):
+        o.merge_entries(w.wakeup(10_000, busy=V * 9 // 100, pending=V // 100))
+        r = o.trace(True)
+    assert w.n_busy() == V * 9 // 100
+    assert 0.09 * r.n_live < r.pseudo_roots < 0.13 * r.n_live

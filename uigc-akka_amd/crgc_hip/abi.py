@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 OK = 0
 E_INVAL = -1
@@ -120,6 +120,8 @@ class CrgcTraceStats(C.Structure):
         ("rounds", _U64),
         ("ids_sent", _U64),
         ("ms_exchange", C.c_double),
+        ("expand_launches", _U64),
+        ("expand_bytes", _U64),
     ]
 
 

@@ -352,6 +352,8 @@ class TraceResult:
     rounds: int = 1
     ids_sent: int = 0
     ms_exchange: float = 0.0
+    expand_launches: int = 0
+    expand_bytes: int = 0
 
     def garbage_set(self):
         return set(int(x) for x in self.garbage)

@@ -72,6 +72,10 @@ class ShadowGraph:
         self.DGS = delta_graph_size
         self.device = device
         self._pending: List[Entry] = []
+        # Device batches (torch tensors) whose merges may still be running on
+        # the graph's stream: held until the next call that synchronises it, so
+        # the caching allocator cannot hand their memory to a later copy.
+        self._inflight: list = []
 
     # -- lifecycle ------------------------------------------------------------
     def close(self):
@@ -107,14 +111,24 @@ class ShadowGraph:
             self._pending = []
             self.merge_entries(b)
 
+    def _hold(self, batch):
+        if batch.memory == abi.MEM_DEVICE:
+            self._inflight.append(batch)
+
+    def _synced(self):
+        """The graph's stream has drained: device batches may be freed."""
+        self._inflight.clear()
+
     def merge_entries(self, batch: EntryBatch):
         self._chk(self.lib.crgc_merge_entries(self.h, C.byref(batch.struct())),
                   "crgc_merge_entries")
+        self._hold(batch)
 
     def merge_deltas(self, batch: DeltaBatch):
         self.flush()
         self._chk(self.lib.crgc_merge_deltas(self.h, C.byref(batch.struct())),
                   "crgc_merge_deltas")
+        self._hold(batch)
 
     def merge_undo(self, log: UndoBatch):
         self.flush()
@@ -130,7 +144,8 @@ class ShadowGraph:
         return TraceResult(g, k, int(out.n_live), int(st.pseudo_roots), int(st.edges_scanned),
                            int(st.sup_edges), int(st.levels), int(st.launches), st.ms_mark,
                            st.ms_sweep, st.ms_total, st.ms_frontier, st.ms_tail, st.ms_expand,
-                           int(st.rounds), int(st.ids_sent), st.ms_exchange)
+                           int(st.rounds), int(st.ids_sent), st.ms_exchange,
+                           int(st.expand_launches), int(st.expand_bytes))
 
     def _trace_into(self, shouldKill, g, k):
         out = abi.CrgcTraceOut()
@@ -159,6 +174,7 @@ class ShadowGraph:
             out.garbage_ids, out.garbage_cap = _ptr(self._gbuf), len(self._gbuf)
             out.kill_ids, out.kill_cap = _ptr(self._kbuf), len(self._kbuf)
             rc = self.lib.crgc_last_trace(self.h, C.byref(out))
+        self._synced()
         self._chk(rc, "crgc_trace")
         ng, nk = int(out.n_garbage), int(out.n_kill)
         return self._result(out, self._gbuf[:ng], self._kbuf[:nk]), ng, nk
@@ -167,9 +183,23 @@ class ShadowGraph:
         """trace() without copying the id lists back (counts and timings only)."""
         self.flush()
         out = abi.CrgcTraceOut()
-        self._chk(self.lib.crgc_trace(self.h, int(bool(shouldKill)), C.byref(out)), "crgc_trace")
+        rc = self.lib.crgc_trace(self.h, int(bool(shouldKill)), C.byref(out))
+        self._synced()
+        self._chk(rc, "crgc_trace")
         e = np.zeros(0, np.uint64)
         return self._result(out, e, e), int(out.n_garbage), int(out.n_kill)
+
+    def last_trace(self):
+        """The retained lists of the last trace (crgc_last_trace), as a fresh
+        (garbage, kill) pair of arrays: the second phase of a two-phase trace."""
+        out = abi.CrgcTraceOut()
+        self._chk(self.lib.crgc_last_trace(self.h, C.byref(out)), "crgc_last_trace")
+        g = np.zeros(max(1, int(out.n_garbage)), np.uint64)
+        k = np.zeros(max(1, int(out.n_kill)), np.uint64)
+        out.garbage_ids, out.garbage_cap = _ptr(g), len(g)
+        out.kill_ids, out.kill_cap = _ptr(k), len(k)
+        self._chk(self.lib.crgc_last_trace(self.h, C.byref(out)), "crgc_last_trace")
+        return g[:int(out.n_garbage)], k[:int(out.n_kill)]
 
     # -- queries --------------------------------------------------------------
     def startWave(self) -> np.ndarray:
@@ -302,6 +332,7 @@ class UndoAccumulator:
     def fold_deltas(self, batch: DeltaBatch):
         ShadowGraph._chk(self.lib.crgc_undo_acc_fold_deltas(self.h, C.byref(batch.struct())),
                          "crgc_undo_acc_fold_deltas")
+        self.graph._hold(batch)
 
     mergeDeltaGraph = fold_deltas
 
@@ -424,7 +455,8 @@ class ShardedShadowGraph:
             max(r.ms_mark for r in rs), max(r.ms_sweep for r in rs), max(r.ms_total for r in rs),
             max(r.ms_frontier for r in rs), max(r.ms_tail for r in rs),
             max(r.ms_expand for r in rs), max(r.rounds for r in rs),
-            sum(r.ids_sent for r in rs), max(r.ms_exchange for r in rs))
+            sum(r.ids_sent for r in rs), max(r.ms_exchange for r in rs),
+            sum(r.expand_launches for r in rs), sum(r.expand_bytes for r in rs))
 
     def count_reachable_from(self, location: int) -> int:
         vals = self._all(lambda s: s.count_reachable_from(location))

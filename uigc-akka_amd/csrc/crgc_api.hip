@@ -45,8 +45,8 @@ void free_arrays(Arrays &a) {
   DevGraph &d = a.d;
   void *ps[] = {d.htab, d.vid, d.recv, d.flags, d.sup, d.adj, d.ecap, d.vseq, d.sseq,
                 d.enew, d.pool, d.etab, d.edelta, d.vis, d.front[0], d.front[1],
-                d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat,
-                d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill, d.fbits[0], d.fbits[1],
+                d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat, d.xbytes,
+                d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill,
                 d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.fx, d.tq, d.tl_buf, d.tl_tag,
                 d.xp_buf, d.xp_cnt, d.rq_buf, d.rq_cnt};
   for (void *p : ps)
@@ -106,12 +106,11 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   A(dmalloc(&d.qh_buf, d.qh_cap));
   A(dmalloc(&d.qn_tag, c.scap / BLK_SLOTS));
   A(dmalloc(&d.blkstat, (uint64_t)STAT_WG * 4));
+  A(dmalloc(&d.xbytes, (uint64_t)STAT_WG));
   A(dmalloc(&d.sweep_cnt, 2 * (c.scap / BLK_SLOTS)));
   A(dmalloc(&d.sweep_off, 2 * (c.scap / BLK_SLOTS)));
   A(dmalloc(&d.out_ids, c.scap));
   A(dmalloc(&d.out_kill, c.scap));
-  A(dmalloc(&d.fbits[0], c.scap / 32));
-  A(dmalloc(&d.fbits[1], c.scap / 32));
   d.rpcap = c.pcap;
   A(dmalloc(&d.nzdeg, c.scap));
   A(dmalloc(&d.radj, c.scap));
@@ -147,8 +146,6 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   hipMemsetAsync(d.front[1], 0, c.scap, s);
   hipMemsetAsync(d.dirty[0], 0, c.scap / BLK_SLOTS, s);
   hipMemsetAsync(d.dirty[1], 0, c.scap / BLK_SLOTS, s);
-  hipMemsetAsync(d.fbits[0], 0, c.scap / 8, s);
-  hipMemsetAsync(d.fbits[1], 0, c.scap / 8, s);
   hipMemsetAsync(d.nzdeg, 0, c.scap * 4, s);
   hipMemsetAsync(d.radj, 0, c.scap * 8, s);
   hipMemsetAsync(d.rcap, 0, c.scap * 4, s);
@@ -301,6 +298,21 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   hipMemsetAsync((char *)h->ctr + CTR_OFF(etab_used), 0, 8, h->stream);
   // src keeps a view of the old counters' bound via src_top (passed by value)
   hipError_t e = launch_rebuild(h->g.d, src_top, dst.d, map, nullptr, offs, scan_tmp, h->stream);
+  // The last trace's garbage / kill lists outlive the generation: crgc_last_trace
+  // may still copy them (two-phase trace, or a trace whose buffers were short).
+  // They can hold more ids than the compacted generation has slots.
+  if (e == hipSuccess && h->have_last) {
+    auto carry = [&](uint64_t *&dptr, const uint64_t *src, uint64_t n) -> hipError_t {
+      if (n > dst.caps.scap) {
+        hipFree(dptr);
+        dptr = nullptr;
+        if (hipError_t r = dmalloc(&dptr, n)) return r;
+      }
+      return n ? hipMemcpyAsync(dptr, src, n * 8, hipMemcpyDeviceToDevice, h->stream) : hipSuccess;
+    };
+    e = carry(dst.d.out_ids, h->g.d.out_ids, h->last_garbage);
+    if (e == hipSuccess) e = carry(dst.d.out_kill, h->g.d.out_kill, h->last_kill);
+  }
   if (e == hipSuccess) e = sync_counters(h);
   tmp.release();
   if (e != hipSuccess) {
@@ -350,6 +362,17 @@ const T *stage(crgc_graph *h, Carver &cv, const T *src, uint64_t n, uint32_t mem
   T *dst = cv.take<T>(n);
   hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyHostToDevice, h->stream);
   return dst;
+}
+
+// Host batches are read by stream-ordered copies; the ABI promises that the
+// caller's buffers are free again when the call returns (crgc.h), so a merge
+// that staged host memory waits for those copies (only: ev[3] is recorded
+// right after them, the kernels behind it keep running).
+hipError_t mark_staged(crgc_graph *h, uint32_t memory) {
+  return memory == CRGC_MEM_HOST ? hipEventRecord(h->ev[3], h->stream) : hipSuccess;
+}
+hipError_t wait_staged(crgc_graph *h, uint32_t memory) {
+  return memory == CRGC_MEM_HOST ? hipEventSynchronize(h->ev[3]) : hipSuccess;
 }
 
 int check_graph(crgc_graph *h) {
@@ -624,6 +647,7 @@ static int gather_batches(crgc_graph *h, const uint64_t *hdr, uint32_t K, const 
   if (h->x_pack.ensure(mine.total) != hipSuccess || h->x_pack_recv.ensure(tot) != hipSuccess)
     return CRGC_E_NOMEM;
   if (int rc = pack(h, mine, src, narr, memory, (char *)h->x_pack.ptr)) return rc;
+  if (memory == CRGC_MEM_HOST && narr) HIP_TRY(hipStreamSynchronize(h->stream));  // caller's buffers free on return
   if (int rc = h->tp->alltoallv(h->shard, h->x_pack.ptr, soff, sb, h->x_pack_recv.ptr, roff.data(), rb,
                                 h->stream)) {
     h->poisoned = true;
@@ -709,6 +733,7 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   a.u_off = stage(h, sc, b->updated_off, n + 1, b->memory);
   a.u_ref = stage(h, sc, b->updated_ref, U, b->memory);
   a.u_info = stage(h, sc, b->updated_info, U, b->memory);
+  HIP_TRY(mark_staged(h, b->memory));
   a.self_slot = wc.take<uint32_t>(n);
   a.spawn_slot = wc.take<uint32_t>(n * h->F);
   a.ct_slot = wc.take<uint32_t>(n * h->F);
@@ -725,6 +750,7 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   HIP_TRY(launch_entries(h->g.d, a, h->stream));
   if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, max_atoms, wc)) return rc;
   note_merge(h, ids, C + U);
+  HIP_TRY(wait_staged(h, b->memory));
   return CRGC_OK;
 }
 
@@ -951,8 +977,9 @@ static int delta_counts(crgc_graph *h, const crgc_delta_batch *b, uint64_t *nout
     if (b->out_off[0]) return CRGC_E_INVAL;
     *nout = b->out_off[n];
   } else {
-    uint32_t v = 0;
-    HIP_TRY(hipMemcpy(&v, b->out_off + n, 4, hipMemcpyDeviceToHost));
+    uint32_t v = 0;  // ordered behind whatever produced the batch on this stream
+    HIP_TRY(hipMemcpyAsync(&v, b->out_off + n, 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
     *nout = v;
   }
   if (*nout && (!b->out_target || !b->out_count)) return CRGC_E_INVAL;
@@ -984,6 +1011,7 @@ static int merge_deltas_one(crgc_graph *h, const crgc_delta_batch *b, uint64_t n
   a.out_off = stage(h, sc, b->out_off, n + 1, b->memory);
   a.out_target = stage(h, sc, b->out_target, nout, b->memory);
   a.out_count = stage(h, sc, b->out_count, nout, b->memory);
+  HIP_TRY(mark_staged(h, b->memory));
   a.self_slot = wc.take<uint32_t>(n);
   a.sup_slot = wc.take<uint32_t>(n);
   a.ot_slot = wc.take<uint32_t>(std::max<uint64_t>(nout, 1));
@@ -994,6 +1022,7 @@ static int merge_deltas_one(crgc_graph *h, const crgc_delta_batch *b, uint64_t n
   HIP_TRY(launch_deltas(h->g.d, a, nout, h->stream));
   if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, nout, wc)) return rc;
   note_merge(h, ids, nout);
+  HIP_TRY(wait_staged(h, b->memory));
   return CRGC_OK;
 }
 
@@ -1152,19 +1181,11 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
                       const std::function<hipError_t()> &after_chunk = nullptr) {
   LevelArgs la{};
   la.location = location;
-  // Tuning switches for A/B runs (results are identical either way).  Defaults
-  // from tools/ab_trace.py on the bench's C2 graph after 12 wakeups
-  // (profiles/r1n): candidate byte read before its store, the edge stream read
-  // non-temporal, no marked-word filter while < 1/16 of the slots is marked.
-  la.flags = LV_NT | LV_CHECK_BEFORE_STORE;
-  la.vis_skip_div = 16;
-  if (const char *m = getenv("CRGC_MARK_CHECK"))
-    la.flags = atoi(m) ? la.flags | LV_CHECK_BEFORE_STORE : la.flags & ~LV_CHECK_BEFORE_STORE;
-  if (const char *m = getenv("CRGC_MARK_BITS")) la.flags |= atoi(m) ? LV_BITMAP_FRONT : 0;
-  if (const char *m = getenv("CRGC_EXP8")) la.flags |= atoi(m) ? LV_EXP8 : 0;
-  if (const char *m = getenv("CRGC_EXPAND_NT")) la.flags = atoi(m) ? la.flags | LV_NT : la.flags & ~LV_NT;
-  if (const char *m = getenv("CRGC_PULL_SEQ")) la.flags |= atoi(m) ? LV_PULL_SEQ : 0;
-  if (const char *m = getenv("CRGC_VIS_SKIP")) la.vis_skip_div = (uint32_t)strtoul(m, nullptr, 10);
+  // Losing A/B variants of round 1 (atomicOr candidate bitmap, 8 edges per lane,
+  // sequential pull walk, plain candidate stores, default-policy edge stream,
+  // always-on marked-word filter) were removed; their records stay in
+  // profiles/r1h, r1n, r1r.
+  la.flags = 0;
   la.sparse_thresh = (uint32_t)std::max<uint64_t>(64, (top / BLK_SLOTS) / 4);
   // Direction optimisation: dense levels after a frontier of >= top/div shadows pull.
   uint64_t pull_div = 16;
@@ -1513,6 +1534,8 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   crgc_trace_stats st{};
   st.edges_scanned = c.edges_scanned;
   st.sup_edges = c.sup_edges;
+  st.expand_launches = lr.launches;
+  st.expand_bytes = c.expand_bytes;
   st.levels = lr.levels;
   st.launches = lr.launches;
   st.ms_mark = lr.ms;
@@ -1825,7 +1848,9 @@ int crgc_undo_acc_fold_deltas(crgc_undo_acc *u, const crgc_delta_batch *b) {
   a.out_off = stage(h, sc, b->out_off, n + 1, b->memory);
   a.out_target = stage(h, sc, b->out_target, nout, b->memory);
   a.out_count = stage(h, sc, b->out_count, nout, b->memory);
+  HIP_TRY(mark_staged(h, b->memory));
   HIP_TRY(launch_ua_fold_deltas(u->d, a, h->stream));
+  HIP_TRY(wait_staged(h, b->memory));
   u->ids_ub += n + nout;
   u->pairs_ub += nout;
   return CRGC_OK;
@@ -1844,7 +1869,8 @@ int crgc_undo_acc_fold_ingress(crgc_undo_acc *u, const crgc_undo_log *f) {
     if (f->created_off[0]) return CRGC_E_INVAL;
     nc32 = f->created_off[n];
   } else {
-    HIP_TRY(hipMemcpy(&nc32, f->created_off + n, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyAsync(&nc32, f->created_off + n, 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
   }
   const uint64_t nc = nc32;
   if (nc && (!f->created_target || !f->created_count)) return CRGC_E_INVAL;
@@ -1862,7 +1888,9 @@ int crgc_undo_acc_fold_ingress(crgc_undo_acc *u, const crgc_undo_log *f) {
   a.c_off = stage(h, sc, f->created_off, n + 1, f->memory);
   a.c_target = stage(h, sc, f->created_target, nc, f->memory);
   a.c_count = stage(h, sc, f->created_count, nc, f->memory);
+  HIP_TRY(mark_staged(h, f->memory));
   HIP_TRY(launch_ua_fold_fields(u->d, a, h->stream));
+  HIP_TRY(wait_staged(h, f->memory));
   u->ids_ub += n + nc;
   u->pairs_ub += nc;
   return CRGC_OK;

@@ -149,15 +149,10 @@ struct EdgeArgs {
   uint64_t *flips;     // [max_atoms] buckets of edges whose count changed sign
 };
 
-constexpr uint32_t LV_CHECK_BEFORE_STORE = 1;  // read the candidate byte before storing it
-constexpr uint32_t LV_BITMAP_FRONT = 2;        // candidates as a bitmap set by atomicOr
 constexpr uint32_t LV_PULL = 4;                // dense levels scan in-candidates (pull)
 constexpr uint32_t LV_TAIL = 8;                // narrow frontiers go to one workgroup (k_tail)
 constexpr uint32_t LV_INVESTIGATE = 16;        // set by launch_level: no supervisor edges
 constexpr uint32_t LV_ROOTS = 32;              // set by launch_level: the pseudo-root level
-constexpr uint32_t LV_EXP8 = 64;               // k_expand: 8 edges per lane per step (else 4)
-constexpr uint32_t LV_NT = 128;                // k_expand: edge stream read non-temporal
-constexpr uint32_t LV_PULL_SEQ = 256;          // pull: a thread's in-candidate lists one after another
 
 struct LevelArgs {
   int level;
@@ -168,7 +163,6 @@ struct LevelArgs {
   uint32_t tail_max;       // ... whose candidates number <= this, and bails above it
   uint32_t frontier_grid;  // workgroups of k_frontier (set by launch_level)
   uint32_t flags;          // LV_*
-  uint32_t vis_skip_div;   // push levels skip the marked-word filter while marked * div < slot_top
   uint32_t pull_cur_div;   // k_expand also pulls once the current frontier is >= slot_top / div
   uint16_t location;
 };

@@ -75,6 +75,7 @@ struct Counters {
   unsigned long long marked;
   unsigned long long edges_scanned;
   unsigned long long sup_edges;
+  unsigned long long expand_bytes;   // bytes k_expand read / wrote over the trace (k_trace_stats)
   unsigned long long n_garbage;
   unsigned long long n_kill;
   unsigned long long n_live;
@@ -148,12 +149,12 @@ struct DevGraph {
   uint32_t *vis;
   uint8_t *front[2];
   uint8_t *dirty[2];
-  uint32_t *fbits[2];  // candidate bitmaps (LV_BITMAP_FRONT variant)
   uint2 *qn_buf;     // per-block regions of light edge ranges {offset, degree}
   uint32_t *qn_tag;   // per block: (level+1) << 12 | number of light ranges
   uint2 *qh_buf;      // RANGE_MAX-edge pieces of hub segments
   uint64_t qn_cap, qh_cap;
   uint64_t *blkstat;  // STAT_WG x 4 per-workgroup statistics partials
+  uint64_t *xbytes;   // STAT_WG per-workgroup k_expand byte counts
   uint32_t *sweep_cnt;  // per block: garbage, kill counts
   uint64_t *sweep_off;  // per block: exclusive offsets of the above
   uint64_t *out_a;    // per-block regions: garbage slots (u32) / generic ids

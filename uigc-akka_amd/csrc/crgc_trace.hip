@@ -27,6 +27,10 @@ constexpr uint32_t RANGE_MAX = 256;  // longer segments (hubs) are cut into piec
 constexpr int FB = 4;               // k_frontier: chunks of 64 frontier shadows per load group
 constexpr uint32_t NO_SLOT = ~0u;
 constexpr uint32_t PULL_K = 4;      // pull: in-candidates per list per round
+// The marked-word filter in front of a candidate store is skipped while fewer
+// than 1/VIS_SKIP_DIV of the slots are marked (a stale byte is dropped by the
+// next k_frontier); profiles/r1n.
+constexpr uint64_t VIS_SKIP_DIV = 16;
 constexpr int STAT_FRONT = 0, STAT_SUP = 1, STAT_EDGES = 2, STAT_LIVE = 3;
 
 __device__ inline bool sparse_level(const Counters *c, int L, uint32_t thr) {
@@ -38,7 +42,7 @@ __device__ inline bool sparse_level(const Counters *c, int L, uint32_t thr) {
 // when the previous frontier was large; the level is then dense, so every
 // block of the slot range is scanned and `fx` is complete.
 __device__ inline bool pull_level(const Counters *c, int L, const LevelArgs &a) {
-  if (!(a.flags & LV_PULL) || (a.flags & LV_BITMAP_FRONT) || L < 1) return false;
+  if (!(a.flags & LV_PULL) || L < 1) return false;
   if (sparse_level(c, L, a.sparse_thresh) || sparse_level(c, L + 1, a.sparse_thresh)) return false;
   const uint64_t prev = c->ring[(L - 1) % LEVEL_RING];
   return a.pull_div ? prev * a.pull_div >= c->slot_top : prev >= a.pull_thresh;
@@ -48,7 +52,7 @@ __device__ inline bool pull_level(const Counters *c, int L, const LevelArgs &a) 
 // pull when the frontier it finds is large although the previous one was not
 // (the decision above is made before the level's own frontier is counted).
 __device__ inline bool fx_level(const Counters *c, int L, const LevelArgs &a) {
-  if (!(a.flags & LV_PULL) || (a.flags & LV_BITMAP_FRONT) || L < 1 || !a.pull_cur_div) return false;
+  if (!(a.flags & LV_PULL) || L < 1 || !a.pull_cur_div) return false;
   return !sparse_level(c, L, a.sparse_thresh) && !sparse_level(c, L + 1, a.sparse_thresh);
 }
 
@@ -64,25 +68,6 @@ __device__ inline bool listing_level(const Counters *c, int L, const LevelArgs &
   return sparse_level(c, L, a.sparse_thresh) || c->ring[(L - 1) % LEVEL_RING] <= a.tail_max;
 }
 
-
-__device__ inline void mark_target(const DevGraph &g, uint8_t *Fn, uint8_t *Dn, bool sp_next,
-                                   uint32_t t, bool check = false) {
-  const uint32_t w = g.vis[t >> 5];
-  if (!((w >> (t & 31)) & 1u)) {
-    if (!check || Fn[t] == 0) Fn[t] = 1;
-    if (sp_next && Dn[t >> 11] == 0) Dn[t >> 11] = 1;
-  }
-}
-
-// Bitmap variant of the candidate set: a plain (possibly stale) read filters,
-// a memory-side atomicOr sets.  Fbits is 1 bit per slot.
-__device__ inline void mark_target_bits(const DevGraph &g, uint32_t *Fbits, uint8_t *Dn,
-                                        bool sp_next, uint32_t t) {
-  const uint32_t bit = 1u << (t & 31);
-  if ((g.vis[t >> 5] | Fbits[t >> 5]) & bit) return;
-  atomicOr(&Fbits[t >> 5], bit);
-  if (sp_next && Dn[t >> 11] == 0) Dn[t >> 11] = 1;
-}
 
 // Workgroup reduction of one value per wave; thread 0 gets the sum.
 __device__ inline uint64_t block_sum4(uint64_t v) {
@@ -128,7 +113,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   uint8_t *Dn = g.dirty[(L + 1) & 1];
   unsigned long long *qh_cnt = &c->qh[L & 1];
   const uint32_t tag = (uint32_t)(L + 1) << 12;
-  const bool bitmode = a.flags & LV_BITMAP_FRONT;
   const bool pull = !ROOTS && pull_level(c, L, a);
   const bool write_fx = !ROOTS && (pull || fx_level(c, L, a));
   const bool listing = !ROOTS && listing_level(c, L, a);
@@ -165,11 +149,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
           m |= root ? (1u << j) : 0u;
         }
       }
-    } else if (bitmode) {
-      uint32_t *fw = g.fbits[L & 1] + (uint64_t)blk * 64 + lane;
-      const uint32_t bits = *fw;
-      if (bits) *fw = 0;
-      m = bits & ~word;
     } else {
       uint4 *fp = (uint4 *)(Fc + base);
       const uint4 x0 = fp[0], x1 = fp[1];
@@ -256,7 +235,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
           sp[b] = NO_SLOT;
         }
         if (sp[b] >= 0xFFFFFFF0u) sp[b] = NO_SLOT;
-        sw[b] = (sp[b] != NO_SLOT && !bitmode) ? g.vis[sp[b] >> 5] : ~0u;
+        sw[b] = sp[b] != NO_SLOT ? g.vis[sp[b] >> 5] : ~0u;
       }
 #pragma unroll
       for (int b = 0; b < FB; ++b) {
@@ -270,9 +249,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         if (sp[b] != NO_SLOT) {
           n_sup++;
           const uint32_t s = sp[b];
-          if (bitmode) {
-            mark_target_bits(g, g.fbits[(L + 1) & 1], Dn, sp_next, s);
-          } else if (!((sw[b] >> (s & 31)) & 1u)) {
+          if (!((sw[b] >> (s & 31)) & 1u)) {
             Fn[s] = 1;
             if (sp_next && Dn[s >> 11] == 0) Dn[s >> 11] = 1;
           }
@@ -313,8 +290,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
 // group of edges instead of two per edge (a byte store may alias any load, so
 // per-edge marking would serialise them).
 template <int U>
-__device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn, bool sp_next, bool check,
-                                    const uint64_t (&ed)[U], uint32_t *Fbits, bool skipvis) {
+__device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn, bool sp_next,
+                                    const uint64_t (&ed)[U], bool skipvis, uint32_t &nb) {
   uint32_t t[U];
   bool go[U];
 #pragma unroll
@@ -322,25 +299,24 @@ __device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn,
     go[u] = edge_count(ed[u]) > 0;
     t[u] = edge_target(ed[u]);
   }
-  if (Fbits) {
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (go[u]) mark_target_bits(g, Fbits, Dn, sp_next, t[u]);
-    return;
-  }
   if (!skipvis) {  // early levels mark few shadows: a store costs less than the filter
     uint32_t w[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) w[u] = go[u] ? g.vis[t[u] >> 5] : ~0u;
+    for (int u = 0; u < U; ++u) {
+      w[u] = go[u] ? g.vis[t[u] >> 5] : ~0u;
+      nb += go[u] ? 4 : 0;
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) go[u] = !((w[u] >> (t[u] & 31)) & 1u);
   }
   uint8_t fb[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) fb[u] = (go[u] && check) ? Fn[t[u]] : 0;
+  for (int u = 0; u < U; ++u) fb[u] = go[u] ? Fn[t[u]] : 0;  // read before the store: most are set
 #pragma unroll
-  for (int u = 0; u < U; ++u)
+  for (int u = 0; u < U; ++u) {
+    nb += go[u] ? (fb[u] == 0 ? 2 : 1) : 0;
     if (go[u] && fb[u] == 0) Fn[t[u]] = 1;
+  }
   if (sp_next) {
     uint8_t db[U];
 #pragma unroll
@@ -356,14 +332,26 @@ __device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn,
 // per step (degree scan + binary search in LDS assigns edges to lanes) or one
 // hub piece per step, U independent edge loads per lane.
 // ---------------------------------------------------------------------------
-template <bool NT>
-__device__ inline uint64_t pool_load(const uint64_t *p) {
-  if (NT) return __builtin_nontemporal_load(p);
-  return *p;
+// The edge stream is read once per level: non-temporal, so it does not evict
+// the marked words and candidate bytes the level keeps re-reading.
+__device__ inline uint64_t pool_load(const uint64_t *p) { return __builtin_nontemporal_load(p); }
+
+constexpr int EXPAND_U = 4;  // independent edge loads per lane per step
+
+// The workgroup's byte count (2x, per thread) into its partial: one add per
+// workgroup, after every wave of it is done.
+__device__ inline void expand_bytes_out(const DevGraph &g, uint32_t nb2) {
+  __shared__ unsigned long long s_nb;
+  if (threadIdx.x == 0) s_nb = 0;
+  __syncthreads();
+  const uint32_t w = wave_sum(nb2);
+  if (lane_id() == 0 && w) atomicAdd(&s_nb, (unsigned long long)w);
+  __syncthreads();
+  if (threadIdx.x == 0) g.xbytes[blockIdx.x] += s_nb / 2;
 }
 
-template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
+  constexpr int U = EXPAND_U;
   __shared__ uint32_t s_start[4][65];
   __shared__ uint32_t s_off[4][64];
   Counters *c = g.ctr;
@@ -372,8 +360,6 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   if (L > 0 && c->ring[(L - 1) % LEVEL_RING] == 0) return;  // nothing was found this level
   const uint64_t nh = min(c->qh[L & 1], (unsigned long long)g.qh_cap);
   const bool sp_next = sparse_level(c, L + 1, a.sparse_thresh);
-  const bool check = a.flags & LV_CHECK_BEFORE_STORE;
-  uint32_t *Fbits = (a.flags & LV_BITMAP_FRONT) ? g.fbits[(L + 1) & 1] : nullptr;
   uint8_t *Fn = g.front[(L + 1) & 1];
   uint8_t *Dn = g.dirty[(L + 1) & 1];
   const int wv = threadIdx.x >> 6;
@@ -384,7 +370,10 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
   // A candidate byte stored for an already-marked target is dropped by the next
   // k_frontier (bits & ~vis), so the filter is an optimisation only.
-  const bool skipvis = !Fbits && a.vis_skip_div && c->marked * a.vis_skip_div < c->slot_top;
+  const bool skipvis = c->marked * VIS_SKIP_DIV < c->slot_top;
+  // Bytes this launch reads and writes, by element width (the roofline
+  // numerator): twice the count, so 8.5-B items stay integral.
+  uint32_t nb2 = 0;
 
   if (pull_now(c, L, a)) {
     // Pull: each unmarked, not-yet-found shadow looks for an expandable
@@ -399,6 +388,7 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
       const uint32_t fl = *(const uint32_t *)(g.flags + v0);
       const uint32_t cand = *(const uint32_t *)(Fn + v0);
       const uint32_t vb = (g.vis[v0 >> 5] >> (v0 & 31)) & 0xFu;
+      nb2 += 17;  // flags + candidate bytes (4 + 4 B) + an eighth of a marked word
       uint32_t todo = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -409,30 +399,11 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
       const uint4 r23 = *(const uint4 *)(g.radj + v0 + 2);
       const uint32_t ro[4] = {r01.x, r01.z, r23.x, r23.z};
       const uint32_t rl[4] = {r01.y, r01.w, r23.y, r23.w};
+      nb2 += 64;  // four in-candidate ranges
       // The thread's (up to) 4 lists are walked together, PULL_K candidates of
       // each per round: one round trip for the candidates, one for their
       // frontier bits, until every list has a hit or is exhausted.
       uint32_t found = 0, live = todo, pos = 0;
-      if (a.flags & LV_PULL_SEQ) {  // A/B: one list after another
-        live = 0;
-        for (int j = 0; j < 4; ++j) {
-          if (!((todo >> j) & 1u)) continue;
-          const uint32_t *rp = g.rpool + ro[j];
-          const uint32_t n = rl[j];
-          bool hit = false;
-          for (uint32_t i = 0; i < n && !hit; i += 4) {
-            uint32_t uu[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) uu[k] = i + k < n ? rp[i + k] : 0u;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const uint32_t sl = uu[k] & ~RC_POS;
-              if ((uu[k] & RC_POS) && ((g.fx[sl >> 5] >> (sl & 31)) & 1u)) hit = true;
-            }
-          }
-          if (hit) found |= 1u << (8 * j);
-        }
-      }
       while (live) {
         uint32_t u[4][PULL_K];
 #pragma unroll
@@ -447,6 +418,7 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
           for (int k = 0; k < PULL_K; ++k) {
             const uint32_t sl = u[j][k] & ~RC_POS;
             w[j][k] = (u[j][k] & RC_POS) ? g.fx[sl >> 5] >> (sl & 31) : 0u;  // 0: no RC_POS
+            nb2 += (((live >> j) & 1u) && pos + k < rl[j] ? 8 : 0) + ((u[j][k] & RC_POS) ? 8 : 0);
           }
         pos += PULL_K;
 #pragma unroll
@@ -459,7 +431,9 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
         }
       }
       if (found) *(uint32_t *)(Fn + v0) = cand | found;
+      nb2 += found ? 8 : 0;
     }
+    expand_bytes_out(g, nb2);
     return;
   }
 
@@ -469,11 +443,13 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
     const uint64_t b = cid % nblk;
     const uint32_t k = (uint32_t)(cid / nblk);
     const uint32_t t = g.qn_tag[b];
+    nb2 += lane == 0 ? 8 : 0;
     if ((t >> 12) != want) continue;
     const uint32_t cnt = t & 0xFFFu;
     if (cnt <= k * 64) continue;
     const uint32_t qi = k * 64 + lane;
     const uint2 r = qi < cnt ? g.qn_buf[b * BLK_SLOTS + qi] : make_uint2(0, 0);
+    nb2 += qi < cnt ? 16 : 0;
     const uint32_t incl = wave_incl_scan(r.y);
     const uint32_t dtot = __shfl(incl, 63);
     s_start[wv][lane] = incl - r.y;
@@ -492,26 +468,34 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
             if (s_start[wv][mid] <= e) lo = mid;
             else hi = mid - 1;
           }
-          ed[u] = pool_load<NT>(&g.pool[(uint64_t)s_off[wv][lo] + (e - s_start[wv][lo])]);
+          ed[u] = pool_load(&g.pool[(uint64_t)s_off[wv][lo] + (e - s_start[wv][lo])]);
+          nb2 += 16;
         }
       }
-      expand_edges(g, Fn, Dn, sp_next, check, ed, Fbits, skipvis);
+      uint32_t nb = 0;
+      expand_edges(g, Fn, Dn, sp_next, ed, skipvis, nb);
+      nb2 += 2 * nb;
     }
     wave_lds_fence();
   }
   // hub pieces: one per step
   for (uint64_t hi = gw; hi < nh; hi += nw) {
     const uint2 r = g.qh_buf[hi];
+    nb2 += lane == 0 ? 16 : 0;
     for (uint32_t e0 = 0; e0 < r.y; e0 += 64 * U) {
       uint64_t ed[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t e = e0 + u * 64 + lane;
-        ed[u] = e < r.y ? pool_load<NT>(&g.pool[(uint64_t)r.x + e]) : 0;
+        ed[u] = e < r.y ? pool_load(&g.pool[(uint64_t)r.x + e]) : 0;
+        nb2 += e < r.y ? 16 : 0;
       }
-      expand_edges(g, Fn, Dn, sp_next, check, ed, Fbits, skipvis);
+      uint32_t nb = 0;
+      expand_edges(g, Fn, Dn, sp_next, ed, skipvis, nb);
+      nb2 += 2 * nb;
     }
   }
+  expand_bytes_out(g, nb2);
 }
 
 
@@ -863,9 +847,7 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
   auto expand = [&](auto kern) {
     hipExtLaunchKernelGGL(kern, dim3(STAT_WG), dim3(256), 0, s, e[4], e[5], 0, g, a);
   };
-  if (a.flags & LV_EXP8) expand(k_expand<8, false>);
-  else if (a.flags & LV_NT) expand(k_expand<4, true>);
-  else expand(k_expand<4, false>);
+  expand(k_expand);
   return hipGetLastError();
 }
 
@@ -884,6 +866,7 @@ __global__ __launch_bounds__(256) void k_trace_reset(DevGraph g, uint64_t nblk, 
     if (g.xp_cnt) g.xp_cnt[i] = 0;
   }
   for (uint64_t i = t0; i < (uint64_t)STAT_WG * 4; i += stride) g.blkstat[i] = 0;
+  for (uint64_t i = t0; i < (uint64_t)STAT_WG; i += stride) g.xbytes[i] = 0;
   unsigned long long *cw = reinterpret_cast<unsigned long long *>(g.ctr) + ctr_from;
   for (uint64_t i = t0; i < ctr_words; i += stride) cw[i] = 0;
 }
@@ -899,24 +882,29 @@ hipError_t launch_trace_reset(const DevGraph &g, uint64_t nblk, uint32_t ctr_fro
 __global__ __launch_bounds__(256) void k_trace_stats(DevGraph g) {
   __shared__ uint64_t red[2][256];
   if (!g.ctr->mark_done) return;  // enqueued behind a level chunk that did not finish the mark
-  uint64_t su = 0, ed = 0;
+  __shared__ uint64_t red_x[256];
+  uint64_t su = 0, ed = 0, xb = 0;
   for (uint32_t b = threadIdx.x; b < STAT_WG; b += 256) {
     su += g.blkstat[b * 4 + STAT_SUP];
     ed += g.blkstat[b * 4 + STAT_EDGES];
+    xb += g.xbytes[b];
   }
   red[0][threadIdx.x] = su;
   red[1][threadIdx.x] = ed;
+  red_x[threadIdx.x] = xb;
   __syncthreads();
   for (int k = 128; k > 0; k >>= 1) {
     if (threadIdx.x < k) {
       red[0][threadIdx.x] += red[0][threadIdx.x + k];
       red[1][threadIdx.x] += red[1][threadIdx.x + k];
+      red_x[threadIdx.x] += red_x[threadIdx.x + k];
     }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
     g.ctr->sup_edges = red[0][0];
     g.ctr->edges_scanned = red[1][0];
+    g.ctr->expand_bytes = red_x[0];
   }
 }
 

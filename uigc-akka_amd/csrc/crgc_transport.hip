@@ -26,7 +26,7 @@ int LocalTransport::barrier() {
     cv.notify_all();
     return CRGC_OK;
   }
-  if (!cv.wait_for(lk, std::chrono::seconds(300), [&] { return generation != gen || broken; })) {
+  if (!cv.wait_for(lk, std::chrono::seconds(wait_s), [&] { return generation != gen || broken; })) {
     broken = true;
     cv.notify_all();
   }
@@ -85,16 +85,20 @@ struct RcclTransport final : crgc_transport {
                        hipMemcpyDeviceToDevice, s) != hipSuccess)
       return CRGC_E_DEVICE;
     if (ncclGroupStart() != ncclSuccess) return CRGC_E_DEVICE;
-    for (uint32_t r = 0; r < n_shards; ++r) {
+    // A failed send / recv still closes the group: a later collective must not
+    // run inside a dangling one.
+    bool ok = true;
+    for (uint32_t r = 0; r < n_shards && ok; ++r) {
       if (r == rank) continue;
       if (sbytes[r] && ncclSend((const char *)send + soff[r], sbytes[r], ncclUint8, (int)r, comm, s) !=
                            ncclSuccess)
-        return CRGC_E_DEVICE;
-      if (rbytes[r] &&
+        ok = false;
+      if (ok && rbytes[r] &&
           ncclRecv((char *)recv + roff[r], rbytes[r], ncclUint8, (int)r, comm, s) != ncclSuccess)
-        return CRGC_E_DEVICE;
+        ok = false;
     }
-    return ncclGroupEnd() == ncclSuccess ? CRGC_OK : CRGC_E_DEVICE;
+    const bool closed = ncclGroupEnd() == ncclSuccess;
+    return ok && closed ? CRGC_OK : CRGC_E_DEVICE;
   }
 };
 

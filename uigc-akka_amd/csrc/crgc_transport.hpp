@@ -16,7 +16,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstddef>
 #include <cstdint>
 #include <mutex>
@@ -51,7 +53,14 @@ struct LocalTransport final : crgc_transport {
   bool broken = false;
   Post post[TRANSPORT_MAX_SHARDS];
 
-  explicit LocalTransport(uint32_t g) { n_shards = g; }
+  // A shard that never arrives (its caller failed before the collective)
+  // breaks the transport after wait_s seconds (CRGC_LOCAL_BARRIER_S, default 60).
+  long wait_s = 60;
+
+  explicit LocalTransport(uint32_t g) {
+    n_shards = g;
+    if (const char *e = getenv("CRGC_LOCAL_BARRIER_S")) wait_s = std::max(1L, atol(e));
+  }
   bool accepts(uint32_t shard, int) const override { return shard < n_shards; }
   int barrier();
   int allgather(uint32_t shard, const void *send, void *recv, size_t bytes, hipStream_t s) override;

@@ -14,6 +14,13 @@
 //                   supervisor chains, dead rings and dead chains.
 //  * wl_simulate    steady state: actors with mail take turns (receive, then
 //                   send / share / release / spawn), RandomSpec-style.
+//  * wl_uniform_graph  C1 shape: uniform acquaintances, counts
+//                   1 / 2 / -1, planted dead components.
+//  * wl_wakeup      one wakeup's batch with turns in flight at its cut: a
+//                   target share of the actors busy (mid-turn, last flush
+//                   isBusy = true) and a target share with undelivered mail
+//                   (receive count not yet flushed), as LocalGC sees a running
+//                   system when its timer drains the queue.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -48,6 +55,9 @@ struct Actor {
   uint32_t mailbox = 0;
   bool root = false;
   bool ready = false;
+  bool busy = false;       // mid-turn across a wakeup boundary (wl_wakeup)
+  uint32_t busy_at = 0;    // index in wl_world::busy
+  float budget_left = 0;   // actions of the turn still to do
   std::vector<uint32_t> held;   // refob indices this actor holds
   std::vector<uint32_t> inbox;  // refobs carried by pending messages
 };
@@ -94,6 +104,7 @@ struct wl_world {
   std::vector<uint32_t> free_refobs;
   std::vector<uint32_t> roots;
   std::vector<uint32_t> ready;  // actors with mail
+  std::vector<uint32_t> busy;   // actors mid-turn (wl_wakeup)
   State st;
   // queued entries (struct of arrays, appended in flush order)
   std::vector<uint64_t> q_self;
@@ -180,7 +191,7 @@ static void deliver(wl_world *w, uint32_t target, int carried) {
   Actor &t = w->actors[target];
   t.mailbox++;
   if (carried >= 0) t.inbox.push_back((uint32_t)carried);
-  if (!t.ready) {
+  if (!t.ready && !t.busy) {  // a busy actor reads it when its turn goes on
     t.ready = true;
     w->ready.push_back(target);
   }
@@ -459,6 +470,222 @@ void wl_simulate(wl_world *w, uint64_t n_entries) {
     turn(w, a);
   }
 }
+
+// C1 shape (BASELINE.json config 1): n_roots roots, a spawn tree
+// (parent uniform among earlier actors), Poisson(mean_acq) acquaintances per
+// live actor with uniform targets whose counts are 1 (90 %), 2 (8 %: two
+// created refs) or -1 (2 %: a release whose creation is still unflushed by a
+// busy creator), and dead components holding dead_frac of the actors: members
+// spawned by a live actor that released them at once, linked in a cycle plus
+// Poisson(2) extra internal refs each — unreachable, not pseudo-roots, killed
+// (their supervisor is live).
+static uint64_t poisson(Rng &g, double mean) {
+  // Knuth, in chunks of 16 so exp() never underflows
+  uint64_t k = 0;
+  while (mean > 0) {
+    const double m = mean > 16 ? 16 : mean;
+    mean -= m;
+    const double L = std::exp(-m);
+    double p = 1.0;
+    for (;;) {
+      p *= g.uni();
+      if (p <= L) break;
+      ++k;
+    }
+  }
+  return k;
+}
+
+void wl_uniform_graph(wl_world *w, uint64_t n_actors, double mean_acq, uint32_t n_roots, double dead_frac) {
+  Rng &g = w->rng;
+  const uint64_t base = w->actors.size();
+  const uint64_t n_dead = (uint64_t)(dead_frac * (double)n_actors);
+  const uint64_t n_live = n_actors - n_dead;
+  w->actors.reserve(base + n_actors);
+  for (uint64_t i = 0; i < n_actors; ++i) new_actor(w);
+  State s;
+  s.F = w->F;
+  for (uint32_t r = 0; r < n_roots && r < n_live; ++r) {
+    const uint32_t a = (uint32_t)(base + r);
+    w->actors[a].root = true;
+    w->roots.push_back(a);
+    s.created.push_back({a, a});
+    flush(w, a, s, false);
+  }
+  auto spawn = [&](uint32_t p, uint32_t c) {
+    State ps;
+    ps.F = w->F;
+    ps.spawned.push_back(c);
+    flush(w, p, ps, false);
+    s.created.push_back({c, c});
+    s.created.push_back({p, c});
+    flush(w, c, s, false);
+  };
+  for (uint64_t i = n_roots; i < n_live; ++i) {
+    const uint32_t c = (uint32_t)(base + i);
+    const uint32_t p = (uint32_t)(base + (i < 4 * (uint64_t)n_roots ? g.below(n_roots) : g.below(i)));
+    spawn(p, c);
+    w->actors[p].held.push_back(new_refob(w, c));
+  }
+  for (uint64_t i = 0; i < n_live; ++i) {
+    const uint32_t a = (uint32_t)(base + i);
+    const uint64_t k = poisson(g, mean_acq);
+    for (uint64_t j = 0; j < k; ++j) {
+      const uint32_t t = (uint32_t)(base + g.below(n_live));
+      const double u = g.uni();
+      if (u < 0.98) {  // count 1, or 2 (two created refs)
+        const int copies = u < 0.90 ? 1 : 2;
+        for (int c = 0; c < copies; ++c) {
+          if (s.created.size() >= w->F) flush(w, a, s, false);
+          s.created.push_back({a, t});
+          w->actors[a].held.push_back(new_refob(w, t));
+        }
+      } else {  // count -1: the owner's release of a ref whose creation is unflushed
+        if (!s.created.empty() || !s.updated.empty()) flush(w, a, s, false);
+        const uint32_t ro = new_refob(w, t);
+        w->refobs[ro].info = 1;
+        w->refobs[ro].recorded = 1;
+        s.updated.push_back(ro);
+        flush(w, a, s, false);
+      }
+    }
+    if (!s.created.empty()) flush(w, a, s, false);
+  }
+  // dead components
+  uint64_t next = n_live;
+  while (next < n_actors) {
+    const uint64_t size = std::min<uint64_t>(n_actors - next, 2 + g.below(19));
+    const uint32_t p = (uint32_t)(base + g.below(n_live));
+    std::vector<uint32_t> comp;
+    for (uint64_t k = 0; k < size; ++k) comp.push_back((uint32_t)(base + next + k));
+    next += size;
+    State ps;
+    ps.F = w->F;
+    for (uint32_t c : comp) {
+      spawn(p, c);
+      const uint32_t ro = new_refob(w, c);  // ... and released at once
+      w->refobs[ro].info = 1;
+      w->refobs[ro].recorded = 1;
+      if (ps.updated.size() >= w->F) flush(w, p, ps, false);
+      ps.updated.push_back(ro);
+    }
+    flush(w, p, ps, false);
+    for (uint64_t k = 0; k < size; ++k) {
+      const uint32_t a = comp[k];
+      const uint64_t extra = poisson(g, 2.0);
+      std::vector<uint32_t> tg{comp[(k + 1) % size]};
+      for (uint64_t e = 0; e < extra; ++e) tg.push_back(comp[g.below(size)]);
+      for (uint32_t t : tg) {
+        if (s.created.size() >= w->F) flush(w, a, s, false);
+        s.created.push_back({a, t});
+        w->actors[a].held.push_back(new_refob(w, t));
+      }
+      flush(w, a, s, false);
+    }
+  }
+}
+
+// ---- a wakeup with turns in flight at its cut (wl_wakeup) --------------------
+// A busy turn starts like a turn (receive the mailbox, act on part of the
+// budget), flushes with isBusy = true (CRGC.scala:215-216 forced flush / a turn
+// running when LocalGC drains the queue) and stays open across the cut; it
+// finishes in a later wakeup (mail that arrived meanwhile, the rest of the
+// budget, the on-block flush with isBusy = false).
+static void busy_remove(wl_world *w, uint32_t a) {
+  Actor &x = w->actors[a];
+  const uint32_t i = x.busy_at, last = w->busy.back();
+  w->busy[i] = last;
+  w->actors[last].busy_at = i;
+  w->busy.pop_back();
+  x.busy = false;
+}
+
+static void run_actions(wl_world *w, uint32_t me, double budget) {
+  while (budget > 0) {
+    if (budget >= 1 || w->rng.uni() < budget) act(w, me);
+    budget -= 1;
+  }
+}
+
+static uint32_t take_mail(wl_world *w, uint32_t me) {
+  Actor &x = w->actors[me];
+  const uint32_t msgs = x.mailbox;
+  x.mailbox = 0;
+  std::vector<uint32_t> inbox;
+  inbox.swap(x.inbox);
+  for (uint32_t m = 0; m < msgs; ++m) {
+    if (w->st.recv >= 32767) flush(w, me, w->st, true);  // onMessageImpl
+    w->st.recv++;
+  }
+  for (uint32_t r : inbox) w->actors[me].held.push_back(r);
+  return msgs;
+}
+
+static void busy_start(wl_world *w, uint32_t me, double apm) {
+  Actor &x = w->actors[me];
+  x.ready = false;
+  x.busy = true;  // before acting: a self-message must not queue it as ready
+  x.busy_at = (uint32_t)w->busy.size();
+  w->busy.push_back(me);
+  const double budget = take_mail(w, me) * apm;
+  const double now = std::ceil(budget * 0.75);
+  run_actions(w, me, now);
+  flush(w, me, w->st, true);
+  w->actors[me].budget_left = (float)(budget - now);  // act() may grow `actors`
+}
+
+static void busy_finish(wl_world *w, uint32_t me, double apm) {
+  busy_remove(w, me);
+  const double budget = w->actors[me].budget_left + take_mail(w, me) * apm;
+  w->actors[me].budget_left = 0;
+  run_actions(w, me, budget);
+  flush(w, me, w->st, false);
+}
+
+// Queue >= n_entries more entries so that, at the cut, about busy_target
+// actors are mid-turn and about pending_target have undelivered mail.  The
+// actions per received message adapt (hi while fewer than pending_target
+// actors have mail, lo above it), which holds the number of actors with mail
+// near the target without external messages (the reference's RandomSpec
+// drives its actors from one root timer at 1 ms; at 1e5-1e7 actors a fixed
+// rate would not keep a tenth of them busy).
+void wl_wakeup(wl_world *w, uint64_t n_entries, uint64_t busy_target, uint64_t pending_target, double apm_lo,
+               double apm_hi) {
+  const uint64_t goal = w->n_entries_emitted + n_entries;
+  // a quarter of the open turns end first (a busy turn spans ~4 wakeups),
+  // at most 40 % of the batch
+  uint64_t nf = std::min<uint64_t>(w->busy.size() / 4, n_entries * 2 / 5);
+  while (w->n_entries_emitted < goal) {
+    const double apm = w->ready.size() < pending_target ? apm_hi : apm_lo;
+    if (nf && !w->busy.empty()) {
+      --nf;
+      busy_finish(w, w->busy[w->rng.below(w->busy.size())], apm);
+      continue;
+    }
+    if (w->ready.empty()) {
+      if (w->roots.empty()) return;
+      const uint32_t r = w->roots[w->rng.below(w->roots.size())];
+      if (!w->actors[r].busy) deliver(w, r, -1);  // a root's timer tick
+      else busy_finish(w, r, apm);               // (a busy root reads it when it goes on)
+      continue;
+    }
+    const uint64_t k = w->rng.below(w->ready.size());
+    const uint32_t a = w->ready[k];
+    w->ready[k] = w->ready.back();
+    w->ready.pop_back();
+    if (w->busy.size() < busy_target) {
+      busy_start(w, a, apm);
+    } else {
+      const double save = w->actions_per_msg;
+      w->actions_per_msg = apm;
+      turn(w, a);
+      w->actions_per_msg = save;
+    }
+  }
+}
+
+uint64_t wl_n_busy(wl_world *w) { return w->busy.size(); }
+uint64_t wl_n_ready(wl_world *w) { return w->ready.size(); }
 
 uint64_t wl_queued(wl_world *w) { return w->q_self.size() - w->head; }
 uint64_t wl_n_actors(wl_world *w) { return w->actors.size(); }

@@ -1,4 +1,5 @@
 """ctypes wrapper of world.cpp: seeded synthetic CRGC entry streams (C1-C4)."""
+
 from __future__ import annotations
 
 import ctypes as C
@@ -52,7 +53,10 @@ def _load():
                                       C.c_uint32, C.c_uint64]
         lib.wl_chain_graph.argtypes = [C.c_void_p] + [C.c_uint32] * 6
         lib.wl_simulate.argtypes = [C.c_void_p, C.c_uint64]
-        for f in ("wl_queued", "wl_n_actors", "wl_n_refobs_held"):
+        lib.wl_uniform_graph.argtypes = [C.c_void_p, C.c_uint64, C.c_double, C.c_uint32, C.c_double]
+        lib.wl_wakeup.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_double,
+                                  C.c_double]
+        for f in ("wl_queued", "wl_n_actors", "wl_n_refobs_held", "wl_n_busy", "wl_n_ready"):
             getattr(lib, f).restype = C.c_uint64
             getattr(lib, f).argtypes = [C.c_void_p]
         lib.wl_take.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(WlBatch)]
@@ -104,6 +108,29 @@ class World:
 
     def simulate(self, n_entries):
         self.lib.wl_simulate(self.h, n_entries)
+
+    def uniform_graph(self, n_actors, mean_acq=8.0, n_roots=None, dead_frac=0.05):
+        """C1 shape: spawn tree, Poisson(mean_acq) uniform acquaintances
+        with counts 1 / 2 / -1 (90 / 8 / 2 %), dead components holding dead_frac."""
+        n_roots = n_roots if n_roots is not None else max(1, n_actors // 100)
+        self.lib.wl_uniform_graph(self.h, n_actors, mean_acq, n_roots, dead_frac)
+
+    def n_busy(self) -> int:
+        """Actors mid-turn (their last flushed entry says isBusy)."""
+        return self.lib.wl_n_busy(self.h)
+
+    def n_ready(self) -> int:
+        """Actors with undelivered mail."""
+        return self.lib.wl_n_ready(self.h)
+
+    def wakeup(self, n_entries, busy, pending, apm=(1.0, 3.0)) -> EntryBatch:
+        """One wakeup's batch of exactly n_entries with turns in flight at the cut:
+        about `busy` actors mid-turn (isBusy) and `pending` with undelivered mail
+        (wl_wakeup); apm = (lo, hi) actions per received message."""
+        need = n_entries - self.queued()
+        if need > 0:
+            self.lib.wl_wakeup(self.h, need, busy, pending, apm[0], apm[1])
+        return self.take(n_entries)
 
     def queued(self) -> int:
         return self.lib.wl_queued(self.h)
