@@ -17,8 +17,9 @@ ACTORS, EDGES, BATCH, WAKEUPS = 100_000, 1_000_000, 10_000, 3
 
 VARIANTS = [
     {},
-    {"CRGC_PULL_CUR_DIV": "0"},           # direction from the previous frontier only
-    {"CRGC_PULL_CUR_DIV": "1000000"},     # pull on every dense level with a frontier
+    {"CRGC_ALPHA": "0"},                  # round-1 rule: the current frontier's size
+    {"CRGC_ALPHA": "0", "CRGC_PULL_CUR_DIV": "0"},  # direction from the previous frontier only
+    {"CRGC_ALPHA": "1000000"},            # pull on every dense level, level 0 included
     {"CRGC_PULL": "0"},                   # push only
     {"CRGC_TAIL": "0"},                   # no narrow-frontier takeover
     {"CRGC_TAIL_START": "1000000", "CRGC_TAIL_MAX": "64"},  # early takeover, frequent bails

@@ -30,11 +30,11 @@ def main():
     import crgc_hip
     import world
     import bench
-    ns = argparse.Namespace(actors=args.actors, edges=args.edges, batch=1_000_000)
+    ns = argparse.Namespace(actors=args.actors, edges=args.edges, batch=1_000_000, workload="c2")
     stream = torch.cuda.Stream()
     w, g = bench.build_graph(crgc_hip, world, 0, 0, stream.cuda_stream, ns)  # bench's C2 graph
     for _ in range(args.wakeups):
-        b = w.wakeup_batch(1_000_000).to_device("cuda")
+        b = bench.wakeup_batches(w, ns, 1)[0].to_device("cuda")
         torch.cuda.synchronize()  # uploaded on torch's stream, merged on the graph's
         g.merge_entries(b)
         g.trace_counts(True)

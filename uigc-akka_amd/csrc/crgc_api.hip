@@ -491,20 +491,18 @@ void crgc_destroy(crgc_graph *h) {
 
 // Shared tail of every merge: the edge pipeline over the staged atoms.
 static int run_edges(crgc_graph *h, uint32_t *ao, uint32_t *at, int32_t *ad, uint64_t max_atoms,
-                     Carver &cv) {
+                     Carver &cv, const uint64_t *n_atoms_dev = nullptr) {
   if (max_atoms == 0) return CRGC_OK;
   EdgeArgs ea{};
   ea.max_atoms = max_atoms;
-  ea.n_atoms_dev = nullptr;
+  ea.n_atoms_dev = n_atoms_dev;
   ea.atom_o = ao;
   ea.atom_t = at;
   ea.atom_d = ad;
   ea.newlist = cv.take<uint64_t>(max_atoms);
   ea.rrank = cv.take<uint32_t>(max_atoms);
   ea.touched = cv.take<uint32_t>(max_atoms);
-  ea.reloc = cv.take<uint32_t>(max_atoms);
   ea.rtouched = cv.take<uint32_t>(max_atoms);
-  ea.rreloc = cv.take<uint32_t>(max_atoms);
   ea.flips = cv.take<uint64_t>(max_atoms);
   // n_touched, n_new_edges, n_rtouched, n_flips
   hipMemsetAsync((char *)h->ctr + CTR_OFF(n_touched), 0, 4 * 8, h->stream);
@@ -713,7 +711,7 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   const bool sh = h->tp;
   const size_t work_bytes =
       Carver::need({n * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4, sh ? n : 0,
-                    sh ? n * h->F * 8 : 0}) +
+                    sh ? n * h->F * 8 : 0, 8}) +
       edge_scratch(max_atoms);
   if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
     return CRGC_E_NOMEM;
@@ -746,9 +744,11 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   a.atom_o = wc.take<uint32_t>(max_atoms);
   a.atom_t = wc.take<uint32_t>(max_atoms);
   a.atom_d = wc.take<int32_t>(max_atoms);
+  a.n_atoms = wc.take<uint64_t>(1);
+  // atoms of entries refused for bad offsets stay zero (never applied)
   hipMemsetAsync(a.atom_d, 0, max_atoms * 4, h->stream);
   HIP_TRY(launch_entries(h->g.d, a, h->stream));
-  if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, max_atoms, wc)) return rc;
+  if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, max_atoms, wc, a.n_atoms)) return rc;
   note_merge(h, ids, C + U);
   HIP_TRY(wait_staged(h, b->memory));
   return CRGC_OK;
@@ -1197,6 +1197,12 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   la.pull_div = (uint32_t)pull_div;  // against the exact slot count, on the device
   la.pull_cur_div = 4;
   if (const char *m = getenv("CRGC_PULL_CUR_DIV")) la.pull_cur_div = (uint32_t)strtoul(m, nullptr, 10);
+  // Beamer's direction rule (alpha = 14, the paper's value); m_u from the edge
+  // keys the graph holds (an upper bound: keys whose count dropped to 0 stay
+  // until a rebuild).  CRGC_ALPHA=0: the round-1 frontier-size rule.
+  la.alpha = 14;
+  if (const char *m = getenv("CRGC_ALPHA")) la.alpha = (uint32_t)strtoul(m, nullptr, 10);
+  la.e_total = h->etab_used + h->atoms_since;
   la.pull_thresh = 0;
   // Test hooks: absolute thresholds (0 disables sparse levels entirely).
   if (const char *m = getenv("CRGC_PULL_THRESH")) {

@@ -92,6 +92,7 @@ struct EntryArgs {
   uint32_t *ct_slot;     // [n*F] created targets, resolved by k_ids
   uint32_t *co_slot;     // [n*F] created owners
   uint32_t *u_slot;      // [n*F] updated refs
+  uint64_t *n_atoms;     // out: C + U, the atoms k_entries_apply wrote (exact edge-pipeline count)
   uint32_t *atom_o;      // [2*n*F]: created atoms, then updated atoms
   uint32_t *atom_t;
   int32_t *atom_d;
@@ -143,9 +144,7 @@ struct EdgeArgs {
   uint64_t *newlist;   // [max_atoms] buckets of new edge keys
   uint32_t *rrank;     // [max_atoms] rank of each new key among its target's new candidates
   uint32_t *touched;   // [max_atoms] owners that got new edges
-  uint32_t *reloc;     // [max_atoms] new segment offset per touched owner
   uint32_t *rtouched;  // [max_atoms] targets that got new candidates
-  uint32_t *rreloc;    // [max_atoms] new candidate-segment offset per touched target
   uint64_t *flips;     // [max_atoms] buckets of edges whose count changed sign
 };
 
@@ -163,7 +162,9 @@ struct LevelArgs {
   uint32_t tail_max;       // ... whose candidates number <= this, and bails above it
   uint32_t frontier_grid;  // workgroups of k_frontier (set by launch_level)
   uint32_t flags;          // LV_*
-  uint32_t pull_cur_div;   // k_expand also pulls once the current frontier is >= slot_top / div
+  uint32_t pull_cur_div;   // alpha == 0: k_expand also pulls once the current frontier is >= slot_top / div
+  uint32_t alpha;          // Beamer: pull when alpha * m_f > m_u (0: the pull_cur_div rule)
+  uint64_t e_total;        // edge keys in the graph (m_u = e_total - explored edges)
   uint16_t location;
 };
 

@@ -76,6 +76,8 @@ struct Counters {
   unsigned long long edges_scanned;
   unsigned long long sup_edges;
   unsigned long long expand_bytes;   // bytes k_expand read / wrote over the trace (k_trace_stats)
+  unsigned long long mf_level;       // nonzero out-edges of the current level's expandable frontier
+  unsigned long long mf_sum;         // ... summed over the levels so far (Beamer's explored edges)
   unsigned long long n_garbage;
   unsigned long long n_kill;
   unsigned long long n_live;

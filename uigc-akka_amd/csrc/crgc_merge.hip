@@ -97,6 +97,10 @@ __global__ __launch_bounds__(256) void k_entries_apply(DevGraph g, EntryArgs a) 
   }
   const uint32_t me = ok ? a.self_slot[i] : SLOT_INVALID;
   if (!ok) a.self_slot[i] = SLOT_INVALID;
+  if (i == 0 && a.n_atoms) {  // atoms [0, C) created, [C, C + U) updated: the edge pipeline's exact count
+    const uint64_t C = min((uint64_t)a.c_off[a.n], cmax), U = min((uint64_t)a.u_off[a.n], cmax);
+    *a.n_atoms = C + U;
+  }
   const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
   const int16_t rc = a.recv[i];
   // Sharded graphs: every record is applied by the home shard of the shadow
@@ -354,12 +358,13 @@ hipError_t launch_undo_apply(const DevGraph &g, const UndoArgs &a, uint64_t slot
 //      get a memory-side atomic add on their pool count; keys new in this merge
 //      accumulate in edelta[bucket], take a rank among the owner's new edges and
 //      among the target's new reverse candidates.
-//   2. k_seg_plan:  owners (targets) whose forward (candidate) segment
-//      overflows get a new power-of-two segment, one atomic per wave.
-//   3. k_seg_move:  one wave per relocated segment copies it.
-//   4. k_edge_append: new edges written after the owner's old degree, the
+//   2. k_seg_grow:  owners (targets) whose forward (candidate) segment
+//      overflows get a new power-of-two segment (one atomic per workgroup)
+//      and are copied there; both directions in one launch.
+//   3. k_edge_append: new edges written after the owner's old degree, the
 //      owner appended to the target's candidate list.
-//   5. k_seg_finish: degrees advance, per-merge counters reset.
+//   4. k_edge_post: degrees advance, per-merge counters reset, candidate
+//      entries of sign-changed counts refreshed.
 // ---------------------------------------------------------------------------
 constexpr int EDGE_THREADS = 1024;
 
@@ -405,7 +410,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_edge_apply(DevGraph g, EdgeArg
     }
     // List appends, one atomic per list per workgroup.  Sign changes of
     // existing counts: their candidate entries are refreshed from the final
-    // count after the merge (k_edge_flip).
+    // count after the merge (k_edge_post).
     const bool first = ins && rank == 0, rfirst = ins && rrank == 0;
     const uint32_t cnt[5] = {ins, first, rfirst, flip, ins};
     unsigned long long at[5];
@@ -437,58 +442,38 @@ struct Seg {
   unsigned long long *top;
   const unsigned long long *ntouched;
   const uint32_t *touched;
-  uint32_t *reloc;
 };
 
+// Owners (targets) whose forward (candidate) segment overflows get a new
+// power-of-two segment and are copied there, in one pass: the pool allocation
+// is one atomic per workgroup (block_append); each lane tests one touched
+// owner, a segment of <= SEG_LANE_COPY entries is copied by its own lane,
+// longer ones by the whole wave one after another.  Both directions run in
+// one launch (the first half of the grid forward, the second reverse).
+constexpr uint32_t SEG_LANE_COPY = 8;
+constexpr int SEG_THREADS = 256;
+
 template <typename T>
-__global__ __launch_bounds__(EDGE_THREADS) void k_seg_plan(Seg<T> s, Counters *c) {
+__device__ inline void seg_grow(Seg<T> s, Counters *c, uint32_t blk, uint32_t nblk) {
   const uint64_t n = *s.ntouched;
-  const uint64_t stride = (uint64_t)gridDim.x * EDGE_THREADS;
   unsigned long long *const tops[1] = {s.top};
-  for (uint64_t base = (uint64_t)blockIdx.x * EDGE_THREADS; base < n; base += stride) {
+  const int lane = lane_id();
+  for (uint64_t base = (uint64_t)blk * SEG_THREADS; base < n; base += (uint64_t)nblk * SEG_THREADS) {
     const uint64_t i = base + threadIdx.x;
-    uint32_t want = 0;
-    if (i < n) {
-      const uint32_t o = s.touched[i];
-      const uint32_t need = s.adj[o].y + s.nnew[o];
-      if (need > s.cap[o]) want = seg_cap(need);
-    }
+    const uint32_t o = i < n ? s.touched[i] : 0;
+    const uint2 ad = i < n ? s.adj[o] : make_uint2(0, 0);
+    const uint32_t nn = i < n ? s.nnew[o] : 0;
+    const uint32_t need = ad.y + nn;
+    const uint32_t want = (i < n && need > s.cap[o]) ? seg_cap(need) : 0u;
     const uint32_t v[1] = {want};
     unsigned long long offs[1];
     block_append<1>(tops, v, offs);  // one pool allocation per workgroup
-    const unsigned long long off = offs[0];
-    if (i < n) {
-      uint32_t r = 0xFFFFFFFFu;  // no move
-      if (want) {
-        if (off + want > s.pcap) {
-          set_err(c, ERR_POOL_FULL);
-          r = 0xFFFFFFFEu;
-        } else {
-          r = (uint32_t)off;
-        }
-      }
-      s.reloc[i] = r;
+    uint32_t r = 0xFFFFFFFFu;        // no move
+    if (want) {
+      if (offs[0] + want > s.pcap) set_err(c, ERR_POOL_FULL);
+      else r = (uint32_t)offs[0];
     }
-  }
-}
-
-// Most touched owners keep their segment: each lane tests one owner's plan, a
-// segment of <= SEG_LANE_COPY entries is copied by its own lane, longer ones by
-// the whole wave one after another (a wave per owner made every wave walk its
-// share of the touched list one dependent load at a time).
-constexpr uint32_t SEG_LANE_COPY = 8;
-
-template <typename T>
-__global__ __launch_bounds__(256) void k_seg_move(Seg<T> s) {
-  const uint64_t n = *s.ntouched;
-  const uint64_t nw = (uint64_t)gridDim.x * 4;
-  const int lane = lane_id();
-  for (uint64_t b = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; b < n; b += nw * 64) {
-    const uint64_t i = b + lane;
-    const uint32_t r = i < n ? s.reloc[i] : 0xFFFFFFFFu;
-    const bool mv = r < 0xFFFFFFFEu;
-    const uint32_t o = mv ? s.touched[i] : 0;
-    const uint2 ad = mv ? s.adj[o] : make_uint2(0, 0);
+    const bool mv = r != 0xFFFFFFFFu;
     const bool small = mv && ad.y <= SEG_LANE_COPY;
     if (small) {
       T x[SEG_LANE_COPY];
@@ -508,20 +493,15 @@ __global__ __launch_bounds__(256) void k_seg_move(Seg<T> s) {
     }
     if (mv) {
       s.adj[o].x = r;
-      s.cap[o] = seg_cap(ad.y + s.nnew[o]);
+      s.cap[o] = want;
     }
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void k_seg_finish(Seg<T> s) {
-  const uint64_t n = *s.ntouched;
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    const uint32_t o = s.touched[i];
-    s.adj[o].y += s.nnew[o];
-    s.nnew[o] = 0;
-  }
+__global__ __launch_bounds__(SEG_THREADS) void k_seg_grow(Seg<uint64_t> fw, Seg<uint32_t> rv, Counters *c) {
+  const uint32_t half = gridDim.x / 2;
+  if (blockIdx.x < half) seg_grow(fw, c, blockIdx.x, half);
+  else seg_grow(rv, c, blockIdx.x - half, gridDim.x - half);
 }
 
 __global__ __launch_bounds__(256) void k_edge_append(DevGraph g, EdgeArgs a) {
@@ -548,19 +528,41 @@ __global__ __launch_bounds__(256) void k_edge_append(DevGraph g, EdgeArgs a) {
   }
 }
 
-// 6. candidate entries of edges whose count changed sign: the final count
-//    decides (an edge may be listed more than once; every copy writes the same).
-__global__ __launch_bounds__(256) void k_edge_flip(DevGraph g, EdgeArgs a) {
-  const uint64_t n = g.ctr->n_flips;
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    const uint64_t b = a.flips[i];
-    const uint4 bk = load_bucket(&g.etab[b]);
-    const uint64_t key = bucket_key(bk);
-    const uint32_t o = (uint32_t)(key >> 32), t = (uint32_t)key;
-    const int32_t cnt = edge_count(g.pool[(uint64_t)g.adj[o].x + bk.z]);
-    const uint32_t r = bk.w;
-    if (r < g.radj[t].y) g.rpool[(uint64_t)g.radj[t].x + r] = o | (cnt > 0 ? RC_POS : 0u);
+// After the appends, in one launch: degrees advance by the merge's new edges
+// (forward) and candidates (reverse), the per-merge counts reset; and the
+// candidate entries of edges whose count changed sign take the final count's
+// sign (an edge may be listed more than once; every copy writes the same).
+// Flips read segment offsets and counts, never the degrees advanced here.
+template <typename T>
+__device__ inline void seg_finish(Seg<T> s, uint64_t i0, uint64_t stride) {
+  const uint64_t n = *s.ntouched;
+  for (uint64_t i = i0; i < n; i += stride) {
+    const uint32_t o = s.touched[i];
+    s.adj[o].y += s.nnew[o];
+    s.nnew[o] = 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_edge_post(DevGraph g, EdgeArgs a, Seg<uint64_t> fw, Seg<uint32_t> rv) {
+  const uint32_t third = gridDim.x / 3;
+  const uint32_t part = min(blockIdx.x / third, 2u);
+  const uint32_t b = blockIdx.x - part * third;
+  const uint32_t nb = part == 2 ? gridDim.x - 2 * third : third;
+  const uint64_t i0 = (uint64_t)b * 256 + threadIdx.x, stride = (uint64_t)nb * 256;
+  if (part == 0) {
+    seg_finish(fw, i0, stride);
+  } else if (part == 1) {
+    seg_finish(rv, i0, stride);
+  } else {
+    const uint64_t n = g.ctr->n_flips;
+    for (uint64_t i = i0; i < n; i += stride) {
+      const uint4 bk = load_bucket(&g.etab[a.flips[i]]);
+      const uint64_t key = bucket_key(bk);
+      const uint32_t o = (uint32_t)(key >> 32), t = (uint32_t)key;
+      const int32_t cnt = edge_count(g.pool[(uint64_t)g.adj[o].x + bk.z]);
+      const uint32_t r = bk.w;
+      if (r < g.rcap[t]) g.rpool[(uint64_t)g.radj[t].x + r] = o | (cnt > 0 ? RC_POS : 0u);
+    }
   }
 }
 
@@ -575,19 +577,16 @@ hipError_t launch_edges(const DevGraph &g, const EdgeArgs &a, hipStream_t s) {
   if (a.max_atoms == 0) return hipSuccess;
   const int grid = grid_for(a.max_atoms, 256, 8192);
   Seg<uint64_t> fw{g.adj, g.ecap, g.enew, g.pool, g.pcap, &g.ctr->pool_top,
-                   &g.ctr->n_touched, a.touched, a.reloc};
+                   &g.ctr->n_touched, a.touched};
   Seg<uint32_t> rv{g.radj, g.rcap, g.rnew, g.rpool, g.rpcap, &g.ctr->rpool_top,
-                   &g.ctr->n_rtouched, a.rtouched, a.rreloc};
+                   &g.ctr->n_rtouched, a.rtouched};
   const int wgrid = grid_for(a.max_atoms, EDGE_THREADS, 2048);
   hipLaunchKernelGGL(k_edge_apply, dim3(wgrid), dim3(EDGE_THREADS), 0, s, g, a);
-  hipLaunchKernelGGL(k_seg_plan<uint64_t>, dim3(wgrid), dim3(EDGE_THREADS), 0, s, fw, g.ctr);
-  hipLaunchKernelGGL(k_seg_plan<uint32_t>, dim3(wgrid), dim3(EDGE_THREADS), 0, s, rv, g.ctr);
-  hipLaunchKernelGGL(k_seg_move<uint64_t>, dim3(grid), dim3(256), 0, s, fw);
-  hipLaunchKernelGGL(k_seg_move<uint32_t>, dim3(grid), dim3(256), 0, s, rv);
+  const int sgrid = 2 * grid_for(a.max_atoms, SEG_THREADS, 2048);
+  hipLaunchKernelGGL(k_seg_grow, dim3(sgrid), dim3(SEG_THREADS), 0, s, fw, rv, g.ctr);
   hipLaunchKernelGGL(k_edge_append, dim3(grid), dim3(256), 0, s, g, a);
-  hipLaunchKernelGGL(k_seg_finish<uint64_t>, dim3(grid), dim3(256), 0, s, fw);
-  hipLaunchKernelGGL(k_seg_finish<uint32_t>, dim3(grid), dim3(256), 0, s, rv);
-  hipLaunchKernelGGL(k_edge_flip, dim3(grid), dim3(256), 0, s, g, a);
+  hipLaunchKernelGGL(k_edge_post, dim3(3 * grid_for(a.max_atoms, 256, 2048)), dim3(256), 0, s, g, a, fw,
+                     rv);
   return hipGetLastError();
 }
 

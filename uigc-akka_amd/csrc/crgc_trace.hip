@@ -32,6 +32,7 @@ constexpr uint32_t PULL_K = 4;      // pull: in-candidates per list per round
 // next k_frontier); profiles/r1n.
 constexpr uint64_t VIS_SKIP_DIV = 16;
 constexpr int STAT_FRONT = 0, STAT_SUP = 1, STAT_EDGES = 2, STAT_LIVE = 3;
+constexpr int STAT_MF = 3;  // during the mark: the level's frontier out-edges (STAT_LIVE after)
 
 __device__ inline bool sparse_level(const Counters *c, int L, uint32_t thr) {
   if (L <= 1) return false;
@@ -51,14 +52,25 @@ __device__ inline bool pull_level(const Counters *c, int L, const LevelArgs &a) 
 // Levels whose k_frontier scans every block write `fx`, so k_expand can still
 // pull when the frontier it finds is large although the previous one was not
 // (the decision above is made before the level's own frontier is counted).
+// Level 0 (the pseudo-roots) scans every block too, so it writes `fx` as well.
 __device__ inline bool fx_level(const Counters *c, int L, const LevelArgs &a) {
-  if (!(a.flags & LV_PULL) || L < 1 || !a.pull_cur_div) return false;
+  if (!(a.flags & LV_PULL) || (!a.pull_cur_div && !a.alpha)) return false;
+  if (L == 0) return a.alpha != 0;
   return !sparse_level(c, L, a.sparse_thresh) && !sparse_level(c, L + 1, a.sparse_thresh);
 }
 
+// k_expand's direction, once k_tail has counted the level: pull when k_frontier
+// already chose to (no ranges listed), else by Beamer's rule (direction-optimising
+// BFS): pull when the frontier's out-edges m_f exceed the unexplored edges m_u
+// over alpha — a pull level reads in-candidate lists that stop at their first hit
+// and probe a frontier bitmap that stays in the XCD's L2, a push level does a
+// random candidate-byte read-modify-write per edge.
 __device__ inline bool pull_now(const Counters *c, int L, const LevelArgs &a) {
   if (pull_level(c, L, a)) return true;
-  return fx_level(c, L, a) && c->ring[L % LEVEL_RING] * a.pull_cur_div >= c->slot_top;
+  if (!fx_level(c, L, a)) return false;
+  if (!a.alpha) return c->ring[L % LEVEL_RING] * a.pull_cur_div >= c->slot_top;
+  const uint64_t mu = a.e_total > c->mf_sum ? a.e_total - c->mf_sum : 0;
+  return c->mf_level * a.alpha > mu;
 }
 
 // Whether level L lists its frontier for k_tail (same answer in k_frontier and
@@ -96,7 +108,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   if (blockIdx.x == 0 && threadIdx.x == 0) c->ring[(L + 1) % LEVEL_RING] = 0;
   uint64_t *stat = g.blkstat + (uint64_t)blockIdx.x * 4;
   if (!ROOTS && c->ring[(L - 1) % LEVEL_RING] == 0) {  // previous level was empty
-    if (threadIdx.x == 0) stat[STAT_FRONT] = 0;
+    if (threadIdx.x == 0) stat[STAT_FRONT] = stat[STAT_MF] = 0;
     return;
   }
   const bool sp_cur = !ROOTS && sparse_level(c, L, a.sparse_thresh);
@@ -114,7 +126,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   unsigned long long *qh_cnt = &c->qh[L & 1];
   const uint32_t tag = (uint32_t)(L + 1) << 12;
   const bool pull = !ROOTS && pull_level(c, L, a);
-  const bool write_fx = !ROOTS && (pull || fx_level(c, L, a));
+  const bool write_fx = pull || fx_level(c, L, a);
   const bool listing = !ROOTS && listing_level(c, L, a);
   const bool sharded = !ROOTS && g.n_shards > 1;
   uint32_t n_front = 0, n_sup = 0, n_edges = 0;
@@ -281,6 +293,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     stat[STAT_FRONT] = tf;
     stat[STAT_SUP] += ts;
     stat[STAT_EDGES] += te;
+    stat[STAT_MF] = te;  // this level's only (the sweep reuses the slot afterwards)
   }
 }
 
@@ -750,7 +763,20 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
   }
   const uint64_t n0 = s_red[0];
   if (!listing_level(c, L, a) || n0 == 0 || n0 > a.tail_start) {
+    // ... and its frontier's out-edges (Beamer's m_f), for k_expand's direction
+    __syncthreads();
+    part = 0;
+    for (uint32_t b = threadIdx.x; b < a.frontier_grid; b += TAIL_THREADS)
+      part += g.blkstat[b * 4 + STAT_MF];
+    s_red[threadIdx.x] = part;
+    __syncthreads();
+    for (int k = TAIL_THREADS / 2; k > 0; k >>= 1) {
+      if (threadIdx.x < k) s_red[threadIdx.x] += s_red[threadIdx.x + k];
+      __syncthreads();
+    }
     if (threadIdx.x == 0) {  // the level kernels go on
+      c->mf_level = s_red[0];
+      c->mf_sum += s_red[0];
       c->ring[L % LEVEL_RING] = n0;
       c->marked += n0;
       c->qh[(L + 1) & 1] = 0;  // next level's hub queue (last read by k_expand(L-1))
