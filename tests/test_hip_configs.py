@@ -24,6 +24,7 @@ def _same(rh, ro):
     assert rh.n_live == ro.n_live
     assert rh.pseudo_roots == ro.pseudo_roots
     assert rh.sup_edges == ro.sup_edges
+    assert rh.edges_scanned == ro.edges_scanned
 
 
 def _load(g, w, batch):
@@ -114,7 +115,11 @@ def test_power_law_wakeups_match_oracle(hip_mod, oracle_mod, actors, edges, batc
     assert h.total_actors_seen() == o.total_actors_seen()
 
 
-def test_c3_deep_chains_and_dead_rings(hip_mod, oracle_mod):
+@pytest.mark.parametrize("chain_after", ["64", "0", "2"])
+def test_c3_deep_chains_and_dead_rings(hip_mod, oracle_mod, monkeypatch, chain_after):
+    """Chains walked by k_tail (CRGC_CHAIN_AFTER=0) or handed to chain mode
+    (pointer jumping) after 64 / 2 links: the same marks."""
+    monkeypatch.setenv("CRGC_CHAIN_AFTER", chain_after)
     w = world.World(seed=0x5EED + 3)
     w.chain_graph(n_chains=20, chain_len=3000, n_sup_chains=5, sup_depth=400,
                   n_rings=30, ring_len=60)
@@ -126,10 +131,10 @@ def test_c3_deep_chains_and_dead_rings(hip_mod, oracle_mod):
     rh, ro = h.trace(True), o.trace(True)
     _same(rh, ro)
     assert len(ro.garbage) == 30 * 60 and len(ro.kill) == 30 * 60
-    # levels = BFS levels until k_tail takes over, then its rounds: a thread walks a
-    # chain a link per step, so the count is far below the chain length
     assert rh.levels >= 1
     assert h.export() == o.export()
+    _same(h.trace(True), o.trace(True))      # again, nothing to collect
+    assert h.count_reachable_from(1) == o.count_reachable_from(1)
 
 
 def test_c5_cluster_deltas_and_undo(hip_mod, oracle_mod):

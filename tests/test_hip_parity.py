@@ -40,6 +40,9 @@ DIRECTIONS = {
     # a bail back to the level kernels whenever a round finds more than 3
     "notail": {"CRGC_TAIL": "0"},
     "tailbail": {"CRGC_TAIL_START": "65536", "CRGC_TAIL_MAX": "3"},
+    # k_tail at every sparse level, handing to chain mode (pointer jumping,
+    # crgc_chain.hip) after a one-link walk
+    "chains": {"CRGC_TAIL_START": "65536", "CRGC_CHAIN_AFTER": "1"},
 }
 
 

@@ -47,7 +47,7 @@ void free_arrays(Arrays &a) {
                 d.enew, d.pool, d.etab, d.edelta, d.vis, d.front[0], d.front[1],
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat, d.xbytes,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill,
-                d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.fx, d.tq, d.tl_buf, d.tl_tag,
+                d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.fx, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
                 d.xp_buf, d.xp_cnt, d.rq_buf, d.rq_cnt};
   for (void *p : ps)
     if (p) hipFree(p);
@@ -121,6 +121,9 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   A(dmalloc(&d.tq, 2 * (uint64_t)TAIL_QCAP));
   A(dmalloc(&d.tl_buf, c.scap));
   A(dmalloc(&d.tl_tag, c.scap / BLK_SLOTS));
+  A(dmalloc(&d.cm, c.scap / 32));
+  A(dmalloc(&d.pb[0], c.scap / 32));
+  A(dmalloc(&d.pb[1], c.scap / 32));
   if (sharded) {
     A(dmalloc(&d.xp_buf, c.scap));
     A(dmalloc(&d.xp_cnt, c.scap / BLK_SLOTS));
@@ -151,6 +154,9 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   hipMemsetAsync(d.rcap, 0, c.scap * 4, s);
   hipMemsetAsync(d.rnew, 0, c.scap * 4, s);
   hipMemsetAsync(d.fx, 0, c.scap / 8, s);
+  hipMemsetAsync(d.cm, 0, c.scap / 8, s);
+  hipMemsetAsync(d.pb[0], 0, c.scap / 8, s);
+  hipMemsetAsync(d.pb[1], 0, c.scap / 8, s);
   if (sharded) {
     hipMemsetAsync(d.xp_cnt, 0, c.scap / BLK_SLOTS * 4, s);
     hipMemsetAsync(d.rq_cnt, 0, c.scap / BLK_SLOTS * 4, s);
@@ -205,6 +211,7 @@ struct crgc_graph {
   Scratch x_send, x_slot, x_recv, x_ans, x_ans_back, x_small, x_pack, x_pack_recv;
   Scratch x_route, x_route_send, x_cat;  // routed entry merges
   Scratch x_dg, x_dg_out;    // DeltaGraph production
+  Scratch x_chain;           // chain mode (crgc_chain.hip)
   uint64_t *h_small = nullptr;       // pinned host staging for small all-gathers
   char *h_route = nullptr;           // pinned RoutePart / ConcatPart tables
   bool route = true;                 // CRGC_ROUTE=0: all-gather every batch instead
@@ -474,7 +481,7 @@ void crgc_destroy(crgc_graph *h) {
   h->work.release();
   for (Scratch *x : {&h->x_send, &h->x_slot, &h->x_recv, &h->x_ans, &h->x_ans_back, &h->x_small,
                      &h->x_pack, &h->x_pack_recv, &h->x_route, &h->x_route_send, &h->x_cat,
-                     &h->x_dg, &h->x_dg_out})
+                     &h->x_dg, &h->x_dg_out, &h->x_chain})
     x->release();
   if (h->ctr) hipFree(h->ctr);
   if (h->hctr) hipHostFree(h->hctr);
@@ -1159,6 +1166,64 @@ int crgc_merge_undo(crgc_graph *h, const crgc_undo_log *log) {
 }
 
 // ---- mark ---------------------------------------------------------------------
+// Chain mode (crgc_chain.hip): close the marked set by pointer jumping along
+// each shadow's unique out-target and its supervisor, expanding shadows with
+// several out-targets edge by edge, until an iteration marks nothing.  One
+// host synchronisation per iteration; each doubling sequence is enqueued in
+// full (ceil(log2 slots) + 1 rounds) and its rounds exit at once after a
+// round that marked nothing.
+static int run_chains(crgc_graph *h, bool investigate, uint64_t top) {
+  const uint64_t words = (top + 31) / 32 + 2;
+  uint32_t R = 1;
+  while ((1ull << (R - 1)) < top) ++R;
+  const size_t need = Carver::need({top * 4, top * 4, top * 4, top * 4, words * 4, (2 * (size_t)R + 8) * 4, 8});
+  if (h->x_chain.ensure(need) != hipSuccess) return CRGC_E_NOMEM;
+  Carver cv(h->x_chain.ptr);
+  ChainArgs ca{};
+  ca.nx0 = cv.take<uint32_t>(top);
+  ca.sp0 = cv.take<uint32_t>(top);
+  uint32_t *ja = cv.take<uint32_t>(top), *jb = cv.take<uint32_t>(top);
+  ca.cx = cv.take<uint32_t>(words);
+  ca.flag = cv.take<uint32_t>(2 * R + 8);
+  ca.n_new = cv.take<unsigned long long>(1);
+  ca.investigate = investigate ? 1 : 0;
+  const DevGraph &g = h->g.d;
+  HIP_TRY(hipMemsetAsync(ca.n_new, 0, 8, h->stream));
+  HIP_TRY(launch_chain(g, ca, 0, nullptr, nullptr, top, 0, 0, 0, h->stream));
+  std::vector<uint32_t> fl(2 * R + 1);
+  uint32_t marked_rounds = 0;
+  int pcur = 0;
+  for (uint64_t it = 0;; ++it) {
+    if (it > top) return CRGC_E_TIMEOUT;  // every iteration but the last marks a shadow
+    ca.pb_in = g.pb[pcur];
+    ca.pb_out = g.pb[pcur ^ 1];
+    HIP_TRY(hipMemsetAsync(ca.flag, 0, (2 * R + 1) * 4, h->stream));
+    for (uint32_t seq = 0; seq < 2; ++seq) {
+      const uint32_t *src = seq ? ca.sp0 : ca.nx0;
+      uint32_t *dst = ja;
+      for (uint32_t r = 0; r < R; ++r) {
+        HIP_TRY(launch_chain(g, ca, 1, src, dst, top, seq * R + r, r == 0, 0, h->stream));
+        src = dst;
+        dst = dst == ja ? jb : ja;
+      }
+    }
+    HIP_TRY(launch_chain(g, ca, 2, nullptr, nullptr, top, 2 * R, 0, 0, h->stream));
+    HIP_TRY(hipMemcpyAsync(fl.data(), ca.flag, fl.size() * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    bool any = false;
+    for (uint32_t f : fl)
+      if (f) {
+        any = true;
+        ++marked_rounds;
+      }
+    if (!any) break;
+    pcur ^= 1;
+  }
+  HIP_TRY(launch_chain(g, ca, 3, nullptr, nullptr, top, 0, 0, 0, h->stream));
+  HIP_TRY(launch_chain(g, ca, 4, nullptr, nullptr, top, 0, 0, marked_rounds, h->stream));
+  return CRGC_OK;
+}
+
 struct LevelRun {
   uint64_t levels = 0, roots = 0, launches = 0, depth = 0;
   double ms = 0, ms_f = 0, ms_t = 0, ms_e = 0;
@@ -1197,10 +1262,13 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   la.pull_div = (uint32_t)pull_div;  // against the exact slot count, on the device
   la.pull_cur_div = 4;
   if (const char *m = getenv("CRGC_PULL_CUR_DIV")) la.pull_cur_div = (uint32_t)strtoul(m, nullptr, 10);
-  // Beamer's direction rule (alpha = 14, the paper's value); m_u from the edge
-  // keys the graph holds (an upper bound: keys whose count dropped to 0 stay
-  // until a rebuild).  CRGC_ALPHA=0: the round-1 frontier-size rule.
-  la.alpha = 14;
+  // Beamer's direction rule (CRGC_ALPHA=a: pull when a * m_f > m_u, level 0
+  // included; m_u from the edge keys the graph holds, an upper bound).  Off by
+  // default: on the C2 wakeup (10 % pseudo-roots) alpha = 14 pulls at level 0
+  // and the mark takes 1.27 ms against 0.89 ms with the frontier-size rule
+  // (k_expand level 0: 670 us pull vs 306 us push; profiles/r2b/ab.json) — a
+  // pull over a 7.6 % frontier walks long in-candidate lists before a hit.
+  la.alpha = 0;
   if (const char *m = getenv("CRGC_ALPHA")) la.alpha = (uint32_t)strtoul(m, nullptr, 10);
   la.e_total = h->etab_used + h->atoms_since;
   la.pull_thresh = 0;
@@ -1218,6 +1286,10 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
     if (!atoi(m)) la.flags &= ~LV_TAIL;
   }
   if (const char *m = getenv("CRGC_TAIL_START")) la.tail_start = (uint32_t)strtoul(m, nullptr, 10);
+  // Deep marks: a k_tail walk of chain_after links hands the rest to chain mode
+  // (pointer jumping, crgc_chain.hip).  Unsharded graphs only.
+  la.chain_after = h->tp ? 0 : 64;
+  if (const char *m = getenv("CRGC_CHAIN_AFTER")) la.chain_after = h->tp ? 0 : (uint32_t)strtoul(m, nullptr, 10);
   if (const char *m = getenv("CRGC_TAIL_MAX")) la.tail_max = (uint32_t)strtoul(m, nullptr, 10);
   la.tail_start = std::min<uint32_t>(la.tail_start, TAIL_QCAP);
   la.tail_max = std::min<uint32_t>(std::max(la.tail_max, 1u), TAIL_QCAP);
@@ -1282,6 +1354,14 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
                            h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     if (roots && first == 0) lr.roots = ring[0];
+    if (tail[0] == TAIL_CHAINS) {  // k_tail handed a deep mark to chain mode, which finishes it
+      HIP_TRY(chunk_event());  // chain mode's device time counts as mark time
+      if (int rc = run_chains(h, investigate, top)) return rc;
+      HIP_TRY(chunk_event());
+      if (after_chunk) HIP_TRY(after_chunk());
+      HIP_TRY(hipMemcpyAsync(tail, (char *)h->ctr + CTR_OFF(tail_state), 24, hipMemcpyDeviceToHost, h->stream));
+      HIP_TRY(hipStreamSynchronize(h->stream));
+    }
     if (tail[0] == TAIL_BAILED) {  // k_tail handed a wide frontier back: resume there
       HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(tail_state), 0, 8, h->stream));
       L = (int)tail[1];

@@ -165,8 +165,23 @@ struct LevelArgs {
   uint32_t pull_cur_div;   // alpha == 0: k_expand also pulls once the current frontier is >= slot_top / div
   uint32_t alpha;          // Beamer: pull when alpha * m_f > m_u (0: the pull_cur_div rule)
   uint64_t e_total;        // edge keys in the graph (m_u = e_total - explored edges)
+  uint32_t chain_after;    // k_tail hands a deep mark to chain mode after this many rounds (0: never)
   uint16_t location;
 };
+
+// Chain mode (crgc_chain.hip).
+struct ChainArgs {
+  uint32_t *nx0, *sp0;        // per slot: unique out-target / supervisor (CH_NONE, CH_COMPLEX)
+  uint32_t *cx;               // bitmap: more than one out-target
+  uint32_t *pb_in, *pb_out;   // pending complex shadows: this iteration's / the next one's
+  uint32_t *flag;             // per round / expansion: marked something
+  unsigned long long *n_new;  // shadows marked by chain mode
+  int investigate;
+};
+// step 0 init, 1 jump round (src -> dst, flag fi, first of its sequence), 2 expand
+// (flag fi), 3 statistics, 4 done (rounds that marked something)
+hipError_t launch_chain(const DevGraph &g, const ChainArgs &ca, int step, const uint32_t *src, uint32_t *dst,
+                        uint64_t top, uint32_t fi, int first, uint32_t rounds, hipStream_t s);
 
 // ---- launchers (return hipError_t of the launch) ---------------------------
 hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s);

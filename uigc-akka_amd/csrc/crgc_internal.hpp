@@ -56,7 +56,7 @@ constexpr int BLK_SLOTS = 2048;          // slots per wave-block (64 lanes x 32)
 constexpr int LEVEL_RING = 4096;         // ring of per-level frontier counts
 constexpr int STAT_WG = 2048;            // max workgroups of the level / sweep kernels
 constexpr int TAIL_QCAP = 1 << 16;       // narrow-frontier queue capacity (per buffer)
-constexpr unsigned long long TAIL_DONE = 1, TAIL_BAILED = 2;
+constexpr unsigned long long TAIL_DONE = 1, TAIL_BAILED = 2, TAIL_CHAINS = 3;
 
 struct Counters {
   unsigned long long inserted;       // vertices created (totalActorsSeen)
@@ -78,6 +78,8 @@ struct Counters {
   unsigned long long expand_bytes;   // bytes k_expand read / wrote over the trace (k_trace_stats)
   unsigned long long mf_level;       // nonzero out-edges of the current level's expandable frontier
   unsigned long long mf_sum;         // ... summed over the levels so far (Beamer's explored edges)
+  unsigned long long chain_marked;   // shadows marked by chain mode (crgc_chain.hip)
+  unsigned long long chain_rounds;   // pointer-jumping rounds that marked something
   unsigned long long n_garbage;
   unsigned long long n_kill;
   unsigned long long n_live;
@@ -141,6 +143,9 @@ struct DevGraph {
   uint32_t *tq;              // narrow-frontier queues, 2 x TAIL_QCAP slots
   uint32_t *tl_buf;          // per-block regions: a listed level's frontier slots
   uint32_t *tl_tag;          // per block: (level+1) << 12 | listed slots
+  // chain mode (crgc_chain.hip): zero outside it
+  uint32_t *cm;              // bitmap: marked by chain mode, or handed to it unexpanded by k_tail
+  uint32_t *pb[2];           // bitmaps: marked, not yet expanded, more than one traceable out-edge
   // edges
   uint64_t pcap;
   uint64_t *pool;

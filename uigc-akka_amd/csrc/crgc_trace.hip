@@ -568,6 +568,7 @@ struct TailOut {
   uint32_t n_sup = 0, n_edges = 0, rounds = 0, n = 0;
   int32_t claims = 0;
   bool bailed = false;
+  bool chained = false;  // handed to chain mode: the pending claims stay marked, unexpanded
 };
 
 // Claim t for the next round; without queue room it becomes a candidate byte
@@ -633,8 +634,12 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
   uint8_t *Fb = g.front[L & 1];        // bail: candidates of level L+2
   uint8_t *Db = g.dirty[L & 1];
   bool first = true;
+  __shared__ uint32_t s_deep;  // a walk ran chain_after links: hand the rest to chain mode
   for (;;) {
-    if (threadIdx.x == 0) *sh.next = 0;
+    if (threadIdx.x == 0) {
+      *sh.next = 0;
+      s_deep = 0;
+    }
     __syncthreads();
     for (uint32_t c0 = 0; c0 < n; c0 += TAIL_THREADS) {
       const uint32_t i = c0 + threadIdx.x;
@@ -642,8 +647,10 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
       uint32_t v = have ? cur.get(i) : 0;
       bool vfirst = first;
       uint2 ad = make_uint2(0, 0);
+      uint32_t steps = 0;
       while (have) {
         have = false;
+        ++steps;
         // every per-shadow field in one round trip (a walk step is one chain link)
         const uint8_t f = g.flags[v];
         const uint2 adv = g.adj[v];
@@ -684,7 +691,10 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
           }
         }
         if (keep != NO_SLOT) {
-          if (ad.y <= TAIL_LIGHT) {  // walk on
+          if (a.chain_after && steps >= a.chain_after) {  // a long chain: queue it, chain mode takes over
+            tail_enqueue_claimed<LV>(g, sh, keep, nxt, Fb, Db, o.claims);
+            s_deep = 1;
+          } else if (ad.y <= TAIL_LIGHT) {  // walk on
             v = keep;
             vfirst = false;
             have = true;
@@ -729,6 +739,19 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
       }
       o.bailed = true;
       n = m;
+      break;
+    }
+    if (s_deep && nn <= a.tail_max) {
+      // A deep, narrow mark (chains): hand the pending claims to chain mode
+      // (crgc_chain.hip), which marks whole chains by pointer jumping.  They
+      // stay marked; chain mode expands them and counts their edges.
+      for (uint32_t i = threadIdx.x; i < nn; i += TAIL_THREADS) {
+        const uint32_t t = nxt.get(i);
+        atomicOr(&g.cm[t >> 5], 1u << (t & 31));
+        atomicOr(&g.pb[0][t >> 5], 1u << (t & 31));
+      }
+      o.chained = true;
+      n = nn;
       break;
     }
     const TailQ tmp = cur;
@@ -826,7 +849,10 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
     g.blkstat[STAT_SUP] += tot_sup;
     g.blkstat[STAT_EDGES] += tot_edges;
     c->tail_from = L;
-    if (o.bailed) {
+    if (o.chained) {
+      c->tail_level = L + o.rounds;
+      c->tail_state = TAIL_CHAINS;  // the host runs chain mode, which finishes the mark
+    } else if (o.bailed) {
       c->ring[L % LEVEL_RING] = 1;  // level L+2 runs sparse over the dirty blocks
       c->ring[(L + 1) % LEVEL_RING] = o.n;
       c->qh[L & 1] = 0;
