@@ -119,6 +119,8 @@ __global__ __launch_bounds__(256) void k_chain_expand(DevGraph g, ChainArgs ca, 
       while (kb) {
         const uint32_t v = (uint32_t)((w0 + k) * 32 + (__ffs(kb) - 1));
         kb &= kb - 1;
+        // k_tail hands over every pending claim: halted ones are marked, never expanded (:226-229)
+        if ((g.flags[v] & (FL_ALIVE | FL_PROXY | FL_HALTED)) != FL_ALIVE) continue;
         const uint2 ad = g.adj[v];
         for (uint32_t e = lane; e < ad.y; e += 64) {
           const uint64_t ed = g.pool[(uint64_t)ad.x + e];

@@ -304,7 +304,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
 // per-edge marking would serialise them).
 template <int U>
 __device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn, bool sp_next,
-                                    const uint64_t (&ed)[U], bool skipvis, uint32_t &nb) {
+                                    const uint64_t (&ed)[U], bool skipvis, uint32_t &nb, bool blind = false) {
   uint32_t t[U];
   bool go[U];
 #pragma unroll
@@ -324,7 +324,7 @@ __device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn,
   }
   uint8_t fb[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) fb[u] = go[u] ? Fn[t[u]] : 0;  // read before the store: most are set
+  for (int u = 0; u < U; ++u) fb[u] = (go[u] && !blind) ? Fn[t[u]] : 0;  // read before the store: most are set
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     nb += go[u] ? (fb[u] == 0 ? 2 : 1) : 0;
@@ -383,7 +383,8 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
   // A candidate byte stored for an already-marked target is dropped by the next
   // k_frontier (bits & ~vis), so the filter is an optimisation only.
-  const bool skipvis = c->marked * VIS_SKIP_DIV < c->slot_top;
+  const bool skipvis = (a.flags & LV_NO_VIS) || c->marked * VIS_SKIP_DIV < c->slot_top;
+  const bool blind = a.flags & LV_BLIND;  // A/B: candidate stores without the read
   // Bytes this launch reads and writes, by element width (the roofline
   // numerator): twice the count, so 8.5-B items stay integral.
   uint32_t nb2 = 0;
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
         }
       }
       uint32_t nb = 0;
-      expand_edges(g, Fn, Dn, sp_next, ed, skipvis, nb);
+      expand_edges(g, Fn, Dn, sp_next, ed, skipvis, nb, blind);
       nb2 += 2 * nb;
     }
     wave_lds_fence();
@@ -504,7 +505,7 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
         nb2 += e < r.y ? 16 : 0;
       }
       uint32_t nb = 0;
-      expand_edges(g, Fn, Dn, sp_next, ed, skipvis, nb);
+      expand_edges(g, Fn, Dn, sp_next, ed, skipvis, nb, blind);
       nb2 += 2 * nb;
     }
   }
