@@ -11,13 +11,9 @@ if [ "${2:-}" = "tests" ]; then
     > "$O/gpu_tests.log" 2>&1
 fi
 cd /tmp
-VARS=${AB_VARIANTS:-"BASE=0 CRGC_ALPHA=4"}
-VA=()
-for v in $VARS; do VA+=(--variant "$v"); done
-timeout -k 10 600 python3 "$ROOT/tools/ab_trace.py" --rounds 6 "${VA[@]}" > "$O/ab.json" 2> "$O/ab.err"
+timeout -k 10 600 python3 "$ROOT/tools/ab_trace.py" --rounds 6 --variant BASE=0 --variant CRGC_ALPHA=0 \
+  --variant CRGC_ALPHA=4 --variant CRGC_ALPHA=40 > "$O/ab.json" 2> "$O/ab.err"
 CRGC_LEVEL_LOG=1 CRGC_KERNEL_TIMING=2 timeout -k 10 420 python3 "$ROOT/bench.py" --steps 2 --warmup 2 \
   --no-cpu-baseline > "$O/levels.json" 2> "$O/levels.err"
 timeout -k 10 420 python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$O/bench.json" 2> "$O/bench.err"
-timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o kt -- \
-  python3 "$ROOT/bench.py" --steps 4 --warmup 2 --no-cpu-baseline > "$O/bench_kt.json" 2> "$O/bench_kt.err"
 echo ab-done

@@ -195,8 +195,6 @@ struct crgc_graph {
   uint64_t inserted_at_trace = 0;  // Counters::inserted when `live` was exact
   Scratch stage, work;
   hipEvent_t ev[4] = {};
-  hipStream_t side = nullptr;          // merge work beside the main stream (k_entries_lww)
-  hipEvent_t fork = nullptr, join = nullptr;
   // last trace
   uint64_t last_garbage = 0, last_kill = 0, last_live = 0;
   crgc_trace_stats last_stats{};
@@ -446,10 +444,6 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     }
     for (auto &e : h->ev)
       if (hipEventCreate(&e) != hipSuccess) rc = CRGC_E_DEVICE;
-    if (hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->join, hipEventDisableTiming) != hipSuccess)
-      rc = CRGC_E_DEVICE;
     if (rc) break;
     if (hipMalloc(&h->ctr, sizeof(Counters)) != hipSuccess ||
         hipHostMalloc(&h->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess ||
@@ -496,12 +490,6 @@ void crgc_destroy(crgc_graph *h) {
   if (h->roots_buf) hipFree(h->roots_buf);
   for (auto &e : h->ev)
     if (e) hipEventDestroy(e);
-  if (h->side) {
-    hipStreamSynchronize(h->side);
-    hipStreamDestroy(h->side);
-  }
-  if (h->fork) hipEventDestroy(h->fork);
-  if (h->join) hipEventDestroy(h->join);
   for (auto &e : h->lvl_ev) hipEventDestroy(e);
   for (auto &e : h->chunk_ev) hipEventDestroy(e);
   if (h->own_stream && h->stream) hipStreamDestroy(h->stream);
@@ -766,10 +754,8 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   a.n_atoms = wc.take<uint64_t>(1);
   // atoms of entries refused for bad offsets stay zero (never applied)
   hipMemsetAsync(a.atom_d, 0, max_atoms * 4, h->stream);
-  HIP_TRY(launch_entries(h->g.d, a, h->stream, h->side, h->fork, h->join));
-  const int erc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, max_atoms, wc, a.n_atoms);
-  HIP_TRY(hipStreamWaitEvent(h->stream, h->join, 0));  // the LWW winners are in before anything reads them
-  if (erc) return erc;
+  HIP_TRY(launch_entries(h->g.d, a, h->stream));
+  if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, max_atoms, wc, a.n_atoms)) return rc;
   note_merge(h, ids, C + U);
   HIP_TRY(wait_staged(h, b->memory));
   return CRGC_OK;

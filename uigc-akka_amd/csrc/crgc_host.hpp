@@ -186,9 +186,7 @@ hipError_t launch_chain(const DevGraph &g, const ChainArgs &ca, int step, const 
                         uint64_t top, uint32_t fi, int first, uint32_t rounds, hipStream_t s);
 
 // ---- launchers (return hipError_t of the launch) ---------------------------
-// side: null, or a stream k_entries_lww runs on (after `fork`, recording `join`)
-hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s, hipStream_t side = nullptr,
-                          hipEvent_t fork = nullptr, hipEvent_t join = nullptr);
+hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s);
 hipError_t launch_deltas(const DevGraph &g, const DeltaArgs &a, uint64_t n_out, hipStream_t s);
 hipError_t launch_undo_check(const DevGraph &g, const UndoArgs &a, hipStream_t s);
 hipError_t launch_undo_apply(const DevGraph &g, const UndoArgs &a, uint64_t slot_top,

@@ -184,8 +184,7 @@ __global__ __launch_bounds__(256) void k_entries_shard_prep(DevGraph g, EntryArg
     a.u_partner[k] = refob_deactivated(a.u_info[k]) ? self : CRGC_NO_ACTOR;
 }
 
-hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s, hipStream_t side,
-                          hipEvent_t fork, hipEvent_t join) {
+hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   const uint64_t nf = a.n * a.F;
   const int blocks = (int)((a.n + 255) / 256);
@@ -201,17 +200,7 @@ hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s, 
                     nullptr};
   if (hipError_t e = launch_ids(g, ia, s)) return e;
   hipLaunchKernelGGL(k_entries_apply, dim3(blocks), dim3(256), 0, s, g, a);
-  // The LWW winners (flags, supervisor) touch nothing the edge pipeline reads
-  // or writes: they run on a side stream beside it; the caller joins before
-  // anything reads flags / sup.
-  if (side) {
-    if (hipError_t e = hipEventRecord(fork, s)) return e;
-    if (hipError_t e = hipStreamWaitEvent(side, fork, 0)) return e;
-    hipLaunchKernelGGL(k_entries_lww, dim3(blocks), dim3(256), 0, side, g, a);
-    if (hipError_t e = hipEventRecord(join, side)) return e;
-  } else {
-    hipLaunchKernelGGL(k_entries_lww, dim3(blocks), dim3(256), 0, s, g, a);
-  }
+  hipLaunchKernelGGL(k_entries_lww, dim3(blocks), dim3(256), 0, s, g, a);
   return hipGetLastError();
 }
 
