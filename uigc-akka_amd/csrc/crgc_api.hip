@@ -1251,8 +1251,6 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   // always-on marked-word filter) were removed; their records stay in
   // profiles/r1h, r1n, r1r.
   la.flags = 0;
-  if (const char *m = getenv("CRGC_BLIND")) la.flags |= atoi(m) ? LV_BLIND : 0;
-  if (const char *m = getenv("CRGC_NO_VIS")) la.flags |= atoi(m) ? LV_NO_VIS : 0;
   la.sparse_thresh = (uint32_t)std::max<uint64_t>(64, (top / BLK_SLOTS) / 4);
   // Direction optimisation: dense levels after a frontier of >= top/div shadows pull.
   uint64_t pull_div = 16;

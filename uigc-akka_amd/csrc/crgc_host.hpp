@@ -152,8 +152,6 @@ constexpr uint32_t LV_PULL = 4;                // dense levels scan in-candidate
 constexpr uint32_t LV_TAIL = 8;                // narrow frontiers go to one workgroup (k_tail)
 constexpr uint32_t LV_INVESTIGATE = 16;        // set by launch_level: no supervisor edges
 constexpr uint32_t LV_ROOTS = 32;              // set by launch_level: the pseudo-root level
-constexpr uint32_t LV_BLIND = 64;              // A/B: push stores candidate bytes without reading them
-constexpr uint32_t LV_NO_VIS = 128;            // A/B: push skips the marked-word filter
 
 struct LevelArgs {
   int level;

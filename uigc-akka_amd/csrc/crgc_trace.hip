@@ -27,10 +27,6 @@ constexpr uint32_t RANGE_MAX = 256;  // longer segments (hubs) are cut into piec
 constexpr int FB = 4;               // k_frontier: chunks of 64 frontier shadows per load group
 constexpr uint32_t NO_SLOT = ~0u;
 constexpr uint32_t PULL_K = 4;      // pull: in-candidates per list per round
-// The marked-word filter in front of a candidate store is skipped while fewer
-// than 1/VIS_SKIP_DIV of the slots are marked (a stale byte is dropped by the
-// next k_frontier); profiles/r1n.
-constexpr uint64_t VIS_SKIP_DIV = 16;
 constexpr int STAT_FRONT = 0, STAT_SUP = 1, STAT_EDGES = 2, STAT_LIVE = 3;
 constexpr int STAT_MF = 3;  // during the mark: the level's frontier out-edges (STAT_LIVE after)
 
@@ -302,9 +298,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
 // targets still unmarked, then the stores — two dependent round trips per
 // group of edges instead of two per edge (a byte store may alias any load, so
 // per-edge marking would serialise them).
+// Candidate bytes are stored blind: no marked-word filter, no read of the
+// byte first.  A byte stored for a marked target is dropped by the next
+// k_frontier (bits & ~vis), and a byte store is idempotent across XCDs, so the
+// edge load is the only round trip an edge costs (mark -13 % on the C2 wakeup
+// against filter + read-before-store: profiles/r2e/ab.json).
 template <int U>
 __device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn, bool sp_next,
-                                    const uint64_t (&ed)[U], bool skipvis, uint32_t &nb, bool blind = false) {
+                                    const uint64_t (&ed)[U], uint32_t &nb) {
   uint32_t t[U];
   bool go[U];
 #pragma unroll
@@ -312,23 +313,10 @@ __device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn,
     go[u] = edge_count(ed[u]) > 0;
     t[u] = edge_target(ed[u]);
   }
-  if (!skipvis) {  // early levels mark few shadows: a store costs less than the filter
-    uint32_t w[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      w[u] = go[u] ? g.vis[t[u] >> 5] : ~0u;
-      nb += go[u] ? 4 : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) go[u] = !((w[u] >> (t[u] & 31)) & 1u);
-  }
-  uint8_t fb[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) fb[u] = (go[u] && !blind) ? Fn[t[u]] : 0;  // read before the store: most are set
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    nb += go[u] ? (fb[u] == 0 ? 2 : 1) : 0;
-    if (go[u] && fb[u] == 0) Fn[t[u]] = 1;
+    nb += go[u] ? 1 : 0;
+    if (go[u]) Fn[t[u]] = 1;
   }
   if (sp_next) {
     uint8_t db[U];
@@ -383,8 +371,6 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
   // A candidate byte stored for an already-marked target is dropped by the next
   // k_frontier (bits & ~vis), so the filter is an optimisation only.
-  const bool skipvis = (a.flags & LV_NO_VIS) || c->marked * VIS_SKIP_DIV < c->slot_top;
-  const bool blind = a.flags & LV_BLIND;  // A/B: candidate stores without the read
   // Bytes this launch reads and writes, by element width (the roofline
   // numerator): twice the count, so 8.5-B items stay integral.
   uint32_t nb2 = 0;
@@ -487,7 +473,7 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
         }
       }
       uint32_t nb = 0;
-      expand_edges(g, Fn, Dn, sp_next, ed, skipvis, nb, blind);
+      expand_edges(g, Fn, Dn, sp_next, ed, nb);
       nb2 += 2 * nb;
     }
     wave_lds_fence();
@@ -505,7 +491,7 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
         nb2 += e < r.y ? 16 : 0;
       }
       uint32_t nb = 0;
-      expand_edges(g, Fn, Dn, sp_next, ed, skipvis, nb, blind);
+      expand_edges(g, Fn, Dn, sp_next, ed, nb);
       nb2 += 2 * nb;
     }
   }
