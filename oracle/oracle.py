@@ -34,7 +34,7 @@ OMP_LIB_PATH = os.path.join(_HERE, "_build", "libcrgc_omp.so")
 def build(force: bool = False) -> str:
     """Compile the oracle (and the OpenMP bench baseline) with g++ (oracle/Makefile)."""
     fresh = all(os.path.exists(lib) and os.path.getmtime(lib) >= os.path.getmtime(os.path.join(_HERE, src))
-                for lib, src in ((LIB_PATH, "crgc_oracle.cpp"), (OMP_LIB_PATH, "omp_baseline.cpp")))
+                for lib, src in ((LIB_PATH, "crgc_oracle.cpp"), (OMP_LIB_PATH, "omp_graph.cpp")))
     if not force and fresh:
         return LIB_PATH
     os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
@@ -130,31 +130,40 @@ class OracleGraph:
         return export_to_state(self.lib.oracle_export, self.h)
 
 
-def omp_trace_baseline(g: "OracleGraph", threads: int, reps: int = 3) -> dict:
-    """BENCH ONLY: the OpenMP trace (oracle/omp_baseline.cpp) over a CSR snapshot
-    of the oracle's graph: best wall seconds of `reps` mark + sweep passes."""
-    lib = C.CDLL(OMP_LIB_PATH)
-    e = abi.CrgcGraphExport()
-    lib_o = g.lib
-    lib_o.oracle_export(g.h, C.byref(e))
-    nv, ne = int(e.n_vertices), int(e.n_edges)
-    ids, rc = np.zeros(nv, np.uint64), np.zeros(nv, np.int32)
-    fl, sup = np.zeros(nv, np.uint8), np.zeros(nv, np.uint64)
-    eo, et, ec = np.zeros(ne, np.uint64), np.zeros(ne, np.uint64), np.zeros(ne, np.int32)
-    e.vertex_cap, e.edge_cap = nv, ne
-    e.id, e.recv_count, e.flags, e.supervisor = _ptr(ids), _ptr(rc), _ptr(fl), _ptr(sup)
-    e.edge_owner, e.edge_target, e.edge_count = _ptr(eo), _ptr(et), _ptr(ec)
-    if lib_o.oracle_export(g.h, C.byref(e)) != abi.OK:
-        raise RuntimeError("oracle export failed")
-    best = C.c_double()
-    out = [C.c_uint64() for _ in range(4)]
-    P = C.c_void_p
-    lib.omp_trace_bench.argtypes = [C.c_uint64, P, P, P, P, C.c_uint64, P, P, P, C.c_int, C.c_int,
-                                    C.POINTER(C.c_double)] + [C.POINTER(C.c_uint64)] * 4
-    lib.omp_trace_bench.restype = C.c_int
-    if lib.omp_trace_bench(nv, _ptr(ids), _ptr(rc), _ptr(fl), _ptr(sup), ne, _ptr(eo), _ptr(et),
-                           _ptr(ec), threads, reps, C.byref(best), *[C.byref(x) for x in out]):
-        raise RuntimeError("omp baseline: malformed snapshot")
-    return {"seconds": best.value, "edges_scanned": out[0].value, "marked": out[1].value,
-            "garbage": out[2].value, "kill": out[3].value, "vertices": nv, "edges": ne}
+class OmpGraph:
+    """BENCH ONLY: the strong CPU baseline (oracle/omp_graph.cpp), a parallel
+    OpenMP merge + trace over the same entry batches.  Counts only."""
 
+    def __init__(self, F: int = 4, vertex_hint: int = 1 << 16, threads: int = 0):
+        build()
+        lib = C.CDLL(OMP_LIB_PATH)
+        lib.omp_graph_create.restype = C.c_void_p
+        lib.omp_graph_create.argtypes = [C.c_uint32, C.c_uint64]
+        lib.omp_graph_destroy.argtypes = [C.c_void_p]
+        lib.omp_graph_merge.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        lib.omp_graph_trace.argtypes = [C.c_void_p, C.c_int, C.c_int] + [C.POINTER(C.c_uint64)] * 5
+        self.lib, self.threads = lib, threads
+        self.h = lib.omp_graph_create(F, vertex_hint)
+
+    def close(self):
+        if self.h:
+            self.lib.omp_graph_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def merge_entries(self, batch):
+        rc = self.lib.omp_graph_merge(self.h, C.addressof(batch.struct()), self.threads)
+        if rc:
+            raise abi.CrgcError(rc, "omp_graph_merge")
+
+    def trace(self, should_kill: bool = True) -> dict:
+        v = [C.c_uint64() for _ in range(5)]
+        rc = self.lib.omp_graph_trace(self.h, int(should_kill), self.threads, *[C.byref(x) for x in v])
+        if rc:
+            raise abi.CrgcError(rc, "omp_graph_trace")
+        return dict(zip(("garbage", "kill", "live", "edges_scanned", "pseudo_roots"), (x.value for x in v)))

@@ -50,20 +50,3 @@ def test_golden_oracle(oracle_mod, path):
 @pytest.mark.parametrize("path", FIXTURES, ids=os.path.basename)
 def test_golden_hip(hip_mod, path):
     replay(hip_mod.ShadowGraph(), path)
-
-
-def test_omp_baseline_counts_match_oracle(oracle_mod):
-    """The bench's strong CPU baseline (oracle/omp_baseline.cpp, OpenMP BFS over a
-    CSR snapshot) traces the same graph to the oracle's garbage / kill counts."""
-    import world
-    w = world.World(seed=0x5EED + 11)
-    w.bulk_graph(20_000, 200_000, alpha=2.1, n_roots=20)
-    o = oracle_mod.OracleGraph()
-    for b in w.batches(1 << 16):
-        o.merge_entries(b)
-    o.trace(True)
-    o.merge_entries(w.wakeup_batch(5_000))
-    par = oracle_mod.omp_trace_baseline(o, threads=4, reps=2)
-    r = o.trace(True)
-    assert (par["garbage"], par["kill"]) == (len(r.garbage), len(r.kill))
-    assert par["marked"] == r.n_live
