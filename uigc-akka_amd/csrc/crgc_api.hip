@@ -44,7 +44,7 @@ void free_arrays(Arrays &a) {
   if (!a.allocated) return;
   DevGraph &d = a.d;
   void *ps[] = {d.htab, d.vid, d.recv, d.flags, d.sup, d.adj, d.ecap, d.vseq, d.sseq,
-                d.enew, d.pool, d.etab, d.edelta, d.vis, d.front[0], d.front[1],
+                d.pool, d.etab, d.vis, d.front[0], d.front[1],
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat, d.xbytes,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill,
                 d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.fx, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
@@ -89,10 +89,8 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   A(dmalloc(&d.ecap, c.scap));
   A(dmalloc(&d.vseq, c.scap));
   A(dmalloc(&d.sseq, c.scap));
-  A(dmalloc(&d.enew, c.scap));
   A(dmalloc(&d.pool, c.pcap));
   A(dmalloc(&d.etab, c.ecap));
-  A(dmalloc(&d.edelta, c.ecap));
   A(dmalloc(&d.vis, c.scap / 32));
   A(dmalloc(&d.front[0], c.scap));
   A(dmalloc(&d.front[1], c.scap));
@@ -141,9 +139,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   hipMemsetAsync(d.ecap, 0, c.scap * 4, s);
   hipMemsetAsync(d.vseq, 0, c.scap * 8, s);
   hipMemsetAsync(d.sseq, 0, c.scap * 8, s);
-  hipMemsetAsync(d.enew, 0, c.scap * 4, s);
   hipMemsetAsync(d.etab, 0xFF, c.ecap * sizeof(EdgeBucket), s);
-  hipMemsetAsync(d.edelta, 0, c.ecap * 4, s);
   hipMemsetAsync(d.vis, 0, c.scap / 8, s);
   hipMemsetAsync(d.front[0], 0, c.scap, s);
   hipMemsetAsync(d.front[1], 0, c.scap, s);
@@ -496,7 +492,31 @@ void crgc_destroy(crgc_graph *h) {
   delete h;
 }
 
-// Shared tail of every merge: the edge pipeline over the staged atoms.
+// Shared tail of every merge: the edge pipeline over the staged atoms
+// (crgc_edges.hip).  Partition geometry: 2..1024 hash buckets of slots (about
+// 256 slots each below that); <= 512 blocks of >= 1024 atoms.
+static void edge_geometry(const crgc_graph *h, uint64_t max_atoms, uint32_t &bshift, uint32_t &nbk,
+                          uint64_t &nblk) {
+  uint32_t lg = 0;
+  while ((1ull << lg) < h->g.d.scap) ++lg;
+  const uint32_t lk = lg > 18 ? 10u : (lg > 9 ? lg - 8 : 1u);
+  bshift = 32 - lk;
+  nbk = 1u << lk;
+  nblk = std::min<uint64_t>((max_atoms + 1023) / 1024, 512);
+}
+
+// Work scratch of a merge's atoms and its edge pipeline.
+static size_t edge_scratch(const crgc_graph *h, uint64_t max_atoms) {
+  uint32_t bshift, nbk;
+  uint64_t nblk;
+  edge_geometry(h, max_atoms, bshift, nbk, nblk);
+  const uint64_t nh = (uint64_t)nbk * nblk;
+  // the callers' atom arrays (o, t, d, exact count), then the pipeline's own
+  return Carver::need({max_atoms * 4, max_atoms * 4, max_atoms * 4, 8, nh * 4, nh * 8,
+                       ((nh + 1023) / 1024) * 4 * 8 + 64, 16, max_atoms * 8, max_atoms * 4, max_atoms * 4,
+                       max_atoms * 4, max_atoms * 4});
+}
+
 static int run_edges(crgc_graph *h, uint32_t *ao, uint32_t *at, int32_t *ad, uint64_t max_atoms,
                      Carver &cv, const uint64_t *n_atoms_dev = nullptr) {
   if (max_atoms == 0) return CRGC_OK;
@@ -506,20 +526,19 @@ static int run_edges(crgc_graph *h, uint32_t *ao, uint32_t *at, int32_t *ad, uin
   ea.atom_o = ao;
   ea.atom_t = at;
   ea.atom_d = ad;
-  ea.newlist = cv.take<uint64_t>(max_atoms);
-  ea.rrank = cv.take<uint32_t>(max_atoms);
-  ea.touched = cv.take<uint32_t>(max_atoms);
-  ea.rtouched = cv.take<uint32_t>(max_atoms);
-  ea.flips = cv.take<uint64_t>(max_atoms);
-  // n_touched, n_new_edges, n_rtouched, n_flips
-  hipMemsetAsync((char *)h->ctr + CTR_OFF(n_touched), 0, 4 * 8, h->stream);
+  edge_geometry(h, max_atoms, ea.bshift, ea.nbk, ea.nblk);
+  const uint64_t nh = (uint64_t)ea.nbk * ea.nblk;
+  ea.hist = cv.take<uint32_t>(nh);
+  ea.hoff = cv.take<uint64_t>(nh);
+  ea.bsum = cv.take<uint64_t>(((nh + 1023) / 1024) * 4 + 8);
+  ea.tot = cv.take<unsigned long long>(2);
+  ea.pk = cv.take<uint64_t>(max_atoms);
+  ea.pv = cv.take<uint32_t>(max_atoms);
+  ea.rv_t = cv.take<uint32_t>(max_atoms);
+  ea.rv_o = cv.take<uint32_t>(max_atoms);
+  ea.rv_b = cv.take<uint32_t>(max_atoms);
   HIP_TRY(launch_edges(h->g.d, ea, h->stream));
   return CRGC_OK;
-}
-
-static size_t edge_scratch(uint64_t max_atoms) {
-  return Carver::need({max_atoms * 4, max_atoms * 4, max_atoms * 4, max_atoms * 8, max_atoms * 4,
-                       max_atoms * 4, max_atoms * 4, max_atoms * 4, max_atoms * 4, max_atoms * 8});
 }
 
 }  // extern "C"
@@ -719,7 +738,7 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   const size_t work_bytes =
       Carver::need({n * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4, sh ? n : 0,
                     sh ? n * h->F * 8 : 0, 8}) +
-      edge_scratch(max_atoms);
+      edge_scratch(h, max_atoms);
   if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
     return CRGC_E_NOMEM;
   Carver sc(h->stage.ptr), wc(h->work.ptr);
@@ -1004,7 +1023,7 @@ static int merge_deltas_one(crgc_graph *h, const crgc_delta_batch *b, uint64_t n
   const bool sh = h->tp;
   const size_t work_bytes =
       Carver::need({n * 4, n * 4, std::max<uint64_t>(nout, 1) * 4, sh ? std::max<uint64_t>(nout, 1) * 8 : 0}) +
-      edge_scratch(nout);
+      edge_scratch(h, nout);
   if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
     return CRGC_E_NOMEM;
   Carver sc(h->stage.ptr), wc(h->work.ptr);
@@ -1104,7 +1123,7 @@ int crgc_merge_undo(crgc_graph *h, const crgc_undo_log *log) {
   for (uint64_t i = 0; i < n; ++i)
     for (uint32_t k = log->created_off[i]; k < log->created_off[i + 1]; ++k) c_actor[k] = log->actor[i];
   const size_t host_bytes = Carver::need({n * 8, n * 4, (n + 1) * 4, nc * 8, nc * 4, nc * 8});
-  const size_t work_bytes = edge_scratch(nc) + Carver::need({n + nc + 8});
+  const size_t work_bytes = edge_scratch(h, nc) + Carver::need({n + nc + 8});
   if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
     return CRGC_E_NOMEM;
   Carver sc(h->stage.ptr), wc(h->work.ptr);

@@ -1,0 +1,462 @@
+// crgc_edges.hip — the edge pipeline: outgoing[o][t] += d for a merge's edge
+// atoms (ShadowGraph.updateOutgoing, ShadowGraph.java:64-73), as a partition by
+// owner, then a segmented reduce with LDS-staged atomics per owner range.
+//
+// Absent == 0: a pair whose deltas sum to 0 changes nothing; zero counts that
+// result from a merge are kept in their segment (never traced, never counted:
+// nzdeg tracks the reference's outgoing.size(), :231) until a rebuild drops them.
+//
+//   1. k_ep_count / run_scan / k_ep_scatter: the atoms, partitioned by owner
+//      (a hash of the slot to one of <= 1024 buckets; an LDS histogram per
+//      block of atoms, a bucket-major scan of the block x bucket counts, a
+//      scatter; <= 512 blocks split the exact atom count between them).
+//   2. k_ep_owner: one workgroup per owner bucket — every atom of an owner is
+//      in its workgroup, so the owner's segment, degree and nonzero count are
+//      written without atomics.  512 atoms at a time: the pairs are reduced in
+//      an LDS hash table (LDS atomics); each distinct pair finds or inserts its
+//      edge-table key; existing edges take the summed delta (a count that
+//      changes sign updates its reverse candidate in place); new edges get a
+//      rank among their owner's new edges (LDS atomics on an LDS owner table),
+//      each owner's segment grows once (one pool allocation per workgroup per
+//      round) and the new edges are written after its old degree.  Every new
+//      edge leaves a reverse atom (target, owner | RC_POS, edge-table bucket).
+//   3. The same partition by target, then k_ep_target: one workgroup per
+//      target bucket appends the new reverse candidates (ranks by LDS atomics,
+//      one growth per target per round) and records their index in the edge
+//      table (`rev`, which later sign changes use).
+// Pool, candidate pool and edge-table sizes follow the same bounds as before
+// (ensure_capacity in crgc_api.hip).
+#include "crgc_host.hpp"
+
+namespace crgc {
+
+constexpr int EP_THREADS = 256;     // partition kernels
+constexpr int EP_WG = 512;          // owner / target range kernels
+constexpr uint32_t EP_CH = 512;     // atoms per round in a bucket workgroup (one per thread)
+constexpr uint32_t EP_TAB = 1024;   // LDS pair / owner tables (load <= 1/2)
+constexpr uint32_t EP_EXIST = 0xFFFFFFFFu;
+constexpr uint32_t EP_SKIP = 0xFFFFFFFEu;
+constexpr uint32_t EP_PENDING = 0x80000000u;  // etab rev: reverse atom (position) not yet appended
+constexpr uint32_t EP_SMALL_COPY = 8;
+
+__device__ inline bool ep_valid(uint32_t s) { return s < 0xFFFFFFF0u; }
+
+__device__ inline uint32_t seg_cap_ep(uint32_t need) {
+  uint32_t c = 4;
+  while (c < need) c <<= 1;
+  return c;
+}
+
+// ---- 1. partition ------------------------------------------------------------
+// Slots go to buckets by a multiplicative hash: fresh slots are contiguous and
+// take most of a wakeup's atoms, so ranges of slots would load a few buckets.
+__device__ inline uint32_t ep_bucket(const EdgeArgs &a, uint32_t slot) {
+  return (slot * 0x9E3779B1u) >> a.bshift;
+}
+
+// REV = false: atoms (ao, at, ad), key o << 32 | t, bucket of o.
+// REV = true : reverse atoms (rv_t, rv_o, rv_b), key t << 32 | (o | RC_POS),
+//              bucket of t; rv_t == ~0 marks an unused position.
+template <bool REV>
+__device__ inline bool ep_atom(const EdgeArgs &a, uint64_t i, uint64_t n, uint32_t &bucket, uint64_t &key,
+                               uint32_t &val) {
+  if (i >= n) return false;
+  if (REV) {
+    const uint32_t t = a.rv_t[i];
+    if (t == 0xFFFFFFFFu) return false;
+    bucket = ep_bucket(a, t);
+    key = ((uint64_t)t << 32) | a.rv_o[i];
+    val = a.rv_b[i];
+    return true;
+  }
+  const int32_t d = a.atom_d[i];
+  const uint32_t o = a.atom_o[i], t = a.atom_t[i];
+  if (d == 0 || !ep_valid(o) || !ep_valid(t)) return false;
+  bucket = ep_bucket(a, o);
+  key = ((uint64_t)o << 32) | t;
+  val = (uint32_t)d;
+  return true;
+}
+
+// Atoms to partition: the merge's (exact count when the device has it), or
+// the reverse atoms, which fill the forward partition's [0, total).
+template <bool REV>
+__device__ inline uint64_t ep_count(const EdgeArgs &a) {
+  if (REV) return a.tot[0];
+  return a.n_atoms_dev ? *a.n_atoms_dev : a.max_atoms;
+}
+
+// [begin, end) of bucket b in the partition (its total ends the last bucket)
+__device__ inline uint64_t ep_end(const EdgeArgs &a, uint32_t b, int which) {
+  return b + 1 == a.nbk ? a.tot[which] : a.hoff[(uint64_t)(b + 1) * a.nblk];
+}
+
+template <bool REV>
+__global__ __launch_bounds__(EP_THREADS) void k_ep_count(EdgeArgs a) {
+  extern __shared__ uint32_t hist[];  // [nbk]
+  const uint64_t n = ep_count<REV>(a);
+  for (uint32_t k = threadIdx.x; k < a.nbk; k += EP_THREADS) hist[k] = 0;
+  __syncthreads();
+  const uint64_t per = (n + a.nblk - 1) / a.nblk;
+  const uint64_t i0 = (uint64_t)blockIdx.x * per, i1 = min(n, i0 + per);
+  for (uint64_t i = i0 + threadIdx.x; i < i1; i += EP_THREADS) {
+    uint32_t b;
+    uint64_t key;
+    uint32_t val;
+    if (ep_atom<REV>(a, i, n, b, key, val)) atomicAdd(&hist[b], 1u);
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < a.nbk; k += EP_THREADS) a.hist[(uint64_t)k * a.nblk + blockIdx.x] = hist[k];
+}
+
+template <bool REV>
+__global__ __launch_bounds__(EP_THREADS) void k_ep_scatter(EdgeArgs a) {
+  extern __shared__ uint32_t cur[];  // [nbk]
+  const uint64_t n = ep_count<REV>(a);
+  for (uint32_t k = threadIdx.x; k < a.nbk; k += EP_THREADS) cur[k] = 0;
+  __syncthreads();
+  const uint64_t per = (n + a.nblk - 1) / a.nblk;
+  const uint64_t i0 = (uint64_t)blockIdx.x * per, i1 = min(n, i0 + per);
+  for (uint64_t i = i0 + threadIdx.x; i < i1; i += EP_THREADS) {
+    uint32_t b;
+    uint64_t key;
+    uint32_t val;
+    if (!ep_atom<REV>(a, i, n, b, key, val)) continue;
+    const uint64_t at = a.hoff[(uint64_t)b * a.nblk + blockIdx.x] + atomicAdd(&cur[b], 1u);
+    a.pk[at] = key;
+    a.pv[at] = val;
+  }
+}
+
+// ---- 2. owner buckets --------------------------------------------------------
+// A segment that outgrows its capacity moves to a new power-of-two segment:
+// a short one is copied by its own lane, longer ones by the whole wave.  Every
+// lane of the wave calls (r = ~0: nothing to move).
+template <typename T>
+__device__ inline void ep_move(T *pool, uint32_t from, uint32_t len, uint32_t r) {
+  const bool mv = r != 0xFFFFFFFFu;
+  const bool small = mv && len <= EP_SMALL_COPY;
+  if (small) {
+    T x[EP_SMALL_COPY];
+#pragma unroll
+    for (uint32_t e = 0; e < EP_SMALL_COPY; ++e)
+      if (e < len) x[e] = pool[(uint64_t)from + e];
+#pragma unroll
+    for (uint32_t e = 0; e < EP_SMALL_COPY; ++e)
+      if (e < len) pool[(uint64_t)r + e] = x[e];
+  }
+  uint64_t big = __ballot(mv && !small);
+  while (big) {
+    const int k = __ffsll((unsigned long long)big) - 1;
+    big &= big - 1;
+    const uint32_t rk = __shfl(r, k), xk = __shfl(from, k), yk = __shfl(len, k);
+    for (uint32_t e = lane_id(); e < yk; e += 64) pool[(uint64_t)rk + e] = pool[(uint64_t)xk + e];
+  }
+}
+
+struct EpOwnerLds {
+  uint64_t key[EP_TAB];   // pair o << 32 | t
+  int32_t sum[EP_TAB];
+  uint32_t rank[EP_TAB];  // rank among the owner's new edges, EP_EXIST, or EP_SKIP
+  uint32_t bkt[EP_TAB];   // edge-table bucket
+  uint32_t okey[EP_TAB];  // owner table: owner slot (~0: free)
+  uint32_t ocnt[EP_TAB];  // new edges of the owner in this round
+  uint32_t obase[EP_TAB]; // the owner's degree before them
+  int32_t onz[EP_TAB];    // change of the owner's nonzero count
+  uint32_t plist[EP_CH];  // pair table entries in use
+  uint32_t olist[EP_CH];  // owner table entries in use
+  uint32_t np, nol, nnew, nrv;
+};
+
+__device__ inline uint32_t ep_owner_slot(EpOwnerLds &L, uint32_t o) {
+  uint32_t h = (uint32_t)mix64(o) & (EP_TAB - 1);
+  for (;;) {
+    const uint32_t k = atomicCAS(&L.okey[h], 0xFFFFFFFFu, o);
+    if (k == 0xFFFFFFFFu) {
+      L.olist[atomicAdd(&L.nol, 1u)] = h;
+      return h;
+    }
+    if (k == o) return h;
+    h = (h + 1) & (EP_TAB - 1);
+  }
+}
+
+// All of a bucket's atoms are in one workgroup, hence every edge of its owners:
+// the owners' segments, degrees and nonzero counts are written without atomics.
+// Workgroup-scope visibility of earlier rounds' global writes (edge-table
+// values, degrees) is the barrier's (one CU, one L1).
+__global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
+  __shared__ EpOwnerLds L;
+  const uint32_t b = blockIdx.x;
+  const uint64_t a0 = a.hoff[(uint64_t)b * a.nblk], a1 = ep_end(a, b, 0);
+  if (a0 == a1) return;
+  if (threadIdx.x == 0) L.nrv = 0;
+  for (uint32_t k = threadIdx.x; k < EP_TAB; k += EP_WG) {
+    L.key[k] = KEY_EMPTY;
+    L.sum[k] = 0;
+    L.okey[k] = 0xFFFFFFFFu;
+    L.ocnt[k] = 0;
+    L.onz[k] = 0;
+  }
+  Counters *c = g.ctr;
+  unsigned long long *const tops[1] = {&c->pool_top};
+  const uint32_t tid = threadIdx.x;
+  for (uint64_t c0 = a0; c0 < a1; c0 += EP_CH) {
+    const uint32_t m = (uint32_t)min((uint64_t)EP_CH, a1 - c0);
+    if (tid == 0) L.np = L.nol = L.nnew = 0;
+    __syncthreads();
+    // reduce the round's atoms (one per thread) per pair
+    if (tid < m) {
+      const uint64_t key = a.pk[c0 + tid];
+      uint32_t h = (uint32_t)mix64(key) & (EP_TAB - 1);
+      for (;;) {
+        const uint64_t k = atomicCAS((unsigned long long *)&L.key[h], (unsigned long long)KEY_EMPTY,
+                                     (unsigned long long)key);
+        if (k == KEY_EMPTY) L.plist[atomicAdd(&L.np, 1u)] = h;
+        if (k == KEY_EMPTY || k == key) break;
+        h = (h + 1) & (EP_TAB - 1);
+      }
+      atomicAdd(&L.sum[h], (int32_t)a.pv[c0 + tid]);
+    }
+    __syncthreads();
+    // each distinct pair (one per thread): its edge-table key; existing edges take the sum
+    const uint32_t np = L.np;
+    const uint32_t ph = tid < np ? L.plist[tid] : 0;
+    if (tid < np) {
+      const uint64_t key = L.key[ph];
+      uint32_t rk = EP_SKIP;
+      const int32_t d = L.sum[ph];
+      if (d != 0) {  // absent == 0: a zero sum changes nothing
+        const uint32_t o = (uint32_t)(key >> 32), t = (uint32_t)key;
+        bool ins = false;
+        uint32_t v = 0;
+        const uint64_t bk = edge_find_or_insert(g, key, &ins, &v);
+        if (bk != KEY_EMPTY) {  // else the table is full: ERR_ETAB_FULL is set
+          L.bkt[ph] = (uint32_t)bk;
+          const uint32_t oh = ep_owner_slot(L, o);
+          if (!ins) {
+            int32_t *p = edge_count_ptr(g.pool, (uint64_t)g.adj[o].x + v);
+            const int32_t old = *p;
+            const int32_t now = (int32_t)((uint32_t)old + (uint32_t)d);
+            *p = now;
+            if ((old != 0) != (now != 0)) atomicAdd(&L.onz[oh], now != 0 ? 1 : -1);
+            if ((old > 0) != (now > 0)) {  // the reverse candidate follows the count's sign
+              const uint32_t r = g.etab[bk].rev;
+              const uint32_t cand = o | (now > 0 ? RC_POS : 0u);
+              if (r != 0xFFFFFFFFu && (r & EP_PENDING)) a.rv_o[a0 + (r & ~EP_PENDING)] = cand;
+              else if (r < g.rcap[t]) g.rpool[(uint64_t)g.radj[t].x + r] = cand;
+            }
+            rk = EP_EXIST;
+          } else {
+            rk = atomicAdd(&L.ocnt[oh], 1u);
+            atomicAdd(&L.nnew, 1u);
+          }
+        }
+      }
+      L.rank[ph] = rk;
+    }
+    __syncthreads();
+    // owners with new edges (one per thread): one growth each, one pool
+    // allocation per workgroup
+    {
+      const uint32_t nol = L.nol;
+      const uint32_t oh = tid < nol ? L.olist[tid] : 0;
+      const uint32_t o = tid < nol ? L.okey[oh] : 0;
+      const uint32_t nn = tid < nol ? L.ocnt[oh] : 0;
+      uint2 ad = make_uint2(0, 0);
+      uint32_t want = 0;
+      if (nn) {
+        ad = g.adj[o];
+        if (ad.y + nn > g.ecap[o]) want = seg_cap_ep(ad.y + nn);
+      }
+      const uint32_t v1[1] = {want};
+      unsigned long long offs[1];
+      block_append<1>(tops, v1, offs);
+      uint32_t r = 0xFFFFFFFFu, add = nn;
+      if (want) {
+        if (offs[0] + want > g.pcap) {
+          set_err(c, ERR_POOL_FULL);  // the owner's new edges are dropped
+          add = 0;
+        } else {
+          r = (uint32_t)offs[0];
+        }
+      }
+      ep_move(g.pool, ad.x, ad.y, r);
+      if (tid < nol) {
+        if (r != 0xFFFFFFFFu) {
+          ad.x = r;
+          g.ecap[o] = want;
+        }
+        L.ocnt[oh] = add;
+        L.obase[oh] = ad.y;
+        if (add) g.adj[o] = make_uint2(ad.x, ad.y + add);
+        const int32_t dz = L.onz[oh] + (int32_t)add;  // new edges have nonzero counts
+        if (dz) g.nzdeg[o] = (uint32_t)((int32_t)g.nzdeg[o] + dz);
+      }
+    }
+    __syncthreads();
+    // the new edges, after their owner's old degree; one reverse atom each
+    if (tid < np) {
+      const uint32_t rk = L.rank[ph];
+      const uint64_t key = L.key[ph];
+      if (rk < EP_SKIP) {  // not EP_SKIP / EP_EXIST
+        const uint32_t o = (uint32_t)(key >> 32), t = (uint32_t)key;
+        const uint32_t oh = ep_owner_slot(L, o);
+        if (L.ocnt[oh]) {  // else the pool is full (error set)
+          const uint32_t idx = L.obase[oh] + rk;
+          const int32_t d = L.sum[ph];
+          const uint32_t bk = L.bkt[ph];
+          g.pool[(uint64_t)g.adj[o].x + idx] = pack_edge(t, d);
+          const uint32_t q = atomicAdd(&L.nrv, 1u);
+          g.etab[bk].val = idx;
+          g.etab[bk].rev = EP_PENDING | q;
+          a.rv_t[a0 + q] = t;
+          a.rv_o[a0 + q] = o | (d > 0 ? RC_POS : 0u);
+          a.rv_b[a0 + q] = bk;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0 && L.nnew) atomicAdd(&c->etab_used, (unsigned long long)L.nnew);
+    if (tid < np) {
+      L.key[ph] = KEY_EMPTY;
+      L.sum[ph] = 0;
+    }
+    if (tid < L.nol) {
+      const uint32_t oh = L.olist[tid];
+      L.okey[oh] = 0xFFFFFFFFu;
+      L.ocnt[oh] = 0;
+      L.onz[oh] = 0;
+    }
+    __syncthreads();
+  }
+  // the rest of the bucket's region holds no reverse atom
+  for (uint64_t i = a0 + L.nrv + tid; i < a1; i += EP_WG) a.rv_t[i] = 0xFFFFFFFFu;
+}
+
+// ---- 3. target buckets -------------------------------------------------------
+struct EpTargetLds {
+  uint32_t tkey[EP_TAB];  // target table: target slot (~0: free)
+  uint32_t tcnt[EP_TAB];  // new candidates of the target in this round
+  uint32_t tbase[EP_TAB]; // its candidate count before them
+  uint32_t toff[EP_TAB];  // its candidate segment
+  uint32_t tlist[EP_CH];
+  uint32_t ntl;
+};
+
+__device__ inline uint32_t ep_target_slot(EpTargetLds &L, uint32_t t) {
+  uint32_t h = (uint32_t)mix64(t) & (EP_TAB - 1);
+  for (;;) {
+    const uint32_t k = atomicCAS(&L.tkey[h], 0xFFFFFFFFu, t);
+    if (k == 0xFFFFFFFFu) {
+      L.tlist[atomicAdd(&L.ntl, 1u)] = h;
+      return h;
+    }
+    if (k == t) return h;
+    h = (h + 1) & (EP_TAB - 1);
+  }
+}
+
+__global__ __launch_bounds__(EP_WG) void k_ep_target(DevGraph g, EdgeArgs a) {
+  __shared__ EpTargetLds L;
+  const uint32_t b = blockIdx.x;
+  const uint64_t a0 = a.hoff[(uint64_t)b * a.nblk], a1 = ep_end(a, b, 1);
+  if (a0 == a1) return;
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t k = tid; k < EP_TAB; k += EP_WG) {
+    L.tkey[k] = 0xFFFFFFFFu;
+    L.tcnt[k] = 0;
+  }
+  Counters *c = g.ctr;
+  unsigned long long *const tops[1] = {&c->rpool_top};
+  for (uint64_t c0 = a0; c0 < a1; c0 += EP_CH) {
+    const uint32_t m = (uint32_t)min((uint64_t)EP_CH, a1 - c0);
+    if (tid == 0) L.ntl = 0;
+    __syncthreads();
+    uint64_t key = 0;
+    uint32_t th = 0, rank = 0;
+    if (tid < m) {
+      key = a.pk[c0 + tid];
+      th = ep_target_slot(L, (uint32_t)(key >> 32));
+      rank = atomicAdd(&L.tcnt[th], 1u);
+    }
+    __syncthreads();
+    {
+      const uint32_t ntl = L.ntl;
+      const uint32_t sh = tid < ntl ? L.tlist[tid] : 0;
+      const uint32_t t = tid < ntl ? L.tkey[sh] : 0;
+      const uint32_t nn = tid < ntl ? L.tcnt[sh] : 0;
+      uint2 rd = make_uint2(0, 0);
+      uint32_t want = 0;
+      if (nn) {
+        rd = g.radj[t];
+        if (rd.y + nn > g.rcap[t]) want = seg_cap_ep(rd.y + nn);
+      }
+      const uint32_t v1[1] = {want};
+      unsigned long long offs[1];
+      block_append<1>(tops, v1, offs);
+      uint32_t r = 0xFFFFFFFFu, add = nn;
+      if (want) {
+        if (offs[0] + want > g.rpcap) {
+          set_err(c, ERR_POOL_FULL);
+          add = 0;
+        } else {
+          r = (uint32_t)offs[0];
+        }
+      }
+      ep_move(g.rpool, rd.x, rd.y, r);
+      if (tid < ntl) {
+        if (r != 0xFFFFFFFFu) {
+          rd.x = r;
+          g.rcap[t] = want;
+        }
+        L.tcnt[sh] = add;
+        L.tbase[sh] = rd.y;
+        L.toff[sh] = rd.x;
+        if (add) g.radj[t] = make_uint2(rd.x, rd.y + add);
+      }
+    }
+    __syncthreads();
+    if (tid < m && L.tcnt[th]) {
+      const uint32_t idx = L.tbase[th] + rank;
+      g.rpool[(uint64_t)L.toff[th] + idx] = (uint32_t)key;
+      g.etab[a.pv[c0 + tid]].rev = idx;
+    }
+    __syncthreads();
+    if (tid < L.ntl) {
+      const uint32_t sh = L.tlist[tid];
+      L.tkey[sh] = 0xFFFFFFFFu;
+      L.tcnt[sh] = 0;
+    }
+    __syncthreads();
+  }
+}
+
+// ---- driver --------------------------------------------------------------------
+hipError_t launch_edges(const DevGraph &g, const EdgeArgs &a, hipStream_t s) {
+  if (a.max_atoms == 0) return hipSuccess;
+  const size_t lds_hist = (size_t)a.nbk * 4;
+  const dim3 pgrid((unsigned)a.nblk);
+  ScanSet q{};
+  q.k = 1;
+  q.n = (uint64_t)a.nbk * a.nblk;
+  q.nb = (q.n + 1023) / 1024;
+  q.in[0] = a.hist;
+  q.out[0] = a.hoff;
+  q.total[0] = a.tot;
+  q.bsum = a.bsum;
+  // forward: partition by owner, then the owner ranges
+  hipLaunchKernelGGL(k_ep_count<false>, pgrid, dim3(EP_THREADS), lds_hist, s, a);
+  if (hipError_t e = run_scan(q, s)) return e;
+  hipLaunchKernelGGL(k_ep_scatter<false>, pgrid, dim3(EP_THREADS), lds_hist, s, a);
+  hipLaunchKernelGGL(k_ep_owner, dim3(a.nbk), dim3(EP_WG), 0, s, g, a);
+  // reverse: the new edges' candidates, partitioned by target
+  hipLaunchKernelGGL(k_ep_count<true>, pgrid, dim3(EP_THREADS), lds_hist, s, a);
+  q.total[0] = a.tot + 1;
+  if (hipError_t e = run_scan(q, s)) return e;
+  hipLaunchKernelGGL(k_ep_scatter<true>, pgrid, dim3(EP_THREADS), lds_hist, s, a);
+  hipLaunchKernelGGL(k_ep_target, dim3(a.nbk), dim3(EP_WG), 0, s, g, a);
+  return hipGetLastError();
+}
+
+}  // namespace crgc

@@ -141,11 +141,16 @@ struct EdgeArgs {
   const uint32_t *atom_o;
   const uint32_t *atom_t;
   const int32_t *atom_d;
-  uint64_t *newlist;   // [max_atoms] buckets of new edge keys
-  uint32_t *rrank;     // [max_atoms] rank of each new key among its target's new candidates
-  uint32_t *touched;   // [max_atoms] owners that got new edges
-  uint32_t *rtouched;  // [max_atoms] targets that got new candidates
-  uint64_t *flips;     // [max_atoms] buckets of edges whose count changed sign
+  // partition (crgc_edges.hip): nbk = 2^(32 - bshift) buckets, nblk blocks of atoms
+  uint32_t bshift, nbk;
+  uint64_t nblk;
+  uint32_t *hist;            // [nbk * nblk] bucket-major block counts
+  uint64_t *hoff;            // [nbk * nblk] their exclusive scan
+  uint64_t *bsum;            // scan scratch
+  unsigned long long *tot;   // [2] atoms in the forward / reverse partition
+  uint64_t *pk;              // [max_atoms] partitioned keys
+  uint32_t *pv;              // [max_atoms] partitioned deltas / edge-table buckets
+  uint32_t *rv_t, *rv_o, *rv_b;  // [max_atoms] reverse atoms: target, owner | RC_POS, bucket
 };
 
 constexpr uint32_t LV_PULL = 4;                // dense levels scan in-candidates (pull)

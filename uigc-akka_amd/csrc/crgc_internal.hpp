@@ -27,7 +27,6 @@ constexpr uint64_t KEY_TOMB = 0xFFFFFFFFFFFFFFFEull;
 constexpr uint32_t SLOT_NONE = 0xFFFFFFFFu;  // Java null supervisor
 constexpr uint32_t SLOT_DEAD = 0xFFFFFFFEu;  // supervisor collected (post-rebuild)
 constexpr uint32_t VAL_PENDING = 0xFFFFFFFFu;
-constexpr uint32_t EVAL_NEW = 0x80000000u;   // eval: edge inserted in this merge
 constexpr uint32_t RC_POS = 0x80000000u;     // reverse candidate: the edge's count is > 0
 
 // flags bits: ALIVE is internal; the rest equal CRGC_F_* of include/crgc.h
@@ -65,10 +64,6 @@ struct Counters {
   unsigned long long rpool_top;      // next free reverse-candidate entry
   unsigned long long etab_used;      // edge-table keys ever inserted
   // per-merge lists (reset together before every edge pipeline)
-  unsigned long long n_touched;      // owners with new edges in this merge
-  unsigned long long n_new_edges;    // new edge keys in this merge
-  unsigned long long n_rtouched;     // targets with new candidates in this merge
-  unsigned long long n_flips;        // existing edges whose count changed sign in this merge
   unsigned long long err;
   unsigned long long spin_max;
   // trace
@@ -107,8 +102,9 @@ struct alignas(16) IdBucket {
 };
 struct alignas(16) EdgeBucket {
   uint64_t key;  // owner << 32 | target
-  uint32_t val;  // entry index in the owner's segment (EVAL_NEW | rank during a merge)
-  uint32_t rev;  // entry index in the target's reverse-candidate segment
+  uint32_t val;  // entry index in the owner's segment
+  uint32_t rev;  // entry index in the target's reverse-candidate segment (during a merge,
+                 // 0x80000000 | reverse-atom position until it is appended)
 };
 
 __device__ inline uint64_t bucket_key(const uint4 &b) { return (uint64_t)b.x | ((uint64_t)b.y << 32); }
@@ -130,13 +126,12 @@ struct DevGraph {
   uint32_t *ecap;
   unsigned long long *vseq;  // last-write-wins tag for busy/root
   unsigned long long *sseq;  // last-write-wins tag for supervisor
-  uint32_t *enew;            // new edges per owner in the current merge
   uint32_t *nzdeg;           // out-edges with count != 0 (reference `outgoing.size()`)
   // reverse candidates (pull BFS): owners that ever created an edge key to the
   // slot; a candidate is verified against the forward count when used
   uint2 *radj;               // {offset, length} into rpool
   uint32_t *rcap;
-  uint32_t *rnew;            // new candidates per target in the current merge
+  uint32_t *rnew;            // rebuild scratch: in-degree per target
   uint32_t *rpool;           // owner slot | RC_POS while count(owner -> slot) > 0
   uint64_t rpcap;
   uint32_t *fx;              // expandable frontier bitmap (frontier & !halted)
@@ -151,7 +146,6 @@ struct DevGraph {
   uint64_t *pool;
   uint64_t ecap_tab, emask;
   EdgeBucket *etab;
-  int32_t *edelta;
   // trace
   uint32_t *vis;
   uint8_t *front[2];
@@ -434,8 +428,7 @@ __device__ inline uint64_t edge_key(uint32_t owner, uint32_t target) {
 }
 
 // Returns the bucket of `key`; *inserted tells whether this thread created it,
-// *val is the bucket's value as loaded (a key created during the current merge
-// reads as EVAL_NEW | rank, or as the all-ones fill before its rank is stored).
+// *val is the bucket's value as loaded.
 __device__ inline uint64_t edge_find_or_insert(const DevGraph &g, uint64_t key, bool *inserted,
                                                uint32_t *val) {
   uint64_t h = mix64(key) & g.emask;

@@ -349,245 +349,13 @@ hipError_t launch_undo_apply(const DevGraph &g, const UndoArgs &a, uint64_t slot
   return hipGetLastError();
 }
 
-// ---------------------------------------------------------------------------
-// Edge pipeline — outgoing[o][t] += d  (ShadowGraph.updateOutgoing, :64-73).
-// Absent == 0, so zero counts are simply kept (they are never traced) until a
-// rebuild drops them; nzdeg[o] tracks how many of o's counts are nonzero (the
-// reference's outgoing.size(), :231) so traced-edge counts stay exact.
-//   1. k_edge_apply: find-or-insert (o,t) in the edge table.  Existing edges
-//      get a memory-side atomic add on their pool count; keys new in this merge
-//      accumulate in edelta[bucket], take a rank among the owner's new edges and
-//      among the target's new reverse candidates.
-//   2. k_seg_grow:  owners (targets) whose forward (candidate) segment
-//      overflows get a new power-of-two segment (one atomic per workgroup)
-//      and are copied there; both directions in one launch.
-//   3. k_edge_append: new edges written after the owner's old degree, the
-//      owner appended to the target's candidate list.
-//   4. k_edge_post: degrees advance, per-merge counters reset, candidate
-//      entries of sign-changed counts refreshed.
-// ---------------------------------------------------------------------------
-constexpr int EDGE_THREADS = 1024;
-
-__global__ __launch_bounds__(EDGE_THREADS) void k_edge_apply(DevGraph g, EdgeArgs a) {
-  const uint64_t n = a.n_atoms_dev ? *a.n_atoms_dev : a.max_atoms;
-  const uint64_t stride = (uint64_t)gridDim.x * EDGE_THREADS;
-  Counters *c = g.ctr;
-  unsigned long long *const lists[5] = {&c->n_new_edges, &c->n_touched, &c->n_rtouched,
-                                        &c->n_flips, &c->etab_used};
-  for (uint64_t base = (uint64_t)blockIdx.x * EDGE_THREADS; base < n; base += stride) {
-    const uint64_t i = base + threadIdx.x;
-    const bool valid = i < n;
-    uint32_t o = 0, t = 0;
-    int32_t d = 0;
-    if (valid) {
-      o = a.atom_o[i];
-      t = a.atom_t[i];
-      d = a.atom_d[i];
-    }
-    bool active = valid && d != 0 && vs(o) && vs(t);
-    bool ins = false, flip = false;
-    uint64_t b = 0;
-    uint32_t v = 0;
-    if (active) {
-      b = edge_find_or_insert(g, edge_key(o, t), &ins, &v);
-      if (b == KEY_EMPTY) active = ins = false;
-    }
-    uint32_t rank = 0, rrank = 0;
-    if (ins) {
-      rank = atomicAdd(&g.enew[o], 1u);
-      rrank = atomicAdd(&g.rnew[t], 1u);
-      g.etab[b].val = EVAL_NEW | rank;
-      atomicAdd(&g.edelta[b], d);
-    } else if (active) {
-      if (v & EVAL_NEW) {
-        atomicAdd(&g.edelta[b], d);
-      } else {
-        const int32_t old = atomicAdd(edge_count_ptr(g.pool, (uint64_t)g.adj[o].x + v), d);
-        const int32_t now = (int32_t)((uint32_t)old + (uint32_t)d);
-        if ((old != 0) != (now != 0)) atomicAdd(&g.nzdeg[o], now != 0 ? 1u : 0xFFFFFFFFu);
-        flip = (old > 0) != (now > 0);
-      }
-    }
-    // List appends, one atomic per list per workgroup.  Sign changes of
-    // existing counts: their candidate entries are refreshed from the final
-    // count after the merge (k_edge_post).
-    const bool first = ins && rank == 0, rfirst = ins && rrank == 0;
-    const uint32_t cnt[5] = {ins, first, rfirst, flip, ins};
-    unsigned long long at[5];
-    block_append<5>(lists, cnt, at);
-    if (ins) {
-      a.newlist[at[0]] = b;
-      a.rrank[at[0]] = rrank;
-    }
-    if (first) a.touched[at[1]] = o;
-    if (rfirst) a.rtouched[at[2]] = t;
-    if (flip) a.flips[at[3]] = b;
-  }
-}
-
-__device__ inline uint32_t seg_cap(uint32_t need) {
-  uint32_t c = 4;
-  while (c < need) c <<= 1;
-  return c;
-}
-
-// One direction's segmented store: forward edges (u64) or reverse candidates (u32).
-template <typename T>
-struct Seg {
-  uint2 *adj;
-  uint32_t *cap;
-  uint32_t *nnew;
-  T *pool;
-  uint64_t pcap;
-  unsigned long long *top;
-  const unsigned long long *ntouched;
-  const uint32_t *touched;
-};
-
-// Owners (targets) whose forward (candidate) segment overflows get a new
-// power-of-two segment and are copied there, in one pass: the pool allocation
-// is one atomic per workgroup (block_append); each lane tests one touched
-// owner, a segment of <= SEG_LANE_COPY entries is copied by its own lane,
-// longer ones by the whole wave one after another.  Both directions run in
-// one launch (the first half of the grid forward, the second reverse).
-constexpr uint32_t SEG_LANE_COPY = 8;
-constexpr int SEG_THREADS = 256;
-
-template <typename T>
-__device__ inline void seg_grow(Seg<T> s, Counters *c, uint32_t blk, uint32_t nblk) {
-  const uint64_t n = *s.ntouched;
-  unsigned long long *const tops[1] = {s.top};
-  const int lane = lane_id();
-  for (uint64_t base = (uint64_t)blk * SEG_THREADS; base < n; base += (uint64_t)nblk * SEG_THREADS) {
-    const uint64_t i = base + threadIdx.x;
-    const uint32_t o = i < n ? s.touched[i] : 0;
-    const uint2 ad = i < n ? s.adj[o] : make_uint2(0, 0);
-    const uint32_t nn = i < n ? s.nnew[o] : 0;
-    const uint32_t need = ad.y + nn;
-    const uint32_t want = (i < n && need > s.cap[o]) ? seg_cap(need) : 0u;
-    const uint32_t v[1] = {want};
-    unsigned long long offs[1];
-    block_append<1>(tops, v, offs);  // one pool allocation per workgroup
-    uint32_t r = 0xFFFFFFFFu;        // no move
-    if (want) {
-      if (offs[0] + want > s.pcap) set_err(c, ERR_POOL_FULL);
-      else r = (uint32_t)offs[0];
-    }
-    const bool mv = r != 0xFFFFFFFFu;
-    const bool small = mv && ad.y <= SEG_LANE_COPY;
-    if (small) {
-      T x[SEG_LANE_COPY];
-#pragma unroll
-      for (uint32_t e = 0; e < SEG_LANE_COPY; ++e)
-        if (e < ad.y) x[e] = s.pool[(uint64_t)ad.x + e];
-#pragma unroll
-      for (uint32_t e = 0; e < SEG_LANE_COPY; ++e)
-        if (e < ad.y) s.pool[(uint64_t)r + e] = x[e];
-    }
-    uint64_t big = __ballot(mv && !small);
-    while (big) {
-      const int k = __ffsll((unsigned long long)big) - 1;
-      big &= big - 1;
-      const uint32_t rk = __shfl(r, k), xk = __shfl(ad.x, k), yk = __shfl(ad.y, k);
-      for (uint32_t e = lane; e < yk; e += 64) s.pool[(uint64_t)rk + e] = s.pool[(uint64_t)xk + e];
-    }
-    if (mv) {
-      s.adj[o].x = r;
-      s.cap[o] = want;
-    }
-  }
-}
-
-__global__ __launch_bounds__(SEG_THREADS) void k_seg_grow(Seg<uint64_t> fw, Seg<uint32_t> rv, Counters *c) {
-  const uint32_t half = gridDim.x / 2;
-  if (blockIdx.x < half) seg_grow(fw, c, blockIdx.x, half);
-  else seg_grow(rv, c, blockIdx.x - half, gridDim.x - half);
-}
-
-__global__ __launch_bounds__(256) void k_edge_append(DevGraph g, EdgeArgs a) {
-  const uint64_t n = g.ctr->n_new_edges;
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    const uint64_t b = a.newlist[i];
-    const uint4 bk = load_bucket(&g.etab[b]);
-    const uint64_t key = bucket_key(bk);
-    const uint32_t o = (uint32_t)(key >> 32), t = (uint32_t)key;
-    const uint32_t rank = bk.z & ~EVAL_NEW;
-    const uint2 ad = g.adj[o];
-    const uint32_t idx = ad.y + rank;
-    if (idx >= g.ecap[o]) continue;  // relocation failed: ERR_POOL_FULL already set
-    const int32_t d = g.edelta[b];
-    g.pool[(uint64_t)ad.x + idx] = pack_edge(t, d);
-    g.etab[b].val = idx;
-    g.edelta[b] = 0;
-    if (d != 0) atomicAdd(&g.nzdeg[o], 1u);
-    const uint2 rd = g.radj[t];
-    const uint32_t ridx = rd.y + a.rrank[i];
-    g.etab[b].rev = ridx;
-    if (ridx < g.rcap[t]) g.rpool[(uint64_t)rd.x + ridx] = o | (d > 0 ? RC_POS : 0u);
-  }
-}
-
-// After the appends, in one launch: degrees advance by the merge's new edges
-// (forward) and candidates (reverse), the per-merge counts reset; and the
-// candidate entries of edges whose count changed sign take the final count's
-// sign (an edge may be listed more than once; every copy writes the same).
-// Flips read segment offsets and counts, never the degrees advanced here.
-template <typename T>
-__device__ inline void seg_finish(Seg<T> s, uint64_t i0, uint64_t stride) {
-  const uint64_t n = *s.ntouched;
-  for (uint64_t i = i0; i < n; i += stride) {
-    const uint32_t o = s.touched[i];
-    s.adj[o].y += s.nnew[o];
-    s.nnew[o] = 0;
-  }
-}
-
-__global__ __launch_bounds__(256) void k_edge_post(DevGraph g, EdgeArgs a, Seg<uint64_t> fw, Seg<uint32_t> rv) {
-  const uint32_t third = gridDim.x / 3;
-  const uint32_t part = min(blockIdx.x / third, 2u);
-  const uint32_t b = blockIdx.x - part * third;
-  const uint32_t nb = part == 2 ? gridDim.x - 2 * third : third;
-  const uint64_t i0 = (uint64_t)b * 256 + threadIdx.x, stride = (uint64_t)nb * 256;
-  if (part == 0) {
-    seg_finish(fw, i0, stride);
-  } else if (part == 1) {
-    seg_finish(rv, i0, stride);
-  } else {
-    const uint64_t n = g.ctr->n_flips;
-    for (uint64_t i = i0; i < n; i += stride) {
-      const uint4 bk = load_bucket(&g.etab[a.flips[i]]);
-      const uint64_t key = bucket_key(bk);
-      const uint32_t o = (uint32_t)(key >> 32), t = (uint32_t)key;
-      const int32_t cnt = edge_count(g.pool[(uint64_t)g.adj[o].x + bk.z]);
-      const uint32_t r = bk.w;
-      if (r < g.rcap[t]) g.rpool[(uint64_t)g.radj[t].x + r] = o | (cnt > 0 ? RC_POS : 0u);
-    }
-  }
-}
+// The edge pipeline (outgoing[o][t] += d) is crgc_edges.hip.
 
 int grid_for(uint64_t threads, int block, int cap) {
   uint64_t b = (threads + block - 1) / block;
   if (b < 1) b = 1;
   if (b > (uint64_t)cap) b = cap;
   return (int)b;
-}
-
-hipError_t launch_edges(const DevGraph &g, const EdgeArgs &a, hipStream_t s) {
-  if (a.max_atoms == 0) return hipSuccess;
-  const int grid = grid_for(a.max_atoms, 256, 8192);
-  Seg<uint64_t> fw{g.adj, g.ecap, g.enew, g.pool, g.pcap, &g.ctr->pool_top,
-                   &g.ctr->n_touched, a.touched};
-  Seg<uint32_t> rv{g.radj, g.rcap, g.rnew, g.rpool, g.rpcap, &g.ctr->rpool_top,
-                   &g.ctr->n_rtouched, a.rtouched};
-  const int wgrid = grid_for(a.max_atoms, EDGE_THREADS, 2048);
-  hipLaunchKernelGGL(k_edge_apply, dim3(wgrid), dim3(EDGE_THREADS), 0, s, g, a);
-  const int sgrid = 2 * grid_for(a.max_atoms, SEG_THREADS, 2048);
-  hipLaunchKernelGGL(k_seg_grow, dim3(sgrid), dim3(SEG_THREADS), 0, s, fw, rv, g.ctr);
-  hipLaunchKernelGGL(k_edge_append, dim3(grid), dim3(256), 0, s, g, a);
-  hipLaunchKernelGGL(k_edge_post, dim3(3 * grid_for(a.max_atoms, 256, 2048)), dim3(256), 0, s, g, a, fw,
-                     rv);
-  return hipGetLastError();
 }
 
 }  // namespace crgc
