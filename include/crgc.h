@@ -17,9 +17,12 @@
  *    bits of the id are the actor's location (the interned akka Address,
  *    `ref.path().address()`, ShadowGraph.java:49); the low 48 bits are free.
  *    Ids CRGC_NO_ACTOR and CRGC_DEAD_ACTOR (and location 0xFFFF) are reserved.
- *  - Input buffers are caller-owned and only read during the call (the
- *    reference recycles an Entry right after merging it: LocalGC.scala:167-169).
- *    `memory` says whether their pointers are host or device (HBM) pointers.
+ *  - Input buffers are caller-owned.  Host buffers are only read during the
+ *    call (a merge waits for its staging copies; the reference recycles an
+ *    Entry right after merging it: LocalGC.scala:167-169).  Device (HBM)
+ *    buffers are read by kernels queued on the graph's stream and must stay
+ *    valid until the next synchronising call (a trace or a query).  `memory`
+ *    says whether the pointers are host or device pointers.
  *  - Merges are stream-ordered and asynchronous with respect to the host; a
  *    trace (and every query) synchronises.  Merges between two traces commute
  *    except for the last-write-wins fields, which follow call order and then

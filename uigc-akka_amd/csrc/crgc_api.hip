@@ -195,7 +195,7 @@ struct crgc_graph {
   uint64_t last_garbage = 0, last_kill = 0, last_live = 0;
   crgc_trace_stats last_stats{};
   bool have_last = false;
-  uint64_t last_levels = 0;
+  uint64_t last_levels = 0;  // level launches (after level 0) the previous trace needed
   std::vector<hipEvent_t> lvl_ev;  // 6 per level launch: start / stop of its 3 kernels
   std::vector<hipEvent_t> chunk_ev;  // start / stop of every chunk of level launches
   uint64_t *roots_buf = nullptr;
@@ -1245,6 +1245,7 @@ static int run_chains(crgc_graph *h, bool investigate, uint64_t top) {
 
 struct LevelRun {
   uint64_t levels = 0, roots = 0, launches = 0, depth = 0;
+  uint64_t first_chunk = 0;  // level launches after level 0 that this trace needed
   double ms = 0, ms_f = 0, ms_t = 0, ms_e = 0;
   bool defer = false;                  // leave the event queries to the caller (pending)
   std::function<void()> pending;
@@ -1257,8 +1258,10 @@ static void collect_times(crgc_graph *h, LevelRun &lr, size_t nl, size_t nc, int
 // from candidates of level `start` (sharded rounds), until a level is empty.
 // Every level is bracketed by events between its three kernels, so the
 // timings are device time of each level kernel.  Levels are enqueued in
-// chunks; the first chunk of a trace is as deep as the previous trace, so a
-// steady-state wakeup needs one host synchronisation.  *end = the first empty
+// chunks; the first chunk of a trace is as long as the previous trace needed
+// (through the level at which k_tail finished the mark, or one level past the
+// first empty one), so a steady-state wakeup needs one host synchronisation
+// and launches no idle levels.  *end = the first empty
 // level (levels start .. *end-1 were non-empty).
 static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64_t top, bool roots,
                       int start, LevelRun &lr, int *end,
@@ -1350,7 +1353,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
     HIP_TRY(launch(0, true));
     L = 1;
   }
-  int chunk = roots ? (int)std::min<uint64_t>(std::max<uint64_t>(4, h->last_levels + 1), 512) : 4;
+  int chunk = roots && h->last_levels ? (int)std::min<uint64_t>(h->last_levels, 512) : 4;
   std::vector<unsigned long long> ring(LEVEL_RING);
   unsigned long long tail[3] = {0, 0, 0};
   const bool log = getenv("CRGC_LEVEL_LOG") != nullptr;
@@ -1392,7 +1395,10 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
         *end = e;
         lr.levels += (uint64_t)std::max(0, e - (roots ? 0 : start));
         // level launches that did work: the first chunk of the next trace
-        if (roots) lr.depth = tail[0] == TAIL_DONE ? (uint64_t)tail[2] + 1 : (uint64_t)lv;
+        if (roots) {
+          lr.depth = tail[0] == TAIL_DONE ? (uint64_t)tail[2] + 1 : (uint64_t)lv;
+          lr.first_chunk = tail[0] == TAIL_DONE ? std::max<uint64_t>(1, tail[2]) : (uint64_t)lv + 1;
+        }
         lr.launches += nl;
         lr.pending = [h, nl, nc, timing, log, roots, start, last, ring, &lr]() {
           collect_times(h, lr, nl, nc, timing, log, roots ? 0 : (size_t)start, (size_t)last, ring);
@@ -1658,7 +1664,7 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   h->n_proxy = c.n_proxy;
   h->inserted_at_trace = c.inserted;
   h->have_last = true;
-  h->last_levels = lr.depth;
+  h->last_levels = lr.first_chunk;
   st.ms_total =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   h->last_stats = st;
@@ -1746,18 +1752,27 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
   };
   uint64_t G = 0;
   if (n) {
+    // The chain, then the count pass and its scans without a host round trip:
+    // graph counts over the bound n + 1 (zero past the device's n_graphs).
+    DgOut none{};
     HIP_TRY(launch_dg_chain(a, 0, h->stream));
+    HIP_TRY(hipMemsetAsync(a.g_size, 0, N * 4, h->stream));
+    HIP_TRY(hipMemsetAsync(a.g_nout, 0, N * 4, h->stream));
+    HIP_TRY(hipMemsetAsync(a.g_bytes, 0, N * 4, h->stream));
+    HIP_TRY(launch_dg_build(a, DG_NG_DEVICE, false, none, h->stream));
+    HIP_TRY(launch_dg_scans(a, N, h->stream));
     if (int rc = fetch()) return rc;
     if (hc.err) return CRGC_E_INVAL;  // malformed offsets or reserved ids: nothing was built
-    while (hc.first_long != ~0u) {  // a chain start whose graph runs past the span window
-      HIP_TRY(launch_dg_chain(a, 1, h->stream));
+    if (hc.first_long != ~0u) {  // a chain start whose graph runs past the span window
+      while (hc.first_long != ~0u) {
+        HIP_TRY(launch_dg_chain(a, 1, h->stream));
+        if (int rc = fetch()) return rc;
+      }
+      HIP_TRY(launch_dg_build(a, hc.n_graphs, false, none, h->stream));
+      HIP_TRY(launch_dg_scans(a, hc.n_graphs, h->stream));
       if (int rc = fetch()) return rc;
     }
     G = hc.n_graphs;
-    DgOut none{};
-    HIP_TRY(launch_dg_build(a, G, false, none, h->stream));
-    HIP_TRY(launch_dg_scans(a, G, h->stream));
-    if (int rc = fetch()) return rc;
   }
   const uint64_t NS = n ? hc.n_shadows : 0, NO = n ? hc.n_out : 0, NW = n ? hc.wire : 0;
   out->n_graphs = G;

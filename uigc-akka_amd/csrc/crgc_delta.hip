@@ -67,13 +67,93 @@ __device__ inline void dg_ids(const DgArgs &a, uint64_t e, const DgRange &r, Fn 
   for (uint32_t k = r.u0; k < r.u1; ++k) fn(a.u_ref[k]);
 }
 
+// The ranges of 64 consecutive entries from cb (lane l: entry cb + l), read
+// once and consumed by several batches.
+struct DgCursor {
+  uint64_t cb;
+  DgRange r;
+  uint32_t m, incl;     // ids of the entry, inclusive scan over the chunk
+  uint8_t eflags;       // Entry.isBusy / isRoot
+  int16_t erecv;        // receive count
+  bool bad;             // offsets the merges reject
+};
+
+__device__ inline void dg_load(const DgArgs &a, DgCursor &C, uint64_t cb, uint64_t e1) {
+  const uint64_t el = cb + lane_id();
+  C.cb = cb;
+  C.r = DgRange{};
+  C.m = 0;
+  C.eflags = 0;
+  C.erecv = 0;
+  C.bad = false;
+  if (el < e1) {
+    C.r = dg_range(a, el);
+    C.m = 1 + 2 * (C.r.c1 - C.r.c0) + (C.r.s1 - C.r.s0) + (C.r.u1 - C.r.u0);
+    C.bad = C.r.bad;
+    C.eflags = a.flags[el];
+    C.erecv = a.recv[el];
+  }
+  C.incl = wave_incl_scan(C.m);
+}
+
+// One batch of whole entries from eb: lane l holds the l-th id, in encode
+// order (:75, 86-89, 100, 111).
+struct DgBatch {
+  uint32_t ne, mt;      // entries, ids
+  uint64_t id;          // lane < mt: its id
+  int16_t info;         // updated refs: the RefobInfo
+  uint32_t e, k;        // the id's entry (batch-local) and position in it
+  uint32_t elane;       // the cursor lane holding that entry
+  uint32_t nc, ns;      // that entry's created / spawned record counts
+  uint32_t base;        // lane of that entry's first id
+  bool bad;             // a reserved id
+};
+
+__device__ inline DgBatch dg_batch(const DgArgs &a, DgCursor &C, uint64_t eb, uint64_t e1) {
+  const int lane = lane_id();
+  if (eb < C.cb || eb - C.cb >= 48) dg_load(a, C, eb, e1);
+  DgBatch B{};
+  const uint32_t off = (uint32_t)(eb - C.cb);  // first cursor lane of the batch
+  const uint32_t before = off ? __shfl(C.incl, off - 1) : 0u;
+  const uint64_t fits = __ballot((uint32_t)lane >= off && C.cb + lane < e1 && C.incl - before <= 64);
+  B.ne = fits ? (uint32_t)__popcll(fits) : 1;  // (m <= 1 + 4F <= 64)
+  B.mt = __shfl(C.incl, off + B.ne - 1) - before;
+  uint32_t my_e = 0;  // the number of entries ending at or before this lane's id
+  for (uint32_t q = 0; q < B.ne; ++q)
+    if (__shfl(C.incl, off + q) - before <= (uint32_t)lane) my_e = q + 1;
+  if (my_e >= B.ne) my_e = B.ne - 1;
+  B.e = my_e;
+  B.elane = off + my_e;
+  const uint32_t c0 = __shfl(C.r.c0, B.elane), c1 = __shfl(C.r.c1, B.elane);
+  const uint32_t s0 = __shfl(C.r.s0, B.elane), s1 = __shfl(C.r.s1, B.elane), u0 = __shfl(C.r.u0, B.elane);
+  B.base = __shfl(C.incl - C.m, B.elane) - before;
+  B.nc = c1 - c0;
+  B.ns = s1 - s0;
+  B.k = lane - B.base;
+  if ((uint32_t)lane < B.mt) {
+    const uint32_t k = B.k, nc = B.nc, ns = B.ns;
+    if (k == 0) B.id = a.self[eb + my_e];
+    else if (k < 1 + 2 * nc) B.id = ((k - 1) & 1) ? a.c_owner[c0 + (k - 1) / 2] : a.c_target[c0 + (k - 1) / 2];
+    else if (k < 1 + 2 * nc + ns) B.id = a.spawned[s0 + (k - 1 - 2 * nc)];
+    else {
+      B.id = a.u_ref[u0 + (k - 1 - 2 * nc - ns)];
+      B.info = a.u_info[u0 + (k - 1 - 2 * nc - ns)];
+    }
+    B.bad = dg_reserved(B.id);
+  }
+  return B;
+}
+
 // ---- the chain of graph starts ----------------------------------------------
 // One wave per 64 consecutive starts (lane l: start s0 + l).  The wave streams
-// entries from s0 through one table of the ids seen so far, each with the last
-// entry it was seen in; an occurrence is new to lane l's graph iff that entry
-// is before s0 + l.  So every entry is read once per wave and no lane keeps a
-// set of its own.  Lanes still short of T after SPAN_WIN entries (or when the
-// table is 3/4 full) are deferred.
+// entries from s0, a batch of whole entries (<= 64 ids, one per lane) at a
+// time, through one table of the ids seen so far with the last entry each was
+// seen in.  An occurrence is new to lane l's graph iff the id's previous
+// entry is before s0 + l: every lane finds its id's previous entry in the
+// table or among the batch's earlier lanes, then every lane walks the batch's
+// (entry, previous entry) pairs in order, counting its graph's actors and
+// stopping after the entry that fills it.  Lanes still short of T after
+// SPAN_WIN entries (or when the table is 3/4 full) are deferred.
 constexpr uint32_t SPAN_P = 1024;    // ids per wave table
 constexpr uint32_t SPAN_WIN = 192;   // entries a wave streams past s0
 
@@ -94,50 +174,72 @@ __global__ __launch_bounds__(256) void k_dg_span(DgArgs a) {
   uint32_t used = 0;
   uint64_t e = s0;
   const uint64_t stop = min(a.n, s0 + SPAN_WIN);
-  for (; e < stop; ++e) {
+  DgCursor C;
+  dg_load(a, C, e, a.n);
+  while (e < stop) {
     if (__ballot(!done) == 0) break;
     if (used > SPAN_P - SPAN_P / 4) break;
-    const DgRange r = dg_range(a, e);
-    bad |= r.bad;
-    const uint32_t nc = r.c1 - r.c0, ns = r.s1 - r.s0, nu = r.u1 - r.u0;
-    const uint32_t m = 1 + 2 * nc + ns + nu;  // <= 1 + 4F <= 64 ids, in encode order
-    uint64_t myid = 0;
-    if ((uint32_t)lane < m) {
-      const uint32_t k = lane;
-      if (k == 0) myid = a.self[e];
-      else if (k < 1 + 2 * nc) myid = ((k - 1) & 1) ? a.c_owner[r.c0 + (k - 1) / 2] : a.c_target[r.c0 + (k - 1) / 2];
-      else if (k < 1 + 2 * nc + ns) myid = a.spawned[r.s0 + (k - 1 - 2 * nc)];
-      else myid = a.u_ref[r.u0 + (k - 1 - 2 * nc - ns)];
-      bad |= dg_reserved(myid);
-    }
-    const bool in = !done && e >= s;
-    for (uint32_t k = 0; k < m; ++k) {
-      const uint64_t x = __shfl(myid, k);
-      uint32_t h = dg_hash(x, 10);
-      int64_t prev = -1;
-      for (;;) {  // every lane walks the same probe sequence (broadcast reads)
+    const DgBatch B = dg_batch(a, C, e, a.n);
+    bad |= B.bad || C.bad;
+    const bool has = (uint32_t)lane < B.mt;
+    const uint64_t x = has ? B.id : CRGC_NO_ACTOR;
+    const uint32_t my_e = (uint32_t)(e - s0) + B.e;  // entry, relative to s0
+    // the previous entry of this occurrence: in the table, or an earlier lane
+    int32_t prev = -1;
+    uint32_t h = dg_hash(x, 10);
+    if (has) {
+      for (;;) {
         const uint64_t y = K[h];
         if (y == x) {
-          prev = Ls[h];
+          prev = (int32_t)Ls[h];
           break;
         }
-        if (y == CRGC_NO_ACTOR) {
-          if (lane == 0) K[h] = x;
-          ++used;
-          break;
-        }
+        if (y == CRGC_NO_ACTOR) break;
         h = (h + 1) & (SPAN_P - 1);
       }
-      if (lane == 0) Ls[h] = (uint32_t)e;
-      wave_lds_fence();
-      if (in && prev < (int64_t)s) ++cnt;
     }
-    if (in && cnt >= a.T) {  // isFull after entry e (:174-180)
-      done = true;
-      end = e + 1;
+    bool later = false;
+    for (uint32_t j = 0; j < B.mt; ++j) {
+      const uint64_t xj = __shfl(x, j);
+      const uint32_t ej = __shfl(my_e, j);
+      if (xj == x) {
+        if (j < (uint32_t)lane) prev = (int32_t)ej;
+        else if (j > (uint32_t)lane) later = true;
+      }
     }
+    // the last occurrence of each id in the batch updates the table
+    bool fresh = false;
+    if (has && !later) {
+      for (;;) {
+        const uint64_t y = atomicCAS((unsigned long long *)&K[h], (unsigned long long)CRGC_NO_ACTOR,
+                                     (unsigned long long)x);
+        if (y == CRGC_NO_ACTOR) fresh = true;
+        if (y == CRGC_NO_ACTOR || y == x) break;
+        h = (h + 1) & (SPAN_P - 1);
+      }
+      Ls[h] = my_e;
+    }
+    used += (uint32_t)__popcll(__ballot(fresh));
+    wave_lds_fence();
+    // each lane's graph: new actors, entry by entry; isFull after an entry (:174-180)
+    const uint32_t me_rel = (uint32_t)lane;  // this lane's start, relative to s0
+    const uint32_t next_e = __shfl(B.e, (lane + 1) & 63);
+    const bool last_of_entry = has && (lane + 1 == (int)B.mt || next_e != B.e);
+    const uint64_t lasts = __ballot(last_of_entry);
+    for (uint32_t j = 0; j < B.mt; ++j) {
+      const uint32_t ej = __shfl(my_e, j);
+      const int32_t pj = __shfl(prev, j);
+      if (!done && ej >= me_rel) {
+        if (pj < (int32_t)me_rel) ++cnt;
+        if (((lasts >> j) & 1) && cnt >= a.T) {
+          done = true;
+          end = s0 + ej + 1;
+        }
+      }
+    }
+    e += B.ne;
   }
-  if (!done && e == a.n) {  // the last graph of the wakeup (LocalGC.scala:174-177)
+  if (!done && e >= a.n) {  // the last graph of the wakeup (LocalGC.scala:174-177)
     done = true;
     end = a.n;
   }
@@ -378,16 +480,27 @@ hipError_t launch_dg_chain(const DgArgs &a, int phase, hipStream_t s) {
 }
 
 // ---- one graph: DeltaGraph.mergeEntry replayed by one wave ------------------
-// The wave loads the graph's entries a batch at a time (whole entries, at most
-// 64 ids: one id per lane), encodes the ids in order against an LDS table
-// (DeltaGraph.encode, :148-156) and applies each entry's effects in order.
-// Outgoing maps are one 64 x 64 count matrix: cnt[o][t] and the time of the
-// key's last insertion, plus each owner's size and largest size — all that
-// java.util.HashMap iteration order depends on.
+// The wave reads the graph's entries a batch at a time (whole entries, at most
+// 64 ids: one id per lane) in two passes, neither serialised per id:
+//   1. every lane inserts its id into an LDS hash table (64-bit LDS CAS) and
+//      records its position with an LDS atomicMin; receive counts add up per
+//      slot (LDS atomics), and isBusy/isRoot/interned and the supervisor are
+//      last-write-wins tags (LDS atomicMax of entry index << 8 | value).
+//      DeltaGraph.encode (:148-156) numbers actors by first appearance, so a
+//      slot's compressed id is the rank of its first position.
+//   2. updateOutgoing (:127-136) in op order, one owner per lane: each batch's
+//      ops are broadcast and the owner's lane applies them to its row of a
+//      64 x 64 count matrix (count and time of the key's last insertion) and
+//      its map's size and largest size — all that java.util.HashMap iteration
+//      order depends on.
 constexpr uint32_t DGW_P = 128;  // id -> cid hash slots
 
 struct DgWave {
-  uint64_t key[DGW_P];
+  uint64_t key[DGW_P];       // id per hash slot (KEY_EMPTY: free)
+  uint64_t hfl[DGW_P];       // per slot: (entry + 1) << 8 | CRGC_DELTA_* of the last entry of the actor
+  uint64_t hsup[DGW_P];      // per slot: (entry + 1) << 8 | slot of the last spawner
+  uint32_t first[DGW_P];     // per slot: position of the id's first appearance
+  int32_t hrecv[DGW_P];      // per slot: receive count
   uint64_t dec[DG_MAX];      // decoder: id per cid (DeltaGraph.java:162-169)
   int32_t cnt[DG_MAX * DG_MAX];   // outgoing[o][t] (0: absent)
   uint32_t ins[DG_MAX * DG_MAX];  // op time of the key's last insertion
@@ -400,135 +513,133 @@ struct DgWave {
 };
 
 // Replays DeltaGraph.mergeEntry (DeltaGraph.java:73-125) over entries
-// [starts[g], starts[g+1]); returns the number of shadows.  Lane-uniform
-// control flow; lane 0 performs the LDS writes of the serial steps.
+// [starts[g], starts[g+1]); returns the number of shadows.
 __device__ uint32_t dg_replay(const DgArgs &a, uint64_t g, DgWave &W) {
   const int lane = lane_id();
-  for (uint32_t k = lane; k < DGW_P; k += 64) W.tabc[k] = NONE8;
-  for (uint32_t k = lane; k < DG_MAX * DG_MAX; k += 64) W.cnt[k] = 0;
+  for (uint32_t k = lane; k < DGW_P; k += 64) {
+    W.key[k] = KEY_EMPTY;
+    W.first[k] = 0xFFFFFFFFu;
+    W.hrecv[k] = 0;
+    W.hfl[k] = 0;
+    W.hsup[k] = 0;
+  }
   wave_lds_fence();
-  uint32_t size = 0, clock = 0;
   const uint64_t e0 = a.starts[g], e1 = a.starts[g + 1];
-  auto op = [&](uint32_t o, uint32_t t, int32_t d) {  // updateOutgoing (:127-136)
-    const uint32_t k = o * DG_MAX + t;
-    const int32_t c = W.cnt[k];
-    const int32_t nc = (int32_t)((uint32_t)c + (uint32_t)d);
-    if (lane == 0) {
-      W.cnt[k] = nc;
-      if (c == 0) {  // put of an absent key: appended to its bin
-        W.ins[k] = clock;
-        const uint32_t sz = W.osz[o] + 1u;
-        W.osz[o] = (uint8_t)sz;
-        if (sz > W.omax[o]) W.omax[o] = (uint8_t)sz;
-      } else if (nc == 0) {  // remove
-        W.osz[o] = (uint8_t)(W.osz[o] - 1u);
-      }
-    }
-    ++clock;
-    wave_lds_fence();
-  };
+  // pass 1: the ids, receive counts and last-write-wins fields, per hash slot
+  uint32_t pos = 0, ei = 0;
+  DgCursor C;
+  dg_load(a, C, e0, e1);
   for (uint64_t eb = e0; eb < e1;) {
-    // a batch of whole entries with at most 64 ids: lane l holds entry eb+l's ranges
-    const uint64_t el = eb + lane;
-    DgRange r{};
-    uint32_t m = 0;
-    if (el < e1) {
-      r = dg_range(a, el);
-      m = 1 + 2 * (r.c1 - r.c0) + (r.s1 - r.s0) + (r.u1 - r.u0);
-    }
-    const uint32_t incl = wave_incl_scan(m);
-    const uint64_t fits = __ballot(el < e1 && incl <= 64);
-    const uint32_t ne = fits ? (uint32_t)__popcll(fits) : 1;  // entries of this batch (m <= 63)
-    const uint32_t mt = __shfl(incl, ne - 1);
-    // lane k: the k-th id of the batch, in encode order
-    uint64_t myid = 0;
-    int16_t myinfo = 0;
-    uint32_t my_e = 0;  // entry of id `lane`: the number of entries ending at or before it
-    for (uint32_t q = 0; q < ne; ++q)
-      if (__shfl(incl, q) <= (uint32_t)lane) my_e = q + 1;
-    if (my_e >= ne) my_e = ne - 1;
-    const uint8_t myflags = el < e1 ? a.flags[el] : 0;
-    const int16_t myrecv = el < e1 ? a.recv[el] : 0;
-    {
-      // every lane needs the ranges of the entry its id belongs to
-      const uint32_t c0 = __shfl(r.c0, my_e), c1 = __shfl(r.c1, my_e);
-      const uint32_t s0 = __shfl(r.s0, my_e), s1 = __shfl(r.s1, my_e), u0 = __shfl(r.u0, my_e);
-      const uint32_t base = __shfl(incl - m, my_e);
-      if ((uint32_t)lane < mt) {
-        const uint32_t k = lane - base, nc = c1 - c0, ns = s1 - s0;
-        if (k == 0) myid = a.self[eb + my_e];
-        else if (k < 1 + 2 * nc) myid = ((k - 1) & 1) ? a.c_owner[c0 + (k - 1) / 2] : a.c_target[c0 + (k - 1) / 2];
-        else if (k < 1 + 2 * nc + ns) myid = a.spawned[s0 + (k - 1 - 2 * nc)];
-        else {
-          myid = a.u_ref[u0 + (k - 1 - 2 * nc - ns)];
-          myinfo = a.u_info[u0 + (k - 1 - 2 * nc - ns)];
-        }
-      }
-    }
-    // encode, in order (:148-156)
-    uint32_t mycid = 0;
-    for (uint32_t k = 0; k < mt; ++k) {
-      const uint64_t x = __shfl(myid, k);
-      uint32_t h = dg_hash(x, 7);
-      uint32_t c;
+    const DgBatch B = dg_batch(a, C, eb, e1);
+    uint32_t h = 0;
+    if ((uint32_t)lane < B.mt) {
+      const uint64_t x = B.id == KEY_EMPTY ? KEY_EMPTY - 1 : B.id;  // reserved ids are errors already
+      h = dg_hash(x, 7);
       for (;;) {
-        c = W.tabc[h];
-        if (c == NONE8) {
-          c = size++;
-          if (lane == 0) {
-            W.tabc[h] = (uint8_t)c;
-            W.key[h] = x;
-            W.dec[c] = x;
-            W.recv[c] = 0;
-            W.sup[c] = NONE8;
-            W.fl[c] = 0;
-            W.osz[c] = 0;
-            W.omax[c] = 0;
-          }
-          wave_lds_fence();
-          break;
-        }
-        if (W.key[h] == x) break;
+        const uint64_t k = atomicCAS((unsigned long long *)&W.key[h], (unsigned long long)KEY_EMPTY,
+                                     (unsigned long long)x);
+        if (k == KEY_EMPTY || k == x) break;
         h = (h + 1) & (DGW_P - 1);
       }
-      if ((uint32_t)lane == k) mycid = c;
+      atomicMin(&W.first[h], pos + lane);
     }
-    // effects, entry by entry
-    for (uint32_t q = 0; q < ne; ++q) {
-      const uint32_t base = __shfl(incl - m, q);
-      const uint32_t c0 = __shfl(r.c0, q), c1 = __shfl(r.c1, q), s0 = __shfl(r.s0, q),
-                     s1 = __shfl(r.s1, q), u0 = __shfl(r.u0, q), u1 = __shfl(r.u1, q);
-      (void)c0;
-      (void)s0;
-      (void)u0;
-      const uint32_t nc = c1 - c0, ns = s1 - s0, nu = u1 - u0;
-      const uint32_t me = __shfl(mycid, base);
-      const uint8_t ef = (uint8_t)__shfl((uint32_t)myflags, q);
-      const int32_t erecv = __shfl((int32_t)myrecv, q);
-      if (lane == 0) {  // local information (:75-80)
-        W.fl[me] = (uint8_t)(CRGC_DELTA_INTERNED | ((ef & CRGC_ENTRY_ROOT) ? CRGC_DELTA_ROOT : 0) |
-                             ((ef & CRGC_ENTRY_BUSY) ? CRGC_DELTA_BUSY : 0));
-        W.recv[me] = (int32_t)((uint32_t)W.recv[me] + (uint32_t)erecv);
+    const uint32_t me = __shfl(h, B.base);
+    const uint8_t ef = (uint8_t)__shfl((uint32_t)C.eflags, B.elane);
+    const int32_t er = __shfl((int32_t)C.erecv, B.elane);
+    if ((uint32_t)lane < B.mt) {
+      const uint64_t tag = (uint64_t)(ei + B.e + 1) << 8;
+      const uint32_t k = B.k;
+      if (k == 0) {  // local information (:75-80)
+        atomicAdd(&W.hrecv[h], er);
+        atomicMax((unsigned long long *)&W.hfl[h],
+                  (unsigned long long)(tag | CRGC_DELTA_INTERNED | ((ef & CRGC_ENTRY_ROOT) ? CRGC_DELTA_ROOT : 0) |
+                                       ((ef & CRGC_ENTRY_BUSY) ? CRGC_DELTA_BUSY : 0)));
+      } else if (k >= 1 + 2 * B.nc && k < 1 + 2 * B.nc + B.ns) {  // spawned actors (:95-104)
+        atomicMax((unsigned long long *)&W.hsup[h], (unsigned long long)(tag | me));
+      } else if (k >= 1 + 2 * B.nc) {  // updated refs (:107-124)
+        const int32_t sc = refob_count(B.info);
+        if (sc > 0) atomicAdd(&W.hrecv[h], -sc);
       }
-      wave_lds_fence();
-      for (uint32_t j = 0; j < nc; ++j)  // created refs (:83-92)
-        op(__shfl(mycid, base + 2 + 2 * j), __shfl(mycid, base + 1 + 2 * j), 1);
-      for (uint32_t j = 0; j < ns; ++j) {  // spawned actors (:95-104)
-        const uint32_t ch = __shfl(mycid, base + 1 + 2 * nc + j);
-        if (lane == 0) W.sup[ch] = (uint8_t)me;
-      }
-      for (uint32_t j = 0; j < nu; ++j) {  // updated refs (:107-124)
-        const uint32_t t = __shfl(mycid, base + 1 + 2 * nc + ns + j);
-        const int16_t info = (int16_t)__shfl((int32_t)myinfo, base + 1 + 2 * nc + ns + j);
-        const int32_t sc = refob_count(info);
-        if (sc > 0 && lane == 0) W.recv[t] = (int32_t)((uint32_t)W.recv[t] - (uint32_t)sc);
-        wave_lds_fence();
-        if (refob_deactivated(info)) op(me, t, -1);
-      }
-      wave_lds_fence();
     }
-    eb += ne;
+    pos += B.mt;
+    ei += B.ne;
+    eb += B.ne;
   }
+  wave_lds_fence();
+  // compressed ids: rank of the first appearance
+  uint32_t size = 0;
+  for (uint32_t s = lane; s < DGW_P; s += 64) {
+    const uint32_t f = W.first[s];
+    size += (uint32_t)__popcll(__ballot(f != 0xFFFFFFFFu));
+    if (f == 0xFFFFFFFFu) continue;
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < DGW_P; ++j) r += W.first[j] < f ? 1u : 0u;
+    W.tabc[s] = (uint8_t)r;
+    W.dec[r] = W.key[s];
+    W.recv[r] = W.hrecv[s];
+    W.fl[r] = (uint8_t)W.hfl[s];
+  }
+  wave_lds_fence();
+  for (uint32_t s = lane; s < DGW_P; s += 64) {
+    if (W.first[s] == 0xFFFFFFFFu) continue;
+    const uint64_t sp = W.hsup[s];
+    W.sup[W.tabc[s]] = sp ? W.tabc[sp & 0xFF] : NONE8;
+  }
+  for (uint32_t k = lane; k < size * DG_MAX; k += 64) W.cnt[k] = 0;
+  wave_lds_fence();
+  // pass 2: updateOutgoing in op order; lane o owns row o
+  uint32_t clock = 0, osz = 0, omax = 0;
+  dg_load(a, C, e0, e1);
+  for (uint64_t eb = e0; eb < e1;) {
+    const DgBatch B = dg_batch(a, C, eb, e1);
+    uint32_t c = 0;
+    if ((uint32_t)lane < B.mt) {
+      const uint64_t x = B.id == KEY_EMPTY ? KEY_EMPTY - 1 : B.id;
+      uint32_t h = dg_hash(x, 7);
+      while (W.key[h] != x) h = (h + 1) & (DGW_P - 1);
+      c = W.tabc[h];
+    }
+    const uint32_t me = __shfl(c, B.base);
+    const uint32_t prev = __shfl(c, (lane + 63) & 63);  // a created owner's target is the lane before
+    const uint32_t k = B.k;
+    bool emit = false;
+    uint32_t op = 0;
+    if ((uint32_t)lane < B.mt && k >= 1) {
+      if (k < 1 + 2 * B.nc) {
+        if ((k - 1) & 1) {  // created ref (:83-92): outgoing[owner][target] += 1
+          emit = true;
+          op = c | (prev << 8) | (1u << 16);
+        }
+      } else if (k >= 1 + 2 * B.nc + B.ns && refob_deactivated(B.info)) {  // :120-123
+        emit = true;
+        op = me | (c << 8);
+      }
+    }
+    uint64_t bits = __ballot(emit);
+    while (bits) {
+      const int j = __ffsll((unsigned long long)bits) - 1;
+      bits &= bits - 1;
+      const uint32_t v = __shfl(op, j);
+      if ((v & 0xFF) == (uint32_t)lane) {
+        const uint32_t kk = (uint32_t)lane * DG_MAX + ((v >> 8) & 0xFF);
+        const int32_t c0 = W.cnt[kk];
+        const int32_t nc = (int32_t)((uint32_t)c0 + ((v >> 16) ? 1u : 0xFFFFFFFFu));
+        W.cnt[kk] = nc;
+        if (c0 == 0) {  // put of an absent key: appended to its bin
+          W.ins[kk] = clock;
+          ++osz;
+          omax = max(omax, osz);
+        } else if (nc == 0) {  // remove
+          --osz;
+        }
+      }
+      ++clock;
+    }
+    eb += B.ne;
+  }
+  W.osz[lane] = (uint8_t)osz;
+  W.omax[lane] = (uint8_t)omax;
+  wave_lds_fence();
   return size;
 }
 
@@ -598,9 +709,16 @@ __device__ void dg_emit(const DgArgs &a, uint64_t g, const DgWave &W, uint32_t s
   }
 }
 
+// ng == DG_NG_DEVICE: the graph count is the device's (n_graphs), and nothing
+// is built while a deferred chain start is unresolved (first_long set): the
+// host then resolves it and runs the count pass again.
 template <bool WRITE>
 __global__ __launch_bounds__(64) void k_dg_build(DgArgs a, uint64_t ng, DgOut o) {
   __shared__ DgWave W;
+  if (ng == DG_NG_DEVICE) {
+    if (a.ctr->first_long != ~0u) return;
+    ng = a.ctr->n_graphs;
+  }
   for (uint64_t g = blockIdx.x; g < ng; g += gridDim.x) {
     const uint32_t size = dg_replay(a, g, W);
     if (WRITE) {
@@ -621,7 +739,7 @@ __global__ __launch_bounds__(64) void k_dg_build(DgArgs a, uint64_t ng, DgOut o)
 
 hipError_t launch_dg_build(const DgArgs &a, uint64_t ng, bool write, const DgOut &o, hipStream_t s) {
   if (ng == 0) return hipSuccess;
-  const dim3 grid((unsigned)std::min<uint64_t>(ng, 4096));
+  const dim3 grid((unsigned)std::min<uint64_t>(ng == DG_NG_DEVICE ? a.n + 1 : ng, 4096));
   if (write) hipLaunchKernelGGL(k_dg_build<true>, grid, dim3(64), 0, s, a, ng, o);
   else hipLaunchKernelGGL(k_dg_build<false>, grid, dim3(64), 0, s, a, ng, o);
   return hipGetLastError();

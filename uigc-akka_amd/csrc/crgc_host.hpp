@@ -349,7 +349,9 @@ struct DgOut {
 // phase 0: spans + doubling + chain from entry 0; 1: chain from a resolved
 // deferred start (k_dg_long, then marking); 2: compaction of the starts.
 hipError_t launch_dg_chain(const DgArgs &a, int phase, hipStream_t s);
-// count (write = false) or write pass: one wave per graph
+// count (write = false) or write pass: one wave per graph (n_graphs ==
+// DG_NG_DEVICE: the count on the device, bounded by n + 1)
+constexpr uint64_t DG_NG_DEVICE = ~0ull;
 hipError_t launch_dg_build(const DgArgs &a, uint64_t n_graphs, bool write, const DgOut &o, hipStream_t s);
 // exclusive scans of the per-graph counts (after the count pass)
 hipError_t launch_dg_scans(const DgArgs &a, uint64_t n_graphs, hipStream_t s);
