@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define CRGC_ABI_VERSION 2u  /* 2: crgc_trace_stats.expand_launches / expand_bytes */
+#define CRGC_ABI_VERSION 3u  /* 2: crgc_trace_stats.expand_launches / expand_bytes; 3: exchange_bytes */
 
 /* ---- status codes ------------------------------------------------------- */
 #define CRGC_OK 0
@@ -189,11 +189,14 @@ typedef struct crgc_trace_stats {
   double ms_expand;        /* k_expand: out-edges of the frontier           */
   /* sharded graphs */
   uint64_t rounds;         /* exchange rounds (1 + frontier all-to-alls)    */
-  uint64_t ids_sent;       /* frontier ids sent to other shards             */
+  uint64_t ids_sent;       /* marked proxies sent to other shards (any form)*/
   double ms_exchange;      /* host wall time spent in exchanges             */
   /* the k_expand roofline */
   uint64_t expand_launches;/* k_expand dispatches of this trace             */
   uint64_t expand_bytes;   /* bytes k_expand read + wrote, by element width  */
+  /* sharded graphs: bytes this shard sent in mark rounds (ids, home slots,
+     frontier bitmaps) and in the home-slot resolution before them */
+  uint64_t exchange_bytes;
 } crgc_trace_stats;
 
 typedef struct crgc_trace_out {

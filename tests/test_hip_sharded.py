@@ -74,8 +74,12 @@ def test_random_spec_sharded_matches_oracle_every_wakeup(sharded, oracle_mod, G,
     assert h.live_count() == 1
 
 
+@pytest.mark.parametrize("xbits", ["1", "2"])
 @pytest.mark.parametrize("G,seed,cap", [(2, 11, 0), (3, 12, 0), (4, 13, 64)])
-def test_fuzz_sharded(sharded, oracle_mod, G, seed, cap):
+def test_fuzz_sharded(sharded, oracle_mod, G, seed, cap, xbits, monkeypatch):
+    # CRGC_XBITS=2: every resolved mark travels in a home-slot bitmap; cap 64
+    # rebuilds the shards often, so cached home slots go stale and re-resolve
+    monkeypatch.setenv("CRGC_XBITS", xbits)
     h, o = sharded(G, vertex_capacity=cap, edge_capacity=cap), oracle_mod.OracleGraph()
     fz = fuzz.Fuzz(seed)
     for step in range(14):
@@ -277,10 +281,13 @@ def test_rccl_transport_single_rank(hip_mod, oracle_mod):
         t.close()
 
 
-def test_c4_shape_eight_shards(sharded, oracle_mod):
+@pytest.mark.parametrize("xbits", ["0", "1", "2"])
+def test_c4_shape_eight_shards(sharded, oracle_mod, xbits, monkeypatch):
     """G = 8 logical shards (the 8-GPU layout of C4) on a scaled C2/C4-shaped
     power-law graph with §8d wakeups (9 % busy, 1 % in flight), split batches:
-    bit-exact against the unsharded oracle at every wakeup."""
+    bit-exact against the unsharded oracle at every wakeup, with marks sent as
+    ids only (0), in the cheaper of home slots / bitmaps (1), or as bitmaps (2)."""
+    monkeypatch.setenv("CRGC_XBITS", xbits)
     V = 200_000
     w = world.World(seed=0x5EED + 4)
     w.bulk_graph(V, 10 * V, alpha=2.1, n_roots=V // 1000, cap=100000)
@@ -296,5 +303,9 @@ def test_c4_shape_eight_shards(sharded, oracle_mod):
         rh = h.trace(True)
         _same(rh, o.trace(True))
         assert rh.rounds >= 2 and rh.ids_sent > 0  # marks crossed shards
+        if xbits == "0":
+            assert rh.exchange_bytes == 8 * rh.ids_sent  # ids only
+        else:  # proxies resolved by the first trace: marks go as slots / bitmaps
+            assert rh.exchange_bytes < 8 * rh.ids_sent
     assert h.export() == o.export()
     assert h.total_actors_seen() == o.total_actors_seen()

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 OK = 0
 E_INVAL = -1
@@ -122,6 +122,7 @@ class CrgcTraceStats(C.Structure):
         ("ms_exchange", C.c_double),
         ("expand_launches", _U64),
         ("expand_bytes", _U64),
+        ("exchange_bytes", _U64),
     ]
 
 

@@ -354,6 +354,7 @@ class TraceResult:
     ms_exchange: float = 0.0
     expand_launches: int = 0
     expand_bytes: int = 0
+    exchange_bytes: int = 0
 
     def garbage_set(self):
         return set(int(x) for x in self.garbage)

@@ -145,7 +145,7 @@ class ShadowGraph:
                            int(st.sup_edges), int(st.levels), int(st.launches), st.ms_mark,
                            st.ms_sweep, st.ms_total, st.ms_frontier, st.ms_tail, st.ms_expand,
                            int(st.rounds), int(st.ids_sent), st.ms_exchange,
-                           int(st.expand_launches), int(st.expand_bytes))
+                           int(st.expand_launches), int(st.expand_bytes), int(st.exchange_bytes))
 
     def _trace_into(self, shouldKill, g, k):
         out = abi.CrgcTraceOut()
@@ -456,7 +456,8 @@ class ShardedShadowGraph:
             max(r.ms_frontier for r in rs), max(r.ms_tail for r in rs),
             max(r.ms_expand for r in rs), max(r.rounds for r in rs),
             sum(r.ids_sent for r in rs), max(r.ms_exchange for r in rs),
-            sum(r.expand_launches for r in rs), sum(r.expand_bytes for r in rs))
+            sum(r.expand_launches for r in rs), sum(r.expand_bytes for r in rs),
+            sum(r.exchange_bytes for r in rs))
 
     def count_reachable_from(self, location: int) -> int:
         vals = self._all(lambda s: s.count_reachable_from(location))

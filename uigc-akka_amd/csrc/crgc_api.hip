@@ -48,7 +48,7 @@ void free_arrays(Arrays &a) {
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat, d.xbytes,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill,
                 d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.fx, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
-                d.xp_buf, d.xp_cnt, d.rq_buf, d.rq_cnt};
+                d.xp_buf, d.xp_cnt, d.rq_buf, d.rq_cnt, d.phs};
   for (void *p : ps)
     if (p) hipFree(p);
   a.allocated = false;
@@ -127,6 +127,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
     A(dmalloc(&d.xp_cnt, c.scap / BLK_SLOTS));
     A(dmalloc(&d.rq_buf, c.scap));
     A(dmalloc(&d.rq_cnt, c.scap / BLK_SLOTS));
+    A(dmalloc(&d.phs, c.scap));
   }
 #undef A
   a.allocated = true;
@@ -154,6 +155,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   hipMemsetAsync(d.pb[0], 0, c.scap / 8, s);
   hipMemsetAsync(d.pb[1], 0, c.scap / 8, s);
   if (sharded) {
+    hipMemsetAsync(d.phs, 0xFF, c.scap * 4, s);  // PHS_NONE: a new generation resolves again
     hipMemsetAsync(d.xp_cnt, 0, c.scap / BLK_SLOTS * 4, s);
     hipMemsetAsync(d.rq_cnt, 0, c.scap / BLK_SLOTS * 4, s);
   }
@@ -211,6 +213,11 @@ struct crgc_graph {
   uint64_t *h_small = nullptr;       // pinned host staging for small all-gathers
   char *h_route = nullptr;           // pinned RoutePart / ConcatPart tables
   bool route = true;                 // CRGC_ROUTE=0: all-gather every batch instead
+  // mark rounds in home-slot form: this shard's slot numbering generation
+  // (bumped by every rebuild), and each home's generation / slot count as of
+  // this shard's last resolution
+  uint64_t slot_gen = 0;
+  std::vector<uint64_t> peer_gen, peer_top;
 };
 
 namespace {
@@ -325,6 +332,7 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   }
   free_arrays(h->g);
   h->g = dst;
+  ++h->slot_gen;  // other shards' cached home slots of this shard are stale now
   h->live = h->slot_top;
   h->inserted_at_trace = h->hctr->inserted;
   if (int rc = device_error(h)) return rc;
@@ -1456,41 +1464,138 @@ static void reset_trace_counters(crgc_graph *h) {
 // Mark to the global fixpoint: local levels, then (sharded graphs) rounds of
 // exporting newly marked proxies to their home shards and continuing from
 // what arrives, until no shard has anything to send.
+// Home-slot resolution before a sharded mark: every shard learns the others'
+// slot generations and counts; proxies of a home whose generation changed
+// forget their cached slots; proxies without one ask their home (one id
+// exchange, one answer exchange — in steady state only the proxies created
+// since the last trace).
+static int resolve_home_slots(crgc_graph *h, uint64_t top, int xmode, uint64_t *bytes) {
+  const uint32_t G = h->G, me = h->shard;
+  const uint64_t mine[2] = {h->slot_gen, top};
+  std::vector<uint64_t> T((size_t)G * 2);
+  if (int rc = ag_host(h, mine, 2, T.data())) return rc;
+  if (h->peer_gen.size() != G) {
+    h->peer_gen.assign(G, ~0ull);
+    h->peer_top.assign(G, 0);
+  }
+  uint32_t mask = 0;
+  for (uint32_t d = 0; d < G; ++d) {
+    if (h->peer_gen[d] != T[2 * d]) mask |= 1u << d;
+    h->peer_gen[d] = T[2 * d];
+    h->peer_top[d] = T[2 * d + 1];
+  }
+  if (xmode == 0) return CRGC_OK;  // ids only: nothing to resolve
+  if (mask) HIP_TRY(launch_resolve(h->g.d, 0, mask, nullptr, nullptr, nullptr, 0, nullptr, top, h->stream));
+  HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(xcnt), 0, 2 * MAX_SHARDS * 8, h->stream));
+  HIP_TRY(launch_resolve(h->g.d, 1, 0, nullptr, nullptr, nullptr, 0, nullptr, top, h->stream));
+  std::vector<uint64_t> M((size_t)G * G);
+  if (int rc = ag_u64(h, {{(char *)h->ctr + CTR_OFF(xcnt), G}}, M.data())) return rc;
+  uint64_t total = 0, nsend = 0;
+  for (uint64_t v : M) total += v;
+  for (uint32_t d = 0; d < G; ++d) nsend += M[(size_t)me * G + d];
+  if (total == 0) return CRGC_OK;
+  if (h->x_send.ensure(nsend * 8 + 8) != hipSuccess || h->x_slot.ensure(nsend * 4 + 8) != hipSuccess)
+    return CRGC_E_NOMEM;
+  HIP_TRY(launch_resolve(h->g.d, 2, 0, (uint64_t *)h->x_send.ptr, (uint32_t *)h->x_slot.ptr, nullptr, 0,
+                         nullptr, top, h->stream));
+  uint64_t nin = 0, nback = 0;
+  if (int rc = a2a(h, h->x_send.ptr, M.data(), 8, h->x_recv, false, &nin)) return rc;
+  if (h->x_ans.ensure(nin * 4 + 8) != hipSuccess) return CRGC_E_NOMEM;
+  HIP_TRY(launch_resolve(h->g.d, 3, 0, nullptr, nullptr, (const uint64_t *)h->x_recv.ptr, nin,
+                         (uint32_t *)h->x_ans.ptr, top, h->stream));
+  if (int rc = a2a(h, h->x_ans.ptr, M.data(), 4, h->x_ans_back, true, &nback)) return rc;
+  HIP_TRY(launch_resolve(h->g.d, 4, 0, nullptr, (uint32_t *)h->x_slot.ptr, nullptr, nsend,
+                         (uint32_t *)h->x_ans_back.ptr, top, h->stream));
+  *bytes += nsend * 8 + nin * 4;
+  return CRGC_OK;
+}
+
+// Sharded marks run in rounds: a local fixpoint, then every shard sends the
+// proxies it marked to their homes, which continue from them.  A marked proxy
+// travels as its home slot when the proxy has one cached — as a u32 list, or
+// as a bitmap over the home's slots once the list would be longer (a dense
+// round) — and as its id otherwise.  CRGC_XBITS: 0 ids only, 1 (default) the
+// cheaper form per destination, 2 bitmaps whenever slots are sent.
 static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t top, LevelRun &lr,
-                    uint64_t *rounds, uint64_t *ids_sent, double *ms_x) {
+                    uint64_t *rounds, uint64_t *ids_sent, double *ms_x, uint64_t *x_bytes) {
   int end = 0;
   if (int rc = run_levels(h, investigate, location, top, true, 0, lr, &end)) return rc;
   *rounds = 1;
   if (!h->tp) return CRGC_OK;
   const uint32_t G = h->G, me = h->shard;
+  int xmode = 1;
+  if (const char *m = getenv("CRGC_XBITS")) xmode = atoi(m);
+  {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (int rc = resolve_home_slots(h, top, xmode, x_bytes)) return rc;
+    *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
   const uint64_t nblk = round_up(std::min<uint64_t>(top, h->g.caps.scap), BLK_SLOTS) / BLK_SLOTS;
-  std::vector<uint64_t> M((size_t)G * G);
+  std::vector<uint64_t> M((size_t)G * 2 * G);
+  auto n_id = [&](uint32_t r, uint32_t d) { return M[(size_t)r * 2 * G + d]; };
+  auto n_sl = [&](uint32_t r, uint32_t d) { return M[(size_t)r * 2 * G + G + d]; };
+  auto words = [&](uint32_t d) { return (h->peer_top[d] + 31) / 32; };
+  auto bitmap = [&](uint32_t r, uint32_t d) {
+    return n_sl(r, d) > 0 && (xmode == 2 || n_sl(r, d) > words(d));
+  };
+  auto seg_bytes = [&](uint32_t r, uint32_t d) {
+    const uint64_t b = 8 * n_id(r, d) + 4 * (bitmap(r, d) ? words(d) : n_sl(r, d));
+    return (b + 7) & ~7ull;
+  };
   for (;;) {
     const auto t0 = std::chrono::steady_clock::now();
-    HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(xcnt), 0, 2 * MAX_SHARDS * 8, h->stream));
-    HIP_TRY(launch_list(h->g.d, 0, false, h->g.d.xp_buf, h->g.d.xp_cnt, nblk, nullptr, nullptr, h->stream));
-    if (int rc = ag_u64(h, {{(char *)h->ctr + CTR_OFF(xcnt), G}}, M.data())) return rc;
+    HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(xcnt), 0, 4 * MAX_SHARDS * 8, h->stream));
+    XSend xs{};
+    xs.use_slots = xmode != 0;
+    HIP_TRY(launch_xlist(h->g.d, false, nblk, nullptr, xs, h->stream));
+    if (int rc = ag_u64(h, {{(char *)h->ctr + CTR_OFF(xcnt), G}, {(char *)h->ctr + CTR_OFF(xcnt2), G}}, M.data()))
+      return rc;
     uint64_t total = 0, nsend = 0;
     for (uint64_t v : M) total += v;
-    for (uint32_t d = 0; d < G; ++d) nsend += M[(size_t)me * G + d];
     if (total == 0) {
       *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       return CRGC_OK;
     }
-    if (h->x_send.ensure(nsend * 8 + 8) != hipSuccess) return CRGC_E_NOMEM;
-    HIP_TRY(launch_list(h->g.d, 0, true, h->g.d.xp_buf, h->g.d.xp_cnt, nblk, (uint64_t *)h->x_send.ptr,
-                        nullptr, h->stream));
+    // this shard's segments: ids, then slots or a bitmap, per destination
+    std::vector<uint64_t> B((size_t)G * G);
+    for (uint32_t r = 0; r < G; ++r)
+      for (uint32_t d = 0; d < G; ++d) B[(size_t)r * G + d] = seg_bytes(r, d);
+    uint64_t so = 0;
+    for (uint32_t d = 0; d < G; ++d) {
+      xs.id_off[d] = so;
+      xs.sl_off[d] = so + 8 * n_id(me, d);
+      xs.bitmap[d] = bitmap(me, d) ? 1 : 0;
+      so += B[(size_t)me * G + d];
+      nsend += n_id(me, d) + n_sl(me, d);
+    }
+    if (h->x_send.ensure(so + 8) != hipSuccess) return CRGC_E_NOMEM;
+    for (uint32_t d = 0; d < G; ++d)
+      if (xs.bitmap[d]) HIP_TRY(hipMemsetAsync((char *)h->x_send.ptr + xs.sl_off[d], 0, 4 * words(d), h->stream));
+    HIP_TRY(launch_xlist(h->g.d, true, nblk, (char *)h->x_send.ptr, xs, h->stream));
     HIP_TRY(hipMemsetAsync(h->g.d.xp_cnt, 0, nblk * 4, h->stream));
     uint64_t nrecv = 0;
-    if (int rc = a2a(h, h->x_send.ptr, M.data(), 8, h->x_recv, false, &nrecv)) return rc;
+    if (int rc = a2a(h, h->x_send.ptr, B.data(), 1, h->x_recv, false, &nrecv)) return rc;
     *ids_sent += nsend;
-    // received ids are candidates of level L (a sparse level after an empty one)
+    *x_bytes += so;
+    XRecv xr{};
+    xr.G = G;
+    uint64_t ro = 0, items = 0;
+    for (uint32_t r = 0; r < G; ++r) {
+      xr.off[r] = ro;
+      xr.n_id[r] = n_id(r, me);
+      xr.bitmap[r] = bitmap(r, me) ? 1 : 0;
+      xr.start[r] = items;
+      items += n_id(r, me) + (xr.bitmap[r] ? words(me) : n_sl(r, me));
+      ro += B[(size_t)r * G + me];
+    }
+    xr.start[G] = items;
+    // received marks are candidates of level L (a sparse level after an empty one)
     const int L = end + 2;
     HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(ring) + ((L - 2) % LEVEL_RING) * 8, 0, 8, h->stream));
     HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(ring) + ((L - 1) % LEVEL_RING) * 8, 0, 8, h->stream));
     HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(tail_state), 0, 8, h->stream));
     HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(qh) + (L & 1) * 8, 0, 8, h->stream));
-    HIP_TRY(launch_import(h->g.d, (const uint64_t *)h->x_recv.ptr, nrecv, L, h->stream));
+    HIP_TRY(launch_ximport(h->g.d, (const char *)h->x_recv.ptr, xr, L, h->stream));
     *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (int rc = run_levels(h, investigate, location, top, false, L, lr, &end)) return rc;
     ++*rounds;
@@ -1601,7 +1706,7 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   const uint64_t top = h->slot_top + h->ids_since;
   reset_trace_counters(h);
   LevelRun lr;
-  uint64_t rounds = 0, ids_sent = 0;
+  uint64_t rounds = 0, ids_sent = 0, x_bytes = 0;
   double ms_x = 0;
   if (!h->tp) {
     // The sweep is enqueued behind every level chunk and runs only once the
@@ -1622,7 +1727,7 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
     if (int rc = run_levels(h, false, 0, top, true, 0, lr, &end, sweep)) return rc;
     absorb_counters(h);  // read back with the last chunk's level counts
   } else {
-    if (int rc = mark_all(h, false, 0, top, lr, &rounds, &ids_sent, &ms_x)) return rc;
+    if (int rc = mark_all(h, false, 0, top, lr, &rounds, &ids_sent, &ms_x, &x_bytes)) return rc;
     HIP_TRY(hipEventRecord(h->ev[1], h->stream));
     HIP_TRY(launch_trace_stats(h->g.d, h->stream));
     if (int rc = sweep_sharded(h, should_kill ? 1 : 0, top, &ms_x)) return rc;
@@ -1655,6 +1760,7 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   st.ms_expand = lr.ms_e;
   st.rounds = rounds;
   st.ids_sent = ids_sent;
+  st.exchange_bytes = x_bytes;
   st.ms_exchange = ms_x;
   float ms = 0;
   hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
@@ -2129,10 +2235,10 @@ int crgc_count_reachable_from(crgc_graph *h, uint16_t location, int64_t *out) {
   if (int rc = device_error(h)) return rc;
   reset_trace_counters(h);
   LevelRun lr;
-  uint64_t rounds = 0, sent = 0;
+  uint64_t rounds = 0, sent = 0, x_bytes = 0;
   double ms_x = 0;
   const uint64_t saved = h->last_levels;
-  const int rl = mark_all(h, true, location, h->slot_top, lr, &rounds, &sent, &ms_x);
+  const int rl = mark_all(h, true, location, h->slot_top, lr, &rounds, &sent, &ms_x, &x_bytes);
   h->last_levels = saved;
   if (rl) return rl;
   if (!h->tp) {

@@ -211,7 +211,28 @@ int level_grid(uint64_t slot_top);
 // sharded graphs
 hipError_t launch_list(const DevGraph &g, int mode, bool scatter, uint32_t *buf, uint32_t *cnt,
                        uint64_t nblk, uint64_t *send, uint32_t *send_slot, hipStream_t s);
-hipError_t launch_import(const DevGraph &g, const uint64_t *ids, uint64_t n, int level, hipStream_t s);
+// mark rounds in home-slot form: what this shard sends each destination
+// (byte offsets into the send buffer; bitmap[d]: a bitmap over d's slots in
+// place of a slot list) and what it received from each source
+struct XSend {
+  uint64_t id_off[MAX_SHARDS], sl_off[MAX_SHARDS];
+  uint8_t bitmap[MAX_SHARDS];
+  int use_slots;
+};
+struct XRecv {
+  uint32_t G;
+  uint64_t off[MAX_SHARDS];        // the source's segment in the receive buffer
+  uint64_t n_id[MAX_SHARDS];       // its ids, then u32 slots or bitmap words
+  uint64_t start[MAX_SHARDS + 1];  // work items before each source (ids + slots / words)
+  uint8_t bitmap[MAX_SHARDS];
+};
+hipError_t launch_xlist(const DevGraph &g, bool scatter, uint64_t nblk, char *send, const XSend &x,
+                        hipStream_t s);
+hipError_t launch_ximport(const DevGraph &g, const char *recv, const XRecv &x, int level, hipStream_t s);
+// home-slot resolution: 0 reset(mask), 1 count unresolved, 2 list them (ids, slots),
+// 3 answer asked ids (at the home), 4 store the answers
+hipError_t launch_resolve(const DevGraph &g, int step, uint32_t mask, uint64_t *send, uint32_t *slots,
+                          const uint64_t *ids, uint64_t n, uint32_t *ans, uint64_t slot_top, hipStream_t s);
 hipError_t launch_requests(const DevGraph &g, int phase, const uint64_t *ids, uint64_t n, uint8_t *ans,
                            const uint32_t *slots, hipStream_t s);
 hipError_t launch_invalidate(const DevGraph &g, const uint64_t *ids, uint64_t n, hipStream_t s);

@@ -23,6 +23,8 @@
 namespace crgc {
 
 constexpr uint64_t KEY_EMPTY = 0xFFFFFFFFFFFFFFFFull;
+constexpr uint32_t PHS_NONE = 0xFFFFFFFFu;    // proxy's home slot not resolved yet
+constexpr uint32_t PHS_ABSENT = 0xFFFFFFFEu;  // the home shard has no live shadow of the id
 constexpr uint64_t KEY_TOMB = 0xFFFFFFFFFFFFFFFEull;
 constexpr uint32_t SLOT_NONE = 0xFFFFFFFFu;  // Java null supervisor
 constexpr uint32_t SLOT_DEAD = 0xFFFFFFFEu;  // supervisor collected (post-rebuild)
@@ -91,6 +93,8 @@ struct Counters {
   unsigned long long n_req;          // kill requests (garbage with a remote supervisor)
   unsigned long long xcnt[MAX_SHARDS];  // ids to send per destination shard
   unsigned long long xpos[MAX_SHARDS];  // scatter cursors
+  unsigned long long xcnt2[MAX_SHARDS]; // mark rounds: home slots to send per destination
+  unsigned long long xpos2[MAX_SHARDS]; // their scatter cursors
   unsigned long long ring[LEVEL_RING];
 };
 
@@ -168,6 +172,7 @@ struct DevGraph {
   uint32_t *xp_cnt;   // per block: listed proxies
   uint32_t *rq_buf;   // per-block regions: garbage slots whose kill waits on a remote mark
   uint32_t *rq_cnt;   // per block: listed requests
+  uint32_t *phs;      // per proxy slot: its slot at the home shard (PHS_NONE / PHS_ABSENT)
   Counters *ctr;
 };
 

@@ -1231,30 +1231,202 @@ hipError_t launch_list(const DevGraph &g, int mode, bool scatter, uint32_t *buf,
   return hipGetLastError();
 }
 
-// Ids received from other shards' marked proxies become candidates of level
-// L (a sparse level: the dirty map names their blocks).  ring[L-1] gets the
-// number of candidates so the level kernels run.
-__global__ __launch_bounds__(256) void k_import(DevGraph g, const uint64_t *ids, uint64_t n, int L) {
-  uint8_t *Fc = g.front[L & 1];
-  uint8_t *Dc = g.dirty[L & 1];
-  uint32_t found = 0;
+// ---- mark rounds in home-slot form (sharded graphs) -------------------------
+// A proxy caches its actor's slot at the home shard (g.phs), resolved once by
+// an id exchange and dropped when the home compacts (renumbers) its slots.
+// A marked proxy with a cached home slot travels as that slot: a list of u32
+// slots, or — when that is longer — a bitmap over the home's slots; one
+// without travels as its id.
+
+// Proxies homed at the shards in `mask` forget their home slots.
+__global__ __launch_bounds__(256) void k_phs_reset(DevGraph g, uint32_t mask) {
+  const uint64_t top = g.ctr->slot_top, stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < top; v += stride)
+    if ((g.flags[v] & FL_PROXY) && ((mask >> shard_of(g.vid[v], g.n_shards)) & 1u)) g.phs[v] = PHS_NONE;
+}
+
+__device__ inline bool unresolved_proxy(const DevGraph &g, uint64_t v) {
+  return (g.flags[v] & (FL_ALIVE | FL_PROXY)) == (FL_ALIVE | FL_PROXY) && g.phs[v] == PHS_NONE;
+}
+
+// Unresolved proxies by home shard: counts (xcnt), then ids + local slots
+// (send / send_slot, grouped by destination; cursors xpos).
+template <bool SCATTER>
+__global__ __launch_bounds__(256) void k_res_list(DevGraph g, uint64_t *send, uint32_t *send_slot) {
+  __shared__ uint32_t hist[MAX_SHARDS];
+  __shared__ unsigned long long base[MAX_SHARDS];
+  for (uint32_t d = threadIdx.x; d < MAX_SHARDS; d += 256) hist[d] = 0;
+  __syncthreads();
+  const uint64_t top = g.ctr->slot_top, stride = (uint64_t)gridDim.x * 256;
+  const uint64_t v0 = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  for (uint64_t v = v0; v < top; v += stride)
+    if (unresolved_proxy(g, v)) atomicAdd(&hist[shard_of(g.vid[v], g.n_shards)], 1u);
+  __syncthreads();
+  if (!SCATTER) {
+    for (uint32_t d = threadIdx.x; d < g.n_shards; d += 256)
+      if (hist[d]) atomicAdd(&g.ctr->xcnt[d], (unsigned long long)hist[d]);
+    return;
+  }
+  if (threadIdx.x < g.n_shards) {
+    const uint32_t d = threadIdx.x;
+    unsigned long long off = 0;
+    for (uint32_t e = 0; e < d; ++e) off += g.ctr->xcnt[e];
+    base[d] = off + (hist[d] ? atomicAdd(&g.ctr->xpos[d], (unsigned long long)hist[d]) : 0ull);
+    hist[d] = 0;
+  }
+  __syncthreads();
+  for (uint64_t v = v0; v < top; v += stride) {
+    if (!unresolved_proxy(g, v)) continue;
+    const uint64_t id = g.vid[v];
+    const uint32_t d = shard_of(id, g.n_shards);
+    const uint64_t at = base[d] + atomicAdd(&hist[d], 1u);
+    send[at] = id;
+    send_slot[at] = (uint32_t)v;
+  }
+}
+
+// At the home: the slot of each asked id (PHS_ABSENT: no live home shadow).
+__global__ __launch_bounds__(256) void k_res_answer(DevGraph g, const uint64_t *ids, uint64_t n, uint32_t *ans) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
     const uint32_t v = id_find(g, ids[i]);
-    if (v >= 0xFFFFFFF0u) continue;  // collected since (cannot happen while proxies are purged)
-    if ((g.flags[v] & (FL_ALIVE | FL_PROXY)) != FL_ALIVE) continue;
-    if ((g.vis[v >> 5] >> (v & 31)) & 1u) continue;
-    Fc[v] = 1;
-    Dc[v >> 11] = 1;
-    ++found;
+    ans[i] = (v < 0xFFFFFFF0u && (g.flags[v] & (FL_ALIVE | FL_PROXY)) == FL_ALIVE) ? v : PHS_ABSENT;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_phs_set(DevGraph g, const uint32_t *slots, const uint32_t *ans,
+                                                 uint64_t n) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) g.phs[slots[i]] = ans[i];
+}
+
+hipError_t launch_resolve(const DevGraph &g, int step, uint32_t mask, uint64_t *send, uint32_t *slots,
+                          const uint64_t *ids, uint64_t n, uint32_t *ans, uint64_t slot_top, hipStream_t s) {
+  const int vgrid = grid_for(slot_top, 256, 4096);
+  switch (step) {
+    case 0: hipLaunchKernelGGL(k_phs_reset, dim3(vgrid), dim3(256), 0, s, g, mask); break;
+    case 1: hipLaunchKernelGGL(k_res_list<false>, dim3(vgrid), dim3(256), 0, s, g, send, slots); break;
+    case 2: hipLaunchKernelGGL(k_res_list<true>, dim3(vgrid), dim3(256), 0, s, g, send, slots); break;
+    case 3:
+      if (n) hipLaunchKernelGGL(k_res_answer, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, g, ids, n, ans);
+      break;
+    default:
+      if (n) hipLaunchKernelGGL(k_phs_set, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, g, slots, ans, n);
+  }
+  return hipGetLastError();
+}
+
+// Marked proxies listed by k_frontier / k_tail, by destination: ids of the
+// unresolved (xcnt), home slots of the resolved (xcnt2); then the scatter
+// into the byte layout the host derived from the all-gathered counts.
+template <bool SCATTER>
+__global__ __launch_bounds__(256) void k_xlist(DevGraph g, const uint32_t *buf, const uint32_t *cnt,
+                                               uint64_t nblk, char *send, XSend x) {
+  __shared__ uint32_t hist[2][MAX_SHARDS];
+  __shared__ unsigned long long base[2][MAX_SHARDS];
+  for (uint32_t d = threadIdx.x; d < 2 * MAX_SHARDS; d += 256) hist[d / MAX_SHARDS][d % MAX_SHARDS] = 0;
+  __syncthreads();
+  const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t blk = gw; blk < nblk; blk += nw) {
+    const uint32_t n = cnt[blk];
+    for (uint32_t i = lane_id(); i < n; i += 64) {
+      const uint32_t v = buf[blk * BLK_SLOTS + i];
+      const uint32_t d = shard_of(g.vid[v], g.n_shards);
+      const bool res = x.use_slots && g.phs[v] < PHS_ABSENT;
+      atomicAdd(&hist[res ? 1 : 0][d], 1u);
+    }
+  }
+  __syncthreads();
+  if (!SCATTER) {
+    for (uint32_t d = threadIdx.x; d < g.n_shards; d += 256) {
+      if (hist[0][d]) atomicAdd(&g.ctr->xcnt[d], (unsigned long long)hist[0][d]);
+      if (hist[1][d]) atomicAdd(&g.ctr->xcnt2[d], (unsigned long long)hist[1][d]);
+    }
+    return;
+  }
+  if (threadIdx.x < g.n_shards) {
+    const uint32_t d = threadIdx.x;
+    base[0][d] = hist[0][d] ? atomicAdd(&g.ctr->xpos[d], (unsigned long long)hist[0][d]) : 0ull;
+    base[1][d] = hist[1][d] && !x.bitmap[d] ? atomicAdd(&g.ctr->xpos2[d], (unsigned long long)hist[1][d]) : 0ull;
+    hist[0][d] = hist[1][d] = 0;
+  }
+  __syncthreads();
+  for (uint64_t blk = gw; blk < nblk; blk += nw) {
+    const uint32_t n = cnt[blk];
+    for (uint32_t i = lane_id(); i < n; i += 64) {
+      const uint32_t v = buf[blk * BLK_SLOTS + i];
+      const uint64_t id = g.vid[v];
+      const uint32_t d = shard_of(id, g.n_shards);
+      const uint32_t hs = x.use_slots ? g.phs[v] : PHS_NONE;
+      if (hs >= PHS_ABSENT) {
+        const uint64_t at = base[0][d] + atomicAdd(&hist[0][d], 1u);
+        ((uint64_t *)(send + x.id_off[d]))[at] = id;
+      } else if (x.bitmap[d]) {
+        atomicOr((uint32_t *)(send + x.sl_off[d]) + (hs >> 5), 1u << (hs & 31));
+      } else {
+        const uint64_t at = base[1][d] + atomicAdd(&hist[1][d], 1u);
+        ((uint32_t *)(send + x.sl_off[d]))[at] = hs;
+      }
+    }
+  }
+}
+
+hipError_t launch_xlist(const DevGraph &g, bool scatter, uint64_t nblk, char *send, const XSend &x,
+                        hipStream_t s) {
+  if (nblk == 0) return hipSuccess;
+  const int grid = (int)((nblk + 3) / 4);
+  if (scatter)
+    hipLaunchKernelGGL(k_xlist<true>, dim3(grid), dim3(256), 0, s, g, g.xp_buf, g.xp_cnt, nblk, send, x);
+  else
+    hipLaunchKernelGGL(k_xlist<false>, dim3(grid), dim3(256), 0, s, g, g.xp_buf, g.xp_cnt, nblk, send, x);
+  return hipGetLastError();
+}
+
+// Received marks become candidates of level L (a sparse level: the dirty map
+// names their blocks); ring[L-1] gets their number so the level kernels run.
+// Work item i: source r = the last with x.start[r] <= i; its ids first, then
+// its home slots (or bitmap words).
+__device__ inline uint32_t import_mark(const DevGraph &g, uint8_t *Fc, uint8_t *Dc, uint32_t v, uint64_t top) {
+  if (v >= top) return 0;
+  if ((g.flags[v] & (FL_ALIVE | FL_PROXY)) != FL_ALIVE) return 0;
+  if ((g.vis[v >> 5] >> (v & 31)) & 1u) return 0;
+  Fc[v] = 1;
+  Dc[v >> 11] = 1;
+  return 1;
+}
+
+__global__ __launch_bounds__(256) void k_ximport(DevGraph g, const char *recv, XRecv x, int L) {
+  uint8_t *Fc = g.front[L & 1];
+  uint8_t *Dc = g.dirty[L & 1];
+  const uint64_t top = g.ctr->slot_top;
+  uint32_t found = 0;
+  const uint64_t total = x.start[x.G], stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += stride) {
+    uint32_t r = 0;
+    while (r + 1 < x.G && x.start[r + 1] <= i) ++r;
+    const uint64_t k = i - x.start[r];
+    const char *seg = recv + x.off[r];
+    if (k < x.n_id[r]) {
+      const uint32_t v = id_find(g, ((const uint64_t *)seg)[k]);
+      if (v < 0xFFFFFFF0u) found += import_mark(g, Fc, Dc, v, top);
+      continue;
+    }
+    const uint64_t j = k - x.n_id[r];
+    const uint32_t w = ((const uint32_t *)(seg + 8 * x.n_id[r]))[j];
+    if (!x.bitmap[r]) {
+      found += import_mark(g, Fc, Dc, w, top);
+    } else {
+      for (uint32_t m = w; m; m &= m - 1) found += import_mark(g, Fc, Dc, (uint32_t)(j * 32) + __ffs(m) - 1, top);
+    }
   }
   const uint64_t t = block_sum4(found);
   if (threadIdx.x == 0 && t) atomicAdd(&g.ctr->ring[(L - 1) % LEVEL_RING], (unsigned long long)t);
 }
 
-hipError_t launch_import(const DevGraph &g, const uint64_t *ids, uint64_t n, int level, hipStream_t s) {
+hipError_t launch_ximport(const DevGraph &g, const char *recv, const XRecv &x, int level, hipStream_t s) {
+  const uint64_t n = x.start[x.G];
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_import, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, g, ids, n, level);
+  hipLaunchKernelGGL(k_ximport, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, g, recv, x, level);
   return hipGetLastError();
 }
 
