@@ -12,7 +12,7 @@
 //      scatter; <= 512 blocks split the exact atom count between them).
 //   2. k_ep_owner: one workgroup per owner bucket — every atom of an owner is
 //      in its workgroup, so the owner's segment, degree and nonzero count are
-//      written without atomics.  512 atoms at a time: the pairs are reduced in
+//      written without atomics.  1024 atoms at a time: the pairs are reduced in
 //      an LDS hash table (LDS atomics); each distinct pair finds or inserts its
 //      edge-table key; existing edges take the summed delta (a count that
 //      changes sign updates its reverse candidate in place); new edges get a
@@ -31,9 +31,9 @@
 namespace crgc {
 
 constexpr int EP_THREADS = 256;     // partition kernels
-constexpr int EP_WG = 512;          // owner / target range kernels
-constexpr uint32_t EP_CH = 512;     // atoms per round in a bucket workgroup (one per thread)
-constexpr uint32_t EP_TAB = 1024;   // LDS pair / owner tables (load <= 1/2)
+constexpr int EP_WG = 1024;         // owner / target bucket kernels (2 workgroups per CU)
+constexpr uint32_t EP_CH = 1024;    // atoms per round in a bucket workgroup (one per thread)
+constexpr uint32_t EP_TAB = 2048;   // LDS pair / owner tables (load <= 1/2)
 constexpr uint32_t EP_EXIST = 0xFFFFFFFFu;
 constexpr uint32_t EP_SKIP = 0xFFFFFFFEu;
 constexpr uint32_t EP_PENDING = 0x80000000u;  // etab rev: reverse atom (position) not yet appended
@@ -161,8 +161,8 @@ struct EpOwnerLds {
   uint32_t bkt[EP_TAB];   // edge-table bucket
   uint32_t okey[EP_TAB];  // owner table: owner slot (~0: free)
   uint32_t ocnt[EP_TAB];  // new edges of the owner in this round
-  uint32_t obase[EP_TAB]; // the owner's degree before them
-  int32_t onz[EP_TAB];    // change of the owner's nonzero count
+  int32_t onz[EP_TAB];    // change of the owner's nonzero count; after the growth,
+                          // the owner's degree before its new edges
   uint32_t plist[EP_CH];  // pair table entries in use
   uint32_t olist[EP_CH];  // owner table entries in use
   uint32_t np, nol, nnew, nrv;
@@ -288,10 +288,10 @@ __global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
           g.ecap[o] = want;
         }
         L.ocnt[oh] = add;
-        L.obase[oh] = ad.y;
         if (add) g.adj[o] = make_uint2(ad.x, ad.y + add);
         const int32_t dz = L.onz[oh] + (int32_t)add;  // new edges have nonzero counts
         if (dz) g.nzdeg[o] = (uint32_t)((int32_t)g.nzdeg[o] + dz);
+        L.onz[oh] = (int32_t)ad.y;
       }
     }
     __syncthreads();
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
         const uint32_t o = (uint32_t)(key >> 32), t = (uint32_t)key;
         const uint32_t oh = ep_owner_slot(L, o);
         if (L.ocnt[oh]) {  // else the pool is full (error set)
-          const uint32_t idx = L.obase[oh] + rk;
+          const uint32_t idx = (uint32_t)L.onz[oh] + rk;
           const int32_t d = L.sum[ph];
           const uint32_t bk = L.bkt[ph];
           g.pool[(uint64_t)g.adj[o].x + idx] = pack_edge(t, d);
