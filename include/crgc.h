@@ -253,6 +253,10 @@ typedef struct crgc_delta_graphs {
 } crgc_delta_graphs;
 
 int crgc_build_delta_graphs(crgc_graph *g, const crgc_entry_batch *batch, crgc_delta_graphs *out);
+/* With CRGC_MEM_DEVICE outputs the arrays are written by kernels queued on the
+   graph's stream when crgc_build_delta_graphs returns (sizes are final): work
+   queued after it on that stream sees them; crgc_sync waits for them. */
+int crgc_sync(crgc_graph *g);
 
 /*
  * UndoLog folding on the device.  A collector folds every
@@ -343,6 +347,14 @@ int crgc_total_actors_seen(crgc_graph *g, uint64_t *out);
 
 /* Number of shadows in the graph (|from| == |shadowMap|). */
 int crgc_live_count(crgc_graph *g, uint64_t *out);
+
+/* Compact the graph now (no reference counterpart: the JVM's own GC does
+   this for ShadowGraph's objects): live shadows renumbered densely, zero-count
+   edges and edges to collected shadows dropped, edge and candidate segments
+   repacked in slot order.  A trace does it by itself once dead slots
+   outnumber live ones, and a merge when a capacity would be exceeded;
+   results are unchanged either way. */
+int crgc_compact(crgc_graph *g);
 
 int crgc_export(crgc_graph *g, crgc_graph_export *out);
 

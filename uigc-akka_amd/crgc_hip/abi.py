@@ -207,6 +207,8 @@ EXPORTED_SYMBOLS = (
     "crgc_count_reachable_from",
     "crgc_total_actors_seen",
     "crgc_live_count",
+    "crgc_compact",
+    "crgc_sync",
     "crgc_export",
     "crgc_build_delta_graphs",
     "crgc_undo_acc_create",
@@ -240,6 +242,9 @@ def _declare(lib: C.CDLL, prefix: str) -> None:
         "export": (C.c_int, [g, P(CrgcGraphExport)]),
         "destroy": (None, [g]),
     }
+    if prefix == "crgc_":  # product-only entry point (the JVM compacts by itself)
+        sig["compact"] = (C.c_int, [g])
+        sig["sync"] = (C.c_int, [g])
     for name, (res, args) in sig.items():
         fn = getattr(lib, prefix + name)
         fn.restype = res

@@ -232,6 +232,11 @@ class ShadowGraph:
     def total_actors_seen(self) -> int:
         return self.totalActorsSeen
 
+    def compact(self):
+        """Compact the graph now (crgc_compact): dense slots, segments in slot order."""
+        self.flush()
+        self._chk(self.lib.crgc_compact(self.h), "crgc_compact")
+
     def live_count(self) -> int:
         self.flush()
         v = C.c_uint64()
@@ -251,14 +256,21 @@ class ShadowGraph:
         self._chk(self.lib.crgc_merge_undo_acc(self.h, acc.h), "crgc_merge_undo_acc")
 
     # -- DeltaGraph production (num-nodes > 1, LocalGC.scala:159-177) --------------
-    def build_delta_graphs(self, batch: EntryBatch, device_out: bool = False):
+    def sync(self):
+        """Wait for everything queued on the graph's stream (crgc_sync)."""
+        self._chk(self.lib.crgc_sync(self.h), "crgc_sync")
+        self._synced()
+
+    def build_delta_graphs(self, batch: EntryBatch, device_out: bool = False, sync: bool = True):
         """The wakeup's entries folded into DeltaGraphs on the device
         (DeltaGraph.java:73-180).  Returns (DeltaBatch of the decoded shadows,
         graph_off, wire bytes, wire_off): graph g is shadows
         graph_off[g]:graph_off[g+1] and payload bytes wire[wire_off[g]:wire_off[g+1]]
         (writeShort(size) + DeltaShadow.serialize per shadow).  device_out: the
         arrays are torch tensors on the graph's device.  The returned arrays are
-        views of buffers reused by the next call with the same device_out."""
+        views of buffers reused by the next call with the same device_out.  Device
+        outputs are stream-ordered: sync=False leaves them to work the caller queues
+        on the graph's stream."""
         s = batch.struct()
         key = "_dg_dev" if device_out else "_dg_host"
         bufs = getattr(self, key, None)
@@ -280,6 +292,8 @@ class ShadowGraph:
             setattr(self, key, bufs)
         else:
             self._chk(rc, "crgc_build_delta_graphs")
+        if device_out and sync:
+            self.sync()
         arrs = bufs[0]
         G, NS, NO, NW = q.n_graphs, q.n_shadows, q.n_out, q.wire_bytes
         cut = lambda k, n: arrs[k][:n]  # noqa: E731
@@ -470,6 +484,9 @@ class ShardedShadowGraph:
 
     def live_count(self) -> int:
         return sum(s.live_count() for s in self.shards)
+
+    def compact(self):
+        self._all(lambda s: s.compact())
 
     def startWave(self):
         return np.concatenate([s.startWave() for s in self.shards])

@@ -1797,7 +1797,8 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
   if (h->DGS > DG_MAX || h->DGS <= 4 * h->F + 1) return CRGC_E_INVAL;
   DeviceGuard dg(h->device);
   uint64_t C = 0, S = 0, U = 0;
-  if (int rc = entry_counts(h, b, true, &C, &S, &U)) return rc;
+  // device batches: bounds only (the kernels read the exact totals), no round trip
+  if (int rc = entry_counts(h, b, false, &C, &S, &U)) return rc;
   const uint64_t n = b->n_entries;
   if (n >= (1ull << 31)) return CRGC_E_INVAL;
   const size_t nh_bytes =
@@ -1805,8 +1806,8 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
           ? Carver::need({n * 8, n * 2, n, (n + 1) * 4, C * 8, C * 8, (n + 1) * 4, S * 8, (n + 1) * 4, U * 8,
                           U * 2})
           : 0;
-  uint32_t levels = 1;
-  while ((1ull << (levels - 1)) < n + 1) ++levels;
+  uint32_t levels = 1;  // J_k jumps 4^k graphs: 4^(levels-1) >= n + 1
+  while ((1ull << (2 * (levels - 1))) < n + 1) ++levels;
   const uint64_t N = n + 1, nblk = (n + 1023) / 1024, nbs = 4 * ((N + 1023) / 1024) + 8;
   const size_t need = Carver::need({sizeof(DgCounters), (size_t)levels * N * 4, N, N, nblk * 4 + 4,
                                     nblk * 8 + 8, nbs * 8, N * 4, N * 4, N * 4, N * 4, N * 8, N * 8, N * 8});
@@ -1856,10 +1857,26 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
     HIP_TRY(hipStreamSynchronize(h->stream));
     return CRGC_OK;
   };
+  // Device outputs of the right shape: the write pass can run on the device's
+  // counts before the host has seen them (capacities checked on the device).
+  const bool dev = out->memory == CRGC_MEM_DEVICE;
+  const bool any = out->graph_off || out->wire_off || out->id || out->recv_count || out->supervisor ||
+                   out->flags || out->out_off || out->out_target || out->out_count || out->wire;
+  const bool complete = out->graph_off && out->wire_off && out->id && out->recv_count && out->supervisor &&
+                        out->flags && out->out_off && out->out_target && out->out_count && out->wire;
+  DgOut o{};
+  if (dev) {
+    o = DgOut{out->graph_off, out->wire_off, out->id, out->recv_count, out->supervisor, out->flags,
+              out->out_off, out->out_target, out->out_count, out->wire,
+              out->graph_cap, out->shadow_cap, out->out_cap, out->wire_cap};
+  }
+  const bool speculate = dev && complete;
   uint64_t G = 0;
+  bool written = false;
   if (n) {
     // The chain, then the count pass and its scans without a host round trip:
-    // graph counts over the bound n + 1 (zero past the device's n_graphs).
+    // graph counts over the bound n + 1 (zero past the device's n_graphs);
+    // with device outputs the write pass and offsets follow the same way.
     DgOut none{};
     HIP_TRY(launch_dg_chain(a, 0, h->stream));
     HIP_TRY(hipMemsetAsync(a.g_size, 0, N * 4, h->stream));
@@ -1867,8 +1884,13 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
     HIP_TRY(hipMemsetAsync(a.g_bytes, 0, N * 4, h->stream));
     HIP_TRY(launch_dg_build(a, DG_NG_DEVICE, false, none, h->stream));
     HIP_TRY(launch_dg_scans(a, N, h->stream));
+    if (speculate) {
+      HIP_TRY(launch_dg_build(a, DG_NG_DEVICE, true, o, h->stream));
+      HIP_TRY(launch_dg_offsets(a, DG_NG_DEVICE, o, h->stream));
+    }
     if (int rc = fetch()) return rc;
     if (hc.err) return CRGC_E_INVAL;  // malformed offsets or reserved ids: nothing was built
+    written = speculate && hc.first_long == ~0u && !hc.overflow;
     if (hc.first_long != ~0u) {  // a chain start whose graph runs past the span window
       while (hc.first_long != ~0u) {
         HIP_TRY(launch_dg_chain(a, 1, h->stream));
@@ -1885,19 +1907,12 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
   out->n_shadows = NS;
   out->n_out = NO;
   out->wire_bytes = NW;
-  const bool any = out->graph_off || out->wire_off || out->id || out->recv_count || out->supervisor ||
-                   out->flags || out->out_off || out->out_target || out->out_count || out->wire;
   if (!any) return CRGC_OK;  // sizes only
   if (!out->graph_off || !out->wire_off || !out->id || !out->recv_count || !out->supervisor || !out->flags ||
       !out->out_off || (NO && (!out->out_target || !out->out_count)) || !out->wire)
     return CRGC_E_INVAL;
   if (out->graph_cap < G || out->shadow_cap < NS || out->out_cap < NO || out->wire_cap < NW) return CRGC_E2BIG;
-  DgOut o{};
-  const bool dev = out->memory == CRGC_MEM_DEVICE;
-  if (dev) {
-    o = DgOut{out->graph_off, out->wire_off, out->id, out->recv_count, out->supervisor, out->flags,
-              out->out_off, out->out_target, out->out_count, out->wire};
-  } else {
+  if (!dev) {
     const size_t ob = Carver::need({(G + 1) * 4, (G + 1) * 8, NS * 8, NS * 4, NS * 8, NS, (NS + 1) * 4, NO * 8,
                                     NO * 4, NW});
     if (h->x_dg_out.ensure(ob) != hipSuccess) return CRGC_E_NOMEM;
@@ -1913,10 +1928,10 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
     o.out_count = oc.take<int32_t>(NO);
     o.wire = oc.take<uint8_t>(NW);
   }
-  if (G) {
+  if (G && !written) {
     HIP_TRY(launch_dg_build(a, G, true, o, h->stream));
     HIP_TRY(launch_dg_offsets(a, G, o, h->stream));
-  } else {  // no graphs: the closing offsets only
+  } else if (!G) {  // no graphs: the closing offsets only
     HIP_TRY(hipMemsetAsync(o.graph_off, 0, 4, h->stream));
     HIP_TRY(hipMemsetAsync(o.wire_off, 0, 8, h->stream));
     HIP_TRY(hipMemsetAsync(o.out_off, 0, 4, h->stream));
@@ -1935,7 +1950,14 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
     HIP_TRY(d2h(out->out_target, o.out_target, NO * 8));
     HIP_TRY(d2h(out->out_count, o.out_count, NO * 4));
     HIP_TRY(d2h(out->wire, o.wire, NW));
+    HIP_TRY(hipStreamSynchronize(h->stream));
   }
+  return CRGC_OK;  // device outputs: stream-ordered (crgc_sync waits for them)
+}
+
+int crgc_sync(crgc_graph *h) {
+  if (int rc = check_graph(h)) return rc;
+  DeviceGuard dg(h->device);
   HIP_TRY(hipStreamSynchronize(h->stream));
   return CRGC_OK;
 }
@@ -2263,6 +2285,12 @@ int crgc_total_actors_seen(crgc_graph *h, uint64_t *out) {
   HIP_TRY(sync_counters(h));
   *out = h->hctr->inserted;
   return CRGC_OK;
+}
+
+int crgc_compact(crgc_graph *h) {
+  if (int rc = check_graph(h)) return rc;
+  DeviceGuard dg(h->device);
+  return rebuild(h, 0, 0);
 }
 
 int crgc_live_count(crgc_graph *h, uint64_t *out) {

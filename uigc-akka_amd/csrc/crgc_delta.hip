@@ -8,7 +8,7 @@
 //   k_dg_span     for every entry s, the end of a graph that would start at
 //                 s (one wave streams the entries past 64 starts through a
 //                 last-seen table; graphs longer than its window are deferred)
-//   k_dg_double   J_{k+1} = J_k o J_k (pointer doubling)
+//   k_dg_double   J_{k+1} = J_k^4 (pointer jumping, base 4)
 //   k_dg_mark     starts reachable from entry 0, top level down
 //   k_dg_long     one workgroup resolves the first deferred start on the
 //                 chain, 64 entries per step
@@ -30,6 +30,13 @@ __device__ inline uint32_t dg_hash(uint64_t id, uint32_t bits) {
 }
 __device__ inline bool dg_reserved(uint64_t id) { return id >= CRGC_DEAD_ACTOR; }
 
+// Lane j's value with j wave-uniform: v_readlane (scalar), not an LDS permute,
+// for the loops that walk a batch lane by lane.
+__device__ inline uint32_t rl32(uint32_t v, uint32_t j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j); }
+__device__ inline uint64_t rl64(uint64_t v, uint32_t j) {
+  return ((uint64_t)rl32((uint32_t)(v >> 32), j) << 32) | rl32((uint32_t)v, j);
+}
+
 struct DgRange {
   uint32_t c0, c1, s0, s1, u0, u1;
   bool bad;
@@ -39,17 +46,22 @@ struct DgRange {
 // reports offsets the merges would reject.
 __device__ inline DgRange dg_range(const DgArgs &a, uint64_t e) {
   DgRange r;
+  // record totals: the offsets' last entries (a.C / a.S / a.U bound them: for a
+  // device batch the host has not read them)
+  const uint64_t Ct = min(a.C, (uint64_t)a.c_off[a.n]), St = min(a.S, (uint64_t)a.s_off[a.n]),
+                 Ut = min(a.U, (uint64_t)a.u_off[a.n]);
   const uint32_t c0 = a.c_off[e], c1 = a.c_off[e + 1], s0 = a.s_off[e], s1 = a.s_off[e + 1];
   const uint32_t u0 = a.u_off[e], u1 = a.u_off[e + 1];
-  r.bad = c1 < c0 || s1 < s0 || u1 < u0 || c1 > a.C || s1 > a.S || u1 > a.U || c1 - c0 > a.F ||
-          s1 - s0 > a.F || u1 - u0 > a.F;
-  r.c1 = (uint32_t)min((uint64_t)c1, a.C);
+  r.bad = c1 < c0 || s1 < s0 || u1 < u0 || c1 > Ct || s1 > St || u1 > Ut || c1 - c0 > a.F ||
+          s1 - s0 > a.F || u1 - u0 > a.F || a.c_off[a.n] > a.C || a.s_off[a.n] > a.S || a.u_off[a.n] > a.U ||
+          a.c_off[0] || a.s_off[0] || a.u_off[0];
+  r.c1 = (uint32_t)min((uint64_t)c1, Ct);
   r.c0 = min(c0, r.c1);
   r.c1 = min(r.c1, r.c0 + a.F);
-  r.s1 = (uint32_t)min((uint64_t)s1, a.S);
+  r.s1 = (uint32_t)min((uint64_t)s1, St);
   r.s0 = min(s0, r.s1);
   r.s1 = min(r.s1, r.s0 + a.F);
-  r.u1 = (uint32_t)min((uint64_t)u1, a.U);
+  r.u1 = (uint32_t)min((uint64_t)u1, Ut);
   r.u0 = min(u0, r.u1);
   r.u1 = min(r.u1, r.u0 + a.F);
   return r;
@@ -114,13 +126,13 @@ __device__ inline DgBatch dg_batch(const DgArgs &a, DgCursor &C, uint64_t eb, ui
   if (eb < C.cb || eb - C.cb >= 48) dg_load(a, C, eb, e1);
   DgBatch B{};
   const uint32_t off = (uint32_t)(eb - C.cb);  // first cursor lane of the batch
-  const uint32_t before = off ? __shfl(C.incl, off - 1) : 0u;
+  const uint32_t before = off ? rl32(C.incl, off - 1) : 0u;
   const uint64_t fits = __ballot((uint32_t)lane >= off && C.cb + lane < e1 && C.incl - before <= 64);
   B.ne = fits ? (uint32_t)__popcll(fits) : 1;  // (m <= 1 + 4F <= 64)
-  B.mt = __shfl(C.incl, off + B.ne - 1) - before;
+  B.mt = rl32(C.incl, off + B.ne - 1) - before;
   uint32_t my_e = 0;  // the number of entries ending at or before this lane's id
   for (uint32_t q = 0; q < B.ne; ++q)
-    if (__shfl(C.incl, off + q) - before <= (uint32_t)lane) my_e = q + 1;
+    if (rl32(C.incl, off + q) - before <= (uint32_t)lane) my_e = q + 1;
   if (my_e >= B.ne) my_e = B.ne - 1;
   B.e = my_e;
   B.elane = off + my_e;
@@ -200,8 +212,8 @@ __global__ __launch_bounds__(256) void k_dg_span(DgArgs a) {
     }
     bool later = false;
     for (uint32_t j = 0; j < B.mt; ++j) {
-      const uint64_t xj = __shfl(x, j);
-      const uint32_t ej = __shfl(my_e, j);
+      const uint64_t xj = rl64(x, j);
+      const uint32_t ej = rl32(my_e, j);
       if (xj == x) {
         if (j < (uint32_t)lane) prev = (int32_t)ej;
         else if (j > (uint32_t)lane) later = true;
@@ -227,8 +239,8 @@ __global__ __launch_bounds__(256) void k_dg_span(DgArgs a) {
     const bool last_of_entry = has && (lane + 1 == (int)B.mt || next_e != B.e);
     const uint64_t lasts = __ballot(last_of_entry);
     for (uint32_t j = 0; j < B.mt; ++j) {
-      const uint32_t ej = __shfl(my_e, j);
-      const int32_t pj = __shfl(prev, j);
+      const uint32_t ej = rl32(my_e, j);
+      const int32_t pj = (int32_t)rl32((uint32_t)prev, j);
       if (!done && ej >= me_rel) {
         if (pj < (int32_t)me_rel) ++cnt;
         if (((lasts >> j) & 1) && cnt >= a.T) {
@@ -256,21 +268,28 @@ __global__ __launch_bounds__(256) void k_dg_span(DgArgs a) {
   if (lane == 0 && dl) atomicAdd(&a.ctr->n_long, (unsigned)__popcll(dl));
 }
 
+// Pointer jumping in base 4 (half the launches of doubling): J_{k+1} = J_k^4.
 __global__ __launch_bounds__(256) void k_dg_double(DgArgs a, uint32_t k) {
   const uint64_t N = a.n + 1;
   const uint32_t *Jk = a.J + (uint64_t)k * N;
   uint32_t *Jn = a.J + (uint64_t)(k + 1) * N;
   for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < N; s += (uint64_t)gridDim.x * 256)
-    Jn[s] = Jk[Jk[s]];
+    Jn[s] = Jk[Jk[Jk[Jk[s]]]];
 }
 
-// Marked after levels L-1 .. k: the chain's starts at multiples of 2^k steps
+// Marked after levels L-1 .. k: the chain's starts at multiples of 4^k steps
 // (a start marked early by a racing thread is a chain start too).
 __global__ __launch_bounds__(256) void k_dg_mark(DgArgs a, uint32_t k) {
   const uint64_t N = a.n + 1;
   const uint32_t *Jk = a.J + (uint64_t)k * N;
-  for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < N; s += (uint64_t)gridDim.x * 256)
-    if (a.mark[s]) a.mark[Jk[s]] = 1;
+  for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < N; s += (uint64_t)gridDim.x * 256) {
+    if (!a.mark[s]) continue;
+    uint32_t t = (uint32_t)s;
+    for (int d = 0; d < 3; ++d) {
+      t = Jk[t];
+      a.mark[t] = 1;
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void k_dg_first_long(DgArgs a) {
@@ -494,6 +513,7 @@ hipError_t launch_dg_chain(const DgArgs &a, int phase, hipStream_t s) {
 //      its map's size and largest size — all that java.util.HashMap iteration
 //      order depends on.
 constexpr uint32_t DGW_P = 128;  // id -> cid hash slots
+constexpr uint32_t DG_OPCAP = 512;  // updateOutgoing ops kept in LDS by pass 1 (more: pass 2 re-reads the ids)
 
 struct DgWave {
   uint64_t key[DGW_P];       // id per hash slot (KEY_EMPTY: free)
@@ -510,6 +530,7 @@ struct DgWave {
   uint8_t fl[DG_MAX];        // CRGC_DELTA_*
   uint8_t osz[DG_MAX];       // outgoing.size()
   uint8_t omax[DG_MAX];      // largest outgoing.size(): the HashMap's capacity
+  uint32_t ops[DG_OPCAP];    // pass 1's ops in order: owner slot | target slot << 8 | (+1) << 16
 };
 
 // Replays DeltaGraph.mergeEntry (DeltaGraph.java:73-125) over entries
@@ -526,7 +547,7 @@ __device__ uint32_t dg_replay(const DgArgs &a, uint64_t g, DgWave &W) {
   wave_lds_fence();
   const uint64_t e0 = a.starts[g], e1 = a.starts[g + 1];
   // pass 1: the ids, receive counts and last-write-wins fields, per hash slot
-  uint32_t pos = 0, ei = 0;
+  uint32_t pos = 0, ei = 0, nops = 0;
   DgCursor C;
   dg_load(a, C, e0, e1);
   for (uint64_t eb = e0; eb < e1;) {
@@ -544,6 +565,27 @@ __device__ uint32_t dg_replay(const DgArgs &a, uint64_t g, DgWave &W) {
       atomicMin(&W.first[h], pos + lane);
     }
     const uint32_t me = __shfl(h, B.base);
+    {  // the batch's updateOutgoing ops, in order, by hash slot (pass 2 maps them to cids)
+      const uint32_t prev_h = __shfl(h, (lane + 63) & 63);  // a created owner's target is the lane before
+      const uint32_t k = B.k;
+      bool emit = false;
+      uint32_t opv = 0;
+      if ((uint32_t)lane < B.mt && k >= 1) {
+        if (k < 1 + 2 * B.nc) {
+          if ((k - 1) & 1) {
+            emit = true;
+            opv = h | (prev_h << 8) | (1u << 16);
+          }
+        } else if (k >= 1 + 2 * B.nc + B.ns && refob_deactivated(B.info)) {
+          emit = true;
+          opv = me | (h << 8);
+        }
+      }
+      const uint64_t eball = __ballot(emit);
+      const uint32_t at = nops + (uint32_t)__popcll(eball & lanemask_lt());
+      if (emit && at < DG_OPCAP) W.ops[at] = opv;
+      nops += (uint32_t)__popcll(eball);
+    }
     const uint8_t ef = (uint8_t)__shfl((uint32_t)C.eflags, B.elane);
     const int32_t er = __shfl((int32_t)C.erecv, B.elane);
     if ((uint32_t)lane < B.mt) {
@@ -589,6 +631,37 @@ __device__ uint32_t dg_replay(const DgArgs &a, uint64_t g, DgWave &W) {
   wave_lds_fence();
   // pass 2: updateOutgoing in op order; lane o owns row o
   uint32_t clock = 0, osz = 0, omax = 0;
+  auto apply = [&](uint32_t v) {  // v = owner cid | target cid << 8 | (+1) << 16
+    if ((v & 0xFF) == (uint32_t)lane) {
+      const uint32_t kk = (uint32_t)lane * DG_MAX + ((v >> 8) & 0xFF);
+      const int32_t c0 = W.cnt[kk];
+      const int32_t nc = (int32_t)((uint32_t)c0 + ((v >> 16) ? 1u : 0xFFFFFFFFu));
+      W.cnt[kk] = nc;
+      if (c0 == 0) {  // put of an absent key: appended to its bin
+        W.ins[kk] = clock;
+        ++osz;
+        omax = max(omax, osz);
+      } else if (nc == 0) {  // remove
+        --osz;
+      }
+    }
+    ++clock;
+  };
+  if (nops <= DG_OPCAP) {  // the ops pass 1 kept: no global reads
+    for (uint32_t c0 = 0; c0 < nops; c0 += 64) {
+      const uint32_t n = min(64u, nops - c0);
+      uint32_t op = 0;
+      if ((uint32_t)lane < n) {
+        const uint32_t v = W.ops[c0 + lane];
+        op = W.tabc[v & 0xFF] | ((uint32_t)W.tabc[(v >> 8) & 0xFF] << 8) | (v & (1u << 16));
+      }
+      for (uint32_t j = 0; j < n; ++j) apply(rl32(op, j));
+    }
+    W.osz[lane] = (uint8_t)osz;
+    W.omax[lane] = (uint8_t)omax;
+    wave_lds_fence();
+    return size;
+  }
   dg_load(a, C, e0, e1);
   for (uint64_t eb = e0; eb < e1;) {
     const DgBatch B = dg_batch(a, C, eb, e1);
@@ -619,21 +692,7 @@ __device__ uint32_t dg_replay(const DgArgs &a, uint64_t g, DgWave &W) {
     while (bits) {
       const int j = __ffsll((unsigned long long)bits) - 1;
       bits &= bits - 1;
-      const uint32_t v = __shfl(op, j);
-      if ((v & 0xFF) == (uint32_t)lane) {
-        const uint32_t kk = (uint32_t)lane * DG_MAX + ((v >> 8) & 0xFF);
-        const int32_t c0 = W.cnt[kk];
-        const int32_t nc = (int32_t)((uint32_t)c0 + ((v >> 16) ? 1u : 0xFFFFFFFFu));
-        W.cnt[kk] = nc;
-        if (c0 == 0) {  // put of an absent key: appended to its bin
-          W.ins[kk] = clock;
-          ++osz;
-          omax = max(omax, osz);
-        } else if (nc == 0) {  // remove
-          --osz;
-        }
-      }
-      ++clock;
+      apply(rl32(op, j));
     }
     eb += B.ne;
   }
@@ -709,15 +768,27 @@ __device__ void dg_emit(const DgArgs &a, uint64_t g, const DgWave &W, uint32_t s
   }
 }
 
+// The outputs hold the graphs the device counted (write passes that run before
+// the host has seen the totals).
+__device__ inline bool dg_fits(const DgArgs &a, uint64_t ng, const DgOut &o) {
+  return ng <= o.graph_cap && a.ctr->n_shadows <= o.shadow_cap && a.ctr->n_out <= o.out_cap &&
+         a.ctr->wire <= o.wire_cap;
+}
+
 // ng == DG_NG_DEVICE: the graph count is the device's (n_graphs), and nothing
 // is built while a deferred chain start is unresolved (first_long set): the
-// host then resolves it and runs the count pass again.
+// host then resolves it and runs the passes again.  A write pass on the
+// device's count also checks the output capacities (overflow: nothing written).
 template <bool WRITE>
 __global__ __launch_bounds__(64) void k_dg_build(DgArgs a, uint64_t ng, DgOut o) {
   __shared__ DgWave W;
   if (ng == DG_NG_DEVICE) {
     if (a.ctr->first_long != ~0u) return;
     ng = a.ctr->n_graphs;
+    if (WRITE && !dg_fits(a, ng, o)) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr->overflow = 1;
+      return;
+    }
   }
   for (uint64_t g = blockIdx.x; g < ng; g += gridDim.x) {
     const uint32_t size = dg_replay(a, g, W);
@@ -763,6 +834,11 @@ hipError_t launch_dg_scans(const DgArgs &a, uint64_t ng, hipStream_t s) {
 }
 
 __global__ __launch_bounds__(256) void k_dg_offsets(DgArgs a, uint64_t ng, DgOut o) {
+  if (ng == DG_NG_DEVICE) {
+    if (a.ctr->first_long != ~0u) return;
+    ng = a.ctr->n_graphs;
+    if (!dg_fits(a, ng, o)) return;
+  }
   for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g <= ng; g += (uint64_t)gridDim.x * 256) {
     if (g < ng) {
       o.graph_off[g] = (uint32_t)a.g_shadow[g];
@@ -776,7 +852,8 @@ __global__ __launch_bounds__(256) void k_dg_offsets(DgArgs a, uint64_t ng, DgOut
 }
 
 hipError_t launch_dg_offsets(const DgArgs &a, uint64_t ng, const DgOut &o, hipStream_t s) {
-  hipLaunchKernelGGL(k_dg_offsets, dim3(dg_grid(ng + 1)), dim3(256), 0, s, a, ng, o);
+  hipLaunchKernelGGL(k_dg_offsets, dim3(dg_grid((ng == DG_NG_DEVICE ? a.n + 1 : ng) + 1)), dim3(256), 0, s, a, ng,
+                     o);
   return hipGetLastError();
 }
 

@@ -323,6 +323,7 @@ struct DgCounters {
   unsigned int n_long;
   unsigned long long n_graphs;  // graph starts (exclusive-scan total)
   unsigned long long n_shadows, n_out, wire;  // totals of the per-graph scans
+  unsigned long long overflow;  // a write pass on the device's count found the outputs too small
 };
 
 struct DgArgs {
@@ -365,6 +366,8 @@ struct DgOut {
   uint64_t *out_target;
   int32_t *out_count;
   uint8_t *wire;
+  // capacities, checked on the device when the pass runs on the device's count
+  uint64_t graph_cap, shadow_cap, out_cap, wire_cap;
 };
 
 // phase 0: spans + doubling + chain from entry 0; 1: chain from a resolved
@@ -376,6 +379,7 @@ constexpr uint64_t DG_NG_DEVICE = ~0ull;
 hipError_t launch_dg_build(const DgArgs &a, uint64_t n_graphs, bool write, const DgOut &o, hipStream_t s);
 // exclusive scans of the per-graph counts (after the count pass)
 hipError_t launch_dg_scans(const DgArgs &a, uint64_t n_graphs, hipStream_t s);
+// (n_graphs == DG_NG_DEVICE: the device's count and the capacities in o)
 hipError_t launch_dg_offsets(const DgArgs &a, uint64_t n_graphs, const DgOut &o, hipStream_t s);
 
 // UndoLog folding on the device (crgc_undo.hip)
