@@ -1,14 +1,20 @@
 """Per-kernel durations from a rocprofv3 rocpd database, restricted to the last
 K dispatches of each kernel (the bench's steady-state wakeups).
-usage: python profiles/kt_summary.py <run_results.db> [K]"""
+usage: python profiles/kt_summary.py <run_results.db | kernel_trace.csv> [K] [--wakeup]"""
 import sqlite3
 import sys
 from collections import defaultdict
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 db, K = args[0], int(args[1]) if len(args) > 1 else 4
-c = sqlite3.connect(db)
-rows = c.execute("select name, start, end, grid_x, workgroup_x from kernels order by start").fetchall()
+if db.endswith(".csv"):  # rocprofv3 --output-format csv kernel_trace.csv
+    import csv
+    rows = sorted(((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                    int(r["Grid_Size_X"]), int(r["Workgroup_Size_X"])) for r in csv.DictReader(open(db))),
+                  key=lambda x: x[1])
+else:
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, start, end, grid_x, workgroup_x from kernels order by start").fetchall()
 by = defaultdict(list)
 for name, s, e, gx, wx in rows:
     by[name].append((e - s, gx // max(wx, 1)))
