@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import ctypes as C
 import dataclasses
+import sys
 from typing import List, Optional
 
 import numpy as np
@@ -32,14 +33,19 @@ from .batch import (Entry, EntryBatch, DeltaBatch, UndoBatch, TraceResult, Graph
 
 
 def _host_ids(n: int) -> np.ndarray:
-    """A host id buffer for trace results: page-locked when torch can provide
-    it (the device copies into it directly), else ordinary memory."""
-    try:
-        import torch
-        if torch.cuda.is_available():
-            return torch.empty(n, dtype=torch.int64, pin_memory=True).numpy().view(np.uint64)
-    except Exception:
-        pass
+    """A host id buffer for trace results: page-locked when the process already
+    uses torch (the device copies into it directly), else ordinary memory.
+    torch is never imported from here: importing it after this library has
+    initialised the HIP runtime makes the process abort in its exit handlers
+    (torch's pinned-memory pool outlives the runtime), so a torch-free caller
+    stays torch-free."""
+    torch = sys.modules.get("torch")
+    if torch is not None:
+        try:
+            if torch.cuda.is_available():
+                return torch.empty(n, dtype=torch.int64, pin_memory=True).numpy().view(np.uint64)
+        except Exception:
+            pass
     return np.zeros(n, np.uint64)
 
 
