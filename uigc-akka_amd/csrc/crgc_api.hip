@@ -525,37 +525,6 @@ static size_t edge_scratch(const crgc_graph *h, uint64_t max_atoms) {
                        max_atoms * 4, max_atoms * 4});
 }
 
-// Work scratch of a merge's vertex atoms and their partition (crgc_vertex.hip).
-static size_t vertex_scratch(const crgc_graph *h, uint64_t max_atoms) {
-  uint32_t bshift, nbk;
-  uint64_t nblk;
-  edge_geometry(h, max_atoms, bshift, nbk, nblk);
-  const uint64_t nh = (uint64_t)nbk * nblk;
-  return Carver::need({max_atoms * 16, 8, nh * 4, nh * 8, ((nh + 1023) / 1024) * 4 * 8 + 64, 16, max_atoms * 16});
-}
-
-static uint4 *take_vertex_atoms(Carver &cv, uint64_t max_atoms) { return cv.take<uint4>(max_atoms); }
-
-// The vertex half of a merge: atoms written by the entry / delta kernels.
-static int run_vertex(crgc_graph *h, const uint4 *atoms, uint64_t max_atoms, const uint64_t *n_dev,
-                      unsigned long long epoch, Carver &cv) {
-  if (max_atoms == 0) return CRGC_OK;
-  VxArgs va{};
-  va.max_atoms = max_atoms;
-  va.n_dev = n_dev;
-  va.atoms = atoms;
-  va.epoch = epoch;
-  edge_geometry(h, max_atoms, va.bshift, va.nbk, va.nblk);
-  const uint64_t nh = (uint64_t)va.nbk * va.nblk;
-  va.hist = cv.take<uint32_t>(nh);
-  va.hoff = cv.take<uint64_t>(nh);
-  va.bsum = cv.take<uint64_t>(((nh + 1023) / 1024) * 4 + 8);
-  va.tot = cv.take<unsigned long long>(2);
-  va.part = cv.take<uint4>(max_atoms);
-  HIP_TRY(launch_vertex(h->g.d, va, h->stream));
-  return CRGC_OK;
-}
-
 static int run_edges(crgc_graph *h, uint32_t *ao, uint32_t *at, int32_t *ad, uint64_t max_atoms,
                      Carver &cv, const uint64_t *n_atoms_dev = nullptr) {
   if (max_atoms == 0) return CRGC_OK;
@@ -777,7 +746,7 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   const size_t work_bytes =
       Carver::need({n * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4, sh ? n : 0,
                     sh ? n * h->F * 8 : 0, 8}) +
-      edge_scratch(h, max_atoms) + vertex_scratch(h, n + max_atoms);
+      edge_scratch(h, max_atoms);
   if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
     return CRGC_E_NOMEM;
   Carver sc(h->stage.ptr), wc(h->work.ptr);
@@ -810,13 +779,9 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   a.atom_t = wc.take<uint32_t>(max_atoms);
   a.atom_d = wc.take<int32_t>(max_atoms);
   a.n_atoms = wc.take<uint64_t>(1);
-  const uint64_t vmax = n + max_atoms;  // self + spawned + updated records
-  a.vx = take_vertex_atoms(wc, vmax);
-  a.vx_n = wc.take<uint64_t>(1);
   // atoms of entries refused for bad offsets stay zero (never applied)
   hipMemsetAsync(a.atom_d, 0, max_atoms * 4, h->stream);
   HIP_TRY(launch_entries(h->g.d, a, h->stream));
-  if (int rc = run_vertex(h, a.vx, vmax, a.vx_n, a.epoch, wc)) return rc;
   if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, max_atoms, wc, a.n_atoms)) return rc;
   note_merge(h, ids, C + U);
   HIP_TRY(wait_staged(h, b->memory));
@@ -1058,7 +1023,6 @@ static int delta_counts(crgc_graph *h, const crgc_delta_batch *b, uint64_t *nout
 static int merge_deltas_one(crgc_graph *h, const crgc_delta_batch *b, uint64_t nout) {
   const uint64_t n = b->n_shadows;
   if (n == 0) return CRGC_OK;
-  if (n > VX_SEQ) return CRGC_E_INVAL;  // record positions are 30-bit in the vertex atoms
   const uint64_t ids = 2 * n + nout;
   if (int rc = ensure_capacity(h, ids, nout)) return rc;
   const size_t host_bytes =
@@ -1067,7 +1031,7 @@ static int merge_deltas_one(crgc_graph *h, const crgc_delta_batch *b, uint64_t n
   const bool sh = h->tp;
   const size_t work_bytes =
       Carver::need({n * 4, n * 4, std::max<uint64_t>(nout, 1) * 4, sh ? std::max<uint64_t>(nout, 1) * 8 : 0}) +
-      edge_scratch(h, nout) + vertex_scratch(h, 2 * n);
+      edge_scratch(h, nout);
   if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
     return CRGC_E_NOMEM;
   Carver sc(h->stage.ptr), wc(h->work.ptr);
@@ -1089,9 +1053,7 @@ static int merge_deltas_one(crgc_graph *h, const crgc_delta_batch *b, uint64_t n
   a.atom_o = wc.take<uint32_t>(std::max<uint64_t>(nout, 1));
   a.atom_t = wc.take<uint32_t>(std::max<uint64_t>(nout, 1));
   a.atom_d = wc.take<int32_t>(std::max<uint64_t>(nout, 1));
-  a.vx = take_vertex_atoms(wc, 2 * n);
   HIP_TRY(launch_deltas(h->g.d, a, nout, h->stream));
-  if (int rc = run_vertex(h, a.vx, 2 * n, nullptr, a.epoch, wc)) return rc;
   if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, nout, wc)) return rc;
   note_merge(h, ids, nout);
   HIP_TRY(wait_staged(h, b->memory));

@@ -93,8 +93,6 @@ struct EntryArgs {
   uint32_t *co_slot;     // [n*F] created owners
   uint32_t *u_slot;      // [n*F] updated refs
   uint64_t *n_atoms;     // out: C + U, the atoms k_entries_apply wrote (exact edge-pipeline count)
-  uint4 *vx;             // [n + 2*n*F] vertex atoms: self [0, n), spawned [n, n+S), updated [n+S, n+S+U)
-  uint64_t *vx_n;        // out: n + S + U
   uint32_t *atom_o;      // [2*n*F]: created atoms, then updated atoms
   uint32_t *atom_t;
   int32_t *atom_d;
@@ -120,7 +118,6 @@ struct DeltaArgs {
   uint32_t *atom_t;
   int32_t *atom_d;
   uint64_t *o_partner;   // sharded graphs: [nout] owning delta shadow of each outgoing entry
-  uint4 *vx;             // [2n] vertex atoms: the shadow's own fields [0, n), its supervisor [n, 2n)
 };
 
 struct UndoArgs {
@@ -137,26 +134,6 @@ struct UndoArgs {
   uint32_t *atom_t;
   int32_t *atom_d;
 };
-
-// Vertex updates of a merge (crgc_vertex.hip): atoms {slot (>= 0xFFFFFFF0:
-// none), seq | VX_FLAGS | VX_SUP, recv delta, flag bits to set or supervisor
-// slot}, partitioned by slot and reduced per slot in LDS.
-constexpr uint32_t VX_FLAGS = 0x80000000u;
-constexpr uint32_t VX_SUP = 0x40000000u;
-constexpr uint32_t VX_SEQ = 0x3FFFFFFFu;
-struct VxArgs {
-  uint64_t max_atoms;
-  const uint64_t *n_dev;   // exact count on the device, or null (max_atoms)
-  const uint4 *atoms;
-  unsigned long long epoch;
-  uint32_t bshift, nbk;
-  uint64_t nblk;
-  uint32_t *hist;
-  uint64_t *hoff, *bsum;
-  unsigned long long *tot;
-  uint4 *part;
-};
-hipError_t launch_vertex(const DevGraph &g, const VxArgs &a, hipStream_t s);
 
 struct EdgeArgs {
   uint64_t max_atoms;          // grid bound

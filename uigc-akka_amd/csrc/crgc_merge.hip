@@ -3,12 +3,12 @@
 // A merge call replaces N sequential ShadowGraph.mergeEntry / mergeDelta calls
 // (ShadowGraph.java:75-156) by one data-parallel pass, exact because the merge
 // is commutative except for last-write-wins fields:
-//   * recvCount        += deltas          -> vertex atoms, summed per slot (crgc_vertex.hip)
-//   * outgoing[o][t]   += deltas          -> edge atoms, summed per pair (crgc_edges.hip)
+//   * recvCount        += deltas          -> wrapping int32 atomics
+//   * outgoing[o][t]   += deltas          -> edge pipeline (k_edge_* below)
 //   * interned/isLocal |= ...             -> written by the LWW winner (every
 //                                            record that sets busy/root sets them)
-//   * isBusy/isRoot     last write wins   -> the highest (epoch<<32 | seq) per slot,
-//   * supervisor        last write wins      resolved in LDS by the slot's workgroup
+//   * isBusy/isRoot     last write wins   -> atomicMax of (epoch<<32 | seq) tags,
+//   * supervisor        last write wins      then the winner writes the field.
 // `epoch` counts merge calls, `seq` is the record's position inside the call,
 // so "last" is exactly the reference's order (LocalGC.scala:152-172).
 #include "crgc_host.hpp"
@@ -77,11 +77,9 @@ hipError_t launch_ids(const DevGraph &g, const IdArgs &a, hipStream_t s) {
 
 // ---------------------------------------------------------------------------
 // Entries — ShadowGraph.mergeEntry, ShadowGraph.java:75-125.  One thread per
-// entry over slots resolved by k_ids: the edge atoms and the vertex atoms
-// (receive counts, flags, supervisors: crgc_vertex.hip applies them).
+// entry over slots resolved by k_ids: receive counts, the LWW tags, and the
+// edge atoms.
 // ---------------------------------------------------------------------------
-__device__ inline uint4 vx_none() { return make_uint4(0xFFFFFFFFu, 0, 0, 0); }
-
 __global__ __launch_bounds__(256) void k_entries_apply(DevGraph g, EntryArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= a.n) return;
@@ -98,13 +96,12 @@ __global__ __launch_bounds__(256) void k_entries_apply(DevGraph g, EntryArgs a) 
     ok = false;
   }
   const uint32_t me = ok ? a.self_slot[i] : SLOT_INVALID;
-  const uint64_t C = min((uint64_t)a.c_off[a.n], cmax), S = min((uint64_t)a.s_off[a.n], cmax),
-                 U = min((uint64_t)a.u_off[a.n], cmax);
-  if (i == 0) {  // exact counts for the edge and vertex pipelines: no host round trip
-    if (a.n_atoms) *a.n_atoms = C + U;
-    *a.vx_n = a.n + S + U;
+  if (!ok) a.self_slot[i] = SLOT_INVALID;
+  if (i == 0 && a.n_atoms) {  // atoms [0, C) created, [C, C + U) updated: the edge pipeline's exact count
+    const uint64_t C = min((uint64_t)a.c_off[a.n], cmax), U = min((uint64_t)a.u_off[a.n], cmax);
+    *a.n_atoms = C + U;
   }
-  const uint32_t seq = (uint32_t)(i + 1);
+  const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
   const int16_t rc = a.recv[i];
   // Sharded graphs: every record is applied by the home shard of the shadow
   // it writes (self, edge owner, spawned child, updated target).  k_ids only
@@ -112,15 +109,10 @@ __global__ __launch_bounds__(256) void k_entries_apply(DevGraph g, EntryArgs a) 
   // a home slot; self may be a proxy (the supervisor of a child homed here).
   const bool sh = g.n_shards > 1;
   const bool self_home = !sh || is_home(g, a.self[i]);
-  // Local information (:77-82): recv delta, busy / root (last write wins),
-  // interned and local.
+  // Local information (:77-82): recv delta and the busy/root LWW tag.
   if (vs(me) && self_home) {
-    const uint8_t ef = a.flags[i];
-    const uint32_t set = FL_INTERNED | FL_LOCAL | ((ef & CRGC_ENTRY_BUSY) ? FL_BUSY : 0) |
-                         ((ef & CRGC_ENTRY_ROOT) ? FL_ROOT : 0);
-    a.vx[i] = make_uint4(me, seq | VX_FLAGS, (uint32_t)(int32_t)rc, set);
-  } else {
-    a.vx[i] = vx_none();
+    if (rc != 0) atomicAdd(&g.recv[me], (int32_t)rc);
+    atomicMax(&g.vseq[me], tag);
   }
   if (!ok) return;
   const uint32_t ctot = a.c_off[a.n];
@@ -134,7 +126,9 @@ __global__ __launch_bounds__(256) void k_entries_apply(DevGraph g, EntryArgs a) 
   // Spawned actors (:96-104): child.supervisor = self, last write wins.
   for (uint32_t k = s0; k < s1; ++k) {
     const uint32_t cs = a.spawn_slot[k];
-    a.vx[a.n + k] = (vs(cs) && vs(me)) ? make_uint4(cs, seq | VX_SUP, 0, me) : vx_none();
+    const bool good = vs(cs) && vs(me);
+    if (!good) a.spawn_slot[k] = SLOT_INVALID;
+    if (good) atomicMax(&g.sseq[cs], tag);
   }
   // Updated refs (:107-123): target.recv -= count; deactivation -> -1 edge.
   for (uint32_t k = u0; k < u1; ++k) {
@@ -143,11 +137,33 @@ __global__ __launch_bounds__(256) void k_entries_apply(DevGraph g, EntryArgs a) 
     const bool good = vs(ts) && vs(me);
     const int32_t cnt = refob_count(info);
     const bool tgt_ok = sh ? (vs(ts) && is_home(g, a.u_ref[k])) : good;
-    a.vx[a.n + S + k] = (tgt_ok && cnt > 0) ? make_uint4(ts, 0, (uint32_t)(-cnt), 0) : vx_none();
+    if (tgt_ok && cnt > 0) atomicAdd(&g.recv[ts], -cnt);
     const uint64_t at = (uint64_t)ctot + k;
     a.atom_o[at] = me;
     a.atom_t[at] = ts;
     a.atom_d[at] = (good && self_home && refob_deactivated(info)) ? -1 : 0;
+  }
+}
+
+// The LWW winners write the flag byte and the supervisor slot.
+__global__ __launch_bounds__(256) void k_entries_lww(DevGraph g, EntryArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const uint32_t me = a.self_slot[i];
+  if (!vs(me)) return;
+  const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
+  if (g.vseq[me] == tag) {
+    const uint8_t ef = a.flags[i];
+    uint8_t f = g.flags[me] & (uint8_t)~(FL_BUSY | FL_ROOT);
+    f |= FL_INTERNED | FL_LOCAL;
+    if (ef & CRGC_ENTRY_BUSY) f |= FL_BUSY;
+    if (ef & CRGC_ENTRY_ROOT) f |= FL_ROOT;
+    g.flags[me] = f;
+  }
+  const uint32_t s0 = a.s_off[i], s1 = a.s_off[i + 1];
+  for (uint32_t k = s0; k < s1; ++k) {
+    const uint32_t cs = a.spawn_slot[k];
+    if (vs(cs) && g.sseq[cs] == tag) g.sup[cs] = me;
   }
 }
 
@@ -184,6 +200,7 @@ hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s) 
                     nullptr};
   if (hipError_t e = launch_ids(g, ia, s)) return e;
   hipLaunchKernelGGL(k_entries_apply, dim3(blocks), dim3(256), 0, s, g, a);
+  hipLaunchKernelGGL(k_entries_lww, dim3(blocks), dim3(256), 0, s, g, a);
   return hipGetLastError();
 }
 
@@ -202,20 +219,18 @@ __global__ __launch_bounds__(256) void k_deltas_apply(DevGraph g, DeltaArgs a) {
     ok = false;
   }
   const uint32_t me = ok ? a.self_slot[i] : SLOT_INVALID;
-  const uint32_t seq = (uint32_t)(i + 1);
-  const uint8_t df = a.flags[i];
+  if (!ok) a.self_slot[i] = SLOT_INVALID;
+  const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
+  const uint8_t fl = a.flags[i];
   const int32_t rc = a.recv[i];
-  // recv delta; flags only when the delta shadow is interned (:139-146), and
-  // isLocal never (:135)
   if (vs(me)) {
-    const bool in = (df & CRGC_DELTA_INTERNED) != 0;
-    const uint32_t set = FL_INTERNED | ((df & CRGC_DELTA_BUSY) ? FL_BUSY : 0) | ((df & CRGC_DELTA_ROOT) ? FL_ROOT : 0);
-    a.vx[i] = make_uint4(me, seq | (in ? VX_FLAGS : 0u), (uint32_t)rc, in ? set : 0u);
-  } else {
-    a.vx[i] = vx_none();
+    if (rc != 0) atomicAdd(&g.recv[me], rc);
+    if (fl & CRGC_DELTA_INTERNED) atomicMax(&g.vseq[me], tag);
   }
   const uint32_t ss = a.sup_slot[i];  // SLOT_INVALID: no supervisor in this delta
-  a.vx[a.n + i] = (vs(ss) && vs(me)) ? make_uint4(me, seq | VX_SUP, 0, ss) : vx_none();
+  const bool sup_ok = vs(ss) && vs(me);
+  a.sup_slot[i] = sup_ok ? ss : SLOT_INVALID;
+  if (sup_ok) atomicMax(&g.sseq[me], tag);
   if (!ok) return;
   for (uint32_t k = o0; k < o1; ++k) {
     const uint32_t ts = a.ot_slot[k];
@@ -223,6 +238,24 @@ __global__ __launch_bounds__(256) void k_deltas_apply(DevGraph g, DeltaArgs a) {
     a.atom_t[k] = ts;
     a.atom_d[k] = (vs(ts) && vs(me)) ? a.out_count[k] : 0;
   }
+}
+
+__global__ __launch_bounds__(256) void k_deltas_lww(DevGraph g, DeltaArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const uint32_t me = a.self_slot[i];
+  if (!vs(me)) return;
+  const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
+  const uint8_t df = a.flags[i];
+  if ((df & CRGC_DELTA_INTERNED) && g.vseq[me] == tag) {
+    uint8_t f = g.flags[me] & (uint8_t)~(FL_BUSY | FL_ROOT);
+    f |= FL_INTERNED;
+    if (df & CRGC_DELTA_BUSY) f |= FL_BUSY;
+    if (df & CRGC_DELTA_ROOT) f |= FL_ROOT;
+    g.flags[me] = f;
+  }
+  const uint32_t ss = a.sup_slot[i];
+  if (vs(ss) && g.sseq[me] == tag) g.sup[me] = ss;
 }
 
 // Sharded graphs: the owning delta shadow of every outgoing entry.
@@ -249,6 +282,7 @@ hipError_t launch_deltas(const DevGraph &g, const DeltaArgs &a, uint64_t n_out, 
                     sh ? a.o_partner : nullptr, nullptr};
   if (hipError_t e = launch_ids(g, ia, s)) return e;
   hipLaunchKernelGGL(k_deltas_apply, dim3(blocks), dim3(256), 0, s, g, a);
+  hipLaunchKernelGGL(k_deltas_lww, dim3(blocks), dim3(256), 0, s, g, a);
   return hipGetLastError();
 }
 
