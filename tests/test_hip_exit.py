@@ -14,7 +14,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 SCRIPT = r"""
 import sys
-sys.path[:0] = [{pkg!r}, {tests!r}]
+sys.path[:0] = [{pkg!r}, {tests!r}, {wl!r}]
 import crgc_hip, kats
 w = kats.RandomWorld(seed=7, max_actors=300, wake_every=13)
 h = crgc_hip.ShadowGraph()
@@ -28,7 +28,8 @@ print("ok")
 
 
 def test_torch_free_process_exits_cleanly():
-    code = SCRIPT.format(pkg=os.path.join(REPO, "uigc-akka_amd"), tests=os.path.join(REPO, "tests"))
+    code = SCRIPT.format(pkg=os.path.join(REPO, "uigc-akka_amd"), tests=os.path.join(REPO, "tests"),
+                         wl=os.path.join(REPO, "workload"))
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, (p.returncode, p.stdout[-500:], p.stderr[-2000:])
     assert p.stdout.strip().endswith("ok")
