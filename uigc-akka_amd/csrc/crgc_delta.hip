@@ -157,7 +157,7 @@ __device__ inline DgBatch dg_batch(const DgArgs &a, DgCursor &C, uint64_t eb, ui
 }
 
 // ---- the chain of graph starts ----------------------------------------------
-// One wave per 64 consecutive starts (lane l: start s0 + l).  The wave streams
+// One wave per SPAN_S consecutive starts (lane l: start s0 + l).  The wave streams
 // entries from s0, a batch of whole entries (<= 64 ids, one per lane) at a
 // time, through one table of the ids seen so far with the last entry each was
 // seen in.  An occurrence is new to lane l's graph iff the id's previous
@@ -168,20 +168,22 @@ __device__ inline DgBatch dg_batch(const DgArgs &a, DgCursor &C, uint64_t eb, ui
 // SPAN_WIN entries (or when the table is 3/4 full) are deferred.
 constexpr uint32_t SPAN_P = 1024;    // ids per wave table
 constexpr uint32_t SPAN_WIN = 192;   // entries a wave streams past s0
+constexpr uint32_t SPAN_S = 64;      // graph starts per wave (32 measured no faster: profiles/r2j)
 
 __global__ __launch_bounds__(256) void k_dg_span(DgArgs a) {
   __shared__ uint64_t key[4][SPAN_P];
-  __shared__ uint32_t last[4][SPAN_P];
+  __shared__ uint16_t last[4][SPAN_P];  // entry relative to s0 (< SPAN_WIN + 64): 40 KB per workgroup, 4 per CU
   const int w = threadIdx.x >> 6, lane = lane_id();
-  const uint64_t s0 = ((uint64_t)blockIdx.x * 4 + w) * 64;
+  const uint64_t s0 = ((uint64_t)blockIdx.x * 4 + w) * SPAN_S;
   if (s0 > a.n) return;
   uint64_t *K = key[w];
-  uint32_t *Ls = last[w];
+  uint16_t *Ls = last[w];
   for (uint32_t k = lane; k < SPAN_P; k += 64) K[k] = CRGC_NO_ACTOR;
   wave_lds_fence();
+  const bool mine = (uint32_t)lane < SPAN_S;  // lanes past SPAN_S only carry ids
   const uint64_t s = s0 + lane;
   uint32_t cnt = 0;
-  bool done = s >= a.n, bad = false;
+  bool done = !mine || s >= a.n, bad = false;
   uint64_t end = s >= a.n ? a.n : s;
   uint32_t used = 0;
   uint64_t e = s0;
@@ -229,7 +231,7 @@ __global__ __launch_bounds__(256) void k_dg_span(DgArgs a) {
         if (y == CRGC_NO_ACTOR || y == x) break;
         h = (h + 1) & (SPAN_P - 1);
       }
-      Ls[h] = my_e;
+      Ls[h] = (uint16_t)my_e;
     }
     used += (uint32_t)__popcll(__ballot(fresh));
     wave_lds_fence();
@@ -256,7 +258,9 @@ __global__ __launch_bounds__(256) void k_dg_span(DgArgs a) {
     end = a.n;
   }
   if (__ballot(bad) && lane == 0) atomicOr(&a.ctr->err, 1ull);
-  if (s > a.n) return;
+  const uint64_t dl = __ballot(mine && s < a.n && !done);
+  if (lane == 0 && dl) atomicAdd(&a.ctr->n_long, (unsigned)__popcll(dl));
+  if (!mine || s > a.n) return;
   if (s == a.n) {
     a.J[s] = (uint32_t)a.n;
     a.lng[s] = 0;
@@ -264,8 +268,6 @@ __global__ __launch_bounds__(256) void k_dg_span(DgArgs a) {
   }
   a.J[s] = (uint32_t)(done ? end : s);  // a deferred start points at itself until k_dg_long
   a.lng[s] = !done;
-  const uint64_t dl = __ballot(!done);
-  if (lane == 0 && dl) atomicAdd(&a.ctr->n_long, (unsigned)__popcll(dl));
 }
 
 // Pointer jumping in base 4 (half the launches of doubling): J_{k+1} = J_k^4.
@@ -470,7 +472,7 @@ static int dg_grid(uint64_t n) { return (int)std::min<uint64_t>((n + 255) / 256,
 hipError_t launch_dg_chain(const DgArgs &a, int phase, hipStream_t s) {
   const uint64_t N = a.n + 1;
   if (phase == 0) {
-    hipLaunchKernelGGL(k_dg_span, dim3((N + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_dg_span, dim3((N + 4 * SPAN_S - 1) / (4 * SPAN_S)), dim3(256), 0, s, a);
     for (uint32_t k = 0; k + 1 < a.levels; ++k)
       hipLaunchKernelGGL(k_dg_double, dim3(dg_grid(N)), dim3(256), 0, s, a, k);
     hipMemsetAsync(a.mark, 0, N, s);
