@@ -47,7 +47,7 @@ void free_arrays(Arrays &a) {
                 d.pool, d.etab, d.vis, d.front[0], d.front[1],
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat, d.xbytes,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill,
-                d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.fx, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
+                d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.par, d.fx, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
                 d.xp_buf, d.xp_cnt, d.rq_buf, d.rq_cnt, d.phs};
   for (void *p : ps)
     if (p) hipFree(p);
@@ -115,6 +115,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   A(dmalloc(&d.rcap, c.scap));
   A(dmalloc(&d.rnew, c.scap));
   A(dmalloc(&d.rpool, d.rpcap));
+  A(dmalloc(&d.par, c.scap));
   A(dmalloc(&d.fx, c.scap / 32));
   A(dmalloc(&d.tq, 2 * (uint64_t)TAIL_QCAP));
   A(dmalloc(&d.tl_buf, c.scap));
@@ -150,6 +151,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   hipMemsetAsync(d.radj, 0, c.scap * 8, s);
   hipMemsetAsync(d.rcap, 0, c.scap * 4, s);
   hipMemsetAsync(d.rnew, 0, c.scap * 4, s);
+  hipMemsetAsync(d.par, 0xFF, c.scap * 4, s);  // no hints in a new generation
   hipMemsetAsync(d.fx, 0, c.scap / 8, s);
   hipMemsetAsync(d.cm, 0, c.scap / 8, s);
   hipMemsetAsync(d.pb[0], 0, c.scap / 8, s);

@@ -245,6 +245,7 @@ __global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
               const uint32_t cand = o | (now > 0 ? RC_POS : 0u);
               if (r != 0xFFFFFFFFu && (r & EP_PENDING)) a.rv_o[a0 + (r & ~EP_PENDING)] = cand;
               else if (r < g.rcap[t]) g.rpool[(uint64_t)g.radj[t].x + r] = cand;
+              if (now <= 0 && g.par[t] == o) g.par[t] = SLOT_NONE;  // the pull hint dies with the count
             }
             rk = EP_EXIST;
           } else {

@@ -137,6 +137,9 @@ struct DevGraph {
   uint32_t *rcap;
   uint32_t *rnew;            // rebuild scratch: in-degree per target
   uint32_t *rpool;           // owner slot | RC_POS while count(owner -> slot) > 0
+  uint32_t *par;             // pull hint per slot: an owner whose edge to it has a positive count
+                             // (the candidate a pull level last found; cleared when that count
+                             // stops being positive), or SLOT_NONE
   uint64_t rpcap;
   uint32_t *fx;              // expandable frontier bitmap (frontier & !halted)
   uint32_t *tq;              // narrow-frontier queues, 2 x TAIL_QCAP slots

@@ -395,6 +395,29 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
         todo |= (((fl >> (8 * j)) & FL_ALIVE) && !((cand >> (8 * j)) & 0xFFu) && !((vb >> j) & 1u))
                     ? (1u << j) : 0u;
       if (!todo) continue;
+      uint32_t found = 0;
+      // Hints first: the owner a pull level found last time, if its edge is
+      // still positive (hints are cleared when it stops being) and it is in
+      // the expandable frontier now — one L2-resident bit, no candidate list.
+      {
+        const uint4 h4 = *(const uint4 *)(g.par + v0);
+        const uint32_t hs[4] = {h4.x, h4.y, h4.z, h4.w};
+        nb2 += 32;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t p = hs[j];
+          if (((todo >> j) & 1u) && p < 0xFFFFFFF0u && ((g.fx[p >> 5] >> (p & 31)) & 1u)) {
+            found |= 1u << (8 * j);
+            todo &= ~(1u << j);
+            nb2 += 8;
+          }
+        }
+      }
+      if (!todo) {
+        *(uint32_t *)(Fn + v0) = cand | found;
+        nb2 += 8;
+        continue;
+      }
       const uint4 r01 = *(const uint4 *)(g.radj + v0);
       const uint4 r23 = *(const uint4 *)(g.radj + v0 + 2);
       const uint32_t ro[4] = {r01.x, r01.z, r23.x, r23.z};
@@ -403,7 +426,7 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
       // The thread's (up to) 4 lists are walked together, PULL_K candidates of
       // each per round: one round trip for the candidates, one for their
       // frontier bits, until every list has a hit or is exhausted.
-      uint32_t found = 0, live = todo, pos = 0;
+      uint32_t live = todo, pos = 0;
       while (live) {
         uint32_t u[4][PULL_K];
 #pragma unroll
@@ -424,9 +447,18 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           bool hit = false;
+          uint32_t who = 0;
 #pragma unroll
-          for (int k = 0; k < PULL_K; ++k) hit |= (w[j][k] & 1u) != 0;
-          if (hit && ((live >> j) & 1u)) found |= 1u << (8 * j);
+          for (int k = PULL_K - 1; k >= 0; --k)
+            if (w[j][k] & 1u) {
+              hit = true;
+              who = u[j][k] & ~RC_POS;
+            }
+          if (hit && ((live >> j) & 1u)) {
+            found |= 1u << (8 * j);
+            g.par[v0 + j] = who;  // the next trace tries this owner first
+            nb2 += 8;
+          }
           if (hit || pos >= rl[j]) live &= ~(1u << j);
         }
       }
