@@ -200,3 +200,23 @@ def test_last_trace_survives_the_compaction_after_a_trace(hip_mod, oracle_mod):
     g2, k2 = h.last_trace()
     assert set(g2.tolist()) == ro.garbage_set() and set(k2.tolist()) == ro.kill_set()
     _same_trace(h.trace(True), o.trace(True))
+
+
+@pytest.mark.parametrize("buckets_log2", ["1", "3"])
+def test_edge_buckets_in_several_rounds(hip_mod, oracle_mod, buckets_log2, monkeypatch):
+    """Two or eight owner / target buckets: every bucket workgroup takes its
+    atoms in several 1024-atom rounds, so pairs repeat across rounds, edges
+    inserted in one round are updated (and flip sign) in the next, and segments
+    grow more than once per merge — still bit-exact, state included."""
+    monkeypatch.setenv("CRGC_BUCKETS_LOG2", buckets_log2)
+    h, o = _pair(hip_mod, oracle_mod)
+    fz = fuzz.Fuzz(17)
+    for step in range(8):
+        eb = fz.entries(2000 + 500 * step)
+        h.merge_entries(eb); o.merge_entries(eb)
+        db = fz.deltas(40)
+        h.merge_deltas(db); o.merge_deltas(db)
+        assert h.export() == o.export()
+        _same_trace(h.trace(True), o.trace(True))
+        fz.sync(o.export())
+    assert h.export() == o.export()

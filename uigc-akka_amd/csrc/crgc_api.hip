@@ -509,7 +509,9 @@ static void edge_geometry(const crgc_graph *h, uint64_t max_atoms, uint32_t &bsh
                           uint64_t &nblk) {
   uint32_t lg = 0;
   while ((1ull << lg) < h->g.d.scap) ++lg;
-  const uint32_t lk = lg > 18 ? 10u : (lg > 9 ? lg - 8 : 1u);
+  uint32_t lk = lg > 18 ? 10u : (lg > 9 ? lg - 8 : 1u);
+  // test hook: fewer buckets, so buckets take several rounds of atoms
+  if (const char *m = getenv("CRGC_BUCKETS_LOG2")) lk = std::min<uint32_t>(10, std::max<uint32_t>(1, (uint32_t)atoi(m)));
   bshift = 32 - lk;
   nbk = 1u << lk;
   nblk = std::min<uint64_t>((max_atoms + 1023) / 1024, 512);
