@@ -2057,7 +2057,11 @@ int crgc_undo_acc_create(crgc_graph *h, uint16_t node_location, crgc_undo_acc **
     return CRGC_E_NOMEM;
   }
   hipError_t e = hipMemsetAsync(u->ctr, 0, 16, h->stream);
-  if (e == hipSuccess) e = ua_alloc(u->d, &u->mem, 1 << 12, 1 << 12, u->ctr, h->stream);
+  // Initial size from the graph's: a node's log names at most the actors the
+  // graph has seen from it, so a quarter of the slots avoids the rehashes of a
+  // log that grows from nothing (HBM is plentiful; an export scans the table).
+  const uint64_t hint = pow2_at_least(std::max<uint64_t>(1 << 12, (h->slot_top + h->ids_since) / 4));
+  if (e == hipSuccess) e = ua_alloc(u->d, &u->mem, hint, 2 * hint, u->ctr, h->stream);
   if (e != hipSuccess) {
     crgc_undo_acc_destroy(u);
     return map_hip(e);
