@@ -135,3 +135,17 @@ def test_decoded_graphs_merge_like_the_oracles(hip_mod, oracle_mod):
         from crgc_hip import DeltaBatch
         o.merge_deltas(DeltaBatch(*(cols[k] for k in COLS)))
         assert remote.export() == o.export()
+
+
+def test_device_outputs_grow_after_a_speculative_write(hip_mod):
+    """Device outputs sized by a small batch, then a larger one: the write pass
+    that runs on the device's counts (before the host sees the totals) finds
+    the outputs too small, writes nothing and reports E2BIG; the wrapper grows
+    them and the second call's bytes are exact.  Then smaller again (the
+    outputs fit: written speculatively)."""
+    g = hip_mod.ShadowGraph()
+    w = world.World(seed=21)
+    w.bulk_graph(20_000, 200_000, alpha=2.1, n_roots=50)
+    for n in (300, 20_000, 1_000):
+        b = w.wakeup_batch(n)
+        assert _check(g, b, device_in=True, device_out=True) > 0
