@@ -39,8 +39,7 @@
 extern "C" {
 #endif
 
-#define CRGC_ABI_VERSION 4u  /* 2: crgc_trace_stats.expand_launches / expand_bytes; 3: exchange_bytes;
-                                4: closure_steps */
+#define CRGC_ABI_VERSION 3u  /* 2: crgc_trace_stats.expand_launches / expand_bytes; 3: exchange_bytes */
 
 /* ---- status codes ------------------------------------------------------- */
 #define CRGC_OK 0
@@ -198,9 +197,6 @@ typedef struct crgc_trace_stats {
   /* sharded graphs: bytes this shard sent in mark rounds (ids, home slots,
      frontier bitmaps) and in the home-slot resolution before them */
   uint64_t exchange_bytes;
-  /* closure mode (unsharded wide marks): steps of the hint
-     closure that did work; 0 when the level BFS traced */
-  uint64_t closure_steps;
 } crgc_trace_stats;
 
 typedef struct crgc_trace_out {

@@ -355,7 +355,6 @@ class TraceResult:
     expand_launches: int = 0
     expand_bytes: int = 0
     exchange_bytes: int = 0
-    closure_steps: int = 0
 
     def garbage_set(self):
         return set(int(x) for x in self.garbage)

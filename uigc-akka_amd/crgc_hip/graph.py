@@ -151,8 +151,7 @@ class ShadowGraph:
                            int(st.sup_edges), int(st.levels), int(st.launches), st.ms_mark,
                            st.ms_sweep, st.ms_total, st.ms_frontier, st.ms_tail, st.ms_expand,
                            int(st.rounds), int(st.ids_sent), st.ms_exchange,
-                           int(st.expand_launches), int(st.expand_bytes), int(st.exchange_bytes),
-                           int(st.closure_steps))
+                           int(st.expand_launches), int(st.expand_bytes), int(st.exchange_bytes))
 
     def _trace_into(self, shouldKill, g, k):
         out = abi.CrgcTraceOut()

@@ -200,13 +200,6 @@ struct crgc_graph {
   crgc_trace_stats last_stats{};
   bool have_last = false;
   uint64_t last_levels = 0;  // level launches (after level 0) the previous trace needed
-  // closure mode (crgc_closure.hip): steps the previous closure trace needed
-  // (incl. the one that ended it), whether the next trace may use it, and the
-  // level traces still to run after a closure that hit its step budget
-  uint32_t last_cl_steps = 0;
-  bool cl_ready = false;
-  uint32_t cl_cooldown = 0;
-  bool cl_mode_used = false;  // the last unsharded trace marked in closure mode
   std::vector<hipEvent_t> lvl_ev;  // 6 per level launch: start / stop of its 3 kernels
   std::vector<hipEvent_t> chunk_ev;  // start / stop of every chunk of level launches
   uint64_t *roots_buf = nullptr;
@@ -1707,69 +1700,6 @@ static int sweep_sharded(crgc_graph *h, int should_kill, uint64_t top, double *m
   return CRGC_OK;
 }
 
-// Closure mode (crgc_closure.hip): steps in chunks, each chunk followed by
-// the sweep (which runs only once a step has ended the mark) and one host
-// synchronisation; the first chunk is as long as the previous closure needed.
-// *done = false: the step budget ran out first, and the caller traces again
-// with the level BFS.
-static int run_closure(crgc_graph *h, uint64_t top, LevelRun &lr,
-                       const std::function<hipError_t()> &after_chunk, uint32_t budget, bool *done) {
-  *done = false;
-  uint32_t k = 0;
-  uint32_t chunk = h->last_cl_steps ? h->last_cl_steps : 16;
-  std::vector<unsigned long long> ring;
-  size_t nc = 0;
-  auto chunk_event = [&]() -> hipError_t {
-    while (h->chunk_ev.size() < nc + 1) {
-      hipEvent_t e;
-      if (hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableSystemFence)) return r;
-      h->chunk_ev.push_back(e);
-    }
-    return hipEventRecord(h->chunk_ev[nc++], h->stream);
-  };
-  for (;;) {
-    chunk = std::min(chunk, budget - k);
-    HIP_TRY(chunk_event());
-    for (uint32_t i = 0; i < chunk; ++i) HIP_TRY(launch_closure(h->g.d, k++, top, h->stream));
-    HIP_TRY(chunk_event());
-    if (after_chunk) HIP_TRY(after_chunk());
-    ring.resize(k);
-    HIP_TRY(hipMemcpyAsync(ring.data(), (char *)h->ctr + CTR_OFF(ring), k * 8, hipMemcpyDeviceToHost, h->stream));
-    unsigned long long roots = 0;
-    HIP_TRY(hipMemcpyAsync(&roots, (char *)h->ctr + CTR_OFF(cl_roots), 8, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    uint32_t end = k;  // the step that found the mark complete
-    for (uint32_t i = 0; i < k; ++i)
-      if ((uint32_t)(ring[i] >> 56) == CL_MODE_DONE) {
-        end = i;
-        break;
-      }
-    if (end < k) {
-      *done = true;
-      lr.roots = roots;
-      lr.levels = end;
-      lr.depth = end;
-      lr.launches = k;
-      h->last_cl_steps = end + 1;
-      for (size_t i = 0; i + 1 < nc; i += 2) {
-        float t = 0;
-        hipEventElapsedTime(&t, h->chunk_ev[i], h->chunk_ev[i + 1]);
-        lr.ms += t;
-      }
-      return CRGC_OK;
-    }
-    if (k >= budget || k >= LEVEL_RING) return CRGC_OK;
-    chunk *= 2;
-  }
-}
-
-// Closure mode for this trace?  CRGC_CLOSURE=0 never, 2 always (unsharded),
-// 1 (default) once a level trace on this handle has shown a shallow mark.
-static int closure_setting() {
-  const char *m = getenv("CRGC_CLOSURE");
-  return m ? atoi(m) : 1;
-}
-
 int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   if (int rc = check_graph(h)) return rc;
   if (!out) return CRGC_E_INVAL;
@@ -1798,35 +1728,7 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
     int end = 0;
     rounds = 1;
     lr.defer = true;
-    const int cl = closure_setting();
-    bool done = false;
-    if (cl == 2 || (cl == 1 && h->cl_ready && h->cl_cooldown == 0)) {
-      uint32_t budget = 48;
-      if (const char *m = getenv("CRGC_CLOSURE_BUDGET")) budget = (uint32_t)std::max(1l, atol(m));
-      budget = std::min<uint32_t>(budget, LEVEL_RING);
-      if (int rc = run_closure(h, top, lr, sweep, budget, &done)) return rc;
-      h->cl_mode_used = done;
-      if (!done) {
-        // Budget spent (a deep mark: chains of fresh shadows, say): trace again
-        // with the level BFS, from clean candidate maps and counters.
-        h->cl_ready = false;
-        h->cl_cooldown = 8;
-        h->last_cl_steps = 0;
-        const size_t scap = h->g.caps.scap;
-        HIP_TRY(hipMemsetAsync(h->g.d.front[0], 0, scap, h->stream));
-        HIP_TRY(hipMemsetAsync(h->g.d.front[1], 0, scap, h->stream));
-        reset_trace_counters(h);
-        lr = LevelRun{};
-        lr.defer = true;
-      }
-    }
-    if (!done) {
-      h->cl_mode_used = false;
-      if (int rc = run_levels(h, false, 0, top, true, 0, lr, &end, sweep)) return rc;
-      if (h->cl_cooldown) --h->cl_cooldown;
-      // a shallow level mark (no chain mode): the next trace may use closure mode
-      h->cl_ready = lr.depth <= 32 && h->hctr->chain_rounds == 0;
-    }
+    if (int rc = run_levels(h, false, 0, top, true, 0, lr, &end, sweep)) return rc;
     absorb_counters(h);  // read back with the last chunk's level counts
   } else {
     if (int rc = mark_all(h, false, 0, top, lr, &rounds, &ids_sent, &ms_x, &x_bytes)) return rc;
@@ -1868,13 +1770,11 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
   st.ms_sweep = ms;
   st.pseudo_roots = lr.roots;
-  st.closure_steps = h->tp || !h->cl_mode_used ? 0 : lr.levels;
-  if (st.closure_steps) st.expand_launches = 0;  // no k_expand: closure steps only
   h->live = c.n_live;
   h->n_proxy = c.n_proxy;
   h->inserted_at_trace = c.inserted;
   h->have_last = true;
-  if (h->tp || !h->cl_mode_used) h->last_levels = lr.first_chunk;
+  h->last_levels = lr.first_chunk;
   st.ms_total =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   h->last_stats = st;

@@ -200,10 +200,6 @@ hipError_t launch_edges(const DevGraph &g, const EdgeArgs &a, hipStream_t s);
 hipError_t launch_level(const DevGraph &g, const LevelArgs &a, bool roots, bool investigate,
                         uint64_t slot_top, hipStream_t s, hipEvent_t *ev = nullptr);
 hipError_t launch_trace_stats(const DevGraph &g, hipStream_t s);
-// closure mode (crgc_closure.hip): step k of the hint closure; its mode comes
-// from step k-1's word in Counters::ring (mode << 56 | work done)
-hipError_t launch_closure(const DevGraph &g, uint32_t step, uint64_t slot_top, hipStream_t s);
-constexpr uint32_t CL_MODE_DONE = 4;
 hipError_t launch_trace_reset(const DevGraph &g, uint64_t nblk, uint32_t ctr_from, uint32_t ctr_words,
                               hipStream_t s);
 // sweep + id compaction + removal of the garbage (skipped on a reference NPE)

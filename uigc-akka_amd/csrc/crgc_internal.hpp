@@ -77,7 +77,6 @@ struct Counters {
   unsigned long long mf_sum;         // ... summed over the levels so far (Beamer's explored edges)
   unsigned long long chain_marked;   // shadows marked by chain mode (crgc_chain.hip)
   unsigned long long chain_rounds;   // pointer-jumping rounds that marked something
-  unsigned long long cl_roots;       // closure mode (crgc_closure.hip): pseudo-roots of its first step
   unsigned long long n_garbage;
   unsigned long long n_kill;
   unsigned long long n_live;
