@@ -1810,8 +1810,7 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
           ? Carver::need({n * 8, n * 2, n, (n + 1) * 4, C * 8, C * 8, (n + 1) * 4, S * 8, (n + 1) * 4, U * 8,
                           U * 2})
           : 0;
-  uint32_t levels = 1;  // J_k jumps 4^k graphs: 4^(levels-1) >= n + 1
-  while ((1ull << (2 * (levels - 1))) < n + 1) ++levels;
+  const uint32_t levels = 2;  // J and J^64
   const uint64_t N = n + 1, nblk = (n + 1023) / 1024, nbs = 4 * ((N + 1023) / 1024) + 8;
   const size_t need = Carver::need({sizeof(DgCounters), (size_t)levels * N * 4, N, N, nblk * 4 + 4,
                                     nblk * 8 + 8, nbs * 8, N * 4, N * 4, N * 4, N * 4, N * 8, N * 8, N * 8});
@@ -1841,7 +1840,6 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
   }
   a.ctr = dc.take<DgCounters>(1);
   a.J = dc.take<uint32_t>((size_t)levels * N);
-  a.levels = levels;
   a.mark = dc.take<uint8_t>(N);
   a.lng = dc.take<uint8_t>(N);
   a.blk = dc.take<uint32_t>(nblk + 1);
@@ -1883,11 +1881,8 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
     // with device outputs the write pass and offsets follow the same way.
     DgOut none{};
     HIP_TRY(launch_dg_chain(a, 0, h->stream));
-    HIP_TRY(hipMemsetAsync(a.g_size, 0, N * 4, h->stream));
-    HIP_TRY(hipMemsetAsync(a.g_nout, 0, N * 4, h->stream));
-    HIP_TRY(hipMemsetAsync(a.g_bytes, 0, N * 4, h->stream));
     HIP_TRY(launch_dg_build(a, DG_NG_DEVICE, false, none, h->stream));
-    HIP_TRY(launch_dg_scans(a, N, h->stream));
+    HIP_TRY(launch_dg_scans(a, DG_NG_DEVICE, h->stream));
     if (speculate) {
       HIP_TRY(launch_dg_build(a, DG_NG_DEVICE, true, o, h->stream));
       HIP_TRY(launch_dg_offsets(a, DG_NG_DEVICE, o, h->stream));

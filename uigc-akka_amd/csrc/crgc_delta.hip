@@ -8,8 +8,8 @@
 //   k_dg_span     for every entry s, the end of a graph that would start at
 //                 s (one wave streams the entries past 64 starts through a
 //                 last-seen table; graphs longer than its window are deferred)
-//   k_dg_double   J_{k+1} = J_k^4 (pointer jumping, base 4)
-//   k_dg_mark     starts reachable from entry 0, top level down
+//   k_dg_jump / k_dg_walk / k_dg_fill   the starts reachable from entry 0:
+//                 64-step jumps, one walk over them, the starts in between
 //   k_dg_long     one workgroup resolves the first deferred start on the
 //                 chain, 64 entries per step
 //   k_dg_count / k_dg_scatter   the starts, compacted
@@ -261,6 +261,7 @@ __global__ __launch_bounds__(256) void k_dg_span(DgArgs a) {
   const uint64_t dl = __ballot(mine && s < a.n && !done);
   if (lane == 0 && dl) atomicAdd(&a.ctr->n_long, (unsigned)__popcll(dl));
   if (!mine || s > a.n) return;
+  a.mark[s] = 0;  // the chain walks mark after this launch
   if (s == a.n) {
     a.J[s] = (uint32_t)a.n;
     a.lng[s] = 0;
@@ -270,25 +271,50 @@ __global__ __launch_bounds__(256) void k_dg_span(DgArgs a) {
   a.lng[s] = !done;
 }
 
-// Pointer jumping in base 4 (half the launches of doubling): J_{k+1} = J_k^4.
-__global__ __launch_bounds__(256) void k_dg_double(DgArgs a, uint32_t k) {
+// The chain from entry 0 in three launches (round 2 used 2 log4(n) + 1
+// pointer-jumping launches, ~95 us at C5's 125 000 entries):
+//   k_dg_jump    J64[s] = J^64(s), 64 dependent L2-resident loads per start
+//   k_dg_walk    one thread walks J64 from the chain's start, marking every
+//                64th graph start (a milestone, mark 2)
+//   k_dg_fill    from each milestone, the next 63 starts along J (mark 1)
+// A start whose span was deferred points at itself (J[s] = s), and so does the
+// batch end n, so every walk stops there; k_dg_long resolves a deferred start,
+// and the chain is walked again from the start after it.
+constexpr uint32_t DG_STRIDE = 64;
+
+__global__ __launch_bounds__(256) void k_dg_jump(DgArgs a) {
   const uint64_t N = a.n + 1;
-  const uint32_t *Jk = a.J + (uint64_t)k * N;
-  uint32_t *Jn = a.J + (uint64_t)(k + 1) * N;
-  for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < N; s += (uint64_t)gridDim.x * 256)
-    Jn[s] = Jk[Jk[Jk[Jk[s]]]];
+  const uint32_t *J = a.J;
+  uint32_t *J64 = a.J + N;
+  for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < N; s += (uint64_t)gridDim.x * 256) {
+    uint32_t t = (uint32_t)s;
+    for (uint32_t i = 0; i < DG_STRIDE; ++i) t = J[t];
+    J64[s] = t;
+  }
 }
 
-// Marked after levels L-1 .. k: the chain's starts at multiples of 4^k steps
-// (a start marked early by a racing thread is a chain start too).
-__global__ __launch_bounds__(256) void k_dg_mark(DgArgs a, uint32_t k) {
+__global__ __launch_bounds__(64) void k_dg_walk(DgArgs a) {
+  if (threadIdx.x != 0) return;
+  const uint32_t *J64 = a.J + (a.n + 1);
+  a.ctr->first_long = ~0u;  // k_dg_first_long looks again after k_dg_fill
+  uint32_t t = a.ctr->walk_from;
+  for (;;) {
+    a.mark[t] = 2;
+    const uint32_t nt = J64[t];
+    if (nt == t) break;
+    t = nt;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_dg_fill(DgArgs a) {
   const uint64_t N = a.n + 1;
-  const uint32_t *Jk = a.J + (uint64_t)k * N;
   for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < N; s += (uint64_t)gridDim.x * 256) {
-    if (!a.mark[s]) continue;
+    if (a.mark[s] != 2) continue;
     uint32_t t = (uint32_t)s;
-    for (int d = 0; d < 3; ++d) {
-      t = Jk[t];
+    for (uint32_t i = 1; i < DG_STRIDE; ++i) {  // never reaches the next milestone (64 steps on)
+      const uint32_t nt = a.J[t];
+      if (nt == t) break;
+      t = nt;
       a.mark[t] = 1;
     }
   }
@@ -365,7 +391,7 @@ __global__ __launch_bounds__(256) void k_dg_long(DgArgs a) {
   if (threadIdx.x == 0) {
     a.J[s] = (uint32_t)s_end;
     a.lng[s] = 0;
-    a.mark[s_end] = 1;
+    a.ctr->walk_from = (uint32_t)s_end;
   }
 }
 
@@ -455,9 +481,67 @@ __global__ __launch_bounds__(SCAN_B) void k_scan_apply(ScanSet q) {
   }
 }
 
+// Small scans in one workgroup (one launch instead of three).  n_dev: the
+// element count on the device (null: q.n); a set *skip (a deferred DeltaGraph
+// chain start, nothing was counted) scans nothing.
+constexpr uint64_t SCAN_ONE_MAX = 1 << 16;  // elements x arrays
+
+__global__ __launch_bounds__(SCAN_B) void k_scan_one(ScanSet q, const unsigned long long *n_dev,
+                                                   const unsigned int *skip) {
+  constexpr uint32_t E = 4;  // consecutive elements per thread per chunk
+  __shared__ uint64_t s_w[4][16];
+  __shared__ uint64_t carry[4];
+  uint64_t n = n_dev ? *n_dev : q.n;
+  if (skip && *skip != ~0u) n = 0;
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  if (threadIdx.x < 4) carry[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint64_t c0 = 0; c0 < n; c0 += (uint64_t)SCAN_B * E) {
+    const uint64_t i0 = c0 + (uint64_t)threadIdx.x * E;
+    uint32_t v[4][E], sum[4], incl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // every array's wave scans, then one barrier
+      sum[j] = 0;
+      incl[j] = 0;
+      if (j >= q.k) continue;
+#pragma unroll
+      for (uint32_t e = 0; e < E; ++e) {
+        v[j][e] = i0 + e < n ? q.in[j][i0 + e] : 0u;
+        sum[j] += v[j][e];
+      }
+      incl[j] = wave_incl_scan(sum[j]);
+      if (lane == 63) s_w[j][wv] = incl[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j >= q.k) continue;
+      uint64_t pre = carry[j], tot = 0;
+      for (int w = 0; w < (int)(SCAN_B / 64); ++w) {
+        if (w < wv) pre += s_w[j][w];
+        tot += s_w[j][w];
+      }
+      uint64_t run = pre + incl[j] - sum[j];
+#pragma unroll
+      for (uint32_t e = 0; e < E; ++e) {
+        if (i0 + e < n) q.out[j][i0 + e] = run;
+        run += v[j][e];
+      }
+      __syncthreads();  // every thread has read carry[j] and s_w[j]
+      if (threadIdx.x == 0) carry[j] += tot;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < (unsigned)q.k) *q.total[threadIdx.x] = carry[threadIdx.x];
+}
+
 hipError_t run_scan(ScanSet q, hipStream_t s) {
   if (q.n == 0) {
     for (int j = 0; j < q.k; ++j) hipMemsetAsync(q.total[j], 0, 8, s);
+    return hipGetLastError();
+  }
+  if (q.n * q.k <= SCAN_ONE_MAX) {
+    hipLaunchKernelGGL(k_scan_one, dim3(1), dim3(SCAN_B), 0, s, q, nullptr, nullptr);
     return hipGetLastError();
   }
   q.nb = (q.n + SCAN_B - 1) / SCAN_B;
@@ -473,17 +557,13 @@ hipError_t launch_dg_chain(const DgArgs &a, int phase, hipStream_t s) {
   const uint64_t N = a.n + 1;
   if (phase == 0) {
     hipLaunchKernelGGL(k_dg_span, dim3((N + 4 * SPAN_S - 1) / (4 * SPAN_S)), dim3(256), 0, s, a);
-    for (uint32_t k = 0; k + 1 < a.levels; ++k)
-      hipLaunchKernelGGL(k_dg_double, dim3(dg_grid(N)), dim3(256), 0, s, a, k);
-    hipMemsetAsync(a.mark, 0, N, s);
-    hipMemsetAsync(a.mark, 1, 1, s);
   } else if (phase == 1) {
     hipLaunchKernelGGL(k_dg_long, dim3(1), dim3(256), 0, s, a);
   }
   if (phase <= 1) {
-    for (uint32_t k = a.levels; k-- > 0;)
-      hipLaunchKernelGGL(k_dg_mark, dim3(dg_grid(N)), dim3(256), 0, s, a, k);
-    hipMemsetAsync(&a.ctr->first_long, 0xFF, 4, s);
+    hipLaunchKernelGGL(k_dg_jump, dim3(dg_grid(N)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_dg_walk, dim3(1), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_dg_fill, dim3(dg_grid(N)), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_dg_first_long, dim3(dg_grid(a.n)), dim3(256), 0, s, a);
   }
   const uint64_t nblk = (a.n + 1023) / 1024;
@@ -832,7 +912,10 @@ hipError_t launch_dg_scans(const DgArgs &a, uint64_t ng, hipStream_t s) {
   q.out[2] = a.g_wire;
   q.total[2] = &a.ctr->wire;
   q.k = 3;
-  return run_scan(q, s);
+  if (ng != DG_NG_DEVICE) return run_scan(q, s);
+  // over the graphs the device counted, so the counts past them need no zeroing
+  hipLaunchKernelGGL(k_scan_one, dim3(1), dim3(SCAN_B), 0, s, q, &a.ctr->n_graphs, &a.ctr->first_long);
+  return hipGetLastError();
 }
 
 __global__ __launch_bounds__(256) void k_dg_offsets(DgArgs a, uint64_t ng, DgOut o) {

@@ -321,6 +321,8 @@ struct DgCounters {
   unsigned long long err;       // malformed offsets / reserved ids
   unsigned int first_long;      // first graph start whose span was deferred (~0: none)
   unsigned int n_long;
+  unsigned int walk_from;       // where the chain walk (re)starts: 0, then past a resolved deferred start
+  unsigned int pad;
   unsigned long long n_graphs;  // graph starts (exclusive-scan total)
   unsigned long long n_shadows, n_out, wire;  // totals of the per-graph scans
   unsigned long long overflow;  // a write pass on the device's count found the outputs too small
@@ -342,8 +344,7 @@ struct DgArgs {
   const uint64_t *u_ref;
   const int16_t *u_info;
   DgCounters *ctr;
-  uint32_t *J;         // [levels][n+1] successor graph start, doubled per level
-  uint32_t levels;
+  uint32_t *J;         // [2][n+1] successor graph start J, then J^64 (k_dg_jump)
   uint8_t *mark;       // [n+1] graph starts
   uint8_t *lng;        // [n+1] span deferred to k_dg_long
   uint32_t *blk;       // [nblk] marked starts per 1024 entries
