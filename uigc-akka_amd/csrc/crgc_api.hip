@@ -1812,8 +1812,13 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
           : 0;
   const uint32_t levels = 2;  // J and J^64
   const uint64_t N = n + 1, nblk = (n + 1023) / 1024, nbs = 4 * ((N + 1023) / 1024) + 8;
+  // the write pass's slots: every shadow of a graph is an id occurrence of its
+  // entries, every outgoing entry a created or updated ref
+  const uint64_t TR = n + 2 * C + S + U, TO = C + U, TW = 2 * N + 13 * TR + 6 * TO;
   const size_t need = Carver::need({sizeof(DgCounters), (size_t)levels * N * 4, N, N, nblk * 4 + 4,
-                                    nblk * 8 + 8, nbs * 8, N * 4, N * 4, N * 4, N * 4, N * 8, N * 8, N * 8});
+                                    nblk * 8 + 8, nbs * 8, N * 4, N * 4, N * 4, N * 4, N * 8, N * 8, N * 8,
+                                    N * 4, N * 4, N * 4, N * 8, N * 8, N * 8, TR * 8, TR * 4, TR * 8, TR,
+                                    TR * 4, TO * 8, TO * 4, TW});
   if (h->stage.ensure(nh_bytes + 256) != hipSuccess || h->x_dg.ensure(need) != hipSuccess)
     return CRGC_E_NOMEM;
   Carver sc(h->stage.ptr), dc(h->x_dg.ptr);
@@ -1852,6 +1857,24 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
   a.g_shadow = dc.take<uint64_t>(N);
   a.g_out = dc.take<uint64_t>(N);
   a.g_wire = dc.take<uint64_t>(N);
+  a.b_size = dc.take<uint32_t>(N);
+  a.b_out = dc.take<uint32_t>(N);
+  a.b_bytes = dc.take<uint32_t>(N);
+  a.t_shadow = dc.take<uint64_t>(N);
+  a.t_out = dc.take<uint64_t>(N);
+  a.t_wire = dc.take<uint64_t>(N);
+  DgOut t{};
+  t.id = dc.take<uint64_t>(TR);
+  t.recv = dc.take<int32_t>(TR);
+  t.sup = dc.take<uint64_t>(TR);
+  t.flags = dc.take<uint8_t>(TR);
+  t.out_off = dc.take<uint32_t>(TR);
+  t.out_target = dc.take<uint64_t>(TO);
+  t.out_count = dc.take<int32_t>(TO);
+  t.wire = dc.take<uint8_t>(TW);
+  t.shadow_cap = TR;
+  t.out_cap = TO;
+  t.wire_cap = TW;
   HIP_TRY(hipMemsetAsync(a.ctr, 0, sizeof(DgCounters), h->stream));
   DgCounters hc{};
   auto fetch = [&]() -> int {
@@ -1876,15 +1899,13 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
   uint64_t G = 0;
   bool written = false;
   if (n) {
-    // The chain, then the count pass and its scans without a host round trip:
-    // graph counts over the bound n + 1 (zero past the device's n_graphs);
-    // with device outputs the write pass and offsets follow the same way.
-    DgOut none{};
+    // The chain, then the write pass into bounded slots and the scans of the
+    // exact sizes, on the device's graph count without a host round trip; with
+    // device outputs the compaction and offsets follow the same way.
     HIP_TRY(launch_dg_chain(a, 0, h->stream));
-    HIP_TRY(launch_dg_build(a, DG_NG_DEVICE, false, none, h->stream));
-    HIP_TRY(launch_dg_scans(a, DG_NG_DEVICE, h->stream));
+    HIP_TRY(launch_dg_write(a, DG_NG_DEVICE, t, h->stream));
     if (speculate) {
-      HIP_TRY(launch_dg_build(a, DG_NG_DEVICE, true, o, h->stream));
+      HIP_TRY(launch_dg_compact(a, DG_NG_DEVICE, t, o, h->stream));
       HIP_TRY(launch_dg_offsets(a, DG_NG_DEVICE, o, h->stream));
     }
     if (int rc = fetch()) return rc;
@@ -1895,9 +1916,9 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
         HIP_TRY(launch_dg_chain(a, 1, h->stream));
         if (int rc = fetch()) return rc;
       }
-      HIP_TRY(launch_dg_build(a, hc.n_graphs, false, none, h->stream));
-      HIP_TRY(launch_dg_scans(a, hc.n_graphs, h->stream));
+      HIP_TRY(launch_dg_write(a, hc.n_graphs, t, h->stream));
       if (int rc = fetch()) return rc;
+      if (hc.err) return CRGC_E_INVAL;
     }
     G = hc.n_graphs;
   }
@@ -1928,7 +1949,7 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
     o.wire = oc.take<uint8_t>(NW);
   }
   if (G && !written) {
-    HIP_TRY(launch_dg_build(a, G, true, o, h->stream));
+    HIP_TRY(launch_dg_compact(a, G, t, o, h->stream));
     HIP_TRY(launch_dg_offsets(a, G, o, h->stream));
   } else if (!G) {  // no graphs: the closing offsets only
     HIP_TRY(hipMemsetAsync(o.graph_off, 0, 4, h->stream));

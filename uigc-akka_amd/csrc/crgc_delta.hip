@@ -14,9 +14,10 @@
 //                 chain, 64 entries per step
 //   k_dg_count / k_dg_scatter   the starts, compacted
 // Then one wave per graph replays DeltaGraph.mergeEntry over its entries
-// (k_dg_build, state in LDS) — once to size the outputs, once to write them:
-// the decoded shadows and the DataOutput bytes of DeltaShadow.serialize, the
-// outgoing map in java.util.HashMap iteration order.
+// (k_dg_write, state in LDS) into slots bounded by the graph's entries: the
+// decoded shadows and the DataOutput bytes of DeltaShadow.serialize, the
+// outgoing map in java.util.HashMap iteration order; k_dg_compact packs the
+// slots at the exact offsets.
 #include "crgc_host.hpp"
 
 namespace crgc {
@@ -797,24 +798,29 @@ __device__ inline void put_be(uint8_t *p, uint32_t v, int bytes) {
 // Short.hashCode is the value) and each bin in insertion order (a removed key
 // re-put goes to the tail; resizes keep the order).  Keys < DGS <= 64 never
 // fill a bin to the treeify threshold.
-__device__ void dg_emit(const DgArgs &a, uint64_t g, const DgWave &W, uint32_t size, const DgOut &o) {
+// Writes go to graph g's bounded slots (k_dg_bounds): rows [row0, row0 +
+// rcap), outgoing entries [ob0, ob0 + ocap), bytes [wb0, wb0 + wcap); a valid
+// batch never reaches the caps, a malformed one (reported by the span kernel)
+// is kept inside them.
+__device__ void dg_emit(const DgWave &W, uint32_t size, const DgOut &o, uint64_t row0, uint64_t ob0,
+                        uint64_t wb0, uint32_t rcap, uint32_t ocap, uint32_t wcap) {
   const uint32_t c = lane_id();
   const bool on = c < size;
   const uint32_t nk = on ? W.osz[c] : 0;
   const uint32_t nb = on ? 13 + 6 * nk : 0;
   const uint32_t oi = wave_incl_scan(nk), bi = wave_incl_scan(nb);
-  if (!on) return;
-  const uint64_t row = a.g_shadow[g] + c;
-  uint64_t ob = a.g_out[g] + oi - nk;
-  uint8_t *w = o.wire + a.g_wire[g] + 2 + bi - nb;
-  if (c == 0) put_be(o.wire + a.g_wire[g], size, 2);
+  if (!on || c >= rcap || oi > ocap || 2 + bi > wcap) return;
+  const uint64_t row = row0 + c;
+  uint64_t ob = ob0 + oi - nk;
+  uint8_t *w = o.wire + wb0 + 2 + bi - nb;
+  if (c == 0) put_be(o.wire + wb0, size, 2);
   const uint8_t sp = W.sup[c], f = W.fl[c];
   const int32_t rc = W.recv[c];
   o.id[row] = W.dec[c];
   o.recv[row] = rc;
   o.sup[row] = sp == NONE8 ? CRGC_NO_ACTOR : W.dec[sp];
   o.flags[row] = f;
-  o.out_off[row] = (uint32_t)ob;
+  o.out_off[row] = (uint32_t)(ob - ob0);  // graph-relative until k_dg_compact
   put_be(w, (uint32_t)rc, 4);
   put_be(w + 4, sp == NONE8 ? 0xFFFFu : sp, 2);
   w[6] = (f & CRGC_DELTA_INTERNED) ? 1 : 0;
@@ -850,51 +856,124 @@ __device__ void dg_emit(const DgArgs &a, uint64_t g, const DgWave &W, uint32_t s
   }
 }
 
-// The outputs hold the graphs the device counted (write passes that run before
-// the host has seen the totals).
+// ng == DG_NG_DEVICE: the graph count is the device's (n_graphs), and nothing
+// is built while a deferred chain start is unresolved (first_long set): the
+// host then resolves it and runs the passes again.
+__device__ inline bool dg_count(const DgArgs &a, uint64_t &ng) {
+  if (ng != DG_NG_DEVICE) return true;
+  if (a.ctr->first_long != ~0u) return false;
+  ng = a.ctr->n_graphs;
+  return true;
+}
+
+// One pass instead of a count pass and a write pass: every graph gets slots
+// bounded by its entries (shadows <= its ids and < DGS, outgoing entries <= its
+// created refs + updated refs), the write pass fills them and records the exact
+// sizes, and k_dg_compact packs the slots once the exact offsets are scanned.
+__global__ __launch_bounds__(256) void k_dg_bounds(DgArgs a, uint64_t ng) {
+  if (!dg_count(a, ng)) return;
+  for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < ng; g += (uint64_t)gridDim.x * 256) {
+    const uint64_t e0 = a.starts[g], e1 = a.starts[g + 1];
+    auto d = [](uint32_t x0, uint32_t x1) { return x1 >= x0 ? (uint64_t)(x1 - x0) : ~0ull >> 8; };
+    const uint64_t cc = d(a.c_off[e0], a.c_off[e1]), uu = d(a.u_off[e0], a.u_off[e1]);
+    const uint64_t ids = (e1 - e0) + 2 * cc + d(a.s_off[e0], a.s_off[e1]) + uu;
+    const uint32_t sh = (uint32_t)min<uint64_t>(ids, DG_MAX);
+    const uint32_t ou = (uint32_t)min<uint64_t>(cc + uu, (uint64_t)DG_MAX * DG_MAX);
+    a.b_size[g] = sh;
+    a.b_out[g] = ou;
+    a.b_bytes[g] = 2 + 13 * sh + 6 * ou;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_dg_write(DgArgs a, uint64_t ng, DgOut t) {
+  __shared__ DgWave W;
+  if (!dg_count(a, ng)) return;
+  for (uint64_t g = blockIdx.x; g < ng; g += gridDim.x) {
+    const uint32_t size = dg_replay(a, g, W);
+    const uint32_t c = lane_id();
+    const uint32_t nk = c < size ? W.osz[c] : 0;
+    const uint32_t nout = __shfl(wave_incl_scan(nk), 63);
+    const uint64_t row0 = a.t_shadow[g], ob0 = a.t_out[g], wb0 = a.t_wire[g];
+    const uint32_t rcap = a.b_size[g], ocap = a.b_out[g], wcap = a.b_bytes[g];
+    const bool fits = row0 + rcap <= t.shadow_cap && ob0 + ocap <= t.out_cap && wb0 + wcap <= t.wire_cap;
+    if (c == 0) {
+      a.g_size[g] = size;
+      a.g_nout[g] = nout;
+      a.g_bytes[g] = 2 + 13 * size + 6 * nout;
+      if (!fits || size > rcap || nout > ocap) atomicOr(&a.ctr->err, 2ull);  // only a malformed batch
+    }
+    if (fits) dg_emit(W, size, t, row0, ob0, wb0, rcap, ocap, wcap);
+    wave_lds_fence();
+  }
+}
+
+// The outputs hold the graphs the device counted (passes that run before the
+// host has seen the totals).
 __device__ inline bool dg_fits(const DgArgs &a, uint64_t ng, const DgOut &o) {
   return ng <= o.graph_cap && a.ctr->n_shadows <= o.shadow_cap && a.ctr->n_out <= o.out_cap &&
          a.ctr->wire <= o.wire_cap;
 }
 
-// ng == DG_NG_DEVICE: the graph count is the device's (n_graphs), and nothing
-// is built while a deferred chain start is unresolved (first_long set): the
-// host then resolves it and runs the passes again.  A write pass on the
-// device's count also checks the output capacities (overflow: nothing written).
-template <bool WRITE>
-__global__ __launch_bounds__(64) void k_dg_build(DgArgs a, uint64_t ng, DgOut o) {
-  __shared__ DgWave W;
-  if (ng == DG_NG_DEVICE) {
-    if (a.ctr->first_long != ~0u) return;
-    ng = a.ctr->n_graphs;
-    if (WRITE && !dg_fits(a, ng, o)) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr->overflow = 1;
-      return;
-    }
+// One wave per graph: its slots, packed at the exact offsets.
+__global__ __launch_bounds__(256) void k_dg_compact(DgArgs a, uint64_t ng, DgOut t, DgOut o) {
+  const bool dev = ng == DG_NG_DEVICE;
+  if (!dg_count(a, ng)) return;
+  if (dev && !dg_fits(a, ng, o)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr->overflow = 1;
+    return;
   }
-  for (uint64_t g = blockIdx.x; g < ng; g += gridDim.x) {
-    const uint32_t size = dg_replay(a, g, W);
-    if (WRITE) {
-      dg_emit(a, g, W, size, o);
-    } else {
-      const uint32_t c = lane_id();
-      const uint32_t nk = c < size ? W.osz[c] : 0;
-      const uint32_t nout = __shfl(wave_incl_scan(nk), 63);
-      if (c == 0) {
-        a.g_size[g] = size;
-        a.g_nout[g] = nout;
-        a.g_bytes[g] = 2 + 13 * size + 6 * nout;
-      }
+  const int lane = lane_id();
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g < ng; g += nw) {
+    const uint64_t r0 = a.t_shadow[g], o0 = a.t_out[g], w0 = a.t_wire[g];
+    const uint64_t R0 = a.g_shadow[g], O0 = a.g_out[g], W0 = a.g_wire[g];
+    const uint32_t size = a.g_size[g], nout = a.g_nout[g], nb = a.g_bytes[g];
+    for (uint32_t i = lane; i < size; i += 64) {
+      o.id[R0 + i] = t.id[r0 + i];
+      o.recv[R0 + i] = t.recv[r0 + i];
+      o.sup[R0 + i] = t.sup[r0 + i];
+      o.flags[R0 + i] = t.flags[r0 + i];
+      o.out_off[R0 + i] = (uint32_t)O0 + t.out_off[r0 + i];
     }
-    wave_lds_fence();
+    for (uint32_t i = lane; i < nout; i += 64) {
+      o.out_target[O0 + i] = t.out_target[o0 + i];
+      o.out_count[O0 + i] = t.out_count[o0 + i];
+    }
+    for (uint32_t i = lane; i < nb; i += 64) o.wire[W0 + i] = t.wire[w0 + i];
   }
 }
 
-hipError_t launch_dg_build(const DgArgs &a, uint64_t ng, bool write, const DgOut &o, hipStream_t s) {
+hipError_t launch_dg_write(const DgArgs &a, uint64_t ng, const DgOut &t, hipStream_t s) {
   if (ng == 0) return hipSuccess;
-  const dim3 grid((unsigned)std::min<uint64_t>(ng == DG_NG_DEVICE ? a.n + 1 : ng, 4096));
-  if (write) hipLaunchKernelGGL(k_dg_build<true>, grid, dim3(64), 0, s, a, ng, o);
-  else hipLaunchKernelGGL(k_dg_build<false>, grid, dim3(64), 0, s, a, ng, o);
+  const uint64_t bound = ng == DG_NG_DEVICE ? a.n + 1 : ng;
+  hipLaunchKernelGGL(k_dg_bounds, dim3(dg_grid(bound)), dim3(256), 0, s, a, ng);
+  ScanSet q{};
+  q.n = ng;
+  q.bsum = a.bsum;
+  q.in[0] = a.b_size;
+  q.out[0] = a.t_shadow;
+  q.total[0] = &a.ctr->t_shadows;
+  q.in[1] = a.b_out;
+  q.out[1] = a.t_out;
+  q.total[1] = &a.ctr->t_out;
+  q.in[2] = a.b_bytes;
+  q.out[2] = a.t_wire;
+  q.total[2] = &a.ctr->t_wire;
+  q.k = 3;
+  if (ng != DG_NG_DEVICE) {
+    if (hipError_t e = run_scan(q, s)) return e;
+  } else {
+    hipLaunchKernelGGL(k_scan_one, dim3(1), dim3(SCAN_B), 0, s, q, &a.ctr->n_graphs, &a.ctr->first_long);
+  }
+  hipLaunchKernelGGL(k_dg_write, dim3((unsigned)std::min<uint64_t>(bound, 4096)), dim3(64), 0, s, a, ng, t);
+  return launch_dg_scans(a, ng, s);
+}
+
+hipError_t launch_dg_compact(const DgArgs &a, uint64_t ng, const DgOut &t, const DgOut &o, hipStream_t s) {
+  if (ng == 0) return hipSuccess;
+  const uint64_t bound = ng == DG_NG_DEVICE ? a.n + 1 : ng;
+  hipLaunchKernelGGL(k_dg_compact, dim3((unsigned)std::min<uint64_t>((bound + 3) / 4, 4096)), dim3(256), 0, s, a,
+                     ng, t, o);
   return hipGetLastError();
 }
 

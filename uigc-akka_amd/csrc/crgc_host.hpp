@@ -326,6 +326,7 @@ struct DgCounters {
   unsigned long long n_graphs;  // graph starts (exclusive-scan total)
   unsigned long long n_shadows, n_out, wire;  // totals of the per-graph scans
   unsigned long long overflow;  // a write pass on the device's count found the outputs too small
+  unsigned long long t_shadows, t_out, t_wire;  // totals of the per-graph slot bounds
 };
 
 struct DgArgs {
@@ -354,6 +355,9 @@ struct DgArgs {
   // per graph: sizes from the count pass, exclusive scans for the write pass
   uint32_t *g_size, *g_nout, *g_bytes;
   uint64_t *g_shadow, *g_out, *g_wire;
+  // per graph: slot bounds of the write pass and their exclusive scans
+  uint32_t *b_size, *b_out, *b_bytes;
+  uint64_t *t_shadow, *t_out, *t_wire;
 };
 
 struct DgOut {
@@ -374,13 +378,17 @@ struct DgOut {
 // phase 0: spans + doubling + chain from entry 0; 1: chain from a resolved
 // deferred start (k_dg_long, then marking); 2: compaction of the starts.
 hipError_t launch_dg_chain(const DgArgs &a, int phase, hipStream_t s);
-// count (write = false) or write pass: one wave per graph (n_graphs ==
+// The write pass (one wave per graph) into bounded per-graph slots of t,
+// recording each graph's exact sizes, and their exclusive scans (n_graphs ==
 // DG_NG_DEVICE: the count on the device, bounded by n + 1)
 constexpr uint64_t DG_NG_DEVICE = ~0ull;
-hipError_t launch_dg_build(const DgArgs &a, uint64_t n_graphs, bool write, const DgOut &o, hipStream_t s);
-// exclusive scans of the per-graph counts (after the count pass)
+hipError_t launch_dg_write(const DgArgs &a, uint64_t n_graphs, const DgOut &t, hipStream_t s);
+// exclusive scans of the per-graph sizes
 hipError_t launch_dg_scans(const DgArgs &a, uint64_t n_graphs, hipStream_t s);
-// (n_graphs == DG_NG_DEVICE: the device's count and the capacities in o)
+// the slots of t packed into o at the exact offsets; then the offset arrays
+// (n_graphs == DG_NG_DEVICE: the device's count, and the capacities in o are
+// checked on the device)
+hipError_t launch_dg_compact(const DgArgs &a, uint64_t n_graphs, const DgOut &t, const DgOut &o, hipStream_t s);
 hipError_t launch_dg_offsets(const DgArgs &a, uint64_t n_graphs, const DgOut &o, hipStream_t s);
 
 // UndoLog folding on the device (crgc_undo.hip)
