@@ -1,0 +1,22 @@
+#!/bin/bash
+# Interleaved bench A/B over environment variants (each "K=V,K2=V2" or BASE),
+# two passes; ms_per_step, merge and mark per variant into summary.txt.
+# usage: bash tools/ab_bench.sh <tag> <variant>...
+set -euo pipefail
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$ROOT/gpurun_out/${1:-abb}
+shift
+mkdir -p "$O"
+export TMPDIR=/tmp
+cd /tmp
+for pass in 1 2; do
+  for v in "$@"; do
+    envs=()
+    [ "$v" != "BASE" ] && IFS=',' read -ra envs <<< "$v"
+    f="$O/p${pass}_$(echo "$v" | tr '=,' '__').json"
+    env "${envs[@]}" timeout -k 10 300 python3 "$ROOT/bench.py" --steps 15 --warmup 3 --no-cpu-baseline \
+      > "$f" 2>> "$O/err.log"
+    python3 -c "import json,sys; d=json.loads(open('$f').read().strip().splitlines()[-1]); b=d['wakeup_breakdown_ms']; print('$v', round(d['ms_per_step'],4), round(b['merge'],4), round(b['mark_kernels'],4))" >> "$O/summary.txt"
+  done
+done
+cat "$O/summary.txt"
