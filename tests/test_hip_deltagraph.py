@@ -149,3 +149,24 @@ def test_device_outputs_grow_after_a_speculative_write(hip_mod):
     for n in (300, 20_000, 1_000):
         b = w.wakeup_batch(n)
         assert _check(g, b, device_in=True, device_out=True) > 0
+
+
+@pytest.mark.parametrize("device_out", [False, True])
+def test_malformed_offsets_are_rejected_without_writes(hip_mod, device_out):
+    """Offsets that decrease, or run past the records, fail the call with
+    E_INVAL (as the merges do); the single replay pass writes into slots bounded
+    by each graph's entries, so even a malformed batch stays inside them.  The
+    handle is usable afterwards."""
+    g = hip_mod.ShadowGraph()
+    good = fuzz.Fuzz(5).entries(600)
+    for field, at, val in (("created_off", 300, 0), ("updated_off", 200, 1 << 30),
+                           ("spawned_off", 599, 0)):
+        arrs = {k: np.array(getattr(good, k)) for k in EntryBatch.__slots__[:11]}
+        arrs[field][at] = val
+        bad = EntryBatch(arrs["self"], arrs["recv_count"], arrs["flags"], arrs["created_off"],
+                         arrs["created_owner"], arrs["created_target"], arrs["spawned_off"],
+                         arrs["spawned"], arrs["updated_off"], arrs["updated_ref"], arrs["updated_info"])
+        with pytest.raises(abi.CrgcError) as e:
+            g.build_delta_graphs(bad, device_out=device_out)
+        assert e.value.code == abi.E_INVAL, field
+    assert _check(g, good, device_out=device_out) > 0

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Parity subset (variants, parity, configs), then tools/ab_bench.sh over the given variants.
+# usage: bash tools/gpu_abt.sh <tag> <variant>...
+set -euo pipefail
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=$1
+O=$ROOT/gpurun_out/$TAG
+mkdir -p "$O"
+cd "$ROOT"
+timeout -k 10 600 python -u -m pytest tests/test_hip_variants.py tests/test_hip_parity.py tests/test_hip_configs.py \
+  -m gpu -x -v --timeout 120 --timeout-method thread > "$O/gpu_tests.log" 2>&1
+shift
+bash "$ROOT/tools/ab_bench.sh" "$TAG" "$@"

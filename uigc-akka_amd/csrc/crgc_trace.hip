@@ -259,7 +259,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
           const uint32_t s = sp[b];
           if (!((sw[b] >> (s & 31)) & 1u)) {
             Fn[s] = 1;
-            if (sp_next && Dn[s >> 11] == 0) Dn[s >> 11] = 1;
+            if (sp_next) Dn[s >> 11] = 1;  // blind: no dependent read
           }
         }
         const uint32_t len = ad[b].y;
@@ -318,13 +318,10 @@ __device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn,
     nb += go[u] ? 1 : 0;
     if (go[u]) Fn[t[u]] = 1;
   }
-  if (sp_next) {
-    uint8_t db[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) db[u] = go[u] ? Dn[t[u] >> 11] : 1;
+  if (sp_next) {  // the block's dirty byte, stored blind like the candidate byte
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (db[u] == 0) Dn[t[u] >> 11] = 1;
+      if (go[u]) Dn[t[u] >> 11] = 1;
   }
 }
 
