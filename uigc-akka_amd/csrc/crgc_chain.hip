@@ -133,10 +133,10 @@ __global__ __launch_bounds__(256) void k_chain_expand(DevGraph g, ChainArgs ca, 
 }
 
 // Statistics of the shadows chain mode expanded (cm: handed over by k_tail or
-// marked here): traced edges and supervisor edges (:231, :258), into the level
-// kernels' partials; cm and the pending maps are left zero.
+// marked here): supervisor edges (:258), into the level kernels' partials (the
+// sweep counts traced edges); cm and the pending maps are left zero.
 __global__ __launch_bounds__(256) void k_chain_stats(DevGraph g, ChainArgs ca, uint64_t words) {
-  uint64_t ed = 0, su = 0;
+  uint64_t su = 0;
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x; w < words; w += stride) {
     uint32_t bits = g.cm[w];
@@ -148,18 +148,15 @@ __global__ __launch_bounds__(256) void k_chain_stats(DevGraph g, ChainArgs ca, u
       const uint32_t v = (uint32_t)(w * 32 + (__ffs(bits) - 1));
       bits &= bits - 1;
       if ((g.flags[v] & (FL_ALIVE | FL_PROXY | FL_HALTED)) != FL_ALIVE) continue;
-      ed += g.nzdeg[v];
       if (!ca.investigate && g.sup[v] < 0xFFFFFFF0u) ++su;
     }
   }
-  __shared__ unsigned long long s_ed, s_su;
-  if (threadIdx.x == 0) s_ed = s_su = 0;
+  __shared__ unsigned long long s_su;
+  if (threadIdx.x == 0) s_su = 0;
   __syncthreads();
-  if (ed) atomicAdd(&s_ed, (unsigned long long)ed);
   if (su) atomicAdd(&s_su, (unsigned long long)su);
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (s_ed) atomicAdd((unsigned long long *)&g.blkstat[STAT_EDGES_SLOT], s_ed);
     if (s_su) atomicAdd((unsigned long long *)&g.blkstat[STAT_SUP_SLOT], s_su);
   }
 }

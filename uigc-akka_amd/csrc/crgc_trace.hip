@@ -77,6 +77,18 @@ __device__ inline bool listing_level(const Counters *c, int L, const LevelArgs &
 }
 
 
+// Workgroup sum of a 64-bit value per thread; every thread gets it.
+__device__ inline uint64_t block_sum64(uint64_t v) {
+  __shared__ uint64_t part[4];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+  if (lane_id() == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const uint64_t s = part[0] + part[1] + part[2] + part[3];
+  __syncthreads();
+  return s;
+}
+
 // Workgroup reduction of one value per wave; thread 0 gets the sum.
 __device__ inline uint64_t block_sum4(uint64_t v) {
   __shared__ uint64_t part[4];
@@ -229,7 +241,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
       for (int b = 0; b < FB; ++b) {
         const bool valid = v[b] != NO_SLOT;
         f[b] = valid ? g.flags[v[b]] : 0;
-        nz[b] = valid ? g.nzdeg[v[b]] : 0;
+        nz[b] = (valid && a.alpha) ? g.nzdeg[v[b]] : 0;  // Beamer's m_f only: the sweep counts traced edges
         ad[b] = (valid && !pull) ? g.adj[v[b]] : make_uint2(0, 0);
         sp[b] = (valid && !INVESTIGATE) ? g.sup[v[b]] : NO_SLOT;
       }
@@ -253,7 +265,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
             g.xp_buf[(uint64_t)blk * BLK_SLOTS + nprox + __popcll(pb & lanemask_lt())] = v[b];
           nprox += __popcll(pb);
         }
-        n_edges += nz[b];  // traced edges = nonzero out-edges of expanded shadows (:231)
+        n_edges += nz[b];  // this level's frontier out-edges (Beamer's m_f)
         if (sp[b] != NO_SLOT) {
           n_sup++;
           const uint32_t s = sp[b];
@@ -288,7 +300,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   if (threadIdx.x == 0) {
     stat[STAT_FRONT] = tf;
     stat[STAT_SUP] += ts;
-    stat[STAT_EDGES] += te;
     stat[STAT_MF] = te;  // this level's only (the sweep reuses the slot afterwards)
   }
 }
@@ -681,7 +692,7 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
         uint32_t keep = NO_SLOT;
         if (expand) {
           ad = adv;
-          if (!vfirst) o.n_edges += nzv;  // level L's were counted by k_frontier
+          (void)nzv;  // traced edges are counted by the sweep
           if (!investigate) {
             const uint32_t s = supv;  // (:258-267)
             if (s < 0xFFFFFFF0u) {
@@ -854,16 +865,14 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
   if (lv)
     for (uint32_t k = threadIdx.x; k < nw; k += TAIL_THREADS) g.vis[k] = s_vis[k];
   // statistics: claims became marked shadows (k_frontier(L) counted level L)
-  uint32_t tot_claims, tot_sup, tot_edges;
+  uint32_t tot_claims, tot_sup;
   tail_scan((uint32_t)o.claims, s_w, tot_claims);
   tail_scan(o.n_sup, s_w, tot_sup);
-  tail_scan(o.n_edges, s_w, tot_edges);
   if (threadIdx.x == 0) {
     const uint64_t marked_new = (uint64_t)tot_claims - (o.bailed ? o.n : 0);  // queued claims undone
     c->ring[L % LEVEL_RING] = n0;
     c->marked += n0 + marked_new;
     g.blkstat[STAT_SUP] += tot_sup;
-    g.blkstat[STAT_EDGES] += tot_edges;
     c->tail_from = L;
     if (o.chained) {
       c->tail_level = L + o.rounds;
@@ -1001,16 +1010,28 @@ __global__ __launch_bounds__(256) void k_sweep(DevGraph g, int should_kill) {
   const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const uint32_t nw = gridDim.x * 4;
   uint32_t n_live = 0, n_npe = 0, n_prox = 0, n_req = 0;
+  uint64_t n_edges = 0;
   for (uint32_t blk = gw; blk < nblk; blk += nw) {
     const uint64_t base = (uint64_t)blk * BLK_SLOTS + (uint64_t)lane * 32;
     const uint32_t word = g.vis[(uint64_t)blk * 64 + lane];
     const uint4 f4[2] = {*(const uint4 *)(g.flags + base), *(const uint4 *)(g.flags + base + 16)};
     const uint8_t *fb = (const uint8_t *)f4;
-    uint32_t alive = 0, kill = 0, req = 0, prox = 0;
+    uint32_t alive = 0, kill = 0, req = 0, prox = 0, halted = 0;
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
       alive |= ((fb[j] & (FL_ALIVE | FL_PROXY)) == FL_ALIVE) ? (1u << j) : 0u;
       prox |= ((fb[j] & (FL_ALIVE | FL_PROXY)) == (FL_ALIVE | FL_PROXY)) ? (1u << j) : 0u;
+      halted |= (fb[j] & FL_HALTED) ? (1u << j) : 0u;
+    }
+    // traced edges (:231): the nonzero out-counts of the marked, unhalted shadows
+    if (const uint32_t ex = alive & word & ~halted) {
+      uint4 z[8];
+      const uint4 *zp = (const uint4 *)(g.nzdeg + base);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) z[q] = zp[q];
+      const uint32_t *zs = (const uint32_t *)z;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) n_edges += ((ex >> j) & 1u) ? zs[j] : 0u;
     }
     const uint32_t garbage = alive & ~word;
     n_live += __popc(alive & word);
@@ -1072,8 +1093,10 @@ __global__ __launch_bounds__(256) void k_sweep(DevGraph g, int should_kill) {
   const uint64_t tn = block_sum4(n_npe);
   const uint64_t tp = block_sum4(n_prox);
   const uint64_t tr = block_sum4(n_req);
+  const uint64_t te = block_sum64(n_edges);
   if (threadIdx.x == 0) {
     g.blkstat[(uint64_t)blockIdx.x * 4 + STAT_LIVE] = tl;
+    g.blkstat[(uint64_t)blockIdx.x * 4 + STAT_EDGES] = te;  // the only writer of this partial
     if (tn) atomicAdd(&c->npe, (unsigned long long)tn);
     if (tp) atomicAdd(&c->n_proxy, (unsigned long long)tp);
     if (tr) atomicAdd(&c->n_req, (unsigned long long)tr);
