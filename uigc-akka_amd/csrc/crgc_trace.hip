@@ -144,8 +144,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     const uint64_t base = (uint64_t)blk * BLK_SLOTS + (uint64_t)lane * 32;
     const uint32_t word = g.vis[(uint64_t)blk * 64 + lane];
     uint32_t m = 0;
+    uint4 f4[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};  // the lane's 32 flag bytes
+    bool have_f = false;
     if (ROOTS) {
-      const uint4 f4[2] = {*(const uint4 *)(g.flags + base), *(const uint4 *)(g.flags + base + 16)};
+      f4[0] = *(const uint4 *)(g.flags + base);
+      f4[1] = *(const uint4 *)(g.flags + base + 16);
+      have_f = true;
       const uint8_t *fb = (const uint8_t *)f4;
       if (INVESTIGATE) {
         // investigateRemotelyHeldActors: every shadow at `location` (:305-310)
@@ -196,27 +200,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     const uint32_t incl = wave_incl_scan(cnt);
     const uint32_t total = __shfl(incl, 63);
     uint32_t pos = incl - cnt;
-    if (write_fx) {
-      // expandable frontier = frontier minus halted shadows (this wave owns the words)
-      uint32_t halted = 0;
-      if (m) {
-        const uint4 f4[2] = {*(const uint4 *)(g.flags + base), *(const uint4 *)(g.flags + base + 16)};
-        const uint8_t *fb = (const uint8_t *)f4;
-#pragma unroll
-        for (int j = 0; j < 32; ++j) halted |= (fb[j] & FL_HALTED) ? (1u << j) : 0u;
+    // The frontier slots' halted / proxy bits travel with their LDS entries
+    // (bits 11, 12), so the per-shadow loop below gathers no flag bytes.
+    uint32_t halted = 0, proxy = 0;
+    if (m) {
+      if (!have_f) {
+        f4[0] = *(const uint4 *)(g.flags + base);
+        f4[1] = *(const uint4 *)(g.flags + base + 16);
       }
-      g.fx[(uint64_t)blk * 64 + lane] = m & ~halted;
+      const uint8_t *fb = (const uint8_t *)f4;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        halted |= (fb[j] & FL_HALTED) ? (1u << j) : 0u;
+        proxy |= (fb[j] & FL_PROXY) ? (1u << j) : 0u;
+      }
     }
+    // expandable frontier = frontier minus halted shadows (this wave owns the words)
+    if (write_fx) g.fx[(uint64_t)blk * 64 + lane] = m & ~halted;
     while (m) {
       const int j = __ffs(m) - 1;
       m &= m - 1;
-      s_front[wv][pos++] = (uint16_t)(lane * 32 + j);
+      s_front[wv][pos++] = (uint16_t)((lane * 32 + j) | (((halted >> j) & 1u) << 11) | (((proxy >> j) & 1u) << 12));
     }
     n_front += cnt;
     wave_lds_fence();
     if (listing && total) {  // into the block's own region: no shared counter
       for (uint32_t i = lane; i < total; i += 64)
-        g.tl_buf[(uint64_t)blk * BLK_SLOTS + i] = blk * BLK_SLOTS + s_front[wv][i];
+        g.tl_buf[(uint64_t)blk * BLK_SLOTS + i] = blk * BLK_SLOTS + (s_front[wv][i] & (BLK_SLOTS - 1));
       if (lane == 0) g.tl_tag[blk] = tag | total;
     }
 
@@ -230,17 +240,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     // round trips per 64*FB shadows instead of two per 64.
     for (uint32_t c0 = 0; c0 < total; c0 += 64 * FB) {
       uint32_t v[FB], nz[FB], sp[FB];
-      uint8_t f[FB];
+      uint8_t f[FB];  // FL_HALTED / FL_PROXY, from the LDS entry
       uint2 ad[FB];
 #pragma unroll
       for (int b = 0; b < FB; ++b) {
         const uint32_t idx = c0 + b * 64 + lane;
-        v[b] = idx < total ? blk * BLK_SLOTS + s_front[wv][idx] : NO_SLOT;
+        const uint32_t e = idx < total ? s_front[wv][idx] : 0u;
+        v[b] = idx < total ? blk * BLK_SLOTS + (e & (BLK_SLOTS - 1)) : NO_SLOT;
+        f[b] = (uint8_t)(((e >> 11) & 1u) ? FL_HALTED : 0) | (uint8_t)(((e >> 12) & 1u) ? FL_PROXY : 0);
       }
 #pragma unroll
       for (int b = 0; b < FB; ++b) {
         const bool valid = v[b] != NO_SLOT;
-        f[b] = valid ? g.flags[v[b]] : 0;
         nz[b] = (valid && a.alpha) ? g.nzdeg[v[b]] : 0;  // Beamer's m_f only: the sweep counts traced edges
         ad[b] = (valid && !pull) ? g.adj[v[b]] : make_uint2(0, 0);
         sp[b] = (valid && !INVESTIGATE) ? g.sup[v[b]] : NO_SLOT;
