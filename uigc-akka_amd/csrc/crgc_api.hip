@@ -509,7 +509,10 @@ static void edge_geometry(const crgc_graph *h, uint64_t max_atoms, uint32_t &bsh
                           uint64_t &nblk) {
   uint32_t lg = 0;
   while ((1ull << lg) < h->g.d.scap) ++lg;
-  uint32_t lk = lg > 18 ? 10u : (lg > 9 ? lg - 8 : 1u);
+  // 512 owner buckets at scale: one 1024-thread workgroup per bucket, two per CU,
+  // so every bucket is resident at once (1024 left a second, partial wave of
+  // workgroups: the C2 merge 20-30 us slower, profiles/r2p/ab_buckets.txt)
+  uint32_t lk = lg > 18 ? 9u : (lg > 9 ? lg - 8 : 1u);
   // test hook: fewer buckets, so buckets take several rounds of atoms
   if (const char *m = getenv("CRGC_BUCKETS_LOG2")) lk = std::min<uint32_t>(10, std::max<uint32_t>(1, (uint32_t)atoi(m)));
   bshift = 32 - lk;
