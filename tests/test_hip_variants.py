@@ -33,7 +33,7 @@ def _stream():
 
 
 def _key(r):
-    return (r.garbage_set(), r.kill_set(), r.n_live, r.pseudo_roots, r.sup_edges)
+    return (r.garbage_set(), r.kill_set(), r.n_live, r.pseudo_roots, r.sup_edges, r.edges_scanned)
 
 
 @pytest.fixture(scope="module")
