@@ -1116,56 +1116,55 @@ __global__ __launch_bounds__(256) void k_sweep(DevGraph g, int should_kill) {
 
 // One workgroup: exclusive offsets over the per-block (garbage, kill) counts,
 // totals into the counters, and the live count from the sweep partials.
+// Each thread owns a contiguous run of blocks, so the counts are loaded in one
+// pass and placed by one workgroup scan (latency-bound: one round trip, not
+// one per 1024 blocks).  Slots are u32, so every count fits 32 bits.
 __global__ __launch_bounds__(1024) void k_sweep_scan(DevGraph g, uint32_t sweep_grid) {
-  __shared__ uint64_t wsum[2][16];
-  __shared__ uint64_t carry[2];
+  __shared__ uint64_t wsum[3][16];
   Counters *c = g.ctr;
   if (!c->mark_done) return;
   const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
   const int lane = lane_id(), wv = threadIdx.x >> 6;
-  if (threadIdx.x == 0) carry[0] = carry[1] = 0;
-  __syncthreads();
-  for (uint64_t b0 = 0; b0 < nblk; b0 += 1024) {
-    const uint64_t b = b0 + threadIdx.x;
-    const uint32_t gv = b < nblk ? g.sweep_cnt[2 * b] : 0;
-    const uint32_t kv = b < nblk ? g.sweep_cnt[2 * b + 1] : 0;
-    const uint32_t gi = wave_incl_scan(gv), ki = wave_incl_scan(kv);
-    if (lane == 63) {
-      wsum[0][wv] = gi;
-      wsum[1][wv] = ki;
-    }
-    __syncthreads();
-    uint64_t gpre = carry[0], kpre = carry[1], gtot = 0, ktot = 0;
-    for (int w = 0; w < 16; ++w) {
-      if (w < wv) {
-        gpre += wsum[0][w];
-        kpre += wsum[1][w];
-      }
-      gtot += wsum[0][w];
-      ktot += wsum[1][w];
-    }
-    if (b < nblk) {
-      g.sweep_off[2 * b] = gpre + gi - gv;
-      g.sweep_off[2 * b + 1] = kpre + ki - kv;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      carry[0] += gtot;
-      carry[1] += ktot;
-    }
-    __syncthreads();
+  const uint64_t per = (nblk + 1023) / 1024;
+  const uint64_t b_lo = min(nblk, (uint64_t)threadIdx.x * per), b_hi = min(nblk, b_lo + per);
+  uint32_t live = 0, gs = 0, ks = 0;
+  for (uint32_t b = threadIdx.x; b < sweep_grid; b += 1024) live += (uint32_t)g.blkstat[b * 4 + STAT_LIVE];
+#pragma unroll 4
+  for (uint64_t b = b_lo; b < b_hi; ++b) {
+    const uint2 gk = *(const uint2 *)(g.sweep_cnt + 2 * b);
+    gs += gk.x;
+    ks += gk.y;
   }
-  uint64_t live = 0;
-  for (uint32_t b = threadIdx.x; b < sweep_grid; b += 1024) live += g.blkstat[b * 4 + STAT_LIVE];
-  const uint64_t wl = __shfl(wave_incl_scan((uint32_t)live), 63);
-  if (lane == 0) wsum[0][wv] = wl;
+  const uint32_t gi = wave_incl_scan(gs), ki = wave_incl_scan(ks), li = wave_incl_scan(live);
+  if (lane == 63) {
+    wsum[0][wv] = gi;
+    wsum[1][wv] = ki;
+    wsum[2][wv] = li;
+  }
   __syncthreads();
+  uint64_t go = 0, ko = 0, gtot = 0, ktot = 0, ltot = 0;
+  for (int w = 0; w < 16; ++w) {
+    if (w < wv) {
+      go += wsum[0][w];
+      ko += wsum[1][w];
+    }
+    gtot += wsum[0][w];
+    ktot += wsum[1][w];
+    ltot += wsum[2][w];
+  }
+  go += gi - gs;
+  ko += ki - ks;
+#pragma unroll 4
+  for (uint64_t b = b_lo; b < b_hi; ++b) {
+    const uint2 gk = *(const uint2 *)(g.sweep_cnt + 2 * b);
+    *(ulonglong2 *)(g.sweep_off + 2 * b) = make_ulonglong2(go, ko);
+    go += gk.x;
+    ko += gk.y;
+  }
   if (threadIdx.x == 0) {
-    uint64_t t = 0;
-    for (int w = 0; w < 16; ++w) t += wsum[0][w];
-    c->n_live = t;
-    c->n_garbage = carry[0];
-    c->n_kill = carry[1];
+    c->n_live = ltot;
+    c->n_garbage = gtot;
+    c->n_kill = ktot;
   }
 }
 
