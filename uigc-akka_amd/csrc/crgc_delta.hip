@@ -482,6 +482,34 @@ __global__ __launch_bounds__(SCAN_B) void k_scan_apply(ScanSet q) {
   }
 }
 
+// Up to SCAN_B block sums: each workgroup adds up the sums before its own (at
+// most SCAN_B loads, one per thread), so no k_scan_top launch; the last block
+// writes the totals.
+__global__ __launch_bounds__(SCAN_B) void k_scan_apply_top(ScanSet q) {
+  __shared__ uint64_t w[4][SCAN_B / 64];
+  const uint64_t i = (uint64_t)blockIdx.x * SCAN_B + threadIdx.x;
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  uint64_t pre[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint64_t p = j < q.k && threadIdx.x < blockIdx.x ? q.bsum[(uint64_t)j * q.nb + threadIdx.x] : 0;
+    for (int d = 32; d > 0; d >>= 1) p += __shfl_xor(p, d);
+    if (lane == 0) w[j][wv] = p;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    pre[j] = 0;
+    for (int k = 0; k < (int)(SCAN_B / 64); ++k) pre[j] += w[j][k];
+  }
+  for (int j = 0; j < q.k; ++j) {
+    uint32_t tot;
+    const uint32_t x = block_excl_1024(i < q.n ? q.in[j][i] : 0u, &tot);
+    if (i < q.n) q.out[j][i] = pre[j] + x;
+    if (blockIdx.x == q.nb - 1 && threadIdx.x == 0) *q.total[j] = pre[j] + tot;
+  }
+}
+
 // Small scans in one workgroup (one launch instead of three).  n_dev: the
 // element count on the device (null: q.n); a set *skip (a deferred DeltaGraph
 // chain start, nothing was counted) scans nothing.
@@ -547,6 +575,10 @@ hipError_t run_scan(ScanSet q, hipStream_t s) {
   }
   q.nb = (q.n + SCAN_B - 1) / SCAN_B;
   hipLaunchKernelGGL(k_scan_sums, dim3(q.nb), dim3(SCAN_B), 0, s, q);
+  if (q.nb <= SCAN_B) {
+    hipLaunchKernelGGL(k_scan_apply_top, dim3(q.nb), dim3(SCAN_B), 0, s, q);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_B), 0, s, q);
   hipLaunchKernelGGL(k_scan_apply, dim3(q.nb), dim3(SCAN_B), 0, s, q);
   return hipGetLastError();
