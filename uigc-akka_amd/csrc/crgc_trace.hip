@@ -806,38 +806,39 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
   __shared__ uint32_t s_off[TAIL_THREADS];
   __shared__ uint32_t s_w[40];
   __shared__ uint32_t s_next;
-  __shared__ unsigned long long s_red[TAIL_THREADS];
+  __shared__ unsigned long long s_red[2 * (TAIL_THREADS / 64)];
   __shared__ uint32_t s_q[2][TAIL_LQ];
   __shared__ uint32_t s_vis[TAIL_LVIS_WORDS];
   Counters *c = g.ctr;
   const int L = a.level;
-  if (c->tail_state) return;
-  // Level count = sum of k_frontier's per-workgroup frontier counts.
-  unsigned long long part = 0;
-  for (uint32_t b = threadIdx.x; b < a.frontier_grid; b += TAIL_THREADS)
-    part += g.blkstat[b * 4 + STAT_FRONT];
-  s_red[threadIdx.x] = part;
-  __syncthreads();
-  for (int k = TAIL_THREADS / 2; k > 0; k >>= 1) {
-    if (threadIdx.x < k) s_red[threadIdx.x] += s_red[threadIdx.x + k];
-    __syncthreads();
+  // Level count = sum of k_frontier's per-workgroup frontier counts, and its
+  // frontier's out-edges (Beamer's m_f) for k_expand's direction: both loaded
+  // in one round trip (before the state check, which they do not depend on)
+  // and summed with wave shuffles.
+  unsigned long long pf = 0, pm = 0;
+  for (uint32_t b = threadIdx.x; b < a.frontier_grid; b += TAIL_THREADS) {
+    pf += g.blkstat[b * 4 + STAT_FRONT];
+    pm += g.blkstat[b * 4 + STAT_MF];
   }
-  const uint64_t n0 = s_red[0];
+  if (c->tail_state) return;
+  for (int d = 32; d > 0; d >>= 1) {
+    pf += __shfl_xor(pf, d);
+    pm += __shfl_xor(pm, d);
+  }
+  if (lane_id() == 0) {
+    s_red[threadIdx.x >> 6] = pf;
+    s_red[16 + (threadIdx.x >> 6)] = pm;
+  }
+  __syncthreads();
+  uint64_t n0 = 0, mf = 0;
+  for (int k = 0; k < TAIL_THREADS / 64; ++k) {
+    n0 += s_red[k];
+    mf += s_red[16 + k];
+  }
   if (!listing_level(c, L, a) || n0 == 0 || n0 > a.tail_start) {
-    // ... and its frontier's out-edges (Beamer's m_f), for k_expand's direction
-    __syncthreads();
-    part = 0;
-    for (uint32_t b = threadIdx.x; b < a.frontier_grid; b += TAIL_THREADS)
-      part += g.blkstat[b * 4 + STAT_MF];
-    s_red[threadIdx.x] = part;
-    __syncthreads();
-    for (int k = TAIL_THREADS / 2; k > 0; k >>= 1) {
-      if (threadIdx.x < k) s_red[threadIdx.x] += s_red[threadIdx.x + k];
-      __syncthreads();
-    }
     if (threadIdx.x == 0) {  // the level kernels go on
-      c->mf_level = s_red[0];
-      c->mf_sum += s_red[0];
+      c->mf_level = mf;
+      c->mf_sum += mf;
       c->ring[L % LEVEL_RING] = n0;
       c->marked += n0;
       c->qh[(L + 1) & 1] = 0;  // next level's hub queue (last read by k_expand(L-1))
