@@ -1722,7 +1722,6 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
     auto sweep = [&]() -> hipError_t {
       hipError_t e = hipEventRecord(h->ev[1], h->stream);
       if (e == hipSuccess) e = launch_sweep(h->g.d, should_kill ? 1 : 0, top, h->stream);
-      if (e == hipSuccess) e = launch_trace_stats(h->g.d, h->stream);  // after the sweep's edge counts
       if (e == hipSuccess) e = hipEventRecord(h->ev[2], h->stream);
       if (e == hipSuccess)
         e = hipMemcpyAsync(h->hctr, h->ctr, offsetof(Counters, ring), hipMemcpyDeviceToHost, h->stream);
@@ -1737,7 +1736,6 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
     if (int rc = mark_all(h, false, 0, top, lr, &rounds, &ids_sent, &ms_x, &x_bytes)) return rc;
     HIP_TRY(hipEventRecord(h->ev[1], h->stream));
     if (int rc = sweep_sharded(h, should_kill ? 1 : 0, top, &ms_x)) return rc;
-    HIP_TRY(launch_trace_stats(h->g.d, h->stream));  // after the sweep's edge counts
     HIP_TRY(hipEventRecord(h->ev[2], h->stream));
     HIP_TRY(sync_counters(h));
   }

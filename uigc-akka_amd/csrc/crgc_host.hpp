@@ -199,7 +199,6 @@ hipError_t launch_edges(const DevGraph &g, const EdgeArgs &a, hipStream_t s);
 // ev: null, or 6 events: start / stop of k_frontier, k_tail, k_expand
 hipError_t launch_level(const DevGraph &g, const LevelArgs &a, bool roots, bool investigate,
                         uint64_t slot_top, hipStream_t s, hipEvent_t *ev = nullptr);
-hipError_t launch_trace_stats(const DevGraph &g, hipStream_t s);
 hipError_t launch_trace_reset(const DevGraph &g, uint64_t nblk, uint32_t ctr_from, uint32_t ctr_words,
                               hipStream_t s);
 // sweep + id compaction + removal of the garbage (skipped on a reference NPE)

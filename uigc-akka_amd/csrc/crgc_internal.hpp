@@ -72,7 +72,7 @@ struct Counters {
   unsigned long long marked;
   unsigned long long edges_scanned;
   unsigned long long sup_edges;
-  unsigned long long expand_bytes;   // bytes k_expand read / wrote over the trace (k_trace_stats)
+  unsigned long long expand_bytes;   // bytes k_expand read / wrote over the trace (summed by k_sweep_scan)
   unsigned long long mf_level;       // nonzero out-edges of the current level's expandable frontier
   unsigned long long mf_sum;         // ... summed over the levels so far (Beamer's explored edges)
   unsigned long long chain_marked;   // shadows marked by chain mode (crgc_chain.hip)

@@ -967,41 +967,6 @@ hipError_t launch_trace_reset(const DevGraph &g, uint64_t nblk, uint32_t ctr_fro
   return hipGetLastError();
 }
 
-// Sum of the per-workgroup sup/edge partials into the counters (once per trace).
-__global__ __launch_bounds__(256) void k_trace_stats(DevGraph g) {
-  __shared__ uint64_t red[2][256];
-  if (!g.ctr->mark_done) return;  // enqueued behind a level chunk that did not finish the mark
-  __shared__ uint64_t red_x[256];
-  uint64_t su = 0, ed = 0, xb = 0;
-  for (uint32_t b = threadIdx.x; b < STAT_WG; b += 256) {
-    su += g.blkstat[b * 4 + STAT_SUP];
-    ed += g.blkstat[b * 4 + STAT_EDGES];
-    xb += g.xbytes[b];
-  }
-  red[0][threadIdx.x] = su;
-  red[1][threadIdx.x] = ed;
-  red_x[threadIdx.x] = xb;
-  __syncthreads();
-  for (int k = 128; k > 0; k >>= 1) {
-    if (threadIdx.x < k) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + k];
-      red[1][threadIdx.x] += red[1][threadIdx.x + k];
-      red_x[threadIdx.x] += red_x[threadIdx.x + k];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    g.ctr->sup_edges = red[0][0];
-    g.ctr->edges_scanned = red[1][0];
-    g.ctr->expand_bytes = red_x[0];
-  }
-}
-
-hipError_t launch_trace_stats(const DevGraph &g, hipStream_t s) {
-  hipLaunchKernelGGL(k_trace_stats, dim3(1), dim3(256), 0, s, g);
-  return hipGetLastError();
-}
-
 // ---------------------------------------------------------------------------
 // Sweep (:270-284): unmarked shadows are garbage; a local one is told StopMsg
 // when its supervisor is marked and it is not halted.  A local garbage shadow
@@ -1119,11 +1084,25 @@ __global__ __launch_bounds__(256) void k_sweep(DevGraph g, int should_kill) {
 // totals into the counters, and the live count from the sweep partials.
 // Each thread owns a contiguous run of blocks, so the counts are loaded in one
 // pass and placed by one workgroup scan (latency-bound: one round trip, not
-// one per 1024 blocks).  Slots are u32, so every count fits 32 bits.
+// one per 1024 blocks).  Slots are u32, so every count fits 32 bits.  It also
+// sums the trace's per-workgroup sup / traced-edge / expand-byte partials into
+// the counters (the sweep wrote the edge partials).
 __global__ __launch_bounds__(1024) void k_sweep_scan(DevGraph g, uint32_t sweep_grid) {
   __shared__ uint64_t wsum[3][16];
+  __shared__ uint64_t wst[3][16];
   Counters *c = g.ctr;
-  if (!c->mark_done) return;
+  uint64_t su = 0, ed = 0, xb = 0;
+  for (uint32_t b = threadIdx.x; b < STAT_WG; b += 1024) {
+    su += g.blkstat[b * 4 + STAT_SUP];
+    ed += g.blkstat[b * 4 + STAT_EDGES];
+    xb += g.xbytes[b];
+  }
+  if (!c->mark_done) return;  // enqueued behind a level chunk that did not finish the mark
+  for (int d = 32; d > 0; d >>= 1) {
+    su += __shfl_xor(su, d);
+    ed += __shfl_xor(ed, d);
+    xb += __shfl_xor(xb, d);
+  }
   const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
   const int lane = lane_id(), wv = threadIdx.x >> 6;
   const uint64_t per = (nblk + 1023) / 1024;
@@ -1141,6 +1120,9 @@ __global__ __launch_bounds__(1024) void k_sweep_scan(DevGraph g, uint32_t sweep_
     wsum[0][wv] = gi;
     wsum[1][wv] = ki;
     wsum[2][wv] = li;
+    wst[0][wv] = su;
+    wst[1][wv] = ed;
+    wst[2][wv] = xb;
   }
   __syncthreads();
   uint64_t go = 0, ko = 0, gtot = 0, ktot = 0, ltot = 0;
@@ -1166,6 +1148,12 @@ __global__ __launch_bounds__(1024) void k_sweep_scan(DevGraph g, uint32_t sweep_
     c->n_live = ltot;
     c->n_garbage = gtot;
     c->n_kill = ktot;
+    uint64_t t[3] = {0, 0, 0};
+    for (int w = 0; w < 16; ++w)
+      for (int k = 0; k < 3; ++k) t[k] += wst[k][w];
+    c->sup_edges = t[0];
+    c->edges_scanned = t[1];
+    c->expand_bytes = t[2];
   }
 }
 
