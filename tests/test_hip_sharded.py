@@ -309,3 +309,27 @@ def test_c4_shape_eight_shards(sharded, oracle_mod, xbits, monkeypatch):
             assert rh.exchange_bytes < 8 * rh.ids_sent
     assert h.export() == o.export()
     assert h.total_actors_seen() == o.total_actors_seen()
+
+
+def test_forty_shards_rebuild_homes_above_32(sharded, oracle_mod):
+    """Home-slot generations of shards >= 32 (the per-home mask is
+    64 bits wide).  Shards 33, 35 and 39 compact between traces, renumbering
+    their slots; every other shard's proxies of them must forget their cached
+    home slots (and only those), or marks land on renumbered shadows."""
+    G = 40
+    h, o = sharded(G, vertex_capacity=64, edge_capacity=64), oracle_mod.OracleGraph()
+    fz = fuzz.Fuzz(41)
+    for step in range(6):
+        eb = fz.entries(800)
+        h.merge_entries(eb, split=True)
+        o.merge_entries(eb)
+        if step >= 1:
+            for r in (33, 35, 39):
+                h.shards[r].compact()  # local: bumps shard r's slot generation only
+        assert h.export() == o.export()
+        rh, ro = h.trace(True), o.trace(True)
+        _same(rh, ro)
+        if step >= 1:
+            assert rh.rounds >= 2
+        fz.sync(o.export())
+    assert h.export() == o.export()

@@ -359,6 +359,7 @@ class UndoAccumulator:
     def fold_ingress(self, fields: UndoBatch):
         ShadowGraph._chk(self.lib.crgc_undo_acc_fold_ingress(self.h, C.byref(fields.struct())),
                          "crgc_undo_acc_fold_ingress")
+        self.graph._hold(fields)  # device input: read on the stream after the call returns
 
     mergeIngressEntry = fold_ingress
 

@@ -227,6 +227,7 @@ namespace {
 int map_hip(hipError_t e) {
   if (e == hipSuccess) return CRGC_OK;
   if (e == hipErrorOutOfMemory) return CRGC_E_NOMEM;
+  if (e == hipErrorLaunchTimeOut) return CRGC_E_TIMEOUT;
   return CRGC_E_DEVICE;
 }
 
@@ -249,6 +250,18 @@ struct DeviceGuard {
   }
 };
 
+// Host wait for the graph's stream.  Sharded graphs wait through their
+// transport: over RCCL that wait is bounded and ends early when the
+// communicator reports an asynchronous error (a failed peer), and the handle
+// is poisoned, instead of blocking forever in a collective.
+hipError_t hsync(crgc_graph *h) {
+  if (!h->tp) return hipStreamSynchronize(h->stream);
+  const int rc = h->tp->wait(h->stream);
+  if (rc == CRGC_OK) return hipSuccess;
+  h->poisoned = true;
+  return rc == CRGC_E_TIMEOUT ? hipErrorLaunchTimeOut : hipErrorLaunchFailure;
+}
+
 void absorb_counters(crgc_graph *h);
 
 // Read back the small counters (blocking).
@@ -256,7 +269,7 @@ hipError_t sync_counters(crgc_graph *h) {
   hipError_t e = hipMemcpyAsync(h->hctr, h->ctr, offsetof(Counters, ring), hipMemcpyDeviceToHost,
                                 h->stream);
   if (e != hipSuccess) return e;
-  e = hipStreamSynchronize(h->stream);
+  e = hsync(h);
   if (e != hipSuccess) return e;
   absorb_counters(h);
   return hipSuccess;
@@ -380,13 +393,27 @@ const T *stage(crgc_graph *h, Carver &cv, const T *src, uint64_t n, uint32_t mem
 // Host batches are read by stream-ordered copies; the ABI promises that the
 // caller's buffers are free again when the call returns (crgc.h), so a merge
 // that staged host memory waits for those copies (only: ev[3] is recorded
-// right after them, the kernels behind it keep running).
-hipError_t mark_staged(crgc_graph *h, uint32_t memory) {
-  return memory == CRGC_MEM_HOST ? hipEventRecord(h->ev[3], h->stream) : hipSuccess;
-}
-hipError_t wait_staged(crgc_graph *h, uint32_t memory) {
-  return memory == CRGC_MEM_HOST ? hipEventSynchronize(h->ev[3]) : hipSuccess;
-}
+// right after them, the kernels behind it keep running).  The guard is armed
+// before the first copy and waits on every return path, errors included.
+struct Staged {
+  crgc_graph *h;
+  bool armed, recorded = false;
+  Staged(crgc_graph *g, uint32_t memory) : h(g), armed(memory == CRGC_MEM_HOST) {}
+  hipError_t mark() {
+    if (!armed) return hipSuccess;
+    const hipError_t e = hipEventRecord(h->ev[3], h->stream);
+    recorded = e == hipSuccess;
+    return e;
+  }
+  hipError_t wait() {
+    if (!armed) return hipSuccess;
+    armed = false;
+    return recorded ? hipEventSynchronize(h->ev[3]) : hipStreamSynchronize(h->stream);
+  }
+  ~Staged() { wait(); }
+  Staged(const Staged &) = delete;
+  Staged &operator=(const Staged &) = delete;
+};
 
 int check_graph(crgc_graph *h) {
   if (!h) return CRGC_E_INVAL;
@@ -578,7 +605,7 @@ static int ag_u64(crgc_graph *h, std::initializer_list<std::pair<const void *, u
     return rc;
   }
   HIP_TRY(hipMemcpyAsync(h->h_small, rcv, bytes * h->G, hipMemcpyDeviceToHost, h->stream));
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hsync(h));
   memcpy(out, h->h_small, bytes * h->G);
   return CRGC_OK;
 }
@@ -686,7 +713,7 @@ static int gather_batches(crgc_graph *h, const uint64_t *hdr, uint32_t K, const 
   if (h->x_pack.ensure(mine.total) != hipSuccess || h->x_pack_recv.ensure(tot) != hipSuccess)
     return CRGC_E_NOMEM;
   if (int rc = pack(h, mine, src, narr, memory, (char *)h->x_pack.ptr)) return rc;
-  if (memory == CRGC_MEM_HOST && narr) HIP_TRY(hipStreamSynchronize(h->stream));  // caller's buffers free on return
+  if (memory == CRGC_MEM_HOST && narr) HIP_TRY(hsync(h));  // caller's buffers free on return
   if (int rc = h->tp->alltoallv(h->shard, h->x_pack.ptr, soff, sb, h->x_pack_recv.ptr, roff.data(), rb,
                                 h->stream)) {
     h->poisoned = true;
@@ -720,13 +747,17 @@ static int entry_counts(crgc_graph *h, const crgc_entry_batch *b, bool exact, ui
     HIP_TRY(hipMemcpyAsync(&v[0], b->created_off + n, 4, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipMemcpyAsync(&v[1], b->spawned_off + n, 4, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipMemcpyAsync(&v[2], b->updated_off + n, 4, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hsync(h));
     *C = v[0];
     *S = v[1];
     *U = v[2];
-  } else {
+  } else if (b->created_owner && b->created_target && b->spawned && b->updated_ref && b->updated_info) {
     *C = *S = *U = n * h->F;  // bounds; kernels read the exact offsets
     return CRGC_OK;
+  } else {
+    // a null record array is legal only when its count is zero: learn the
+    // counts (one round trip) so the checks below refuse the batch otherwise
+    return entry_counts(h, b, true, C, S, U);
   }
   if (*C > n * h->F || *S > n * h->F || *U > n * h->F) return CRGC_E_INVAL;
   if ((*C && (!b->created_owner || !b->created_target)) || (*S && !b->spawned) ||
@@ -757,6 +788,7 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
     return CRGC_E_NOMEM;
   Carver sc(h->stage.ptr), wc(h->work.ptr);
+  Staged staged(h, b->memory);
   EntryArgs a{};
   a.n = n;
   a.F = h->F;
@@ -772,7 +804,7 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   a.u_off = stage(h, sc, b->updated_off, n + 1, b->memory);
   a.u_ref = stage(h, sc, b->updated_ref, U, b->memory);
   a.u_info = stage(h, sc, b->updated_info, U, b->memory);
-  HIP_TRY(mark_staged(h, b->memory));
+  HIP_TRY(staged.mark());
   a.self_slot = wc.take<uint32_t>(n);
   a.spawn_slot = wc.take<uint32_t>(n * h->F);
   a.ct_slot = wc.take<uint32_t>(n * h->F);
@@ -791,7 +823,7 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   HIP_TRY(launch_entries(h->g.d, a, h->stream));
   if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, max_atoms, wc, a.n_atoms)) return rc;
   note_merge(h, ids, C + U);
-  HIP_TRY(wait_staged(h, b->memory));
+  HIP_TRY(staged.wait());
   return CRGC_OK;
 }
 
@@ -1020,7 +1052,7 @@ static int delta_counts(crgc_graph *h, const crgc_delta_batch *b, uint64_t *nout
   } else {
     uint32_t v = 0;  // ordered behind whatever produced the batch on this stream
     HIP_TRY(hipMemcpyAsync(&v, b->out_off + n, 4, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hsync(h));
     *nout = v;
   }
   if (*nout && (!b->out_target || !b->out_count)) return CRGC_E_INVAL;
@@ -1042,6 +1074,7 @@ static int merge_deltas_one(crgc_graph *h, const crgc_delta_batch *b, uint64_t n
   if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
     return CRGC_E_NOMEM;
   Carver sc(h->stage.ptr), wc(h->work.ptr);
+  Staged staged(h, b->memory);
   DeltaArgs a{};
   a.n = n;
   a.epoch = ++h->epoch;
@@ -1052,7 +1085,7 @@ static int merge_deltas_one(crgc_graph *h, const crgc_delta_batch *b, uint64_t n
   a.out_off = stage(h, sc, b->out_off, n + 1, b->memory);
   a.out_target = stage(h, sc, b->out_target, nout, b->memory);
   a.out_count = stage(h, sc, b->out_count, nout, b->memory);
-  HIP_TRY(mark_staged(h, b->memory));
+  HIP_TRY(staged.mark());
   a.self_slot = wc.take<uint32_t>(n);
   a.sup_slot = wc.take<uint32_t>(n);
   a.ot_slot = wc.take<uint32_t>(std::max<uint64_t>(nout, 1));
@@ -1063,7 +1096,7 @@ static int merge_deltas_one(crgc_graph *h, const crgc_delta_batch *b, uint64_t n
   HIP_TRY(launch_deltas(h->g.d, a, nout, h->stream));
   if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, nout, wc)) return rc;
   note_merge(h, ids, nout);
-  HIP_TRY(wait_staged(h, b->memory));
+  HIP_TRY(staged.wait());
   return CRGC_OK;
 }
 
@@ -1183,7 +1216,7 @@ int crgc_merge_undo(crgc_graph *h, const crgc_undo_log *log) {
       }
     } else {
       HIP_TRY(hipMemcpyAsync(ex.data(), a.exists, n + nc, hipMemcpyDeviceToHost, h->stream));
-      HIP_TRY(hipStreamSynchronize(h->stream));
+      HIP_TRY(hsync(h));
     }
   }
   for (uint64_t i = 0; i < n; ++i) {
@@ -1243,7 +1276,7 @@ static int run_chains(crgc_graph *h, bool investigate, uint64_t top) {
     }
     HIP_TRY(launch_chain(g, ca, 2, nullptr, nullptr, top, 2 * R, 0, 0, h->stream));
     HIP_TRY(hipMemcpyAsync(fl.data(), ca.flag, fl.size() * 4, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hsync(h));
     bool any = false;
     for (uint32_t f : fl)
       if (f) {
@@ -1372,7 +1405,17 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   std::vector<unsigned long long> ring(LEVEL_RING);
   unsigned long long tail[3] = {0, 0, 0};
   const bool log = getenv("CRGC_LEVEL_LOG") != nullptr;
-  for (;;) {
+  // Bounds on the host loop: every pass either reaches an
+  // empty level, finishes in k_tail / chain mode, or moves L forward (a bail
+  // must resume past the level it bailed from before); levels are bounded by
+  // the (level + 1) << 12 tag width, passes by a count and a wall clock.
+  const auto loop_t0 = std::chrono::steady_clock::now();
+  int last_bail = -1;
+  for (uint64_t pass = 0;; ++pass) {
+    if (pass > 4096 || std::chrono::steady_clock::now() - loop_t0 > std::chrono::seconds(300)) {
+      h->poisoned = true;
+      return CRGC_E_TIMEOUT;
+    }
     if (nc % 2 == 0) HIP_TRY(chunk_event());
     for (int k = 0; k < chunk; ++k) HIP_TRY(launch(L + k, false));
     HIP_TRY(chunk_event());
@@ -1389,7 +1432,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
     }
     HIP_TRY(hipMemcpyAsync(tail, (char *)h->ctr + CTR_OFF(tail_state), 24, hipMemcpyDeviceToHost,
                            h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hsync(h));
     if (roots && first == 0) lr.roots = ring[0];
     if (tail[0] == TAIL_CHAINS) {  // k_tail handed a deep mark to chain mode, which finishes it
       HIP_TRY(chunk_event());  // chain mode's device time counts as mark time
@@ -1397,9 +1440,14 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
       HIP_TRY(chunk_event());
       if (after_chunk) HIP_TRY(after_chunk());
       HIP_TRY(hipMemcpyAsync(tail, (char *)h->ctr + CTR_OFF(tail_state), 24, hipMemcpyDeviceToHost, h->stream));
-      HIP_TRY(hipStreamSynchronize(h->stream));
+      HIP_TRY(hsync(h));
     }
     if (tail[0] == TAIL_BAILED) {  // k_tail handed a wide frontier back: resume there
+      if ((int)tail[1] <= last_bail || (uint64_t)tail[1] > (1ull << 19)) {
+        h->poisoned = true;  // no progress since the last bail
+        return CRGC_E_TIMEOUT;
+      }
+      last_bail = (int)tail[1];
       HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(tail_state), 0, 8, h->stream));
       L = (int)tail[1];
       continue;
@@ -1435,28 +1483,22 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
 // deferred by crgc_trace until the result copies are in flight).
 static void collect_times(crgc_graph *h, LevelRun &lr, size_t nl, size_t nc, int timing, bool log,
                           size_t first_level, size_t last, const std::vector<unsigned long long> &ring) {
-  {
-    {
-      {
-        for (size_t i = 0; i + 1 < nc; i += 2) {
-          float t = 0;
-          hipEventElapsedTime(&t, h->chunk_ev[i], h->chunk_ev[i + 1]);
-          lr.ms += t;
-        }
-        for (size_t i = 0; i < (timing ? nl : 0); ++i) {
-          float t[3] = {0, 0, 0};
-          for (int k = timing >= 2 ? 0 : 2; k < 3; ++k)
-            hipEventElapsedTime(&t[k], h->lvl_ev[6 * i + 2 * k], h->lvl_ev[6 * i + 2 * k + 1]);
-          lr.ms_f += t[0];
-          lr.ms_t += t[1];
-          lr.ms_e += t[2];
-          if (log)
-            fprintf(stderr, "[crgc] level %zu frontier %llu  %.1f us (frontier %.1f tail %.1f expand %.1f)\n",
-                    first_level + i, first_level + i <= last ? ring[(first_level + i) % LEVEL_RING] : 0ull,
-                    (t[0] + t[1] + t[2]) * 1e3, t[0] * 1e3, t[1] * 1e3, t[2] * 1e3);
-        }
-      }
-    }
+  for (size_t i = 0; i + 1 < nc; i += 2) {
+    float t = 0;
+    hipEventElapsedTime(&t, h->chunk_ev[i], h->chunk_ev[i + 1]);
+    lr.ms += t;
+  }
+  for (size_t i = 0; i < (timing ? nl : 0); ++i) {
+    float t[3] = {0, 0, 0};
+    for (int k = timing >= 2 ? 0 : 2; k < 3; ++k)
+      hipEventElapsedTime(&t[k], h->lvl_ev[6 * i + 2 * k], h->lvl_ev[6 * i + 2 * k + 1]);
+    lr.ms_f += t[0];
+    lr.ms_t += t[1];
+    lr.ms_e += t[2];
+    if (log)
+      fprintf(stderr, "[crgc] level %zu frontier %llu  %.1f us (frontier %.1f tail %.1f expand %.1f)\n",
+              first_level + i, first_level + i <= last ? ring[(first_level + i) % LEVEL_RING] : 0ull,
+              (t[0] + t[1] + t[2]) * 1e3, t[0] * 1e3, t[1] * 1e3, t[2] * 1e3);
   }
 }
 
@@ -1485,9 +1527,9 @@ static int resolve_home_slots(crgc_graph *h, uint64_t top, int xmode, uint64_t *
     h->peer_gen.assign(G, ~0ull);
     h->peer_top.assign(G, 0);
   }
-  uint32_t mask = 0;
+  uint64_t mask = 0;  // one bit per home: MAX_SHARDS = 64
   for (uint32_t d = 0; d < G; ++d) {
-    if (h->peer_gen[d] != T[2 * d]) mask |= 1u << d;
+    if (h->peer_gen[d] != T[2 * d]) mask |= 1ull << d;
     h->peer_gen[d] = T[2 * d];
     h->peer_top[d] = T[2 * d + 1];
   }
@@ -1627,7 +1669,7 @@ static int copy_lists(crgc_graph *h, crgc_trace_out *out, bool sync = true) {
       HIP_TRY(hipMemcpyAsync(out->kill_ids, h->g.d.out_kill, h->last_kill * 8, hipMemcpyDeviceToHost,
                              h->stream));
   }
-  if (sync) HIP_TRY(hipStreamSynchronize(h->stream));
+  if (sync) HIP_TRY(hsync(h));
   return big ? CRGC_E2BIG : CRGC_OK;
 }
 
@@ -1653,7 +1695,7 @@ static int sweep_sharded(crgc_graph *h, int should_kill, uint64_t top, double *m
   if (npe) {  // the reference's NullPointerException on some shard: nobody commits
     HIP_TRY(hipMemcpyAsync((char *)h->ctr + CTR_OFF(npe), &npe, 8, hipMemcpyHostToDevice, h->stream));
     HIP_TRY(launch_sweep(h->g.d, should_kill, top, h->stream, 2));
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hsync(h));
     *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return CRGC_OK;
   }
@@ -1751,7 +1793,7 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
     lr.pending();
     lr.pending = nullptr;
   }
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hsync(h));
   crgc_trace_stats st{};
   st.edges_scanned = c.edges_scanned;
   st.sup_edges = c.sup_edges;
@@ -1880,7 +1922,7 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
   DgCounters hc{};
   auto fetch = [&]() -> int {
     HIP_TRY(hipMemcpyAsync(&hc, a.ctr, sizeof(DgCounters), hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hsync(h));
     return CRGC_OK;
   };
   // Device outputs of the right shape: the write pass can run on the device's
@@ -1971,7 +2013,7 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
     HIP_TRY(d2h(out->out_target, o.out_target, NO * 8));
     HIP_TRY(d2h(out->out_count, o.out_count, NO * 4));
     HIP_TRY(d2h(out->wire, o.wire, NW));
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hsync(h));
   }
   return CRGC_OK;  // device outputs: stream-ordered (crgc_sync waits for them)
 }
@@ -1979,7 +2021,7 @@ int crgc_build_delta_graphs(crgc_graph *h, const crgc_entry_batch *b, crgc_delta
 int crgc_sync(crgc_graph *h) {
   if (int rc = check_graph(h)) return rc;
   DeviceGuard dg(h->device);
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hsync(h));
   return CRGC_OK;
 }
 
@@ -2027,7 +2069,7 @@ static int ua_reserve(crgc_undo_acc *u, uint64_t ids, uint64_t pairs) {
   if (u->ids_ub + ids <= u->d.cap / 2 && u->pairs_ub + pairs <= u->d.pcap / 2) return CRGC_OK;
   unsigned long long c[2];
   HIP_TRY(hipMemcpyAsync(c, u->ctr, 16, hipMemcpyDeviceToHost, h->stream));
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hsync(h));
   u->ids_ub = c[0];
   u->pairs_ub = c[1];
   const bool grow_ids = u->ids_ub + ids > u->d.cap / 2;
@@ -2044,7 +2086,7 @@ static int ua_reserve(crgc_undo_acc *u, uint64_t ids, uint64_t pairs) {
     return CRGC_E_NOMEM;
   }
   hipError_t e = launch_ua_rehash(u->d, n, map, true, h->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e == hipSuccess) e = hsync(h);
   if (map) hipFree(map);
   if (e != hipSuccess) {
     hipFree(mem);
@@ -2112,6 +2154,7 @@ int crgc_undo_acc_fold_deltas(crgc_undo_acc *u, const crgc_delta_batch *b) {
       b->memory == CRGC_MEM_HOST ? Carver::need({n * 8, n * 4, n, (n + 1) * 4, nout * 8, nout * 4}) : 0;
   if (u->stage.ensure(host_bytes + 256) != hipSuccess) return CRGC_E_NOMEM;
   Carver sc(u->stage.ptr);
+  Staged staged(h, b->memory);
   UaDeltaArgs a{};
   a.n = n;
   a.nout = nout;
@@ -2121,9 +2164,9 @@ int crgc_undo_acc_fold_deltas(crgc_undo_acc *u, const crgc_delta_batch *b) {
   a.out_off = stage(h, sc, b->out_off, n + 1, b->memory);
   a.out_target = stage(h, sc, b->out_target, nout, b->memory);
   a.out_count = stage(h, sc, b->out_count, nout, b->memory);
-  HIP_TRY(mark_staged(h, b->memory));
+  HIP_TRY(staged.mark());
   HIP_TRY(launch_ua_fold_deltas(u->d, a, h->stream));
-  HIP_TRY(wait_staged(h, b->memory));
+  HIP_TRY(staged.wait());
   u->ids_ub += n + nout;
   u->pairs_ub += nout;
   return CRGC_OK;
@@ -2143,7 +2186,7 @@ int crgc_undo_acc_fold_ingress(crgc_undo_acc *u, const crgc_undo_log *f) {
     nc32 = f->created_off[n];
   } else {
     HIP_TRY(hipMemcpyAsync(&nc32, f->created_off + n, 4, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hsync(h));
   }
   const uint64_t nc = nc32;
   if (nc && (!f->created_target || !f->created_count)) return CRGC_E_INVAL;
@@ -2152,6 +2195,7 @@ int crgc_undo_acc_fold_ingress(crgc_undo_acc *u, const crgc_undo_log *f) {
       f->memory == CRGC_MEM_HOST ? Carver::need({n * 8, n * 4, (n + 1) * 4, nc * 8, nc * 4}) : 0;
   if (u->stage.ensure(host_bytes + 256) != hipSuccess) return CRGC_E_NOMEM;
   Carver sc(u->stage.ptr);
+  Staged staged(h, f->memory);
   UaFieldArgs a{};
   a.n = n;
   a.nc = nc;
@@ -2161,9 +2205,9 @@ int crgc_undo_acc_fold_ingress(crgc_undo_acc *u, const crgc_undo_log *f) {
   a.c_off = stage(h, sc, f->created_off, n + 1, f->memory);
   a.c_target = stage(h, sc, f->created_target, nc, f->memory);
   a.c_count = stage(h, sc, f->created_count, nc, f->memory);
-  HIP_TRY(mark_staged(h, f->memory));
+  HIP_TRY(staged.mark());
   HIP_TRY(launch_ua_fold_fields(u->d, a, h->stream));
-  HIP_TRY(wait_staged(h, f->memory));
+  HIP_TRY(staged.wait());
   u->ids_ub += n + nc;
   u->pairs_ub += nc;
   return CRGC_OK;
@@ -2189,7 +2233,7 @@ int crgc_undo_acc_export(crgc_undo_acc *u, crgc_undo_log_out *out) {
   HIP_TRY(launch_ua_export(u->d, x, 0, h->stream));
   unsigned long long nn[2];
   HIP_TRY(hipMemcpyAsync(nn, x.n_fields, 16, hipMemcpyDeviceToHost, h->stream));
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hsync(h));
   const uint64_t NF = nn[0], NC = nn[1];
   out->n_fields = NF;
   out->n_created = NC;
@@ -2215,7 +2259,7 @@ int crgc_undo_acc_export(crgc_undo_acc *u, crgc_undo_log_out *out) {
   d2h(out->created_off, x.c_off, (NF + 1) * 4);
   d2h(out->created_target, x.c_target, NC * 8);
   d2h(out->created_count, x.c_count, NC * 4);
-  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e == hipSuccess) e = hsync(h);
   o.release();
   return map_hip(e);
 }
@@ -2266,7 +2310,7 @@ int crgc_local_roots(crgc_graph *h, uint64_t *out, uint64_t cap, uint64_t *n) {
   unsigned long long k = 0;
   HIP_TRY(hipMemcpyAsync(&k, (char *)h->ctr + CTR_OFF(n_out), 8, hipMemcpyDeviceToHost,
                          h->stream));
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hsync(h));
   *n = k;
   if (!out) return CRGC_OK;
   if (cap < k) return CRGC_E2BIG;

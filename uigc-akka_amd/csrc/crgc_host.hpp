@@ -230,7 +230,7 @@ hipError_t launch_xlist(const DevGraph &g, bool scatter, uint64_t nblk, char *se
 hipError_t launch_ximport(const DevGraph &g, const char *recv, const XRecv &x, int level, hipStream_t s);
 // home-slot resolution: 0 reset(mask), 1 count unresolved, 2 list them (ids, slots),
 // 3 answer asked ids (at the home), 4 store the answers
-hipError_t launch_resolve(const DevGraph &g, int step, uint32_t mask, uint64_t *send, uint32_t *slots,
+hipError_t launch_resolve(const DevGraph &g, int step, uint64_t mask, uint64_t *send, uint32_t *slots,
                           const uint64_t *ids, uint64_t n, uint32_t *ans, uint64_t slot_top, hipStream_t s);
 hipError_t launch_requests(const DevGraph &g, int phase, const uint64_t *ids, uint64_t n, uint8_t *ans,
                            const uint32_t *slots, hipStream_t s);

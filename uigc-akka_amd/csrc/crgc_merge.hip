@@ -87,8 +87,12 @@ __global__ __launch_bounds__(256) void k_entries_apply(DevGraph g, EntryArgs a) 
   const uint32_t s0 = a.s_off[i], s1 = a.s_off[i + 1];
   const uint32_t u0 = a.u_off[i], u1 = a.u_off[i + 1];
   const uint64_t cmax = a.n * a.F;
+  // the totals place the updated atoms after the created ones: a batch whose
+  // final offsets exceed n*F is refused whole, so no atom lands past 2nF
+  const uint32_t ctot = a.c_off[a.n];
   bool ok = true;
-  if (c1 < c0 || s1 < s0 || u1 < u0 || c1 > cmax || s1 > cmax || u1 > cmax) {
+  if (c1 < c0 || s1 < s0 || u1 < u0 || c1 > cmax || s1 > cmax || u1 > cmax || ctot > cmax ||
+      a.u_off[a.n] > cmax) {
     set_err(g.ctr, ERR_BAD_OFFSETS);
     ok = false;
   } else if (c1 - c0 > a.F || s1 - s0 > a.F || u1 - u0 > a.F) {
@@ -115,7 +119,6 @@ __global__ __launch_bounds__(256) void k_entries_apply(DevGraph g, EntryArgs a) 
     atomicMax(&g.vseq[me], tag);
   }
   if (!ok) return;
-  const uint32_t ctot = a.c_off[a.n];
   // Created refs (:85-93): outgoing[owner][target] += 1.
   for (uint32_t k = c0; k < c1; ++k) {
     const uint32_t os = a.co_slot[k], ts = a.ct_slot[k];

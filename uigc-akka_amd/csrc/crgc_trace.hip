@@ -1290,10 +1290,10 @@ hipError_t launch_list(const DevGraph &g, int mode, bool scatter, uint32_t *buf,
 // without travels as its id.
 
 // Proxies homed at the shards in `mask` forget their home slots.
-__global__ __launch_bounds__(256) void k_phs_reset(DevGraph g, uint32_t mask) {
+__global__ __launch_bounds__(256) void k_phs_reset(DevGraph g, uint64_t mask) {
   const uint64_t top = g.ctr->slot_top, stride = (uint64_t)gridDim.x * 256;
   for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < top; v += stride)
-    if ((g.flags[v] & FL_PROXY) && ((mask >> shard_of(g.vid[v], g.n_shards)) & 1u)) g.phs[v] = PHS_NONE;
+    if ((g.flags[v] & FL_PROXY) && ((mask >> shard_of(g.vid[v], g.n_shards)) & 1ull)) g.phs[v] = PHS_NONE;
 }
 
 __device__ inline bool unresolved_proxy(const DevGraph &g, uint64_t v) {
@@ -1351,7 +1351,7 @@ __global__ __launch_bounds__(256) void k_phs_set(DevGraph g, const uint32_t *slo
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) g.phs[slots[i]] = ans[i];
 }
 
-hipError_t launch_resolve(const DevGraph &g, int step, uint32_t mask, uint64_t *send, uint32_t *slots,
+hipError_t launch_resolve(const DevGraph &g, int step, uint64_t mask, uint64_t *send, uint32_t *slots,
                           const uint64_t *ids, uint64_t n, uint32_t *ans, uint64_t slot_top, hipStream_t s) {
   const int vgrid = grid_for(slot_top, 256, 4096);
   switch (step) {

@@ -9,6 +9,7 @@
 #include "../../include/crgc.h"
 #include "crgc_internal.hpp"
 #include "crgc_transport.hpp"
+#include "crgc_xpost.hpp"
 
 namespace crgc {
 
@@ -64,41 +65,78 @@ int LocalTransport::alltoallv(uint32_t shard, const void *send, const size_t *so
 }
 
 // ---- RcclTransport -------------------------------------------------------------
+// Error discipline (crgc_xpost.hpp): every operation of an exchange is posted
+// and the group closed even after a failure, any failure aborts the
+// communicator (the peers' pending operations then fail instead of waiting),
+// and host waits poll the stream and the communicator's asynchronous error
+// under CRGC_RCCL_TIMEOUT_S (default 300 s).  An aborted transport refuses
+// every later call; the graph handles using it are poisoned by their callers.
 struct RcclTransport final : crgc_transport {
   ncclComm_t comm = nullptr;
   uint32_t rank = 0;
   int device = 0;
+  long timeout_s = 300;
   ~RcclTransport() override {
     if (comm) ncclCommDestroy(comm);
   }
+  void abort() {
+    if (comm) ncclCommAbort(comm);
+    comm = nullptr;
+  }
   bool accepts(uint32_t shard, int dev) const override { return shard == rank && dev == device; }
   int allgather(uint32_t, const void *send, void *recv, size_t bytes, hipStream_t s) override {
+    if (!comm) return CRGC_E_DEVICE;
     if (!bytes) return CRGC_OK;
-    return ncclAllGather(send, recv, bytes, ncclUint8, comm, s) == ncclSuccess ? CRGC_OK
-                                                                               : CRGC_E_DEVICE;
+    if (ncclAllGather(send, recv, bytes, ncclUint8, comm, s) == ncclSuccess) return CRGC_OK;
+    abort();
+    return CRGC_E_DEVICE;
   }
   int alltoallv(uint32_t, const void *send, const size_t *soff, const size_t *sbytes, void *recv,
                 const size_t *roff, const size_t *rbytes, hipStream_t s) override {
+    if (!comm) return CRGC_E_DEVICE;
     // own block: a device copy; peers: one grouped send/recv per direction
     if (rbytes[rank] &&
         hipMemcpyAsync((char *)recv + roff[rank], (const char *)send + soff[rank], rbytes[rank],
-                       hipMemcpyDeviceToDevice, s) != hipSuccess)
+                       hipMemcpyDeviceToDevice, s) != hipSuccess) {
+      abort();  // the peers' exchange with this rank is never posted: fail it for them
       return CRGC_E_DEVICE;
-    if (ncclGroupStart() != ncclSuccess) return CRGC_E_DEVICE;
-    // A failed send / recv still closes the group: a later collective must not
-    // run inside a dangling one.
-    bool ok = true;
-    for (uint32_t r = 0; r < n_shards && ok; ++r) {
-      if (r == rank) continue;
-      if (sbytes[r] && ncclSend((const char *)send + soff[r], sbytes[r], ncclUint8, (int)r, comm, s) !=
-                           ncclSuccess)
-        ok = false;
-      if (ok && rbytes[r] &&
-          ncclRecv((char *)recv + roff[r], rbytes[r], ncclUint8, (int)r, comm, s) != ncclSuccess)
-        ok = false;
     }
-    const bool closed = ncclGroupEnd() == ncclSuccess;
-    return ok && closed ? CRGC_OK : CRGC_E_DEVICE;
+    struct Ops {
+      RcclTransport *t;
+      const char *sbuf;
+      const size_t *soff, *sbytes;
+      char *rbuf;
+      const size_t *roff, *rbytes;
+      hipStream_t s;
+      bool group_start() { return ncclGroupStart() == ncclSuccess; }
+      bool send(uint32_t r) {
+        return ncclSend(sbuf + soff[r], sbytes[r], ncclUint8, (int)r, t->comm, s) == ncclSuccess;
+      }
+      bool recv(uint32_t r) {
+        return ncclRecv(rbuf + roff[r], rbytes[r], ncclUint8, (int)r, t->comm, s) == ncclSuccess;
+      }
+      bool group_end() { return ncclGroupEnd() == ncclSuccess; }
+      void abort() { t->abort(); }
+    } ops{this, (const char *)send, soff, sbytes, (char *)recv, roff, rbytes, s};
+    return post_alltoallv(ops, n_shards, rank, sbytes, rbytes);
+  }
+  int wait(hipStream_t s) override {
+    struct Q {
+      RcclTransport *t;
+      hipStream_t s;
+      int query() {
+        const hipError_t e = hipStreamQuery(s);
+        return e == hipSuccess ? 0 : (e == hipErrorNotReady ? 1 : -1);
+      }
+      bool async_error() {
+        if (!t->comm) return true;
+        ncclResult_t ae = ncclSuccess;
+        if (ncclCommGetAsyncError(t->comm, &ae) != ncclSuccess) return true;
+        return ae != ncclSuccess && ae != ncclInProgress;
+      }
+      void abort() { t->abort(); }
+    } q{this, s};
+    return poll_wait(q, std::chrono::seconds(timeout_s));
   }
 };
 
@@ -120,6 +158,7 @@ crgc_transport *make_rccl_transport(const uint8_t id[128], uint32_t n_shards, ui
   t->n_shards = n_shards;
   t->rank = shard;
   t->device = device;
+  if (const char *e = getenv("CRGC_RCCL_TIMEOUT_S")) t->timeout_s = std::max(1L, atol(e));
   int prev = 0;
   hipGetDevice(&prev);
   hipSetDevice(device);

@@ -34,6 +34,10 @@ struct crgc_transport {
   // for it into recv[roff[r] .. +rbytes[r]).  rbytes[r] must equal r's sbytes[me].
   virtual int alltoallv(uint32_t shard, const void *send, const size_t *soff, const size_t *sbytes,
                         void *recv, const size_t *roff, const size_t *rbytes, hipStream_t s) = 0;
+  // Host wait for the graph's stream.  RCCL: bounded, and ended early by the
+  // communicator's asynchronous error, so a failed or hung peer cannot block
+  // this rank forever (crgc_xpost.hpp).
+  virtual int wait(hipStream_t s) { return hipStreamSynchronize(s) == hipSuccess ? 0 : -3; }
 };
 
 namespace crgc {
