@@ -179,8 +179,54 @@ Caps caps_for(uint64_t live, uint64_t edges, uint64_t ids_pending, uint64_t atom
 
 }  // namespace
 
+// Tuning and test switches, read once when the handle is created (not per
+// call): the A/B variants and test hooks of DESIGN.md §4 / tests/.
+struct Knobs {
+  bool pull = true;              // CRGC_PULL=0: push only
+  uint64_t pull_div = 16;        // CRGC_PULL_DIV: pull after a frontier of >= slots / div
+  uint32_t pull_cur_div = 4;     // CRGC_PULL_CUR_DIV
+  uint32_t alpha = 0;            // CRGC_ALPHA: Beamer's rule (off by default)
+  bool has_pull_thresh = false;  // CRGC_PULL_THRESH: absolute threshold (test hook)
+  uint64_t pull_thresh = 0;
+  bool has_sparse = false;       // CRGC_SPARSE_THRESH (test hook)
+  uint32_t sparse_thresh = 0;
+  bool tail = true;              // CRGC_TAIL=0: no narrow-frontier takeover
+  uint32_t tail_start = 8192;    // CRGC_TAIL_START
+  uint32_t tail_max = 32768;     // CRGC_TAIL_MAX
+  uint32_t chain_after = 64;     // CRGC_CHAIN_AFTER
+  int kernel_timing = 1;         // CRGC_KERNEL_TIMING: 0 chunks, 1 k_expand, 2 all level kernels
+  bool level_log = false;        // CRGC_LEVEL_LOG
+  int xbits = 1;                 // CRGC_XBITS: sharded mark form (0 ids, 1 cheaper, 2 bitmaps)
+  int buckets_log2 = 0;          // CRGC_BUCKETS_LOG2: edge-pipeline buckets (test hook; 0 = by size)
+  void read() {
+    auto env = [](const char *k) { return getenv(k); };
+    if (const char *m = env("CRGC_PULL")) pull = atoi(m) != 0;
+    if (const char *m = env("CRGC_PULL_DIV")) pull_div = std::max<uint64_t>(1, strtoull(m, nullptr, 10));
+    if (const char *m = env("CRGC_PULL_CUR_DIV")) pull_cur_div = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_ALPHA")) alpha = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_PULL_THRESH")) {
+      has_pull_thresh = true;
+      pull_thresh = strtoull(m, nullptr, 10);
+    }
+    if (const char *m = env("CRGC_SPARSE_THRESH")) {
+      has_sparse = true;
+      sparse_thresh = (uint32_t)strtoul(m, nullptr, 10);
+    }
+    if (const char *m = env("CRGC_TAIL")) tail = atoi(m) != 0;
+    if (const char *m = env("CRGC_TAIL_START")) tail_start = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_TAIL_MAX")) tail_max = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_CHAIN_AFTER")) chain_after = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_KERNEL_TIMING")) kernel_timing = atoi(m);
+    level_log = env("CRGC_LEVEL_LOG") != nullptr;
+    if (const char *m = env("CRGC_XBITS")) xbits = atoi(m);
+    if (const char *m = env("CRGC_BUCKETS_LOG2"))
+      buckets_log2 = std::min(10, std::max(1, atoi(m)));
+  }
+};
+
 struct crgc_graph {
   int device = 0;
+  Knobs knobs;
   hipStream_t stream = nullptr;
   bool own_stream = false;
   uint32_t F = 4, DGS = 64;
@@ -195,6 +241,11 @@ struct crgc_graph {
   uint64_t inserted_at_trace = 0;  // Counters::inserted when `live` was exact
   Scratch stage, work;
   hipEvent_t ev[4] = {};
+  // The edge pipeline of a merge runs on `side` beside the vertex updates on
+  // `stream` (they touch disjoint arrays); fork / join events order them.
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  bool use_side = true;  // CRGC_SIDE_STREAM=0 (read at create): one stream
   // last trace
   uint64_t last_garbage = 0, last_kill = 0, last_live = 0;
   crgc_trace_stats last_stats{};
@@ -449,6 +500,7 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
   h->device = cfg ? cfg->device : 0;
   h->F = (cfg && cfg->entry_field_size) ? cfg->entry_field_size : 4;
   h->DGS = (cfg && cfg->delta_graph_size) ? cfg->delta_graph_size : 64;
+  h->knobs.read();
   // A transport makes the handle a shard (a transport with n_shards == 1 runs
   // the sharded protocol on one shard: a self-check of the transport).
   if (cfg && (cfg->n_shards > 1 || cfg->transport)) {
@@ -477,6 +529,11 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     }
     for (auto &e : h->ev)
       if (hipEventCreate(&e) != hipSuccess) rc = CRGC_E_DEVICE;
+    if (const char *m = getenv("CRGC_SIDE_STREAM")) h->use_side = atoi(m) != 0;
+    if (hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess)
+      rc = CRGC_E_DEVICE;
     if (rc) break;
     if (hipMalloc(&h->ctr, sizeof(Counters)) != hipSuccess ||
         hipHostMalloc(&h->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess ||
@@ -521,6 +578,12 @@ void crgc_destroy(crgc_graph *h) {
   if (h->h_small) hipHostFree(h->h_small);
   if (h->h_route) hipHostFree(h->h_route);
   if (h->roots_buf) hipFree(h->roots_buf);
+  if (h->side) {
+    hipStreamSynchronize(h->side);
+    hipStreamDestroy(h->side);
+  }
+  if (h->ev_fork) hipEventDestroy(h->ev_fork);
+  if (h->ev_join) hipEventDestroy(h->ev_join);
   for (auto &e : h->ev)
     if (e) hipEventDestroy(e);
   for (auto &e : h->lvl_ev) hipEventDestroy(e);
@@ -541,7 +604,7 @@ static void edge_geometry(const crgc_graph *h, uint64_t max_atoms, uint32_t &bsh
   // workgroups: the C2 merge 20-30 us slower, profiles/r2p/ab_buckets.txt)
   uint32_t lk = lg > 18 ? 9u : (lg > 9 ? lg - 8 : 1u);
   // test hook: fewer buckets, so buckets take several rounds of atoms
-  if (const char *m = getenv("CRGC_BUCKETS_LOG2")) lk = std::min<uint32_t>(10, std::max<uint32_t>(1, (uint32_t)atoi(m)));
+  if (h->knobs.buckets_log2) lk = (uint32_t)h->knobs.buckets_log2;
   bshift = 32 - lk;
   nbk = 1u << lk;
   nblk = std::min<uint64_t>((max_atoms + 1023) / 1024, 512);
@@ -560,9 +623,10 @@ static size_t edge_scratch(const crgc_graph *h, uint64_t max_atoms) {
 }
 
 static int run_edges(crgc_graph *h, uint32_t *ao, uint32_t *at, int32_t *ad, uint64_t max_atoms,
-                     Carver &cv, const uint64_t *n_atoms_dev = nullptr) {
+                     Carver &cv, const uint64_t *n_atoms_dev = nullptr, hipStream_t s = nullptr) {
   if (max_atoms == 0) return CRGC_OK;
   EdgeArgs ea{};
+  ea.err = &h->g.d.ctr->err;
   ea.max_atoms = max_atoms;
   ea.n_atoms_dev = n_atoms_dev;
   ea.atom_o = ao;
@@ -579,9 +643,34 @@ static int run_edges(crgc_graph *h, uint32_t *ao, uint32_t *at, int32_t *ad, uin
   ea.rv_t = cv.take<uint32_t>(max_atoms);
   ea.rv_o = cv.take<uint32_t>(max_atoms);
   ea.rv_b = cv.take<uint32_t>(max_atoms);
-  HIP_TRY(launch_edges(h->g.d, ea, h->stream));
+  HIP_TRY(launch_edges(h->g.d, ea, s ? s : h->stream));
   return CRGC_OK;
 }
+
+// The edge pipeline on the side stream, forked from the graph's stream after
+// the atoms are written and joined before the merge returns (on every path).
+struct SideFork {
+  crgc_graph *h;
+  bool forked = false;
+  explicit SideFork(crgc_graph *g) : h(g) {}
+  hipError_t fork() {
+    if (!h->use_side) return hipSuccess;
+    hipError_t e = hipEventRecord(h->ev_fork, h->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(h->side, h->ev_fork, 0);
+    forked = e == hipSuccess;
+    return e;
+  }
+  hipStream_t stream() const { return forked ? h->side : h->stream; }
+  hipError_t join() {
+    if (!forked) return hipSuccess;
+    forked = false;
+    hipError_t e = hipEventRecord(h->ev_join, h->side);
+    if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, h->ev_join, 0);
+    if (e != hipSuccess) hipStreamSynchronize(h->side);  // never leave the side stream unordered
+    return e;
+  }
+  ~SideFork() { join(); }
+};
 
 }  // extern "C"
 
@@ -818,10 +907,16 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   a.atom_t = wc.take<uint32_t>(max_atoms);
   a.atom_d = wc.take<int32_t>(max_atoms);
   a.n_atoms = wc.take<uint64_t>(1);
-  // atoms of entries refused for bad offsets stay zero (never applied)
-  hipMemsetAsync(a.atom_d, 0, max_atoms * 4, h->stream);
-  HIP_TRY(launch_entries(h->g.d, a, h->stream));
-  if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, max_atoms, wc, a.n_atoms)) return rc;
+  // a batch refused for its offsets writes no atoms and the edge pipeline
+  // skips it (EdgeArgs::err), so the atom arrays need no clearing
+  HIP_TRY(launch_entries(h->g.d, a, h->stream, 0));
+  {
+    SideFork sf(h);
+    HIP_TRY(sf.fork());
+    if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, max_atoms, wc, a.n_atoms, sf.stream())) return rc;
+    HIP_TRY(launch_entries(h->g.d, a, h->stream, 1));
+    HIP_TRY(sf.join());
+  }
   note_merge(h, ids, C + U);
   HIP_TRY(staged.wait());
   return CRGC_OK;
@@ -1077,6 +1172,7 @@ static int merge_deltas_one(crgc_graph *h, const crgc_delta_batch *b, uint64_t n
   Staged staged(h, b->memory);
   DeltaArgs a{};
   a.n = n;
+  a.nout = nout;
   a.epoch = ++h->epoch;
   a.id = stage(h, sc, b->id, n, b->memory);
   a.recv = stage(h, sc, b->recv_count, n, b->memory);
@@ -1093,8 +1189,14 @@ static int merge_deltas_one(crgc_graph *h, const crgc_delta_batch *b, uint64_t n
   a.atom_o = wc.take<uint32_t>(std::max<uint64_t>(nout, 1));
   a.atom_t = wc.take<uint32_t>(std::max<uint64_t>(nout, 1));
   a.atom_d = wc.take<int32_t>(std::max<uint64_t>(nout, 1));
-  HIP_TRY(launch_deltas(h->g.d, a, nout, h->stream));
-  if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, nout, wc)) return rc;
+  HIP_TRY(launch_deltas(h->g.d, a, nout, h->stream, 0));
+  {
+    SideFork sf(h);
+    HIP_TRY(sf.fork());
+    if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, nout, wc, nullptr, sf.stream())) return rc;
+    HIP_TRY(launch_deltas(h->g.d, a, nout, h->stream, 1));
+    HIP_TRY(sf.join());
+  }
   note_merge(h, ids, nout);
   HIP_TRY(staged.wait());
   return CRGC_OK;
@@ -1320,56 +1422,41 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   // sequential pull walk, plain candidate stores, default-policy edge stream,
   // always-on marked-word filter) were removed; their records stay in
   // profiles/r1h, r1n, r1r.
+  const Knobs &kn = h->knobs;
   la.flags = 0;
   la.sparse_thresh = (uint32_t)std::max<uint64_t>(64, (top / BLK_SLOTS) / 4);
   // Direction optimisation: dense levels after a frontier of >= top/div shadows pull.
-  uint64_t pull_div = 16;
-  la.flags |= LV_PULL;
-  if (const char *m = getenv("CRGC_PULL")) {
-    if (!atoi(m)) la.flags &= ~LV_PULL;
-  }
-  if (const char *m = getenv("CRGC_PULL_DIV")) pull_div = std::max<uint64_t>(1, strtoull(m, nullptr, 10));
-  la.pull_div = (uint32_t)pull_div;  // against the exact slot count, on the device
-  la.pull_cur_div = 4;
-  if (const char *m = getenv("CRGC_PULL_CUR_DIV")) la.pull_cur_div = (uint32_t)strtoul(m, nullptr, 10);
+  if (kn.pull) la.flags |= LV_PULL;
+  la.pull_div = (uint32_t)kn.pull_div;  // against the exact slot count, on the device
+  la.pull_cur_div = kn.pull_cur_div;
   // Beamer's direction rule (CRGC_ALPHA=a: pull when a * m_f > m_u, level 0
   // included; m_u from the edge keys the graph holds, an upper bound).  Off by
   // default: on the C2 wakeup (10 % pseudo-roots) alpha = 14 pulls at level 0
   // and the mark takes 1.27 ms against 0.89 ms with the frontier-size rule
   // (k_expand level 0: 670 us pull vs 306 us push; profiles/r2b/ab.json) — a
   // pull over a 7.6 % frontier walks long in-candidate lists before a hit.
-  la.alpha = 0;
-  if (const char *m = getenv("CRGC_ALPHA")) la.alpha = (uint32_t)strtoul(m, nullptr, 10);
+  la.alpha = kn.alpha;
   la.e_total = h->etab_used + h->atoms_since;
   la.pull_thresh = 0;
   // Test hooks: absolute thresholds (0 disables sparse levels entirely).
-  if (const char *m = getenv("CRGC_PULL_THRESH")) {
-    la.pull_thresh = strtoull(m, nullptr, 10);
+  if (kn.has_pull_thresh) {
+    la.pull_thresh = kn.pull_thresh;
     la.pull_div = 0;
   }
-  if (const char *m = getenv("CRGC_SPARSE_THRESH")) la.sparse_thresh = (uint32_t)strtoul(m, nullptr, 10);
+  if (kn.has_sparse) la.sparse_thresh = kn.sparse_thresh;
   // Narrow frontiers: one workgroup finishes the mark (k_tail).
-  la.flags |= LV_TAIL;
-  la.tail_start = 8192;
-  la.tail_max = 32768;
-  if (const char *m = getenv("CRGC_TAIL")) {
-    if (!atoi(m)) la.flags &= ~LV_TAIL;
-  }
-  if (const char *m = getenv("CRGC_TAIL_START")) la.tail_start = (uint32_t)strtoul(m, nullptr, 10);
+  if (kn.tail) la.flags |= LV_TAIL;
   // Deep marks: a k_tail walk of chain_after links hands the rest to chain mode
   // (pointer jumping, crgc_chain.hip).  Unsharded graphs only.
-  la.chain_after = h->tp ? 0 : 64;
-  if (const char *m = getenv("CRGC_CHAIN_AFTER")) la.chain_after = h->tp ? 0 : (uint32_t)strtoul(m, nullptr, 10);
-  if (const char *m = getenv("CRGC_TAIL_MAX")) la.tail_max = (uint32_t)strtoul(m, nullptr, 10);
-  la.tail_start = std::min<uint32_t>(la.tail_start, TAIL_QCAP);
-  la.tail_max = std::min<uint32_t>(std::max(la.tail_max, 1u), TAIL_QCAP);
+  la.chain_after = h->tp ? 0 : kn.chain_after;
+  la.tail_start = std::min<uint32_t>(kn.tail_start, TAIL_QCAP);
+  la.tail_max = std::min<uint32_t>(std::max(kn.tail_max, 1u), TAIL_QCAP);
   // Device times, from timing-only events (no system-scope fence):
   //   every chunk of levels: an event pair around it (ms_mark, dispatch gaps included);
   //   CRGC_KERNEL_TIMING=1 (default): k_expand's start / stop carried by its dispatch;
   //   CRGC_KERNEL_TIMING=2: all three level kernels (each timed dispatch costs a few us);
   //   CRGC_KERNEL_TIMING=0: chunks only.
-  const char *kt = getenv("CRGC_KERNEL_TIMING");
-  const int timing = kt ? atoi(kt) : 1;
+  const int timing = kn.kernel_timing;
   auto new_event = [&](std::vector<hipEvent_t> &v, size_t n) -> hipError_t {
     while (v.size() < n) {
       hipEvent_t e;
@@ -1404,7 +1491,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   int chunk = roots && h->last_levels ? (int)std::min<uint64_t>(h->last_levels, 512) : 4;
   std::vector<unsigned long long> ring(LEVEL_RING);
   unsigned long long tail[3] = {0, 0, 0};
-  const bool log = getenv("CRGC_LEVEL_LOG") != nullptr;
+  const bool log = kn.level_log;
   // Bounds on the host loop: every pass either reaches an
   // empty level, finishes in k_tail / chain mode, or moves L forward (a bail
   // must resume past the level it bailed from before); levels are bounded by
@@ -1572,8 +1659,7 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
   *rounds = 1;
   if (!h->tp) return CRGC_OK;
   const uint32_t G = h->G, me = h->shard;
-  int xmode = 1;
-  if (const char *m = getenv("CRGC_XBITS")) xmode = atoi(m);
+  const int xmode = h->knobs.xbits;
   {
     const auto t0 = std::chrono::steady_clock::now();
     if (int rc = resolve_home_slots(h, top, xmode, x_bytes)) return rc;

@@ -83,6 +83,9 @@ __device__ inline bool ep_atom(const EdgeArgs &a, uint64_t i, uint64_t n, uint32
 template <bool REV>
 __device__ inline uint64_t ep_count(const EdgeArgs &a) {
   if (REV) return a.tot[0];
+  // a batch refused for its offsets (or > F records) left unwritten atoms:
+  // nothing of it is applied (the handle is poisoned by that error anyway)
+  if (a.err && (*a.err & (ERR_BAD_OFFSETS | ERR_TOO_MANY))) return 0;
   return a.n_atoms_dev ? *a.n_atoms_dev : a.max_atoms;
 }
 

@@ -102,7 +102,7 @@ struct EntryArgs {
 };
 
 struct DeltaArgs {
-  uint64_t n;
+  uint64_t n, nout;
   unsigned long long epoch;
   const uint64_t *id;
   const int32_t *recv;
@@ -136,6 +136,7 @@ struct UndoArgs {
 };
 
 struct EdgeArgs {
+  const unsigned long long *err;  // the graph's error word: a batch refused for its offsets has no atoms
   uint64_t max_atoms;          // grid bound
   const uint64_t *n_atoms_dev; // exact count on device (or null: use max_atoms)
   const uint32_t *atom_o;
@@ -189,8 +190,9 @@ hipError_t launch_chain(const DevGraph &g, const ChainArgs &ca, int step, const 
                         uint64_t top, uint32_t fi, int first, uint32_t rounds, hipStream_t s);
 
 // ---- launchers (return hipError_t of the launch) ---------------------------
-hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s);
-hipError_t launch_deltas(const DevGraph &g, const DeltaArgs &a, uint64_t n_out, hipStream_t s);
+// phase 0: ids and edge atoms (the edge pipeline may start behind it); 1: vertex updates
+hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s, int phase);
+hipError_t launch_deltas(const DevGraph &g, const DeltaArgs &a, uint64_t n_out, hipStream_t s, int phase);
 hipError_t launch_undo_check(const DevGraph &g, const UndoArgs &a, hipStream_t s);
 hipError_t launch_undo_apply(const DevGraph &g, const UndoArgs &a, uint64_t slot_top,
                              hipStream_t s);

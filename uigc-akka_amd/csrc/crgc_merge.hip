@@ -26,6 +26,19 @@ __device__ inline bool vs(uint32_t s) { return s < 0xFFFFFFF0u; }
 // reference's `from` order.
 // ---------------------------------------------------------------------------
 constexpr int IDS_THREADS = 1024;
+constexpr int IDS_K = 4;  // ids per thread per round: their first-bucket loads are in flight together
+
+// Continues a probe whose first bucket `b` (at h) was already loaded.
+__device__ inline int id_probe_from(const DevGraph &g, uint64_t id, uint64_t h, uint4 b, uint64_t &bucket,
+                                    uint32_t &slot) {
+  const uint64_t k = bucket_key(b);
+  if (k == id && b.z != VAL_PENDING) {  // the common case: an existing shadow, one load
+    bucket = h;
+    slot = b.z;
+    return RS_FOUND;
+  }
+  return id_probe(g, id, bucket, slot);
+}
 
 __global__ __launch_bounds__(IDS_THREADS) void k_ids(DevGraph g, IdArgs a) {
   uint64_t cnt[5], total = 0;
@@ -34,36 +47,67 @@ __global__ __launch_bounds__(IDS_THREADS) void k_ids(DevGraph g, IdArgs a) {
     if (cnt[k] > a.seg[k].n) cnt[k] = a.seg[k].n;  // bad offsets: flagged by the apply kernel
     total += cnt[k];
   }
-  const uint64_t stride = (uint64_t)gridDim.x * IDS_THREADS;
-  for (uint64_t base = (uint64_t)blockIdx.x * IDS_THREADS; base < total; base += stride) {
-    uint64_t r = base + threadIdx.x;
-    int k = 0;
-    bool has = r < total;
-    if (has)
-      while (r >= cnt[k]) r -= cnt[k++];
-    const IdSeg &sg = a.seg[has ? k : 0];
-    uint64_t id = has ? sg.ids[r] : 0;
-    if (has && id == CRGC_NO_ACTOR && sg.none_ok) has = false;
-    else if (has && reserved_id(id)) {
-      set_err(g.ctr, ERR_RESERVED_ID);
-      has = false;
+  const uint64_t per = (uint64_t)IDS_THREADS * IDS_K;
+  const uint64_t stride = (uint64_t)gridDim.x * per;
+  for (uint64_t base = (uint64_t)blockIdx.x * per; base < total; base += stride) {
+    uint64_t id[IDS_K], h[IDS_K], bucket[IDS_K], r[IDS_K];
+    uint32_t slot[IDS_K];
+    int kseg[IDS_K], st[IDS_K];
+    bool has[IDS_K], in[IDS_K];
+    uint4 b0[IDS_K];
+#pragma unroll
+    for (int j = 0; j < IDS_K; ++j) {
+      r[j] = base + (uint64_t)j * IDS_THREADS + threadIdx.x;
+      in[j] = r[j] < total;
+      int k = 0;
+      if (in[j])
+        while (r[j] >= cnt[k]) r[j] -= cnt[k++];
+      kseg[j] = in[j] ? k : 0;
+      id[j] = in[j] ? a.seg[kseg[j]].ids[r[j]] : 0;
     }
-    if (has && g.n_shards > 1 && !is_home(g, id)) {
-      // not home here: resolve only as the far end of a local edge / supervisor
-      bool want = false;
-      if (sg.partner) {
-        const uint64_t p = sg.partner[r];
-        want = p != CRGC_NO_ACTOR && is_home(g, p);
+#pragma unroll
+    for (int j = 0; j < IDS_K; ++j) {
+      const IdSeg &sg = a.seg[kseg[j]];
+      has[j] = in[j];
+      if (has[j] && id[j] == CRGC_NO_ACTOR && sg.none_ok) has[j] = false;
+      else if (has[j] && reserved_id(id[j])) {
+        set_err(g.ctr, ERR_RESERVED_ID);
+        has[j] = false;
       }
-      if (!want && sg.need) want = sg.need[r] != 0;
-      has = want;
+      if (has[j] && g.n_shards > 1 && !is_home(g, id[j])) {
+        // not home here: resolve only as the far end of a local edge / supervisor
+        bool want = false;
+        if (sg.partner) {
+          const uint64_t p = sg.partner[r[j]];
+          want = p != CRGC_NO_ACTOR && is_home(g, p);
+        }
+        if (!want && sg.need) want = sg.need[r[j]] != 0;
+        has[j] = want;
+      }
+      h[j] = mix64(id[j]) & g.hmask;
+      b0[j] = has[j] ? load_bucket(&g.htab[h[j]]) : make_uint4(0, 0, 0, 0);
     }
-    uint64_t bucket = 0;
-    uint32_t slot = SLOT_INVALID;
-    int st = RS_NONE;
-    if (has) st = id_probe(g, id, bucket, slot);
-    slot = id_settle_block(g, id, bucket, slot, st);
-    if (base + threadIdx.x < total) sg.slots[r] = slot;
+    bool settle = false;
+#pragma unroll
+    for (int j = 0; j < IDS_K; ++j) {
+      bucket[j] = 0;
+      slot[j] = SLOT_INVALID;
+      st[j] = has[j] ? id_probe_from(g, id[j], h[j], b0[j], bucket[j], slot[j]) : RS_NONE;
+      settle |= st[j] == RS_INSERTED || st[j] == RS_PENDING;
+    }
+    // Slot allocation (one atomic per workgroup) only in rounds that created or
+    // wait for a shadow: a steady-state wakeup mostly finds existing ones.
+    if (__syncthreads_or(settle)) {
+#pragma unroll
+      for (int j = 0; j < IDS_K; ++j) slot[j] = id_settle_block(g, id[j], bucket[j], slot[j], st[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < IDS_K; ++j)
+        if (st[j] == RS_NONE) slot[j] = SLOT_INVALID;
+    }
+#pragma unroll
+    for (int j = 0; j < IDS_K; ++j)
+      if (in[j]) a.seg[kseg[j]].slots[r[j]] = slot[j];
   }
 }
 
@@ -71,40 +115,80 @@ hipError_t launch_ids(const DevGraph &g, const IdArgs &a, hipStream_t s) {
   uint64_t n = 0;
   for (int k = 0; k < a.nseg; ++k) n += a.seg[k].n;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ids, dim3(grid_for(n, IDS_THREADS, 1024)), dim3(IDS_THREADS), 0, s, g, a);
+  hipLaunchKernelGGL(k_ids, dim3(grid_for((n + IDS_K - 1) / IDS_K, IDS_THREADS, 1024)), dim3(IDS_THREADS), 0, s, g, a);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
 // Entries — ShadowGraph.mergeEntry, ShadowGraph.java:75-125.  One thread per
-// entry over slots resolved by k_ids: receive counts, the LWW tags, and the
-// edge atoms.
+// entry over slots resolved by k_ids, in two kernels so the edge pipeline can
+// start as soon as its atoms exist (it runs on a side stream beside the
+// vertex updates, crgc_api.hip merge_entries_one):
+//   k_entries_atoms   validation, the edge atoms, their exact count
+//   k_entries_vertex  receive counts and the LWW tags (vertex state only)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_entries_apply(DevGraph g, EntryArgs a) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.n) return;
+// An entry's offsets are well formed (:85-123 read at most F records of each
+// kind); a batch whose final offsets exceed n*F, or do not start at 0, is
+// refused whole, so the atoms [0, C + U) are exactly the valid entries' atoms.
+__device__ inline bool entry_ok(const EntryArgs &a, uint64_t i, bool report, Counters *c) {
   const uint32_t c0 = a.c_off[i], c1 = a.c_off[i + 1];
   const uint32_t s0 = a.s_off[i], s1 = a.s_off[i + 1];
   const uint32_t u0 = a.u_off[i], u1 = a.u_off[i + 1];
   const uint64_t cmax = a.n * a.F;
-  // the totals place the updated atoms after the created ones: a batch whose
-  // final offsets exceed n*F is refused whole, so no atom lands past 2nF
-  const uint32_t ctot = a.c_off[a.n];
-  bool ok = true;
-  if (c1 < c0 || s1 < s0 || u1 < u0 || c1 > cmax || s1 > cmax || u1 > cmax || ctot > cmax ||
-      a.u_off[a.n] > cmax) {
-    set_err(g.ctr, ERR_BAD_OFFSETS);
-    ok = false;
-  } else if (c1 - c0 > a.F || s1 - s0 > a.F || u1 - u0 > a.F) {
-    set_err(g.ctr, ERR_TOO_MANY);
-    ok = false;
+  if (c1 < c0 || s1 < s0 || u1 < u0 || c1 > cmax || s1 > cmax || u1 > cmax || a.c_off[a.n] > cmax ||
+      a.u_off[a.n] > cmax || a.c_off[0] || a.s_off[0] || a.u_off[0]) {
+    if (report) set_err(c, ERR_BAD_OFFSETS);
+    return false;
   }
-  const uint32_t me = ok ? a.self_slot[i] : SLOT_INVALID;
-  if (!ok) a.self_slot[i] = SLOT_INVALID;
+  if (c1 - c0 > a.F || s1 - s0 > a.F || u1 - u0 > a.F) {
+    if (report) set_err(c, ERR_TOO_MANY);
+    return false;
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_entries_atoms(DevGraph g, EntryArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const bool ok = entry_ok(a, i, true, g.ctr);
   if (i == 0 && a.n_atoms) {  // atoms [0, C) created, [C, C + U) updated: the edge pipeline's exact count
+    const uint64_t cmax = a.n * a.F;
     const uint64_t C = min((uint64_t)a.c_off[a.n], cmax), U = min((uint64_t)a.u_off[a.n], cmax);
     *a.n_atoms = C + U;
   }
+  if (!ok) {
+    a.self_slot[i] = SLOT_INVALID;
+    return;
+  }
+  const uint32_t me = a.self_slot[i];
+  const bool sh = g.n_shards > 1;
+  const bool self_home = !sh || is_home(g, a.self[i]);
+  // Created refs (:85-93): outgoing[owner][target] += 1.
+  const uint32_t c0 = a.c_off[i], c1 = a.c_off[i + 1];
+  for (uint32_t k = c0; k < c1; ++k) {
+    const uint32_t os = a.co_slot[k], ts = a.ct_slot[k];
+    a.atom_o[k] = os;
+    a.atom_t[k] = ts;
+    a.atom_d[k] = ((sh || vs(me)) && vs(os) && vs(ts)) ? 1 : 0;
+  }
+  // Deactivated refs (:120-122): outgoing[self][target] -= 1.
+  const uint32_t ctot = a.c_off[a.n];
+  const uint32_t u0 = a.u_off[i], u1 = a.u_off[i + 1];
+  for (uint32_t k = u0; k < u1; ++k) {
+    const uint32_t ts = a.u_slot[k];
+    const uint64_t at = (uint64_t)ctot + k;
+    a.atom_o[at] = me;
+    a.atom_t[at] = ts;
+    a.atom_d[at] = (vs(ts) && vs(me) && self_home && refob_deactivated(a.u_info[k])) ? -1 : 0;
+  }
+}
+
+// Receive counts and last-write-wins tags; the winners write in k_entries_lww.
+__global__ __launch_bounds__(256) void k_entries_vertex(DevGraph g, EntryArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  if (!entry_ok(a, i, false, g.ctr)) return;  // reported (and self_slot cleared) by k_entries_atoms
+  const uint32_t me = a.self_slot[i];
   const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
   const int16_t rc = a.recv[i];
   // Sharded graphs: every record is applied by the home shard of the shadow
@@ -118,33 +202,21 @@ __global__ __launch_bounds__(256) void k_entries_apply(DevGraph g, EntryArgs a) 
     if (rc != 0) atomicAdd(&g.recv[me], (int32_t)rc);
     atomicMax(&g.vseq[me], tag);
   }
-  if (!ok) return;
-  // Created refs (:85-93): outgoing[owner][target] += 1.
-  for (uint32_t k = c0; k < c1; ++k) {
-    const uint32_t os = a.co_slot[k], ts = a.ct_slot[k];
-    a.atom_o[k] = os;
-    a.atom_t[k] = ts;
-    a.atom_d[k] = ((sh || vs(me)) && vs(os) && vs(ts)) ? 1 : 0;
-  }
   // Spawned actors (:96-104): child.supervisor = self, last write wins.
+  const uint32_t s0 = a.s_off[i], s1 = a.s_off[i + 1];
   for (uint32_t k = s0; k < s1; ++k) {
     const uint32_t cs = a.spawn_slot[k];
     const bool good = vs(cs) && vs(me);
     if (!good) a.spawn_slot[k] = SLOT_INVALID;
     if (good) atomicMax(&g.sseq[cs], tag);
   }
-  // Updated refs (:107-123): target.recv -= count; deactivation -> -1 edge.
+  // Updated refs (:107-119): target.recv -= count.
+  const uint32_t u0 = a.u_off[i], u1 = a.u_off[i + 1];
   for (uint32_t k = u0; k < u1; ++k) {
     const uint32_t ts = a.u_slot[k];
-    const int16_t info = a.u_info[k];
-    const bool good = vs(ts) && vs(me);
-    const int32_t cnt = refob_count(info);
-    const bool tgt_ok = sh ? (vs(ts) && is_home(g, a.u_ref[k])) : good;
+    const int32_t cnt = refob_count(a.u_info[k]);
+    const bool tgt_ok = sh ? (vs(ts) && is_home(g, a.u_ref[k])) : (vs(ts) && vs(me));
     if (tgt_ok && cnt > 0) atomicAdd(&g.recv[ts], -cnt);
-    const uint64_t at = (uint64_t)ctot + k;
-    a.atom_o[at] = me;
-    a.atom_t[at] = ts;
-    a.atom_d[at] = (good && self_home && refob_deactivated(info)) ? -1 : 0;
   }
 }
 
@@ -187,11 +259,18 @@ __global__ __launch_bounds__(256) void k_entries_shard_prep(DevGraph g, EntryArg
     a.u_partner[k] = refob_deactivated(a.u_info[k]) ? self : CRGC_NO_ACTOR;
 }
 
-hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s) {
+// phase 0: (sharded prep) ids, atoms — the edge pipeline may start after it;
+// phase 1: vertex updates, LWW winners.
+hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s, int phase) {
   if (a.n == 0) return hipSuccess;
   const uint64_t nf = a.n * a.F;
   const int blocks = (int)((a.n + 255) / 256);
   const bool sh = g.n_shards > 1;
+  if (phase == 1) {
+    hipLaunchKernelGGL(k_entries_vertex, dim3(blocks), dim3(256), 0, s, g, a);
+    hipLaunchKernelGGL(k_entries_lww, dim3(blocks), dim3(256), 0, s, g, a);
+    return hipGetLastError();
+  }
   if (sh) hipLaunchKernelGGL(k_entries_shard_prep, dim3(blocks), dim3(256), 0, s, g, a);
   IdArgs ia{};
   ia.nseg = 5;
@@ -202,8 +281,7 @@ hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s) 
   ia.seg[4] = IdSeg{a.u_ref, a.u_slot, nf, a.u_off + a.n, false, sh ? a.u_partner : nullptr,
                     nullptr};
   if (hipError_t e = launch_ids(g, ia, s)) return e;
-  hipLaunchKernelGGL(k_entries_apply, dim3(blocks), dim3(256), 0, s, g, a);
-  hipLaunchKernelGGL(k_entries_lww, dim3(blocks), dim3(256), 0, s, g, a);
+  hipLaunchKernelGGL(k_entries_atoms, dim3(blocks), dim3(256), 0, s, g, a);
   return hipGetLastError();
 }
 
@@ -217,7 +295,9 @@ __global__ __launch_bounds__(256) void k_deltas_apply(DevGraph g, DeltaArgs a) {
   if (i >= a.n) return;
   const uint32_t o0 = a.out_off[i], o1 = a.out_off[i + 1];
   bool ok = true;
-  if (o1 < o0) {
+  // the atoms [0, nout) are exactly the valid shadows' outgoing entries: a
+  // batch whose offsets do not start at 0 or run past nout is refused whole
+  if (o1 < o0 || o1 > a.nout || a.out_off[0] || a.out_off[a.n] != a.nout) {
     set_err(g.ctr, ERR_BAD_OFFSETS);
     ok = false;
   }
@@ -269,9 +349,15 @@ __global__ __launch_bounds__(256) void k_deltas_shard_prep(DeltaArgs a, uint64_t
   for (uint32_t k = o0; k < o1; ++k) a.o_partner[k] = a.id[i];
 }
 
-hipError_t launch_deltas(const DevGraph &g, const DeltaArgs &a, uint64_t n_out, hipStream_t s) {
+// phase 0: (sharded prep) ids, apply — the edge pipeline may start after it;
+// phase 1: LWW winners.
+hipError_t launch_deltas(const DevGraph &g, const DeltaArgs &a, uint64_t n_out, hipStream_t s, int phase) {
   if (a.n == 0) return hipSuccess;
   const int blocks = (int)((a.n + 255) / 256);
+  if (phase == 1) {
+    hipLaunchKernelGGL(k_deltas_lww, dim3(blocks), dim3(256), 0, s, g, a);
+    return hipGetLastError();
+  }
   const bool sh = g.n_shards > 1;
   if (sh && n_out)
     hipLaunchKernelGGL(k_deltas_shard_prep, dim3(blocks), dim3(256), 0, s, a, n_out);
@@ -285,7 +371,6 @@ hipError_t launch_deltas(const DevGraph &g, const DeltaArgs &a, uint64_t n_out, 
                     sh ? a.o_partner : nullptr, nullptr};
   if (hipError_t e = launch_ids(g, ia, s)) return e;
   hipLaunchKernelGGL(k_deltas_apply, dim3(blocks), dim3(256), 0, s, g, a);
-  hipLaunchKernelGGL(k_deltas_lww, dim3(blocks), dim3(256), 0, s, g, a);
   return hipGetLastError();
 }
 
