@@ -333,3 +333,52 @@ def test_forty_shards_rebuild_homes_above_32(sharded, oracle_mod):
             assert rh.rounds >= 2
         fz.sync(o.export())
     assert h.export() == o.export()
+
+
+@pytest.mark.parametrize("G,seed", [(2, 31), (3, 32), (8, 33)])
+def test_fuzz_sharded_closure(sharded, oracle_mod, G, seed, monkeypatch):
+    """The replicated chain closure (crgc_xchain.hip) forced from the first
+    round of every mark (it normally takes over deep, narrow marks after 8
+    rounds): branching shadows, halted shadows (undo logs), proxies of
+    collected actors, supervisors across shards, investigate mode."""
+    monkeypatch.setenv("CRGC_XCLOSURE_AFTER", "1")
+    monkeypatch.setenv("CRGC_XCLOSURE_NARROW", "0")
+    h, o = sharded(G), oracle_mod.OracleGraph()
+    fz = fuzz.Fuzz(seed)
+    for step in range(12):
+        eb = fz.entries(300 + 60 * step)
+        h.merge_entries(eb, split=step % 2 == 0)
+        o.merge_entries(eb)
+        if step % 2 == 1:
+            db = fz.deltas(5)
+            h.merge_deltas(db); o.merge_deltas(db)
+        if step == 7:
+            ub = fz.undo(o.export().vertices.keys())
+            h.merge_undo(ub); o.merge_undo(ub)
+        assert h.export() == o.export()
+        for loc in (1, 2, 3):
+            assert h.count_reachable_from(loc) == o.count_reachable_from(loc)
+        _same(h.trace(True), o.trace(True))
+        fz.sync(o.export())
+    assert h.export() == o.export()
+
+
+def test_c4_shape_eight_shards_closure(sharded, oracle_mod, monkeypatch):
+    """The closure forced on the G = 8 C4-shaped power-law graph: wide marks,
+    many branching shadows, supervisor chains across shards."""
+    monkeypatch.setenv("CRGC_XCLOSURE_AFTER", "1")
+    monkeypatch.setenv("CRGC_XCLOSURE_NARROW", "0")
+    V = 100_000
+    w = world.World(seed=0x5EED + 4)
+    w.bulk_graph(V, 10 * V, alpha=2.1, n_roots=V // 1000, cap=100000)
+    h, o = sharded(8), oracle_mod.OracleGraph()
+    for b in w.batches(1 << 18):
+        h.merge_entries(b, split=True)
+        o.merge_entries(b)
+    _same(h.trace(True), o.trace(True))
+    for _ in range(2):
+        b = w.wakeup(V // 10, busy=V * 9 // 100, pending=V // 100)
+        h.merge_entries(b, split=True)
+        o.merge_entries(b)
+        _same(h.trace(True), o.trace(True))
+    assert h.export() == o.export()

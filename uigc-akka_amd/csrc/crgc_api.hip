@@ -198,6 +198,11 @@ struct Knobs {
   bool level_log = false;        // CRGC_LEVEL_LOG
   int xbits = 1;                 // CRGC_XBITS: sharded mark form (0 ids, 1 cheaper, 2 bitmaps)
   int buckets_log2 = 0;          // CRGC_BUCKETS_LOG2: edge-pipeline buckets (test hook; 0 = by size)
+  // Sharded deep marks switch to the replicated chain closure (crgc_xchain.hip)
+  // after this many rounds (0: never), once a round's marks are at most
+  // 1 / xclosure_narrow of the graph's slots (0: at any width; a test hook).
+  uint32_t xclosure_after = 8;   // CRGC_XCLOSURE_AFTER
+  uint32_t xclosure_narrow = 1024;  // CRGC_XCLOSURE_NARROW
   void read() {
     auto env = [](const char *k) { return getenv(k); };
     if (const char *m = env("CRGC_PULL")) pull = atoi(m) != 0;
@@ -221,6 +226,8 @@ struct Knobs {
     if (const char *m = env("CRGC_XBITS")) xbits = atoi(m);
     if (const char *m = env("CRGC_BUCKETS_LOG2"))
       buckets_log2 = std::min(10, std::max(1, atoi(m)));
+    if (const char *m = env("CRGC_XCLOSURE_AFTER")) xclosure_after = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_XCLOSURE_NARROW")) xclosure_narrow = (uint32_t)strtoul(m, nullptr, 10);
   }
 };
 
@@ -263,6 +270,7 @@ struct crgc_graph {
   Scratch x_route, x_route_send, x_cat;  // routed entry merges
   Scratch x_dg, x_dg_out;    // DeltaGraph production
   Scratch x_chain;           // chain mode (crgc_chain.hip)
+  Scratch x_gc, x_gc_list;   // replicated chain closure of sharded marks (crgc_xchain.hip)
   uint64_t *h_small = nullptr;       // pinned host staging for small all-gathers
   char *h_route = nullptr;           // pinned RoutePart / ConcatPart tables
   bool route = true;                 // CRGC_ROUTE=0: all-gather every batch instead
@@ -571,7 +579,7 @@ void crgc_destroy(crgc_graph *h) {
   h->work.release();
   for (Scratch *x : {&h->x_send, &h->x_slot, &h->x_recv, &h->x_ans, &h->x_ans_back, &h->x_small,
                      &h->x_pack, &h->x_pack_recv, &h->x_route, &h->x_route_send, &h->x_cat,
-                     &h->x_dg, &h->x_dg_out, &h->x_chain})
+                     &h->x_dg, &h->x_dg_out, &h->x_chain, &h->x_gc, &h->x_gc_list})
     x->release();
   if (h->ctr) hipFree(h->ctr);
   if (h->hctr) hipHostFree(h->hctr);
@@ -1646,6 +1654,137 @@ static int resolve_home_slots(crgc_graph *h, uint64_t top, int xmode, uint64_t *
   return CRGC_OK;
 }
 
+// The replicated chain closure (crgc_xchain.hip) from this round's received
+// marks: every shard all-gathers the successor structure of its home shadows,
+// closes the marked set by pointer doubling (the same work on every shard, so
+// the same result), expands branching shadows at their homes and all-gathers
+// what that marks, until an iteration marks nothing; then keeps its own range.
+// Decided identically on every shard (from all-gathered counts), so every
+// shard takes this path or none does.
+static int xclosure(crgc_graph *h, bool investigate, const XRecv &xr, uint64_t *rounds, uint64_t *x_bytes) {
+  const uint32_t G = h->G, me = h->shard;
+  XcArgs x{};
+  x.G = G;
+  x.me = me;
+  x.investigate = investigate ? 1 : 0;
+  uint64_t P[MAX_SHARDS], N = 0;
+  for (uint32_t d = 0; d < G; ++d) {
+    P[d] = round_up(std::max<uint64_t>(h->peer_top[d], 1), 64);
+    x.off[d] = N;
+    N += P[d];
+  }
+  x.off[G] = N;
+  x.N = N;
+  x.P_me = P[me];
+  uint32_t R = 1;
+  while ((1ull << (R - 1)) < N) ++R;
+  const uint32_t nflag = 2 * R + 4, fi_apply = 2 * R + 1;
+  const size_t need = Carver::need({x.P_me * 4, x.P_me * 4, x.P_me / 8, x.P_me / 8, x.P_me / 8, x.P_me / 8,
+                                    N * 4, N * 4, N * 4, N * 4, N / 8, N / 8, N / 8, N / 8, (size_t)nflag * 4,
+                                    N * 4, 8});
+  if (h->x_gc.ensure(need) != hipSuccess) return CRGC_E_NOMEM;
+  Carver cv(h->x_gc.ptr);
+  x.lnx = cv.take<uint32_t>(x.P_me);
+  x.lsp = cv.take<uint32_t>(x.P_me);
+  x.lvis = cv.take<uint32_t>(x.P_me / 32);
+  x.lcx = cv.take<uint32_t>(x.P_me / 32);
+  x.lpb = cv.take<uint32_t>(x.P_me / 32);
+  x.seed = cv.take<uint32_t>(x.P_me / 32);
+  x.gnx = cv.take<uint32_t>(N);
+  x.gsp = cv.take<uint32_t>(N);
+  uint32_t *ja = cv.take<uint32_t>(N), *jb = cv.take<uint32_t>(N);
+  x.gvis = cv.take<uint32_t>(N / 32);
+  x.gcx = cv.take<uint32_t>(N / 32);
+  x.gpb_in = cv.take<uint32_t>(N / 32);
+  x.gpb_out = cv.take<uint32_t>(N / 32);
+  x.flag = cv.take<uint32_t>(nflag);
+  x.xl = cv.take<uint32_t>(N);
+  x.xl_n = cv.take<unsigned long long>(1);
+  const DevGraph &g = h->g.d;
+  HIP_TRY(hipMemsetAsync(x.seed, 0, x.P_me / 8, h->stream));
+  HIP_TRY(hipMemsetAsync(x.flag, 0, (size_t)nflag * 4, h->stream));
+  HIP_TRY(hipMemsetAsync(x.gpb_out, 0, N / 8, h->stream));
+  HIP_TRY(launch_xclosure(g, x, 0, h->x_recv.ptr, (uint32_t *)&xr, 0, 0, 0, h->stream));
+  HIP_TRY(launch_xclosure(g, x, 1, nullptr, nullptr, 0, 0, 0, h->stream));
+  // the blocks to every shard: five all-gathers of variable-size blocks
+  auto gather = [&](const void *send, void *recv, uint64_t unit_num, uint64_t unit_den) -> int {
+    size_t soff[MAX_SHARDS], sb[MAX_SHARDS], roff[MAX_SHARDS], rb[MAX_SHARDS];
+    for (uint32_t d = 0; d < G; ++d) {
+      soff[d] = 0;
+      sb[d] = P[me] * unit_num / unit_den;
+      roff[d] = x.off[d] * unit_num / unit_den;
+      rb[d] = P[d] * unit_num / unit_den;
+    }
+    if (int rc = h->tp->alltoallv(me, send, soff, sb, recv, roff, rb, h->stream)) {
+      h->poisoned = true;
+      return rc;
+    }
+    *x_bytes += sb[0] * (G - 1);
+    return CRGC_OK;
+  };
+  if (int rc = gather(x.lnx, x.gnx, 4, 1)) return rc;
+  if (int rc = gather(x.lsp, x.gsp, 4, 1)) return rc;
+  if (int rc = gather(x.lvis, x.gvis, 1, 8)) return rc;
+  if (int rc = gather(x.lcx, x.gcx, 1, 8)) return rc;
+  if (int rc = gather(x.lpb, x.gpb_in, 1, 8)) return rc;
+  std::vector<uint32_t> fl(nflag);
+  std::vector<uint64_t> cnt(G);
+  for (uint64_t it = 0;; ++it) {
+    if (it > N) {
+      h->poisoned = true;
+      return CRGC_E_TIMEOUT;  // every iteration but the last marks a shadow
+    }
+    if (it) HIP_TRY(hipMemsetAsync(x.flag + 1, 0, (size_t)(nflag - 1) * 4, h->stream));
+    HIP_TRY(hipMemsetAsync(x.xl_n, 0, 8, h->stream));
+    for (uint32_t seq = 0; seq < 2; ++seq) {
+      const uint32_t *src = seq ? x.gsp : x.gnx;
+      uint32_t *dst = ja;
+      for (uint32_t r = 0; r < R; ++r) {
+        HIP_TRY(launch_xclosure(g, x, 2, src, dst, 0, 1 + seq * R + r, r == 0, h->stream));
+        src = dst;
+        dst = dst == ja ? jb : ja;
+      }
+    }
+    HIP_TRY(launch_xclosure(g, x, 3, nullptr, nullptr, 0, 0, 0, h->stream));
+    HIP_TRY(hipMemcpyAsync(fl.data(), x.flag, (size_t)nflag * 4, hipMemcpyDeviceToHost, h->stream));
+    if (int rc = ag_u64(h, {{x.xl_n, 1}}, cnt.data())) return rc;  // synchronises
+    if (fl[0]) {
+      h->poisoned = true;
+      return CRGC_E_DEVICE;  // a proxy without a resolved home slot: the resolution step failed
+    }
+    ++*rounds;
+    bool jumped = false;
+    for (uint32_t k = 1; k <= 2 * R; ++k) jumped |= fl[k] != 0;
+    uint64_t total = 0;
+    for (uint32_t d = 0; d < G; ++d) {
+      cnt[d] = std::min<uint64_t>(cnt[d], N);
+      total += cnt[d];
+    }
+    if (!jumped && total == 0) break;
+    if (total) {
+      size_t soff[MAX_SHARDS], sb[MAX_SHARDS], roff[MAX_SHARDS], rb[MAX_SHARDS];
+      size_t ro = 0;
+      for (uint32_t d = 0; d < G; ++d) {
+        soff[d] = 0;
+        sb[d] = cnt[me] * 4;
+        roff[d] = ro;
+        rb[d] = cnt[d] * 4;
+        ro += rb[d];
+      }
+      if (h->x_gc_list.ensure(ro + 8) != hipSuccess) return CRGC_E_NOMEM;
+      if (int rc = h->tp->alltoallv(me, x.xl, soff, sb, h->x_gc_list.ptr, roff, rb, h->stream)) {
+        h->poisoned = true;
+        return rc;
+      }
+      *x_bytes += cnt[me] * 4 * (G - 1);
+      HIP_TRY(launch_xclosure(g, x, 4, h->x_gc_list.ptr, nullptr, total, fi_apply, 0, h->stream));
+    }
+    std::swap(x.gpb_in, x.gpb_out);
+  }
+  HIP_TRY(launch_xclosure(g, x, 5, nullptr, nullptr, 0, 0, 0, h->stream));
+  return CRGC_OK;
+}
+
 // Sharded marks run in rounds: a local fixpoint, then every shard sends the
 // proxies it marked to their homes, which continue from them.  A marked proxy
 // travels as its home slot when the proxy has one cached — as a u32 list, or
@@ -1724,6 +1863,23 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
       ro += B[(size_t)r * G + me];
     }
     xr.start[G] = items;
+    // A deep, narrow mark (chains across shards: about one round per link)
+    // finishes in the replicated chain closure.  Every shard decides from the
+    // same all-gathered counts.
+    {
+      const Knobs &kn = h->knobs;
+      uint64_t n_all = 0, marks = 0;
+      for (uint32_t d = 0; d < G; ++d) n_all += h->peer_top[d];
+      for (uint64_t v : M) marks += v;
+      if (xmode != 0 && kn.xclosure_after && *rounds >= kn.xclosure_after &&
+          (kn.xclosure_narrow == 0 || marks * kn.xclosure_narrow <= n_all) && n_all < 0xF0000000ull) {
+        *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        const auto t1 = std::chrono::steady_clock::now();
+        const int rc = xclosure(h, investigate, xr, rounds, x_bytes);
+        *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+        return rc;
+      }
+    }
     // received marks are candidates of level L (a sparse level after an empty one)
     const int L = end + 2;
     HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(ring) + ((L - 2) % LEVEL_RING) * 8, 0, 8, h->stream));

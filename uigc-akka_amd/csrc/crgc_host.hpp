@@ -229,6 +229,26 @@ struct XRecv {
 };
 hipError_t launch_xlist(const DevGraph &g, bool scatter, uint64_t nblk, char *send, const XSend &x,
                         hipStream_t s);
+// The replicated chain closure of deep sharded marks (crgc_xchain.hip).
+struct XcArgs {
+  uint32_t G, me;
+  int investigate;
+  uint64_t off[MAX_SHARDS + 1];  // first global index of each shard's slots (multiples of 64)
+  uint64_t N, P_me;              // global indices; this shard's (padded) slot range
+  uint32_t *lnx, *lsp;           // [P_me] this shard's block: successor, supervisor (global)
+  uint32_t *lvis, *lcx, *lpb;    // [P_me / 32] marked / branching / pending bits of the block
+  uint32_t *seed;                // [P_me / 32] marks imported this round (not yet expanded)
+  uint32_t *gnx, *gsp;           // [N] all shards' blocks
+  uint32_t *gvis, *gcx, *gpb_in, *gpb_out;  // [N / 32]
+  uint32_t *flag;                // [0] a proxy without a home slot; jump / apply flags after it
+  uint32_t *xl;                  // [N] shadows this shard's expansions marked
+  unsigned long long *xl_n;
+};
+// step 0 import (p0 = receive buffer, p1 = XRecv*), 1 local block, 2 jump
+// (p0 -> p1, flag fi, first of its sequence), 3 expand, 4 apply (p0 = list of
+// n), 5 finish
+hipError_t launch_xclosure(const DevGraph &g, const XcArgs &x, int step, const void *p0, uint32_t *p1, uint64_t n,
+                           uint32_t fi, int first, hipStream_t s);
 hipError_t launch_ximport(const DevGraph &g, const char *recv, const XRecv &x, int level, hipStream_t s);
 // home-slot resolution: 0 reset(mask), 1 count unresolved, 2 list them (ids, slots),
 // 3 answer asked ids (at the home), 4 store the answers

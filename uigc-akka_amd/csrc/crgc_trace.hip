@@ -489,45 +489,59 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   }
 
   // light ranges: chunk (block b, k-th 64) of every block's region; chunk ids
-  // run over blocks first so consecutive waves take different blocks
-  for (uint64_t cid = gw; cid < nblk * 32; cid += nw) {
-    const uint64_t b = cid % nblk;
-    const uint32_t k = (uint32_t)(cid / nblk);
-    const uint32_t t = g.qn_tag[b];
-    nb2 += lane == 0 ? 8 : 0;
-    if ((t >> 12) != want) continue;
-    const uint32_t cnt = t & 0xFFFu;
-    if (cnt <= k * 64) continue;
-    const uint32_t qi = k * 64 + lane;
-    const uint2 r = qi < cnt ? g.qn_buf[b * BLK_SLOTS + qi] : make_uint2(0, 0);
-    nb2 += qi < cnt ? 16 : 0;
-    const uint32_t incl = wave_incl_scan(r.y);
-    const uint32_t dtot = __shfl(incl, 63);
-    s_start[wv][lane] = incl - r.y;
-    s_off[wv][lane] = r.x;
-    wave_lds_fence();
-    for (uint32_t e0 = 0; e0 < dtot; e0 += 64 * U) {
-      uint64_t ed[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t e = e0 + u * 64 + lane;
-        ed[u] = 0;  // count 0: neither traced nor counted
-        if (e < dtot) {
-          int lo = 0, hi = 63;
-          while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_start[wv][mid] <= e) lo = mid;
-            else hi = mid - 1;
-          }
-          ed[u] = pool_load(&g.pool[(uint64_t)s_off[wv][lo] + (e - s_start[wv][lo])]);
-          nb2 += 16;
-        }
-      }
-      uint32_t nb = 0;
-      expand_edges(g, Fn, Dn, sp_next, ed, nb);
-      nb2 += 2 * nb;
+  // run over blocks first so consecutive waves take different blocks.  A wave
+  // reads the tags of 64 chunk ids at once (one per lane) and walks the chunks
+  // that have ranges: one tag round trip per 64 ids, not one per id (a sparse
+  // level's scan of nblk * 32 ids was a chain of dependent L2 reads).
+  const uint64_t ncid = nblk * 32;
+  for (uint64_t cb = gw * 64; cb < ncid; cb += nw * 64) {
+    const uint64_t mc = cb + lane;
+    uint32_t mt = 0;
+    if (mc < ncid) {
+      const uint32_t t = g.qn_tag[mc % nblk];
+      const uint32_t mk = (uint32_t)(mc / nblk);
+      if ((t >> 12) == want && (t & 0xFFFu) > mk * 64) mt = t;
     }
-    wave_lds_fence();
+    nb2 += mc < ncid ? 8 : 0;
+    uint64_t todo = __ballot(mt != 0);
+    while (todo) {
+      const int jl = __ffsll((unsigned long long)todo) - 1;
+      todo &= todo - 1;
+      const uint64_t cid = cb + jl;
+      const uint64_t b = cid % nblk;
+      const uint32_t k = (uint32_t)(cid / nblk);
+      const uint32_t cnt = __shfl(mt, jl) & 0xFFFu;
+      const uint32_t qi = k * 64 + lane;
+      const uint2 r = qi < cnt ? g.qn_buf[b * BLK_SLOTS + qi] : make_uint2(0, 0);
+      nb2 += qi < cnt ? 16 : 0;
+      const uint32_t incl = wave_incl_scan(r.y);
+      const uint32_t dtot = __shfl(incl, 63);
+      s_start[wv][lane] = incl - r.y;
+      s_off[wv][lane] = r.x;
+      wave_lds_fence();
+      for (uint32_t e0 = 0; e0 < dtot; e0 += 64 * U) {
+        uint64_t ed[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t e = e0 + u * 64 + lane;
+          ed[u] = 0;  // count 0: neither traced nor counted
+          if (e < dtot) {
+            int lo = 0, hi = 63;
+            while (lo < hi) {
+              const int mid = (lo + hi + 1) >> 1;
+              if (s_start[wv][mid] <= e) lo = mid;
+              else hi = mid - 1;
+            }
+            ed[u] = pool_load(&g.pool[(uint64_t)s_off[wv][lo] + (e - s_start[wv][lo])]);
+            nb2 += 16;
+          }
+        }
+        uint32_t nb = 0;
+        expand_edges(g, Fn, Dn, sp_next, ed, nb);
+        nb2 += 2 * nb;
+      }
+      wave_lds_fence();
+    }
   }
   // hub pieces: one per step
   for (uint64_t hi = gw; hi < nh; hi += nw) {
