@@ -203,6 +203,7 @@ struct Knobs {
   // 1 / xclosure_narrow of the graph's slots (0: at any width; a test hook).
   uint32_t xclosure_after = 8;   // CRGC_XCLOSURE_AFTER
   uint32_t xclosure_narrow = 1024;  // CRGC_XCLOSURE_NARROW
+  uint32_t xslices = 1;          // CRGC_XSLICES: push-level target slices (1, 2, 4, 8)
   void read() {
     auto env = [](const char *k) { return getenv(k); };
     if (const char *m = env("CRGC_PULL")) pull = atoi(m) != 0;
@@ -228,6 +229,10 @@ struct Knobs {
       buckets_log2 = std::min(10, std::max(1, atoi(m)));
     if (const char *m = env("CRGC_XCLOSURE_AFTER")) xclosure_after = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_XCLOSURE_NARROW")) xclosure_narrow = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_XSLICES")) {
+      const uint32_t v = (uint32_t)strtoul(m, nullptr, 10);
+      xslices = v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
+    }
   }
 };
 
@@ -1457,6 +1462,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   // Deep marks: a k_tail walk of chain_after links hands the rest to chain mode
   // (pointer jumping, crgc_chain.hip).  Unsharded graphs only.
   la.chain_after = h->tp ? 0 : kn.chain_after;
+  la.xslices = kn.xslices;
   la.tail_start = std::min<uint32_t>(kn.tail_start, TAIL_QCAP);
   la.tail_max = std::min<uint32_t>(std::max(kn.tail_max, 1u), TAIL_QCAP);
   // Device times, from timing-only events (no system-scope fence):

@@ -172,6 +172,7 @@ struct LevelArgs {
   uint32_t alpha;          // Beamer: pull when alpha * m_f > m_u (0: the pull_cur_div rule)
   uint64_t e_total;        // edge keys in the graph (m_u = e_total - explored edges)
   uint32_t chain_after;    // k_tail hands a deep mark to chain mode after this many rounds (0: never)
+  uint32_t xslices;        // push levels: 1, 2, 4 or 8 target slices (k_expand: XCD-local candidate stores)
   uint16_t location;
 };
 

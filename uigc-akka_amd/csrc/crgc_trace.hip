@@ -325,15 +325,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
 // k_frontier (bits & ~vis), and a byte store is idempotent across XCDs, so the
 // edge load is the only round trip an edge costs (mark -13 % on the C2 wakeup
 // against filter + read-before-store: profiles/r2e/ab.json).
+// smask / slice: with target slices (LevelArgs::xslices > 1) a workgroup
+// stores only the candidates of its slice, ((t >> 11) & smask) == slice.
 template <int U>
 __device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn, bool sp_next,
-                                    const uint64_t (&ed)[U], uint32_t &nb) {
+                                    const uint64_t (&ed)[U], uint32_t &nb, uint32_t smask, uint32_t slice) {
   uint32_t t[U];
   bool go[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    go[u] = edge_count(ed[u]) > 0;
     t[u] = edge_target(ed[u]);
+    go[u] = edge_count(ed[u]) > 0 && ((t[u] >> 11) & smask) == slice;
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -384,8 +386,8 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   uint8_t *Dn = g.dirty[(L + 1) & 1];
   const int wv = threadIdx.x >> 6;
   const int lane = lane_id();
-  const uint64_t gw = (uint64_t)blockIdx.x * 4 + wv;
-  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  uint64_t gw = (uint64_t)blockIdx.x * 4 + wv;
+  uint64_t nw = (uint64_t)gridDim.x * 4;
   const uint32_t want = (uint32_t)(L + 1);
   const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
   // A candidate byte stored for an already-marked target is dropped by the next
@@ -488,13 +490,23 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
     return;
   }
 
+  // Push with target slices: the grid is split into S sub-grids, workgroup b
+  // in slice b % S (blocks are dealt round-robin over the 8 XCDs, so a slice
+  // stays on S / 8 of them); every sub-grid walks all the level's edges and
+  // stores only its slice's candidate bytes, so a candidate line is dirtied by
+  // one slice's XCDs instead of by all eight (partial-line write-backs).
+  const uint32_t S = a.xslices > 1 ? a.xslices : 1u;
+  const uint32_t smask = S - 1, slice = blockIdx.x & smask;
+  gw = (uint64_t)(blockIdx.x / S) * 4 + wv;
+  nw = (uint64_t)(gridDim.x / S) * 4;
+  if (blockIdx.x >= (gridDim.x / S) * S) nw = 0;  // a partial last set of slices: idle
   // light ranges: chunk (block b, k-th 64) of every block's region; chunk ids
   // run over blocks first so consecutive waves take different blocks.  A wave
   // reads the tags of 64 chunk ids at once (one per lane) and walks the chunks
   // that have ranges: one tag round trip per 64 ids, not one per id (a sparse
   // level's scan of nblk * 32 ids was a chain of dependent L2 reads).
   const uint64_t ncid = nblk * 32;
-  for (uint64_t cb = gw * 64; cb < ncid; cb += nw * 64) {
+  for (uint64_t cb = gw * 64; nw && cb < ncid; cb += nw * 64) {
     const uint64_t mc = cb + lane;
     uint32_t mt = 0;
     if (mc < ncid) {
@@ -537,14 +549,14 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
           }
         }
         uint32_t nb = 0;
-        expand_edges(g, Fn, Dn, sp_next, ed, nb);
+        expand_edges(g, Fn, Dn, sp_next, ed, nb, smask, slice);
         nb2 += 2 * nb;
       }
       wave_lds_fence();
     }
   }
   // hub pieces: one per step
-  for (uint64_t hi = gw; hi < nh; hi += nw) {
+  for (uint64_t hi = gw; nw && hi < nh; hi += nw) {
     const uint2 r = g.qh_buf[hi];
     nb2 += lane == 0 ? 16 : 0;
     for (uint32_t e0 = 0; e0 < r.y; e0 += 64 * U) {
@@ -556,7 +568,7 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
         nb2 += e < r.y ? 16 : 0;
       }
       uint32_t nb = 0;
-      expand_edges(g, Fn, Dn, sp_next, ed, nb);
+      expand_edges(g, Fn, Dn, sp_next, ed, nb, smask, slice);
       nb2 += 2 * nb;
     }
   }
