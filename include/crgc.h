@@ -358,6 +358,16 @@ int crgc_compact(crgc_graph *g);
 
 int crgc_export(crgc_graph *g, crgc_graph_export *out);
 
+/* Pins a caller-owned host buffer for DMA, as a JVM would its direct
+   ByteBuffers (packed by the Wakeup drain loop, LocalGC.scala:152-172, and
+   reused every wakeup): host batches whose arrays lie in registered buffers
+   are copied by the DMA engines, without the driver's pageable staging copy.
+   No reference counterpart (the reference has no device boundary).  The
+   buffer must stay valid until crgc_host_unregister or crgc_destroy;
+   registering an overlapping range is CRGC_E_INVAL. */
+int crgc_host_register(crgc_graph *g, void *ptr, uint64_t bytes);
+int crgc_host_unregister(crgc_graph *g, void *ptr);
+
 /* Human-readable text for a status code. */
 const char *crgc_strerror(int code);
 

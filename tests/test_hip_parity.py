@@ -220,3 +220,27 @@ def test_edge_buckets_in_several_rounds(hip_mod, oracle_mod, buckets_log2, monke
         _same_trace(h.trace(True), o.trace(True))
         fz.sync(o.export())
     assert h.export() == o.export()
+
+
+def test_registered_host_arena_matches_oracle(hip_mod, oracle_mod):
+    """Host batches packed into a buffer pinned by crgc_host_register (the JNI
+    shim's reused direct buffers) merge exactly like any host batch; an
+    overlapping registration is refused."""
+    from crgc_hip import HostArena
+    h, o = _pair(hip_mod, oracle_mod)
+    arena = HostArena(8 << 20)
+    h.register_host(arena.buf)
+    with pytest.raises(abi.CrgcError) as e:
+        h.register_host(arena.buf[4096:8192])
+    assert e.value.code == abi.E_INVAL
+    fz = fuzz.Fuzz(23)
+    for step in range(6):
+        eb = fz.entries(3000)
+        h.merge_entries(arena.pack(eb))
+        o.merge_entries(eb)
+        assert h.export() == o.export()
+        _same_trace(h.trace(True), o.trace(True))
+        fz.sync(o.export())
+    h.unregister_host(arena.buf)
+    with pytest.raises(abi.CrgcError):
+        h.unregister_host(arena.buf)

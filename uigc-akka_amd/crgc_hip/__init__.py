@@ -5,9 +5,9 @@ HIP kernels for gfx950); this package is its host-side mirror of the reference
 ShadowGraph surface (ShadowGraph.java), bound through ctypes.
 """
 from . import abi
-from .batch import Entry, EntryBatch, DeltaBatch, UndoBatch, TraceResult, RefobInfo, GraphState
+from .batch import Entry, EntryBatch, DeltaBatch, UndoBatch, TraceResult, RefobInfo, GraphState, HostArena
 from .graph import ShadowGraph, ShardedShadowGraph, Transport, UndoAccumulator, shard_of
 
-__all__ = ["abi", "Entry", "EntryBatch", "DeltaBatch", "UndoBatch", "TraceResult", "RefobInfo",
+__all__ = ["abi", "Entry", "EntryBatch", "HostArena", "DeltaBatch", "UndoBatch", "TraceResult", "RefobInfo",
            "GraphState", "ShadowGraph", "ShardedShadowGraph", "Transport", "UndoAccumulator",
            "shard_of"]

@@ -399,3 +399,27 @@ def export_to_state(fn_export, handle) -> GraphState:
     assert len(verts) == nv, "duplicate vertex ids in export"
     assert len(edges) == ne, "duplicate edges in export"
     return GraphState(verts, edges)
+
+
+class HostArena:
+    """A reused host buffer that entry batches are packed into — what a JVM's
+    direct ByteBuffers are to the JNI shim: allocated once,
+    registered with the graph (crgc_host_register) so merges DMA from it, and
+    refilled by every wakeup's drain loop (LocalGC.scala:152-172)."""
+
+    def __init__(self, nbytes: int):
+        self.buf = np.empty(int(nbytes) + 4096, dtype=np.uint8)
+
+    def pack(self, b: "EntryBatch") -> "EntryBatch":
+        assert b.memory == abi.MEM_HOST
+        views, off = [], 0
+        for k in EntryBatch.__slots__[:11]:
+            a = np.ascontiguousarray(getattr(b, k))
+            off = (off + 255) & ~255
+            if off + a.nbytes > self.buf.nbytes:
+                raise ValueError("batch larger than the arena")
+            v = self.buf[off:off + a.nbytes].view(a.dtype)
+            v[...] = a
+            views.append(v)
+            off += a.nbytes
+        return EntryBatch(*views)

@@ -238,6 +238,14 @@ class ShadowGraph:
     def total_actors_seen(self) -> int:
         return self.totalActorsSeen
 
+    def register_host(self, buf: np.ndarray):
+        """Pin a host buffer for DMA (crgc_host_register): batches packed into it
+        (HostArena) are copied without the driver's pageable staging."""
+        self._chk(self.lib.crgc_host_register(self.h, buf.ctypes.data, buf.nbytes), "crgc_host_register")
+
+    def unregister_host(self, buf: np.ndarray):
+        self._chk(self.lib.crgc_host_unregister(self.h, buf.ctypes.data), "crgc_host_unregister")
+
     def compact(self):
         """Compact the graph now (crgc_compact): dense slots, segments in slot order."""
         self.flush()

@@ -284,6 +284,8 @@ struct crgc_graph {
   // this shard's last resolution
   uint64_t slot_gen = 0;
   std::vector<uint64_t> peer_gen, peer_top;
+  // host buffers pinned by crgc_host_register: (base, bytes)
+  std::vector<std::pair<char *, uint64_t>> pinned;
 };
 
 namespace {
@@ -595,6 +597,7 @@ void crgc_destroy(crgc_graph *h) {
     hipStreamSynchronize(h->side);
     hipStreamDestroy(h->side);
   }
+  for (auto &p : h->pinned) hipHostUnregister(p.first);
   if (h->ev_fork) hipEventDestroy(h->ev_fork);
   if (h->ev_join) hipEventDestroy(h->ev_join);
   for (auto &e : h->ev)
@@ -2602,6 +2605,32 @@ int crgc_total_actors_seen(crgc_graph *h, uint64_t *out) {
   HIP_TRY(sync_counters(h));
   *out = h->hctr->inserted;
   return CRGC_OK;
+}
+
+int crgc_host_register(crgc_graph *h, void *ptr, uint64_t bytes) {
+  if (int rc = check_graph(h)) return rc;
+  if (!ptr || !bytes) return CRGC_E_INVAL;
+  char *b = (char *)ptr;
+  for (auto &p : h->pinned)
+    if (b < p.first + p.second && p.first < b + bytes) return CRGC_E_INVAL;
+  DeviceGuard dg(h->device);
+  const hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
+  if (e != hipSuccess) return e == hipErrorOutOfMemory ? CRGC_E_NOMEM : CRGC_E_INVAL;
+  h->pinned.emplace_back(b, bytes);
+  return CRGC_OK;
+}
+
+int crgc_host_unregister(crgc_graph *h, void *ptr) {
+  if (!h || !ptr) return CRGC_E_INVAL;
+  for (size_t i = 0; i < h->pinned.size(); ++i)
+    if (h->pinned[i].first == (char *)ptr) {
+      DeviceGuard dg(h->device);
+      // merges read registered buffers by DMA until they return; nothing is in flight here
+      hipHostUnregister(ptr);
+      h->pinned.erase(h->pinned.begin() + (long)i);
+      return CRGC_OK;
+    }
+  return CRGC_E_INVAL;
 }
 
 int crgc_compact(crgc_graph *h) {
