@@ -97,9 +97,53 @@ __global__ __launch_bounds__(IDS_THREADS) void k_ids(DevGraph g, IdArgs a) {
     }
     // Slot allocation (one atomic per workgroup) only in rounds that created or
     // wait for a shadow: a steady-state wakeup mostly finds existing ones.
+    // Every claim of the round is published before any wait (a pending key may
+    // have been claimed by another thread's later id), so waits always end.
     if (__syncthreads_or(settle)) {
+      uint32_t nins = 0, nhome = 0;
 #pragma unroll
-      for (int j = 0; j < IDS_K; ++j) slot[j] = id_settle_block(g, id[j], bucket[j], slot[j], st[j]);
+      for (int j = 0; j < IDS_K; ++j)
+        if (st[j] == RS_INSERTED) {
+          ++nins;
+          nhome += is_home(g, id[j]) ? 1u : 0u;
+        }
+      unsigned long long *const ctrs[2] = {&g.ctr->slot_top, &g.ctr->inserted};
+      const uint32_t v[2] = {nins, nhome};
+      unsigned long long base[2];
+      block_append<2>(ctrs, v, base);
+      unsigned long long s = base[0];
+#pragma unroll
+      for (int j = 0; j < IDS_K; ++j) {
+        if (st[j] != RS_INSERTED) continue;
+        const bool home = is_home(g, id[j]);
+        if (s >= g.scap) {
+          set_err(g.ctr, ERR_SLOTS_FULL);
+          slot[j] = SLOT_INVALID;
+        } else {
+          slot[j] = (uint32_t)s;
+          g.vid[s] = id[j];
+          g.flags[s] = home ? FL_ALIVE : (FL_ALIVE | FL_PROXY);
+        }
+        ++s;
+        atomicExch(&g.htab[bucket[j]].val, slot[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < IDS_K; ++j) {
+        if (st[j] == RS_PENDING) {
+          slot[j] = SLOT_INVALID;
+          for (uint32_t spin = 0; spin < (1u << 24); ++spin) {
+            const uint32_t v2 = atomicOr(&g.htab[bucket[j]].val, 0u);
+            if (v2 != VAL_PENDING) {
+              slot[j] = v2;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (slot[j] == SLOT_INVALID) set_err(g.ctr, ERR_SPIN);
+        } else if (st[j] == RS_NONE) {
+          slot[j] = SLOT_INVALID;
+        }
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < IDS_K; ++j)
