@@ -244,3 +244,39 @@ def test_registered_host_arena_matches_oracle(hip_mod, oracle_mod):
     h.unregister_host(arena.buf)
     with pytest.raises(abi.CrgcError):
         h.unregister_host(arena.buf)
+
+
+@pytest.mark.parametrize("pull", ["0", "1000000"])
+def test_fan_in_candidate_overflow(hip_mod, oracle_mod, monkeypatch, pull):
+    """Thousands of new in-edges to a few targets in one merge: their reverse
+    candidate segments overflow (k_rv_grow / k_rv_place), some of those edges
+    change sign again within the same merge's later rounds (CRGC_BUCKETS_LOG2=1:
+    two owner buckets, many rounds), and every level pulls (CRGC_ALPHA) so the
+    marks depend on the candidates."""
+    from crgc_hip import Entry, EntryBatch
+    monkeypatch.setenv("CRGC_ALPHA", pull)
+    monkeypatch.setenv("CRGC_BUCKETS_LOG2", "1")
+    h, o = _pair(hip_mod, oracle_mod)
+    loc = 1 << 48
+    root = loc | 1
+    hubs = [loc | (2 + k) for k in range(3)]
+    owners = [loc | (100 + k) for k in range(3000)]
+    first = [Entry(self=root, isRoot=True, spawnedActors=hubs,
+                   createdOwners=[root] * 2, createdTargets=hubs[:2])]
+    # the root spawns every owner (F records per entry) and keeps refs to them
+    for k in range(0, len(owners), 4):
+        first.append(Entry(self=root, isRoot=True, spawnedActors=owners[k:k + 4],
+                           createdOwners=[root] * len(owners[k:k + 4]), createdTargets=owners[k:k + 4]))
+    b0 = EntryBatch.from_entries(first)
+    h.merge_entries(b0); o.merge_entries(b0)
+    for wake in range(4):
+        es = []
+        for i, ow in enumerate(owners):
+            if wake == 0 or (wake == 3 and i % 2):  # refs to every hub: new keys, then 0 -> 1
+                es.append(Entry(self=root, isRoot=True, createdOwners=[ow] * 3, createdTargets=hubs))
+            if wake in (1, 2) and i % 2:  # released again: 1 -> 0 on one hub per wakeup
+                es.append(Entry(self=ow, updatedRefs=[hubs[wake]], updatedInfos=[1]))
+        b = EntryBatch.from_entries(es)
+        h.merge_entries(b); o.merge_entries(b)
+        assert h.export() == o.export()
+        _same_trace(h.trace(True), o.trace(True))

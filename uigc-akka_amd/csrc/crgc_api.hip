@@ -635,7 +635,7 @@ static size_t edge_scratch(const crgc_graph *h, uint64_t max_atoms) {
   // the callers' atom arrays (o, t, d, exact count), then the pipeline's own
   return Carver::need({max_atoms * 4, max_atoms * 4, max_atoms * 4, 8, nh * 4, nh * 8,
                        ((nh + 1023) / 1024) * 4 * 8 + 64, 16, max_atoms * 8, max_atoms * 4, max_atoms * 4,
-                       max_atoms * 4, max_atoms * 4});
+                       max_atoms * 4, max_atoms * 4, max_atoms * 4, 8});
 }
 
 static int run_edges(crgc_graph *h, uint32_t *ao, uint32_t *at, int32_t *ad, uint64_t max_atoms,
@@ -657,8 +657,10 @@ static int run_edges(crgc_graph *h, uint32_t *ao, uint32_t *at, int32_t *ad, uin
   ea.pk = cv.take<uint64_t>(max_atoms);
   ea.pv = cv.take<uint32_t>(max_atoms);
   ea.rv_t = cv.take<uint32_t>(max_atoms);
+  ea.rv_i = cv.take<uint32_t>(max_atoms);
   ea.rv_o = cv.take<uint32_t>(max_atoms);
   ea.rv_b = cv.take<uint32_t>(max_atoms);
+  ea.n_ov = cv.take<unsigned long long>(1);
   HIP_TRY(launch_edges(h->g.d, ea, s ? s : h->stream));
   return CRGC_OK;
 }

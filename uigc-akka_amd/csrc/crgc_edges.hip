@@ -19,11 +19,16 @@
 //      rank among their owner's new edges (LDS atomics on an LDS owner table),
 //      each owner's segment grows once (one pool allocation per workgroup per
 //      round) and the new edges are written after its old degree.  Every new
-//      edge leaves a reverse atom (target, owner | RC_POS, edge-table bucket).
-//   3. The same partition by target, then k_ep_target: one workgroup per
-//      target bucket appends the new reverse candidates (ranks by LDS atomics,
-//      one growth per target per round) and records their index in the edge
-//      table (`rev`, which later sign changes use).
+//      edge appends its reverse candidate (owner | RC_POS) to its target's
+//      candidate segment with one 64-bit atomic on radj[target] = {offset,
+//      length}: the old length is the candidate's index, written at once when
+//      it is below the segment's capacity.
+//   3. The candidates past a capacity (a target whose segment fills up this
+//      merge) go to an overflow list; k_rv_grow moves each such target's
+//      segment to a power-of-two segment for its final length (one pool
+//      allocation per workgroup) and k_rv_place writes them there.  Round 2
+//      partitioned every new edge by target for this (two partition passes and
+//      a target-bucket kernel); now only the overflow is handled apart.
 // Pool, candidate pool and edge-table sizes follow the same bounds as before
 // (ensure_capacity in crgc_api.hip).
 #include "crgc_host.hpp"
@@ -54,21 +59,10 @@ __device__ inline uint32_t ep_bucket(const EdgeArgs &a, uint32_t slot) {
   return (slot * 0x9E3779B1u) >> a.bshift;
 }
 
-// REV = false: atoms (ao, at, ad), key o << 32 | t, bucket of o.
-// REV = true : reverse atoms (rv_t, rv_o, rv_b), key t << 32 | (o | RC_POS),
-//              bucket of t; rv_t == ~0 marks an unused position.
-template <bool REV>
+// An atom (ao, at, ad) as (bucket of the owner, key o << 32 | t, delta).
 __device__ inline bool ep_atom(const EdgeArgs &a, uint64_t i, uint64_t n, uint32_t &bucket, uint64_t &key,
                                uint32_t &val) {
   if (i >= n) return false;
-  if (REV) {
-    const uint32_t t = a.rv_t[i];
-    if (t == 0xFFFFFFFFu) return false;
-    bucket = ep_bucket(a, t);
-    key = ((uint64_t)t << 32) | a.rv_o[i];
-    val = a.rv_b[i];
-    return true;
-  }
   const int32_t d = a.atom_d[i];
   const uint32_t o = a.atom_o[i], t = a.atom_t[i];
   if (d == 0 || !ep_valid(o) || !ep_valid(t)) return false;
@@ -78,11 +72,8 @@ __device__ inline bool ep_atom(const EdgeArgs &a, uint64_t i, uint64_t n, uint32
   return true;
 }
 
-// Atoms to partition: the merge's (exact count when the device has it), or
-// the reverse atoms, which fill the forward partition's [0, total).
-template <bool REV>
+// Atoms to partition: the merge's (exact count when the device has it).
 __device__ inline uint64_t ep_count(const EdgeArgs &a) {
-  if (REV) return a.tot[0];
   // a batch refused for its offsets (or > F records) left unwritten atoms:
   // nothing of it is applied (the handle is poisoned by that error anyway)
   if (a.err && (*a.err & (ERR_BAD_OFFSETS | ERR_TOO_MANY))) return 0;
@@ -94,10 +85,10 @@ __device__ inline uint64_t ep_end(const EdgeArgs &a, uint32_t b, int which) {
   return b + 1 == a.nbk ? a.tot[which] : a.hoff[(uint64_t)(b + 1) * a.nblk];
 }
 
-template <bool REV>
 __global__ __launch_bounds__(EP_THREADS) void k_ep_count(EdgeArgs a) {
   extern __shared__ uint32_t hist[];  // [nbk]
-  const uint64_t n = ep_count<REV>(a);
+  const uint64_t n = ep_count(a);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.n_ov = 0;  // k_ep_owner's overflow list
   for (uint32_t k = threadIdx.x; k < a.nbk; k += EP_THREADS) hist[k] = 0;
   __syncthreads();
   const uint64_t per = (n + a.nblk - 1) / a.nblk;
@@ -106,16 +97,15 @@ __global__ __launch_bounds__(EP_THREADS) void k_ep_count(EdgeArgs a) {
     uint32_t b;
     uint64_t key;
     uint32_t val;
-    if (ep_atom<REV>(a, i, n, b, key, val)) atomicAdd(&hist[b], 1u);
+    if (ep_atom(a, i, n, b, key, val)) atomicAdd(&hist[b], 1u);
   }
   __syncthreads();
   for (uint32_t k = threadIdx.x; k < a.nbk; k += EP_THREADS) a.hist[(uint64_t)k * a.nblk + blockIdx.x] = hist[k];
 }
 
-template <bool REV>
 __global__ __launch_bounds__(EP_THREADS) void k_ep_scatter(EdgeArgs a) {
   extern __shared__ uint32_t cur[];  // [nbk]
-  const uint64_t n = ep_count<REV>(a);
+  const uint64_t n = ep_count(a);
   for (uint32_t k = threadIdx.x; k < a.nbk; k += EP_THREADS) cur[k] = 0;
   __syncthreads();
   const uint64_t per = (n + a.nblk - 1) / a.nblk;
@@ -124,7 +114,7 @@ __global__ __launch_bounds__(EP_THREADS) void k_ep_scatter(EdgeArgs a) {
     uint32_t b;
     uint64_t key;
     uint32_t val;
-    if (!ep_atom<REV>(a, i, n, b, key, val)) continue;
+    if (!ep_atom(a, i, n, b, key, val)) continue;
     const uint64_t at = a.hoff[(uint64_t)b * a.nblk + blockIdx.x] + atomicAdd(&cur[b], 1u);
     a.pk[at] = key;
     a.pv[at] = val;
@@ -168,7 +158,7 @@ struct EpOwnerLds {
                           // the owner's degree before its new edges
   uint32_t plist[EP_CH];  // pair table entries in use
   uint32_t olist[EP_CH];  // owner table entries in use
-  uint32_t np, nol, nnew, nrv;
+  uint32_t np, nol, nnew;
 };
 
 __device__ inline uint32_t ep_owner_slot(EpOwnerLds &L, uint32_t o) {
@@ -193,7 +183,6 @@ __global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
   const uint32_t b = blockIdx.x;
   const uint64_t a0 = a.hoff[(uint64_t)b * a.nblk], a1 = ep_end(a, b, 0);
   if (a0 == a1) return;
-  if (threadIdx.x == 0) L.nrv = 0;
   for (uint32_t k = threadIdx.x; k < EP_TAB; k += EP_WG) {
     L.key[k] = KEY_EMPTY;
     L.sum[k] = 0;
@@ -246,7 +235,7 @@ __global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
             if ((old > 0) != (now > 0)) {  // the reverse candidate follows the count's sign
               const uint32_t r = g.etab[bk].rev;
               const uint32_t cand = o | (now > 0 ? RC_POS : 0u);
-              if (r != 0xFFFFFFFFu && (r & EP_PENDING)) a.rv_o[a0 + (r & ~EP_PENDING)] = cand;
+              if (r != 0xFFFFFFFFu && (r & EP_PENDING)) a.rv_o[r & ~EP_PENDING] = cand;  // still in the overflow list
               else if (r < g.rcap[t]) g.rpool[(uint64_t)g.radj[t].x + r] = cand;
               if (now <= 0 && g.par[t] == o) g.par[t] = SLOT_NONE;  // the pull hint dies with the count
             }
@@ -299,25 +288,48 @@ __global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
       }
     }
     __syncthreads();
-    // the new edges, after their owner's old degree; one reverse atom each
+    // the new edges, after their owner's old degree; each appends its reverse
+    // candidate to its target's segment (or to the overflow list)
+    uint32_t ovf = 0, nt = 0, ridx = 0, cand = 0, nbk = 0, nidx = 0;
     if (tid < np) {
       const uint32_t rk = L.rank[ph];
       const uint64_t key = L.key[ph];
       if (rk < EP_SKIP) {  // not EP_SKIP / EP_EXIST
-        const uint32_t o = (uint32_t)(key >> 32), t = (uint32_t)key;
+        const uint32_t o = (uint32_t)(key >> 32);
+        nt = (uint32_t)key;
         const uint32_t oh = ep_owner_slot(L, o);
         if (L.ocnt[oh]) {  // else the pool is full (error set)
-          const uint32_t idx = (uint32_t)L.onz[oh] + rk;
+          nidx = (uint32_t)L.onz[oh] + rk;
           const int32_t d = L.sum[ph];
-          const uint32_t bk = L.bkt[ph];
-          g.pool[(uint64_t)g.adj[o].x + idx] = pack_edge(t, d);
-          const uint32_t q = atomicAdd(&L.nrv, 1u);
-          g.etab[bk].val = idx;
-          g.etab[bk].rev = EP_PENDING | q;
-          a.rv_t[a0 + q] = t;
-          a.rv_o[a0 + q] = o | (d > 0 ? RC_POS : 0u);
-          a.rv_b[a0 + q] = bk;
+          nbk = L.bkt[ph];
+          g.pool[(uint64_t)g.adj[o].x + nidx] = pack_edge(nt, d);
+          cand = o | (d > 0 ? RC_POS : 0u);
+          const uint32_t cap = g.rcap[nt];
+          const unsigned long long old = atomicAdd((unsigned long long *)&g.radj[nt], 1ull << 32);
+          ridx = (uint32_t)(old >> 32);
+          if (ridx < cap) {
+            g.rpool[(uint64_t)(uint32_t)old + ridx] = cand;
+            g.etab[nbk].val = nidx;
+            g.etab[nbk].rev = ridx;
+          } else {
+            ovf = 1;
+          }
         }
+      }
+    }
+    {
+      unsigned long long *const otop[1] = {a.n_ov};
+      const uint32_t vo[1] = {ovf};
+      unsigned long long ob[1];
+      block_append<1>(otop, vo, ob);
+      if (ovf) {
+        const uint64_t q = ob[0];
+        a.rv_t[q] = nt;
+        a.rv_i[q] = ridx;
+        a.rv_o[q] = cand;
+        a.rv_b[q] = nbk;
+        g.etab[nbk].val = nidx;
+        g.etab[nbk].rev = EP_PENDING | (uint32_t)q;
       }
     }
     __syncthreads();
@@ -334,105 +346,56 @@ __global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
     }
     __syncthreads();
   }
-  // the rest of the bucket's region holds no reverse atom
-  for (uint64_t i = a0 + L.nrv + tid; i < a1; i += EP_WG) a.rv_t[i] = 0xFFFFFFFFu;
 }
 
-// ---- 3. target buckets -------------------------------------------------------
-struct EpTargetLds {
-  uint32_t tkey[EP_TAB];  // target table: target slot (~0: free)
-  uint32_t tcnt[EP_TAB];  // new candidates of the target in this round
-  uint32_t tbase[EP_TAB]; // its candidate count before them
-  uint32_t toff[EP_TAB];  // its candidate segment
-  uint32_t tlist[EP_CH];
-  uint32_t ntl;
-};
+// ---- 3. overflow candidates ---------------------------------------------------
+// A target whose candidate segment filled up during k_ep_owner: the candidate
+// with index == the old capacity (exactly one per such target: indices come
+// from one counter) moves the segment to a power-of-two segment for the final
+// length; k_rv_place then writes every overflow candidate at its index.
+constexpr int RV_THREADS = 256;
 
-__device__ inline uint32_t ep_target_slot(EpTargetLds &L, uint32_t t) {
-  uint32_t h = (uint32_t)mix64(t) & (EP_TAB - 1);
-  for (;;) {
-    const uint32_t k = atomicCAS(&L.tkey[h], 0xFFFFFFFFu, t);
-    if (k == 0xFFFFFFFFu) {
-      L.tlist[atomicAdd(&L.ntl, 1u)] = h;
-      return h;
-    }
-    if (k == t) return h;
-    h = (h + 1) & (EP_TAB - 1);
-  }
-}
-
-__global__ __launch_bounds__(EP_WG) void k_ep_target(DevGraph g, EdgeArgs a) {
-  __shared__ EpTargetLds L;
-  const uint32_t b = blockIdx.x;
-  const uint64_t a0 = a.hoff[(uint64_t)b * a.nblk], a1 = ep_end(a, b, 1);
-  if (a0 == a1) return;
-  const uint32_t tid = threadIdx.x;
-  for (uint32_t k = tid; k < EP_TAB; k += EP_WG) {
-    L.tkey[k] = 0xFFFFFFFFu;
-    L.tcnt[k] = 0;
-  }
+__global__ __launch_bounds__(RV_THREADS) void k_rv_grow(DevGraph g, EdgeArgs a) {
+  const uint64_t n = *a.n_ov;
   Counters *c = g.ctr;
   unsigned long long *const tops[1] = {&c->rpool_top};
-  for (uint64_t c0 = a0; c0 < a1; c0 += EP_CH) {
-    const uint32_t m = (uint32_t)min((uint64_t)EP_CH, a1 - c0);
-    if (tid == 0) L.ntl = 0;
-    __syncthreads();
-    uint64_t key = 0;
-    uint32_t th = 0, rank = 0;
-    if (tid < m) {
-      key = a.pk[c0 + tid];
-      th = ep_target_slot(L, (uint32_t)(key >> 32));
-      rank = atomicAdd(&L.tcnt[th], 1u);
-    }
-    __syncthreads();
-    {
-      const uint32_t ntl = L.ntl;
-      const uint32_t sh = tid < ntl ? L.tlist[tid] : 0;
-      const uint32_t t = tid < ntl ? L.tkey[sh] : 0;
-      const uint32_t nn = tid < ntl ? L.tcnt[sh] : 0;
-      uint2 rd = make_uint2(0, 0);
-      uint32_t want = 0;
-      if (nn) {
-        rd = g.radj[t];
-        if (rd.y + nn > g.rcap[t]) want = seg_cap_ep(rd.y + nn);
-      }
-      const uint32_t v1[1] = {want};
-      unsigned long long offs[1];
-      block_append<1>(tops, v1, offs);
-      uint32_t r = 0xFFFFFFFFu, add = nn;
-      if (want) {
-        if (offs[0] + want > g.rpcap) {
-          set_err(c, ERR_POOL_FULL);
-          add = 0;
-        } else {
-          r = (uint32_t)offs[0];
-        }
-      }
-      ep_move(g.rpool, rd.x, rd.y, r);
-      if (tid < ntl) {
-        if (r != 0xFFFFFFFFu) {
-          rd.x = r;
-          g.rcap[t] = want;
-        }
-        L.tcnt[sh] = add;
-        L.tbase[sh] = rd.y;
-        L.toff[sh] = rd.x;
-        if (add) g.radj[t] = make_uint2(rd.x, rd.y + add);
+  const uint64_t stride = (uint64_t)gridDim.x * RV_THREADS;
+  for (uint64_t b0 = (uint64_t)blockIdx.x * RV_THREADS; b0 < n; b0 += stride) {  // uniform per block
+    const uint64_t q = b0 + threadIdx.x;
+    uint32_t t = 0, cap = 0, want = 0;
+    uint2 rd = make_uint2(0, 0);
+    if (q < n) {
+      t = a.rv_t[q];
+      cap = g.rcap[t];
+      if (a.rv_i[q] == cap) {  // the first overflow of t
+        rd = g.radj[t];        // final length: every append of the merge is done
+        want = seg_cap_ep(rd.y);
       }
     }
-    __syncthreads();
-    if (tid < m && L.tcnt[th]) {
-      const uint32_t idx = L.tbase[th] + rank;
-      g.rpool[(uint64_t)L.toff[th] + idx] = (uint32_t)key;
-      g.etab[a.pv[c0 + tid]].rev = idx;
+    const uint32_t v1[1] = {want};
+    unsigned long long offs[1];
+    block_append<1>(tops, v1, offs);
+    uint32_t r = 0xFFFFFFFFu;
+    if (want) {
+      if (offs[0] + want > g.rpcap) set_err(c, ERR_POOL_FULL);  // candidates dropped: the handle is poisoned
+      else r = (uint32_t)offs[0];
     }
-    __syncthreads();
-    if (tid < L.ntl) {
-      const uint32_t sh = L.tlist[tid];
-      L.tkey[sh] = 0xFFFFFFFFu;
-      L.tcnt[sh] = 0;
+    ep_move(g.rpool, rd.x, cap, r);  // the candidates that fitted
+    if (r != 0xFFFFFFFFu) {
+      g.radj[t].x = r;
+      g.rcap[t] = want;
     }
-    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(RV_THREADS) void k_rv_place(DevGraph g, EdgeArgs a) {
+  const uint64_t n = *a.n_ov;
+  const uint64_t stride = (uint64_t)gridDim.x * RV_THREADS;
+  for (uint64_t q = (uint64_t)blockIdx.x * RV_THREADS + threadIdx.x; q < n; q += stride) {
+    const uint32_t t = a.rv_t[q], i = a.rv_i[q];
+    if (i >= g.rcap[t]) continue;  // its growth failed (ERR_POOL_FULL)
+    g.rpool[(uint64_t)g.radj[t].x + i] = a.rv_o[q];
+    g.etab[a.rv_b[q]].rev = i;
   }
 }
 
@@ -450,16 +413,14 @@ hipError_t launch_edges(const DevGraph &g, const EdgeArgs &a, hipStream_t s) {
   q.total[0] = a.tot;
   q.bsum = a.bsum;
   // forward: partition by owner, then the owner ranges
-  hipLaunchKernelGGL(k_ep_count<false>, pgrid, dim3(EP_THREADS), lds_hist, s, a);
+  hipLaunchKernelGGL(k_ep_count, pgrid, dim3(EP_THREADS), lds_hist, s, a);
   if (hipError_t e = run_scan(q, s)) return e;
-  hipLaunchKernelGGL(k_ep_scatter<false>, pgrid, dim3(EP_THREADS), lds_hist, s, a);
+  hipLaunchKernelGGL(k_ep_scatter, pgrid, dim3(EP_THREADS), lds_hist, s, a);
   hipLaunchKernelGGL(k_ep_owner, dim3(a.nbk), dim3(EP_WG), 0, s, g, a);
-  // reverse: the new edges' candidates, partitioned by target
-  hipLaunchKernelGGL(k_ep_count<true>, pgrid, dim3(EP_THREADS), lds_hist, s, a);
-  q.total[0] = a.tot + 1;
-  if (hipError_t e = run_scan(q, s)) return e;
-  hipLaunchKernelGGL(k_ep_scatter<true>, pgrid, dim3(EP_THREADS), lds_hist, s, a);
-  hipLaunchKernelGGL(k_ep_target, dim3(a.nbk), dim3(EP_WG), 0, s, g, a);
+  // the reverse candidates that did not fit their targets' segments
+  const int og = grid_for(a.max_atoms, RV_THREADS, 512);
+  hipLaunchKernelGGL(k_rv_grow, dim3(og), dim3(RV_THREADS), 0, s, g, a);
+  hipLaunchKernelGGL(k_rv_place, dim3(og), dim3(RV_THREADS), 0, s, g, a);
   return hipGetLastError();
 }
 

@@ -151,7 +151,10 @@ struct EdgeArgs {
   unsigned long long *tot;   // [2] atoms in the forward / reverse partition
   uint64_t *pk;              // [max_atoms] partitioned keys
   uint32_t *pv;              // [max_atoms] partitioned deltas / edge-table buckets
-  uint32_t *rv_t, *rv_o, *rv_b;  // [max_atoms] reverse atoms: target, owner | RC_POS, bucket
+  // [max_atoms] reverse candidates past their target segment's capacity:
+  // target, index, owner | RC_POS, edge-table bucket; *n_ov of them
+  uint32_t *rv_t, *rv_i, *rv_o, *rv_b;
+  unsigned long long *n_ov;
 };
 
 constexpr uint32_t LV_PULL = 4;                // dense levels scan in-candidates (pull)
