@@ -300,10 +300,11 @@ def load_library(path: str | None = None) -> C.CDLL:
     lib.crgc_undo_acc_export.argtypes = [_P, C.POINTER(CrgcUndoLogOut)]
     lib.crgc_merge_undo_acc.restype = C.c_int
     lib.crgc_merge_undo_acc.argtypes = [_P, _P]
-    lib.crgc_host_register.restype = C.c_int
-    lib.crgc_host_register.argtypes = [_P, _P, _U64]
-    lib.crgc_host_unregister.restype = C.c_int
-    lib.crgc_host_unregister.argtypes = [_P, _P]
+    if hasattr(lib, "crgc_host_register") or not os.environ.get("CRGC_LIB_AB"):  # an A/B build may predate it
+        lib.crgc_host_register.restype = C.c_int
+        lib.crgc_host_register.argtypes = [_P, _P, _U64]
+        lib.crgc_host_unregister.restype = C.c_int
+        lib.crgc_host_unregister.argtypes = [_P, _P]
     lib.crgc_build_delta_graphs.restype = C.c_int
     lib.crgc_build_delta_graphs.argtypes = [_P, C.POINTER(CrgcEntryBatch), C.POINTER(CrgcDeltaGraphs)]
     _declare(lib, "crgc_")

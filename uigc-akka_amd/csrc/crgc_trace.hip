@@ -501,13 +501,14 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
   nw = (uint64_t)(gridDim.x / S) * 4;
   if (blockIdx.x >= (gridDim.x / S) * S) nw = 0;  // a partial last set of slices: idle
   // light ranges: chunk (block b, k-th 64) of every block's region; chunk ids
-  // run over blocks first so consecutive waves take different blocks.  A wave
-  // reads the tags of 64 chunk ids at once (one per lane) and walks the chunks
-  // that have ranges: one tag round trip per 64 ids, not one per id (a sparse
-  // level's scan of nblk * 32 ids was a chain of dependent L2 reads).
+  // run over blocks first so consecutive waves take different blocks, and wave
+  // gw takes ids gw, gw + nw, gw + 2 nw, ...  It reads the tags of 64 of its
+  // ids at once (one per lane) and walks the chunks that have ranges: one tag
+  // round trip per 64 ids, not one per id (a sparse level's scan of nblk * 32
+  // ids was a chain of dependent L2 reads).
   const uint64_t ncid = nblk * 32;
-  for (uint64_t cb = gw * 64; nw && cb < ncid; cb += nw * 64) {
-    const uint64_t mc = cb + lane;
+  for (uint64_t cb = gw; nw && cb < ncid; cb += nw * 64) {
+    const uint64_t mc = cb + (uint64_t)lane * nw;
     uint32_t mt = 0;
     if (mc < ncid) {
       const uint32_t t = g.qn_tag[mc % nblk];
@@ -519,7 +520,7 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
     while (todo) {
       const int jl = __ffsll((unsigned long long)todo) - 1;
       todo &= todo - 1;
-      const uint64_t cid = cb + jl;
+      const uint64_t cid = cb + (uint64_t)jl * nw;
       const uint64_t b = cid % nblk;
       const uint32_t k = (uint32_t)(cid / nblk);
       const uint32_t cnt = __shfl(mt, jl) & 0xFFFu;
