@@ -14,7 +14,7 @@ for pass in 1 2; do
     envs=()
     [ "$v" != "BASE" ] && IFS=',' read -ra envs <<< "$v"
     f="$O/p${pass}_$(echo "$v" | tr '=,/' '___').json"
-    env "${envs[@]}" timeout -k 10 300 python3 "$ROOT/bench.py" --steps 15 --warmup 3 --no-cpu-baseline \
+    env "${envs[@]}" timeout -k 10 300 python3 "$ROOT/bench.py" --steps 15 --warmup 3 --no-cpu-baseline --no-pcie \
       > "$f" 2>> "$O/err.log"
     python3 -c "import json,sys; d=json.loads(open('$f').read().strip().splitlines()[-1]); b=d['wakeup_breakdown_ms']; print('$v', round(d['ms_per_step'],4), round(b['merge'],4), round(b['mark_kernels'],4))" >> "$O/summary.txt"
   done
