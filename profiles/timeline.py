@@ -13,7 +13,8 @@ busy = 0
 for r in seq:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("crgc::", "")[:30]
-    print(f"{(s - t0) / 1e3:8.1f} gap {(s - prev) / 1e3:7.1f} dur {(e - s) / 1e3:7.1f} {name}")
+    q = r.get("Queue_Id", "?")
+    print(f"{(s - t0) / 1e3:8.1f} gap {(s - prev) / 1e3:7.1f} dur {(e - s) / 1e3:7.1f} q{q} {name}")
     busy += e - s
-    prev = e
+    prev = max(prev, e)
 print(f"span {(prev - t0) / 1e3:.1f} us, kernels busy {busy / 1e3:.1f} us")

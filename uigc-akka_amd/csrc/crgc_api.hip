@@ -257,7 +257,12 @@ struct crgc_graph {
   // `stream` (they touch disjoint arrays); fork / join events order them.
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // Large host batches are copied in chunks on `cpy` while the chunks before
+  // them merge on `stream` (merge_entries_chunked).
+  hipStream_t cpy = nullptr;
+  hipEvent_t ev_cstart = nullptr, ev_chunk[8] = {};
   bool use_side = true;  // CRGC_SIDE_STREAM=0 (read at create): one stream
+  bool chunk_host = true;  // CRGC_CHUNK_HOST=0: large host batches in one piece
   // last trace
   uint64_t last_garbage = 0, last_kill = 0, last_live = 0;
   crgc_trace_stats last_stats{};
@@ -545,6 +550,12 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     for (auto &e : h->ev)
       if (hipEventCreate(&e) != hipSuccess) rc = CRGC_E_DEVICE;
     if (const char *m = getenv("CRGC_SIDE_STREAM")) h->use_side = atoi(m) != 0;
+    if (const char *m = getenv("CRGC_CHUNK_HOST")) h->chunk_host = atoi(m) != 0;
+    if (hipStreamCreateWithFlags(&h->cpy, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_cstart, hipEventDisableTiming) != hipSuccess)
+      rc = CRGC_E_DEVICE;
+    for (auto &e : h->ev_chunk)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = CRGC_E_DEVICE;
     if (hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess)
@@ -598,6 +609,13 @@ void crgc_destroy(crgc_graph *h) {
     hipStreamDestroy(h->side);
   }
   for (auto &p : h->pinned) hipHostUnregister(p.first);
+  if (h->cpy) {
+    hipStreamSynchronize(h->cpy);
+    hipStreamDestroy(h->cpy);
+  }
+  if (h->ev_cstart) hipEventDestroy(h->ev_cstart);
+  for (auto &e : h->ev_chunk)
+    if (e) hipEventDestroy(e);
   if (h->ev_fork) hipEventDestroy(h->ev_fork);
   if (h->ev_join) hipEventDestroy(h->ev_join);
   for (auto &e : h->ev)
@@ -1107,12 +1125,121 @@ static int merge_entries_routed(crgc_graph *h, const crgc_entry_batch *b, int vr
   return merge_entries_one(h, &v, Ct, St, Ut);
 }
 
+// A large host batch in K chunks of whole entries: chunk j's arrays are copied
+// on the copy stream while chunks < j merge on the graph's stream, so the
+// hand-off's PCIe time overlaps the merge (pinned buffers registered with
+// crgc_host_register copy by DMA; pageable ones through the driver's staging,
+// which still overlaps the kernels already queued).  Every chunk is a merge of
+// its own (its own epoch): merges commute, and the last-write-wins fields
+// follow chunk order, then record order — the batch's order.
+// Offsets are rebased on the device (k_rebase).  The caller's buffers are
+// free when this returns (the last copy is waited for).
+constexpr uint64_t CHUNK_MIN = 1u << 18;  // entries per chunk at least
+constexpr uint32_t CHUNK_MAX = 4;
+
+static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint32_t K) {
+  const uint64_t n = b->n_entries;
+  struct Part {
+    uint64_t lo, hi, c0, c1, s0, s1, u0, u1;
+    size_t off[11];
+  };
+  Part p[CHUNK_MAX];
+  size_t total = 0;
+  for (uint32_t j = 0; j < K; ++j) {
+    Part &q = p[j];
+    q.lo = n * j / K;
+    q.hi = n * (j + 1) / K;
+    q.c0 = b->created_off[q.lo], q.c1 = b->created_off[q.hi];
+    q.s0 = b->spawned_off[q.lo], q.s1 = b->spawned_off[q.hi];
+    q.u0 = b->updated_off[q.lo], q.u1 = b->updated_off[q.hi];
+    if (q.c1 < q.c0 || q.s1 < q.s0 || q.u1 < q.u0) return CRGC_E_INVAL;  // offsets run backwards
+    const uint64_t m = q.hi - q.lo, C = q.c1 - q.c0, S = q.s1 - q.s0, U = q.u1 - q.u0;
+    const size_t sz[11] = {m * 8, m * 2, m, (m + 1) * 4, C * 8, C * 8, (m + 1) * 4, S * 8, (m + 1) * 4, U * 8, U * 2};
+    for (int i = 0; i < 11; ++i) {
+      total = (total + 255) & ~(size_t)255;
+      q.off[i] = total;
+      total += sz[i];
+    }
+  }
+  if (h->stage.ensure(total + 256) != hipSuccess) return CRGC_E_NOMEM;
+  char *base = (char *)h->stage.ptr;
+  // the staging area is free once the work already queued on the graph's stream is done
+  HIP_TRY(hipEventRecord(h->ev_cstart, h->stream));
+  HIP_TRY(hipStreamWaitEvent(h->cpy, h->ev_cstart, 0));
+  auto copy_chunk = [&](uint32_t j) -> hipError_t {
+    const Part &q = p[j];
+    const uint64_t m = q.hi - q.lo;
+    const void *src[11] = {b->self + q.lo, b->recv_count + q.lo, b->flags + q.lo, b->created_off + q.lo,
+                           b->created_owner + q.c0, b->created_target + q.c0, b->spawned_off + q.lo,
+                           b->spawned + q.s0, b->updated_off + q.lo, b->updated_ref + q.u0,
+                           b->updated_info + q.u0};
+    const size_t sz[11] = {m * 8, m * 2, m, (m + 1) * 4, (q.c1 - q.c0) * 8, (q.c1 - q.c0) * 8, (m + 1) * 4,
+                           (q.s1 - q.s0) * 8, (m + 1) * 4, (q.u1 - q.u0) * 8, (q.u1 - q.u0) * 2};
+    for (int i = 0; i < 11; ++i)
+      if (sz[i]) {
+        hipError_t e = hipMemcpyAsync(base + q.off[i], src[i], sz[i], hipMemcpyHostToDevice, h->cpy);
+        if (e != hipSuccess) return e;
+      }
+    return hipEventRecord(h->ev_chunk[j], h->cpy);
+  };
+  int rc = CRGC_OK;
+  uint32_t copied = 0;
+  for (uint32_t j = 0; j < K && rc == CRGC_OK; ++j) {
+    // keep one chunk's copy ahead of the merges
+    while (copied < K && copied <= j + 1) {
+      if (hipError_t e = copy_chunk(copied)) {
+        rc = map_hip(e);
+        break;
+      }
+      ++copied;
+    }
+    if (rc) break;
+    const Part &q = p[j];
+    const uint64_t m = q.hi - q.lo;
+    if (hipError_t e = hipStreamWaitEvent(h->stream, h->ev_chunk[j], 0)) {
+      rc = map_hip(e);
+      break;
+    }
+    uint32_t *co = (uint32_t *)(base + q.off[3]), *so = (uint32_t *)(base + q.off[6]),
+             *uo = (uint32_t *)(base + q.off[8]);
+    if (hipError_t e = launch_rebase(co, so, uo, m + 1, (uint32_t)q.c0, (uint32_t)q.s0, (uint32_t)q.u0,
+                                     h->stream)) {
+      rc = map_hip(e);
+      break;
+    }
+    crgc_entry_batch v{};
+    v.n_entries = m;
+    v.self = (const uint64_t *)(base + q.off[0]);
+    v.recv_count = (const int16_t *)(base + q.off[1]);
+    v.flags = (const uint8_t *)(base + q.off[2]);
+    v.created_off = co;
+    v.created_owner = (const uint64_t *)(base + q.off[4]);
+    v.created_target = (const uint64_t *)(base + q.off[5]);
+    v.spawned_off = so;
+    v.spawned = (const uint64_t *)(base + q.off[7]);
+    v.updated_off = uo;
+    v.updated_ref = (const uint64_t *)(base + q.off[9]);
+    v.updated_info = (const int16_t *)(base + q.off[10]);
+    v.memory = CRGC_MEM_DEVICE;
+    rc = merge_entries_one(h, &v, q.c1 - q.c0, q.s1 - q.s0, q.u1 - q.u0);
+  }
+  // the caller's buffers are read only during the call
+  const hipError_t e = hipStreamSynchronize(h->cpy);
+  if (rc == CRGC_OK && e != hipSuccess) rc = map_hip(e);
+  return rc;
+}
+
 int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
   if (int rc = check_graph(h)) return rc;
   DeviceGuard dg(h->device);
   uint64_t C = 0, S = 0, U = 0;
   const int vrc = entry_counts(h, b, h->tp, &C, &S, &U);
-  if (!h->tp) return vrc ? vrc : merge_entries_one(h, b, C, S, U);
+  if (!h->tp) {
+    if (vrc) return vrc;
+    if (b->memory == CRGC_MEM_HOST && b->n_entries >= 2 * CHUNK_MIN && h->chunk_host)
+      return merge_entries_chunked(h, b, (uint32_t)std::min<uint64_t>(CHUNK_MAX, b->n_entries / CHUNK_MIN));
+    return merge_entries_one(h, b, C, S, U);
+  }
   if (h->route && h->G <= ROUTE_MAX_SHARDS && h->F <= ROUTE_MAX_F)
     return merge_entries_routed(h, b, vrc, C, S, U);
   // Sharded: every shard applies its part of every shard's batch, in shard order.

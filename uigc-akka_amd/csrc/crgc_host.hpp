@@ -197,6 +197,9 @@ hipError_t launch_chain(const DevGraph &g, const ChainArgs &ca, int step, const 
 // phase 0: ids and edge atoms (the edge pipeline may start behind it); 1: vertex updates
 hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s, int phase);
 hipError_t launch_deltas(const DevGraph &g, const DeltaArgs &a, uint64_t n_out, hipStream_t s, int phase);
+// the offsets of a chunk of a host batch, rebased to its first entry
+hipError_t launch_rebase(uint32_t *c_off, uint32_t *s_off, uint32_t *u_off, uint64_t n, uint32_t c0, uint32_t s0,
+                         uint32_t u0, hipStream_t s);
 hipError_t launch_undo_check(const DevGraph &g, const UndoArgs &a, hipStream_t s);
 hipError_t launch_undo_apply(const DevGraph &g, const UndoArgs &a, uint64_t slot_top,
                              hipStream_t s);

@@ -483,6 +483,23 @@ hipError_t launch_undo_apply(const DevGraph &g, const UndoArgs &a, uint64_t slot
 
 // The edge pipeline (outgoing[o][t] += d) is crgc_edges.hip.
 
+// A chunk of a host batch: its offsets relative to its first entry.
+__global__ __launch_bounds__(256) void k_rebase(uint32_t *c_off, uint32_t *s_off, uint32_t *u_off, uint64_t n,
+                                                uint32_t c0, uint32_t s0, uint32_t u0) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  c_off[i] -= c0;
+  s_off[i] -= s0;
+  u_off[i] -= u0;
+}
+
+hipError_t launch_rebase(uint32_t *c_off, uint32_t *s_off, uint32_t *u_off, uint64_t n, uint32_t c0, uint32_t s0,
+                         uint32_t u0, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rebase, dim3((n + 255) / 256), dim3(256), 0, s, c_off, s_off, u_off, n, c0, s0, u0);
+  return hipGetLastError();
+}
+
 int grid_for(uint64_t threads, int block, int cap) {
   uint64_t b = (threads + block - 1) / block;
   if (b < 1) b = 1;
