@@ -556,7 +556,13 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
       rc = CRGC_E_DEVICE;
     for (auto &e : h->ev_chunk)
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = CRGC_E_DEVICE;
-    if (hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
+    // CRGC_SIDE_PRIO=1: the side stream (the merge's critical path) at the
+    // device's highest priority, so its workgroups dispatch first
+    int prio_lo = 0, prio_hi = 0;
+    hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    const char *sp = getenv("CRGC_SIDE_PRIO");
+    const int side_prio = (sp && atoi(sp)) ? prio_hi : 0;
+    if (hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, side_prio) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess)
       rc = CRGC_E_DEVICE;

@@ -26,7 +26,10 @@ __device__ inline bool vs(uint32_t s) { return s < 0xFFFFFFF0u; }
 // reference's `from` order.
 // ---------------------------------------------------------------------------
 constexpr int IDS_THREADS = 1024;
-constexpr int IDS_K = 4;  // ids per thread per round: their first-bucket loads are in flight together
+#ifndef CRGC_IDS_K
+#define CRGC_IDS_K 4
+#endif
+constexpr int IDS_K = CRGC_IDS_K;  // ids per thread per round: their first-bucket loads are in flight together
 
 // Continues a probe whose first bucket `b` (at h) was already loaded.
 __device__ inline int id_probe_from(const DevGraph &g, uint64_t id, uint64_t h, uint4 b, uint64_t &bucket,
