@@ -153,7 +153,8 @@ struct EpOwnerLds {
   uint32_t rank[EP_TAB];  // rank among the owner's new edges, EP_EXIST, or EP_SKIP
   uint32_t bkt[EP_TAB];   // edge-table bucket
   uint32_t okey[EP_TAB];  // owner table: owner slot (~0: free)
-  uint32_t ocnt[EP_TAB];  // new edges of the owner in this round
+  uint32_t ocnt[EP_TAB];  // new edges of the owner in this round; after the growth, its
+                          // segment offset + 1 (0: its new edges were dropped, pool full)
   int32_t onz[EP_TAB];    // change of the owner's nonzero count; after the growth,
                           // the owner's degree before its new edges
   uint32_t plist[EP_CH];  // pair table entries in use
@@ -221,19 +222,21 @@ __global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
       if (d != 0) {  // absent == 0: a zero sum changes nothing
         const uint32_t o = (uint32_t)(key >> 32), t = (uint32_t)key;
         bool ins = false;
-        uint32_t v = 0;
-        const uint64_t bk = edge_find_or_insert(g, key, &ins, &v);
+        uint32_t v = 0, rv = 0;
+        // the owner's segment, loaded beside the probe (an existing edge needs it)
+        const uint32_t seg = g.adj[o].x;
+        const uint64_t bk = edge_find_or_insert(g, key, &ins, &v, &rv);
         if (bk != KEY_EMPTY) {  // else the table is full: ERR_ETAB_FULL is set
           L.bkt[ph] = (uint32_t)bk;
           const uint32_t oh = ep_owner_slot(L, o);
           if (!ins) {
-            int32_t *p = edge_count_ptr(g.pool, (uint64_t)g.adj[o].x + v);
+            int32_t *p = edge_count_ptr(g.pool, (uint64_t)seg + v);
             const int32_t old = *p;
             const int32_t now = (int32_t)((uint32_t)old + (uint32_t)d);
             *p = now;
             if ((old != 0) != (now != 0)) atomicAdd(&L.onz[oh], now != 0 ? 1 : -1);
             if ((old > 0) != (now > 0)) {  // the reverse candidate follows the count's sign
-              const uint32_t r = g.etab[bk].rev;
+              const uint32_t r = rv;  // loaded with the key: this workgroup owns the pair
               const uint32_t cand = o | (now > 0 ? RC_POS : 0u);
               if (r != 0xFFFFFFFFu && (r & EP_PENDING)) a.rv_o[r & ~EP_PENDING] = cand;  // still in the overflow list
               else if (r < g.rcap[t]) g.rpool[(uint64_t)g.radj[t].x + r] = cand;
@@ -280,7 +283,7 @@ __global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
           ad.x = r;
           g.ecap[o] = want;
         }
-        L.ocnt[oh] = add;
+        L.ocnt[oh] = add ? ad.x + 1 : 0u;  // (LDS: two 1024-thread workgroups per CU need <= 80 KiB each)
         if (add) g.adj[o] = make_uint2(ad.x, ad.y + add);
         const int32_t dz = L.onz[oh] + (int32_t)add;  // new edges have nonzero counts
         if (dz) g.nzdeg[o] = (uint32_t)((int32_t)g.nzdeg[o] + dz);
@@ -302,7 +305,7 @@ __global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
           nidx = (uint32_t)L.onz[oh] + rk;
           const int32_t d = L.sum[ph];
           nbk = L.bkt[ph];
-          g.pool[(uint64_t)g.adj[o].x + nidx] = pack_edge(nt, d);
+          g.pool[(uint64_t)(L.ocnt[oh] - 1) + nidx] = pack_edge(nt, d);
           cand = o | (d > 0 ? RC_POS : 0u);
           const uint32_t cap = g.rcap[nt];
           const unsigned long long old = atomicAdd((unsigned long long *)&g.radj[nt], 1ull << 32);

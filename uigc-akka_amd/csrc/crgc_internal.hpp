@@ -436,15 +436,16 @@ __device__ inline uint64_t edge_key(uint32_t owner, uint32_t target) {
 }
 
 // Returns the bucket of `key`; *inserted tells whether this thread created it,
-// *val is the bucket's value as loaded.
+// *val / *rev are the bucket's value and reverse index as loaded.
 __device__ inline uint64_t edge_find_or_insert(const DevGraph &g, uint64_t key, bool *inserted,
-                                               uint32_t *val) {
+                                               uint32_t *val, uint32_t *rev = nullptr) {
   uint64_t h = mix64(key) & g.emask;
   *inserted = false;
   for (uint64_t probe = 0; probe < g.ecap_tab; ++probe) {
     const uint4 b = load_bucket(&g.etab[h]);
     uint64_t k = bucket_key(b);
     *val = b.z;
+    if (rev) *rev = b.w;
     if (k == KEY_EMPTY) {
       k = atomicCAS((unsigned long long *)&g.etab[h].key, (unsigned long long)KEY_EMPTY,
                     (unsigned long long)key);
@@ -453,6 +454,7 @@ __device__ inline uint64_t edge_find_or_insert(const DevGraph &g, uint64_t key, 
         return h;
       }
       *val = g.etab[h].val;
+      if (rev) *rev = g.etab[h].rev;
     }
     if (k == key) return h;
     h = (h + 1) & g.emask;
