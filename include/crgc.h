@@ -109,7 +109,7 @@ uint32_t crgc_shard_of(uint64_t id, uint32_t n_shards);
 typedef struct crgc_config {
   uint32_t abi_version;        /* CRGC_ABI_VERSION                          */
   int32_t device;              /* HIP device ordinal                        */
-  uint32_t entry_field_size;   /* F, uigc.crgc.entry-field-size (default 4) */
+  uint32_t entry_field_size;   /* F, uigc.crgc.entry-field-size (default 4; at most 255) */
   uint32_t delta_graph_size;   /* uigc.crgc.delta-graph-size (default 64)   */
   uint64_t vertex_capacity;    /* hint: expected live shadows (this shard)  */
   uint64_t edge_capacity;      /* hint: expected live (owner,target) pairs  */

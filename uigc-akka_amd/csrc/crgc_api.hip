@@ -519,6 +519,10 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
   if (!h) return CRGC_E_NOMEM;
   h->device = cfg ? cfg->device : 0;
   h->F = (cfg && cfg->entry_field_size) ? cfg->entry_field_size : 4;
+  if (h->F > 255) {  // reference.conf:40 is 4; per-block record counts are packed in 16 bits
+    delete h;
+    return CRGC_E_INVAL;
+  }
   h->DGS = (cfg && cfg->delta_graph_size) ? cfg->delta_graph_size : 64;
   h->knobs.read();
   // A transport makes the handle a shard (a transport with n_shards == 1 runs
@@ -912,9 +916,10 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
                           U * 8, U * 2})
           : 0;
   const bool sh = h->tp;
+  const uint64_t nb256 = (n + 255) / 256;
   const size_t work_bytes =
       Carver::need({n * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4, sh ? n : 0,
-                    sh ? n * h->F * 8 : 0, 8}) +
+                    sh ? n * h->F * 8 : 0, 8, nb256 * 256 * 4, nb256 * 256 * h->F * 4, nb256 * 4}) +
       edge_scratch(h, max_atoms);
   if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
     return CRGC_E_NOMEM;
@@ -949,6 +954,9 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   a.atom_t = wc.take<uint32_t>(max_atoms);
   a.atom_d = wc.take<int32_t>(max_atoms);
   a.n_atoms = wc.take<uint64_t>(1);
+  a.conf_v = wc.take<uint32_t>(nb256 * 256);
+  a.conf_s = wc.take<uint32_t>(nb256 * 256 * h->F);
+  a.conf_n = wc.take<uint32_t>(nb256);
   // a batch refused for its offsets writes no atoms and the edge pipeline
   // skips it (EdgeArgs::err), so the atom arrays need no clearing
   HIP_TRY(launch_entries(h->g.d, a, h->stream, 0));

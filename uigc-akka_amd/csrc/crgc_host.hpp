@@ -93,6 +93,10 @@ struct EntryArgs {
   uint32_t *co_slot;     // [n*F] created owners
   uint32_t *u_slot;      // [n*F] updated refs
   uint64_t *n_atoms;     // out: C + U, the atoms k_entries_apply wrote (exact edge-pipeline count)
+  // last-write-wins conflicts, per block of 256 entries (k_entries_vertex -> k_entries_lww)
+  uint32_t *conf_v;      // [n rounded to 256] slots whose busy/root several entries tagged
+  uint32_t *conf_s;      // [same * F] children whose supervisor several entries tagged
+  uint32_t *conf_n;      // [blocks] counts: self | spawn << 16
   uint32_t *atom_o;      // [2*n*F]: created atoms, then updated atoms
   uint32_t *atom_t;
   int32_t *atom_d;

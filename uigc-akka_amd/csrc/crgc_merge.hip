@@ -230,62 +230,82 @@ __global__ __launch_bounds__(256) void k_entries_atoms(DevGraph g, EntryArgs a) 
   }
 }
 
-// Receive counts and last-write-wins tags; the winners write in k_entries_lww.
-__global__ __launch_bounds__(256) void k_entries_vertex(DevGraph g, EntryArgs a) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.n) return;
-  if (!entry_ok(a, i, false, g.ctr)) return;  // reported (and self_slot cleared) by k_entries_atoms
-  const uint32_t me = a.self_slot[i];
-  const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
-  const int16_t rc = a.recv[i];
-  // Sharded graphs: every record is applied by the home shard of the shadow
-  // it writes (self, edge owner, spawned child, updated target).  k_ids only
-  // resolved the ids this shard needs, so a valid slot of a child / owner is
-  // a home slot; self may be a proxy (the supervisor of a child homed here).
-  const bool sh = g.n_shards > 1;
-  const bool self_home = !sh || is_home(g, a.self[i]);
-  // Local information (:77-82): recv delta and the busy/root LWW tag.
-  if (vs(me) && self_home) {
-    if (rc != 0) atomicAdd(&g.recv[me], (int32_t)rc);
-    atomicMax(&g.vseq[me], tag);
-  }
-  // Spawned actors (:96-104): child.supervisor = self, last write wins.
-  const uint32_t s0 = a.s_off[i], s1 = a.s_off[i + 1];
-  for (uint32_t k = s0; k < s1; ++k) {
-    const uint32_t cs = a.spawn_slot[k];
-    const bool good = vs(cs) && vs(me);
-    if (!good) a.spawn_slot[k] = SLOT_INVALID;
-    if (good) atomicMax(&g.sseq[cs], tag);
-  }
-  // Updated refs (:107-119): target.recv -= count.
-  const uint32_t u0 = a.u_off[i], u1 = a.u_off[i + 1];
-  for (uint32_t k = u0; k < u1; ++k) {
-    const uint32_t ts = a.u_slot[k];
-    const int32_t cnt = refob_count(a.u_info[k]);
-    const bool tgt_ok = sh ? (vs(ts) && is_home(g, a.u_ref[k])) : (vs(ts) && vs(me));
-    if (tgt_ok && cnt > 0) atomicAdd(&g.recv[ts], -cnt);
-  }
+// Receive counts and last-write-wins tags.  The first entry of this merge to
+// tag a slot (the atomicMax returns an older epoch) writes the field at once;
+// any later one finds this merge's epoch and lists the slot in its block's
+// conflict region, where k_entries_lww rewrites the field from the true
+// winner (the tag's entry).  Most shadows appear once per batch, so the winners
+// need no second random pass over every entry's tag.
+__device__ inline void entry_flags(const DevGraph &g, uint32_t me, uint8_t ef) {
+  uint8_t f = g.flags[me] & (uint8_t)~(FL_BUSY | FL_ROOT);
+  f |= FL_INTERNED | FL_LOCAL;
+  if (ef & CRGC_ENTRY_BUSY) f |= FL_BUSY;
+  if (ef & CRGC_ENTRY_ROOT) f |= FL_ROOT;
+  g.flags[me] = f;
 }
 
-// The LWW winners write the flag byte and the supervisor slot.
-__global__ __launch_bounds__(256) void k_entries_lww(DevGraph g, EntryArgs a) {
+__global__ __launch_bounds__(256) void k_entries_vertex(DevGraph g, EntryArgs a) {
+  __shared__ uint32_t s_nv, s_ns;
+  if (threadIdx.x == 0) s_nv = s_ns = 0;
+  __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.n) return;
-  const uint32_t me = a.self_slot[i];
-  if (!vs(me)) return;
-  const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
-  if (g.vseq[me] == tag) {
-    const uint8_t ef = a.flags[i];
-    uint8_t f = g.flags[me] & (uint8_t)~(FL_BUSY | FL_ROOT);
-    f |= FL_INTERNED | FL_LOCAL;
-    if (ef & CRGC_ENTRY_BUSY) f |= FL_BUSY;
-    if (ef & CRGC_ENTRY_ROOT) f |= FL_ROOT;
-    g.flags[me] = f;
+  uint32_t *cv = a.conf_v + (uint64_t)blockIdx.x * 256;
+  uint32_t *cs_ = a.conf_s + (uint64_t)blockIdx.x * 256 * a.F;
+  if (i < a.n && entry_ok(a, i, false, g.ctr)) {  // a refused entry is reported (and its self cleared) by k_entries_atoms
+    const uint32_t me = a.self_slot[i];
+    const unsigned long long tag = (a.epoch << 32) | (unsigned long long)(i + 1);
+    const int16_t rc = a.recv[i];
+    // Sharded graphs: every record is applied by the home shard of the shadow
+    // it writes (self, edge owner, spawned child, updated target).  k_ids only
+    // resolved the ids this shard needs, so a valid slot of a child / owner is
+    // a home slot; self may be a proxy (the supervisor of a child homed here).
+    const bool sh = g.n_shards > 1;
+    const bool self_home = !sh || is_home(g, a.self[i]);
+    // Local information (:77-82): recv delta and the busy/root LWW tag.
+    if (vs(me) && self_home) {
+      if (rc != 0) atomicAdd(&g.recv[me], (int32_t)rc);
+      const unsigned long long old = atomicMax(&g.vseq[me], tag);
+      if ((old >> 32) != a.epoch) entry_flags(g, me, a.flags[i]);
+      else cv[atomicAdd(&s_nv, 1u)] = me;
+    }
+    // Spawned actors (:96-104): child.supervisor = self, last write wins.
+    const uint32_t s0 = a.s_off[i], s1 = a.s_off[i + 1];
+    for (uint32_t k = s0; k < s1; ++k) {
+      const uint32_t cs = a.spawn_slot[k];
+      if (!(vs(cs) && vs(me))) continue;
+      const unsigned long long old = atomicMax(&g.sseq[cs], tag);
+      if ((old >> 32) != a.epoch) g.sup[cs] = me;
+      else cs_[atomicAdd(&s_ns, 1u)] = cs;
+    }
+    // Updated refs (:107-119): target.recv -= count.
+    const uint32_t u0 = a.u_off[i], u1 = a.u_off[i + 1];
+    for (uint32_t k = u0; k < u1; ++k) {
+      const uint32_t ts = a.u_slot[k];
+      const int32_t cnt = refob_count(a.u_info[k]);
+      const bool tgt_ok = sh ? (vs(ts) && is_home(g, a.u_ref[k])) : (vs(ts) && vs(me));
+      if (tgt_ok && cnt > 0) atomicAdd(&g.recv[ts], -cnt);
+    }
   }
-  const uint32_t s0 = a.s_off[i], s1 = a.s_off[i + 1];
-  for (uint32_t k = s0; k < s1; ++k) {
-    const uint32_t cs = a.spawn_slot[k];
-    if (vs(cs) && g.sseq[cs] == tag) g.sup[cs] = me;
+  __syncthreads();
+  if (threadIdx.x == 0) a.conf_n[blockIdx.x] = s_nv | (s_ns << 16);  // <= 256, <= 256 * F (F <= 255)
+}
+
+// The slots several entries of this merge tagged: the tag's entry (the last
+// in batch order) writes the field.  One block per k_entries_vertex block.
+__global__ __launch_bounds__(256) void k_entries_lww(DevGraph g, EntryArgs a) {
+  const uint32_t cn = a.conf_n[blockIdx.x];
+  const uint32_t nv = cn & 0xFFFFu, ns = cn >> 16;
+  const uint32_t *cv = a.conf_v + (uint64_t)blockIdx.x * 256;
+  const uint32_t *cs_ = a.conf_s + (uint64_t)blockIdx.x * 256 * a.F;
+  for (uint32_t k = threadIdx.x; k < nv; k += 256) {
+    const uint32_t me = cv[k];
+    const uint64_t w = (uint64_t)(g.vseq[me] & 0xFFFFFFFFull) - 1;  // the winning entry
+    entry_flags(g, me, a.flags[w]);
+  }
+  for (uint32_t k = threadIdx.x; k < ns; k += 256) {
+    const uint32_t cs = cs_[k];
+    const uint64_t w = (uint64_t)(g.sseq[cs] & 0xFFFFFFFFull) - 1;
+    g.sup[cs] = a.self_slot[w];
   }
 }
 
