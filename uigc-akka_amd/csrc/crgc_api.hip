@@ -261,7 +261,11 @@ struct crgc_graph {
   // them merge on `stream` (merge_entries_chunked).
   hipStream_t cpy = nullptr;
   hipEvent_t ev_cstart = nullptr, ev_chunk[8] = {};
-  bool use_side = true;  // CRGC_SIDE_STREAM=0 (read at create): one stream
+  // CRGC_SIDE_STREAM=1 (read at create): the edge pipeline beside the vertex
+  // updates.  Off: both halves are bound by random memory operations, so the
+  // overlap bought nothing (merge 0.578-0.587 ms alone vs 0.588-0.598 ms with
+  // it on C2, profiles/r3f/ab_merge.txt)
+  bool use_side = false;
   bool chunk_host = true;  // CRGC_CHUNK_HOST=0: large host batches in one piece
   // last trace
   uint64_t last_garbage = 0, last_kill = 0, last_live = 0;
@@ -553,7 +557,7 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     }
     for (auto &e : h->ev)
       if (hipEventCreate(&e) != hipSuccess) rc = CRGC_E_DEVICE;
-    if (const char *m = getenv("CRGC_SIDE_STREAM")) h->use_side = atoi(m) != 0;
+    if (const char *m = getenv("CRGC_SIDE_STREAM")) h->use_side = atoi(m) != 0;  // A/B switch
     if (const char *m = getenv("CRGC_CHUNK_HOST")) h->chunk_host = atoi(m) != 0;
     if (hipStreamCreateWithFlags(&h->cpy, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_cstart, hipEventDisableTiming) != hipSuccess)

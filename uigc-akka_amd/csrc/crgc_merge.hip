@@ -27,9 +27,9 @@ __device__ inline bool vs(uint32_t s) { return s < 0xFFFFFFF0u; }
 // ---------------------------------------------------------------------------
 constexpr int IDS_THREADS = 1024;
 #ifndef CRGC_IDS_K
-#define CRGC_IDS_K 4
+#define CRGC_IDS_K 1
 #endif
-constexpr int IDS_K = CRGC_IDS_K;  // ids per thread per round: their first-bucket loads are in flight together
+constexpr int IDS_K = CRGC_IDS_K;  // ids per thread per round (4: merge +20 us on C2, profiles/r3f/ab_merge.txt)
 
 // Continues a probe whose first bucket `b` (at h) was already loaded.
 __device__ inline int id_probe_from(const DevGraph &g, uint64_t id, uint64_t h, uint4 b, uint64_t &bucket,
