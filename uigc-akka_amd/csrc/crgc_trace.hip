@@ -26,7 +26,6 @@ namespace crgc {
 constexpr uint32_t RANGE_MAX = 256;  // longer segments (hubs) are cut into pieces
 constexpr int FB = 4;               // k_frontier: chunks of 64 frontier shadows per load group
 constexpr uint32_t NO_SLOT = ~0u;
-constexpr uint32_t PULL_K = 4;      // pull: in-candidates per list per round
 constexpr int STAT_FRONT = 0, STAT_SUP = 1, STAT_EDGES = 2, STAT_LIVE = 3;
 constexpr int STAT_MF = 3;  // during the mark: the level's frontier out-edges (STAT_LIVE after)
 
@@ -100,6 +99,18 @@ __device__ inline uint64_t block_sum4(uint64_t v) {
   return s;
 }
 
+// Bit j of the result: flag byte j of the 32 in f4 has (any bit of) `bit`.
+// Four bytes per word by a multiply (bits 0, 8, 16, 24 -> 21 .. 24; the partial
+// products never overlap), not 32 byte extractions held in registers.
+__device__ inline uint32_t flag_bits(const uint4 (&f4)[2], uint8_t bit) {
+  const uint32_t w[8] = {f4[0].x, f4[0].y, f4[0].z, f4[0].w, f4[1].x, f4[1].y, f4[1].z, f4[1].w};
+  const uint32_t sh = __builtin_ctz(bit);
+  uint32_t m = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) m |= ((((w[q] >> sh) & 0x01010101u) * 0x00204081u) >> 21 & 0xFu) << (4 * q);
+  return m;
+}
+
 // ---------------------------------------------------------------------------
 // k_frontier: one wave per 2048-slot block.  Candidate bytes (or, at level 0,
 // the pseudo-root predicate) -> new frontier bits -> vis (the wave owns those
@@ -137,6 +148,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   const bool write_fx = pull || fx_level(c, L, a);
   const bool listing = !ROOTS && listing_level(c, L, a);
   const bool sharded = !ROOTS && g.n_shards > 1;
+  // pull levels without listing, proxies or Beamer's m_f: the per-lane path below
+  const bool lane_pull = pull && !listing && !sharded && !a.alpha;
   uint32_t n_front = 0, n_sup = 0, n_edges = 0;
 
   for (uint32_t blk = gw; blk < nblk; blk += nw) {
@@ -165,13 +178,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
 #pragma unroll
         for (int q = 0; q < 8; ++q) r4[q] = rp[q];
         const int32_t *rb = (const int32_t *)r4;
+        uint32_t nz = 0;
 #pragma unroll
-        for (int j = 0; j < 32; ++j) {
-          const uint8_t f = fb[j];
-          const bool root = (f & (FL_ALIVE | FL_HALTED | FL_PROXY)) == FL_ALIVE &&
-                            ((f & (FL_ROOT | FL_BUSY)) || !(f & FL_INTERNED) || rb[j] != 0);
-          m |= root ? (1u << j) : 0u;
-        }
+        for (int j = 0; j < 32; ++j) nz |= rb[j] != 0 ? (1u << j) : 0u;
+        m = flag_bits(f4, FL_ALIVE) & ~flag_bits(f4, FL_HALTED) & ~flag_bits(f4, FL_PROXY) &
+            (flag_bits(f4, FL_ROOT) | flag_bits(f4, FL_BUSY) | ~flag_bits(f4, FL_INTERNED) | nz);
       }
     } else {
       uint4 *fp = (uint4 *)(Fc + base);
@@ -208,15 +219,55 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         f4[0] = *(const uint4 *)(g.flags + base);
         f4[1] = *(const uint4 *)(g.flags + base + 16);
       }
-      const uint8_t *fb = (const uint8_t *)f4;
-#pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        halted |= (fb[j] & FL_HALTED) ? (1u << j) : 0u;
-        proxy |= (fb[j] & FL_PROXY) ? (1u << j) : 0u;
-      }
+      halted = flag_bits(f4, FL_HALTED);
+      proxy = flag_bits(f4, FL_PROXY);
     }
     // expandable frontier = frontier minus halted shadows (this wave owns the words)
     if (write_fx) g.fx[(uint64_t)blk * 64 + lane] = m & ~halted;
+    if (lane_pull) {
+      // Pull level: no edge ranges to list, only supervisor edges (:258-267).
+      // The block's supervisors are read in 8 coalesced 16-B loads per lane
+      // (load q, lane l: slots q*256 + 4l .. +3, whose frontier bits come from
+      // lane q*8 + l/8 by one shuffle), then their marked words in two groups
+      // of 16 loads in flight: three dependent round trips per block instead
+      // of two per 64*FB frontier shadows after an LDS compaction.
+      n_front += cnt;
+      const uint32_t e = INVESTIGATE ? 0u : (m & ~halted);
+      if (__ballot(e != 0)) {
+        const uint4 *sp4 = (const uint4 *)(g.sup + (uint64_t)blk * BLK_SLOTS);
+        uint4 s4[8];
+        uint32_t eb = 0;  // 4 bits per load
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const uint32_t b4 = (__shfl(e, q * 8 + (lane >> 3)) >> ((lane & 7) * 4)) & 0xFu;
+          eb |= b4 << (4 * q);
+          s4[q] = b4 ? sp4[q * 64 + lane] : make_uint4(~0u, ~0u, ~0u, ~0u);
+        }
+        const uint32_t *ss = (const uint32_t *)s4;
+        uint32_t sv = 0;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) sv |= (((eb >> j) & 1u) && ss[j] < 0xFFFFFFF0u) ? (1u << j) : 0u;
+        n_sup += __popc(sv);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          uint32_t w[16];
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            const int j = 16 * h + k;
+            w[k] = ((sv >> j) & 1u) ? g.vis[ss[j] >> 5] : ~0u;
+          }
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            const uint32_t s = ss[16 * h + k];
+            if (!((w[k] >> (s & 31)) & 1u)) {
+              Fn[s] = 1;
+              if (sp_next) Dn[s >> 11] = 1;  // blind: no dependent read
+            }
+          }
+        }
+      }
+      continue;
+    }
     while (m) {
       const int j = __ffs(m) - 1;
       m &= m - 1;
@@ -404,6 +455,9 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
     // flags / bytes / radj are coalesced across the wave.
     const uint64_t nq = (c->slot_top + 3) / 4;
     const uint64_t gs = (uint64_t)gridDim.x * 256;
+    // (Loading the hints and in-candidate ranges with the flags while a
+    // quarter of the slots are unmarked, and the hints' frontier bits with
+    // the lists' first chunks, made level 1 slower: 146 -> 181 us, r3g/ab4.)
     for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += gs) {
       const uint64_t v0 = q * 4;
       const uint32_t fl = *(const uint32_t *)(g.flags + v0);
@@ -426,8 +480,8 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
         nb2 += 32;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const uint32_t p = hs[j];
-          if (((todo >> j) & 1u) && p < 0xFFFFFFF0u && ((g.fx[p >> 5] >> (p & 31)) & 1u)) {
+          const uint32_t h = hs[j];
+          if (((todo >> j) & 1u) && h < 0xFFFFFFF0u && ((g.fx[h >> 5] >> (h & 31)) & 1u)) {
             found |= 1u << (8 * j);
             todo &= ~(1u << j);
             nb2 += 8;
@@ -444,33 +498,52 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
       const uint32_t ro[4] = {r01.x, r01.z, r23.x, r23.z};
       const uint32_t rl[4] = {r01.y, r01.w, r23.y, r23.w};
       nb2 += 64;  // four in-candidate ranges
-      // The thread's (up to) 4 lists are walked together, PULL_K candidates of
-      // each per round: one round trip for the candidates, one for their
-      // frontier bits, until every list has a hit or is exhausted.
-      uint32_t live = todo, pos = 0;
+      // The thread's (up to) 4 lists are walked together, one round trip for
+      // the candidates and one for their frontier bits per round, until every
+      // list has a hit or is exhausted.  Each list is read as aligned 16-B
+      // chunks (one request for up to four candidates; entries outside
+      // [ro, ro + rl) belong to other segments and are masked).
+      uint32_t p[4], e[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        p[j] = ro[j];
+        e[j] = ro[j] + rl[j];
+      }
+      uint32_t live = todo;
       while (live) {
-        uint32_t u[4][PULL_K];
+        uint4 u4[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int k = 0; k < PULL_K; ++k)
-            u[j][k] = ((live >> j) & 1u) && pos + k < rl[j] ? g.rpool[(uint64_t)ro[j] + pos + k] : 0u;
-        uint32_t w[4][PULL_K];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int k = 0; k < PULL_K; ++k) {
-            const uint32_t sl = u[j][k] & ~RC_POS;
-            w[j][k] = (u[j][k] & RC_POS) ? g.fx[sl >> 5] >> (sl & 31) : 0u;  // 0: no RC_POS
-            nb2 += (((live >> j) & 1u) && pos + k < rl[j] ? 8 : 0) + ((u[j][k] & RC_POS) ? 8 : 0);
-          }
-        pos += PULL_K;
+          u4[j] = ((live >> j) & 1u) && p[j] < e[j] ? *(const uint4 *)(g.rpool + (p[j] & ~3u))
+                                                    : make_uint4(0, 0, 0, 0);
+        uint32_t u[4][4];
+        uint32_t w[4][4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
+          const uint32_t a0 = p[j] & ~3u;
+          const uint32_t uu[4] = {u4[j].x, u4[j].y, u4[j].z, u4[j].w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const bool in = ((live >> j) & 1u) && a0 + k >= p[j] && a0 + k < e[j];
+            u[j][k] = in ? uu[k] : 0u;
+            nb2 += in ? 8 : 0;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t sl = u[j][k] & ~RC_POS;
+            w[j][k] = (u[j][k] & RC_POS) ? g.fx[sl >> 5] >> (sl & 31) : 0u;  // 0: no RC_POS
+            nb2 += (u[j][k] & RC_POS) ? 8 : 0;
+          }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          p[j] = (p[j] & ~3u) + 4;
           bool hit = false;
           uint32_t who = 0;
 #pragma unroll
-          for (int k = PULL_K - 1; k >= 0; --k)
+          for (int k = 3; k >= 0; --k)
             if (w[j][k] & 1u) {
               hit = true;
               who = u[j][k] & ~RC_POS;
@@ -480,7 +553,7 @@ __global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
             g.par[v0 + j] = who;  // the next trace tries this owner first
             nb2 += 8;
           }
-          if (hit || pos >= rl[j]) live &= ~(1u << j);
+          if (hit || p[j] >= e[j]) live &= ~(1u << j);
         }
       }
       if (found) *(uint32_t *)(Fn + v0) = cand | found;
@@ -636,42 +709,51 @@ struct TailOut {
   bool chained = false;  // handed to chain mode: the pending claims stay marked, unexpanded
 };
 
-// Claim t for the next round; without queue room it becomes a candidate byte
-// of the resume level instead (and the round ends in a bail).
-template <bool LV>
-__device__ inline void tail_claim(const DevGraph &g, const TailLds &sh, uint32_t t, const TailQ &nxt,
-                                  uint8_t *Fb, uint8_t *Db, int32_t &claims) {
-  const uint32_t bit = 1u << (t & 31);
-  uint32_t *w = LV ? &sh.vis[t >> 5] : &g.vis[t >> 5];
-  if (*w & bit) return;
-  if (atomicOr(w, bit) & bit) return;
-  const uint32_t pos = atomicAdd(sh.next, 1u);
-  if (pos < TAIL_QCAP) {
-    nxt.put(pos, t);
-    ++claims;
-  } else {
-    atomicAnd(w, ~bit);
-    Fb[t] = 1;
-    Db[t >> 11] = 1;
+// Claims for the next round; without queue room a claim becomes a candidate
+// byte of the resume level instead (and the round ends in a bail).  Walks: a
+// thread keeps the first shadow it claims while processing one and processes
+// it next itself, in the same round (a chain link per step instead of per
+// round); any further claim goes to the next round's queue.
+// Claims of up to N targets at once (bit k of `valid`: t[k] is a target): the
+// marked words of all of them are loaded together, then the atomics of those
+// still unmarked are issued together, so a batch costs two round trips instead
+// of two per target (a walked shadow's edges were claimed one after another:
+// the C2 tail took 48 us for a 440-shadow frontier, 37 us now).  With `keep`, the first
+// target claimed is kept for the thread to walk next; the rest are queued.
+template <bool LV, int N>
+__device__ inline void tail_claim_batch(const DevGraph &g, const TailLds &sh, const uint32_t (&t)[N],
+                                        uint32_t valid, const TailQ &nxt, uint8_t *Fb, uint8_t *Db,
+                                        int32_t &claims, uint32_t *keep) {
+  // (atomics without the probe: the C2 tail 37 -> 40 us, profiles/r3g/ab4)
+  uint32_t w[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k)
+    w[k] = ((valid >> k) & 1u) ? (LV ? sh.vis[t[k] >> 5] : g.vis[t[k] >> 5]) : ~0u;
+  uint32_t go = 0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) go |= ((w[k] >> (t[k] & 31)) & 1u) ? 0u : (1u << k);
+  if (!go) return;
+#pragma unroll
+  for (int k = 0; k < N; ++k)
+    w[k] = ((go >> k) & 1u) ? atomicOr(LV ? &sh.vis[t[k] >> 5] : &g.vis[t[k] >> 5], 1u << (t[k] & 31)) : ~0u;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    if ((w[k] >> (t[k] & 31)) & 1u) continue;  // marked already, or not a target
+    if (keep && *keep == NO_SLOT) {
+      *keep = t[k];
+      ++claims;
+      continue;
+    }
+    const uint32_t pos = atomicAdd(sh.next, 1u);
+    if (pos < TAIL_QCAP) {
+      nxt.put(pos, t[k]);
+      ++claims;
+    } else {
+      atomicAnd(LV ? &sh.vis[t[k] >> 5] : &g.vis[t[k] >> 5], ~(1u << (t[k] & 31)));
+      Fb[t[k]] = 1;
+      Db[t[k] >> 11] = 1;
+    }
   }
-}
-
-// Walks: a thread keeps the first shadow it claims while processing one and
-// processes it next itself, in the same round (a chain link per step instead
-// of per round); any further claim goes to the next round's queue.
-template <bool LV>
-__device__ inline void tail_claim_keep(const DevGraph &g, const TailLds &sh, uint32_t t, const TailQ &nxt,
-                                       uint8_t *Fb, uint8_t *Db, int32_t &claims, uint32_t &keep) {
-  if (keep != NO_SLOT) {
-    tail_claim<LV>(g, sh, t, nxt, Fb, Db, claims);
-    return;
-  }
-  const uint32_t bit = 1u << (t & 31);
-  uint32_t *w = LV ? &sh.vis[t >> 5] : &g.vis[t >> 5];
-  if (*w & bit) return;
-  if (atomicOr(w, bit) & bit) return;
-  keep = t;
-  ++claims;
 }
 
 // A kept shadow that is not walked after all (a hub): queued like a claim.
@@ -719,7 +801,6 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
         // every per-shadow field in one round trip (a walk step is one chain link)
         const uint8_t f = g.flags[v];
         const uint2 adv = g.adj[v];
-        const uint32_t nzv = g.nzdeg[v];
         const uint32_t supv = investigate ? NO_SLOT : g.sup[v];
         const bool expand = !(f & FL_HALTED);  // (:226-229)
         if (!vfirst && (f & FL_PROXY)) {  // level L's were listed by k_frontier
@@ -728,33 +809,33 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
         }
         ad = make_uint2(0, 0);
         uint32_t keep = NO_SLOT;
+        // targets: [0] the supervisor (:258-267), [1 ..] the out-edges of a
+        // light shadow (:231-241), all claimed in one batch
+        uint32_t tg[TAIL_LIGHT + 1];
+        uint32_t valid = 0;
+        tg[0] = 0;
         if (expand) {
           ad = adv;
-          (void)nzv;  // traced edges are counted by the sweep
-          if (!investigate) {
-            const uint32_t s = supv;  // (:258-267)
-            if (s < 0xFFFFFFF0u) {
-              if (vfirst) {
-                Fn[s] = 0;
-                Dn[s >> 11] = 0;
-              } else {
-                ++o.n_sup;
-              }
-              tail_claim_keep<LV>(g, sh, s, nxt, Fb, Db, o.claims, keep);
+          const uint32_t s = supv;
+          if (s < 0xFFFFFFF0u) {
+            if (vfirst) {
+              Fn[s] = 0;
+              Dn[s >> 11] = 0;
+            } else {
+              ++o.n_sup;
             }
+            tg[0] = s;
+            valid = 1;
           }
         }
-        if (ad.y <= TAIL_LIGHT) {  // this thread walks its shadow's out-edges (:231-241)
-          for (uint32_t e = 0; e < ad.y; e += 4) {
-            uint64_t ed[4];
+        const bool light = ad.y <= TAIL_LIGHT;  // this thread walks its shadow's out-edges
 #pragma unroll
-            for (int u = 0; u < 4; ++u) ed[u] = e + u < ad.y ? g.pool[(uint64_t)ad.x + e + u] : 0;
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              if (edge_count(ed[u]) > 0)
-                tail_claim_keep<LV>(g, sh, edge_target(ed[u]), nxt, Fb, Db, o.claims, keep);
-          }
+        for (uint32_t u = 0; u < TAIL_LIGHT; ++u) {
+          const uint64_t ed = (light && u < ad.y) ? g.pool[(uint64_t)ad.x + u] : 0;
+          tg[u + 1] = edge_target(ed);
+          valid |= edge_count(ed) > 0 ? (2u << u) : 0u;
         }
+        tail_claim_batch<LV, TAIL_LIGHT + 1>(g, sh, tg, valid, nxt, Fb, Db, o.claims, &keep);
         if (keep != NO_SLOT) {
           if (a.chain_after && steps >= a.chain_after) {  // a long chain: queue it, chain mode takes over
             tail_enqueue_claimed<LV>(g, sh, keep, nxt, Fb, Db, o.claims);
@@ -775,15 +856,25 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
         sh.start[threadIdx.x] = st;
         sh.off[threadIdx.x] = ad.x;
         __syncthreads();
-        for (uint32_t e = threadIdx.x; e < total; e += TAIL_THREADS) {
-          int lo = 0, hi = TAIL_THREADS - 1;  // last item whose start <= e
-          while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (sh.start[mid] <= e) lo = mid;
-            else hi = mid - 1;
+        for (uint32_t e0 = threadIdx.x; e0 < total; e0 += 4 * TAIL_THREADS) {
+          uint32_t t4[4], v4 = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t e = e0 + k * TAIL_THREADS;
+            t4[k] = 0;
+            if (e < total) {
+              int lo = 0, hi = TAIL_THREADS - 1;  // last item whose start <= e
+              while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (sh.start[mid] <= e) lo = mid;
+                else hi = mid - 1;
+              }
+              const uint64_t ed = g.pool[(uint64_t)sh.off[lo] + (e - sh.start[lo])];
+              t4[k] = edge_target(ed);
+              v4 |= edge_count(ed) > 0 ? (1u << k) : 0u;
+            }
           }
-          const uint64_t ed = g.pool[(uint64_t)sh.off[lo] + (e - sh.start[lo])];
-          if (edge_count(ed) > 0) tail_claim<LV>(g, sh, edge_target(ed), nxt, Fb, Db, o.claims);
+          tail_claim_batch<LV, 4>(g, sh, t4, v4, nxt, Fb, Db, o.claims, nullptr);
         }
         __syncthreads();
       }
@@ -879,15 +970,28 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
   {
     const uint32_t nblk = (uint32_t)((top + BLK_SLOTS - 1) / BLK_SLOTS);
     const uint32_t want = (uint32_t)(L + 1);
+    // 8 tags per thread in flight, one workgroup scan per 8 x 1024 blocks
+    // (one per 1024 blocks was a chain of dependent loads: 5 at C2 scale)
+    constexpr int TG = 8;
     uint32_t base = 0;
-    for (uint32_t b0 = 0; b0 < nblk; b0 += TAIL_THREADS) {
-      const uint32_t b = b0 + threadIdx.x;
-      const uint32_t t = b < nblk ? g.tl_tag[b] : 0;
-      const uint32_t cnt = (t >> 12) == want ? (t & 0xFFFu) : 0u;
+    for (uint32_t b0 = 0; b0 < nblk; b0 += TG * TAIL_THREADS) {
+      uint32_t cnt[TG], sum = 0;
+#pragma unroll
+      for (int k = 0; k < TG; ++k) {
+        const uint32_t b = b0 + k * TAIL_THREADS + threadIdx.x;
+        const uint32_t t = b < nblk ? g.tl_tag[b] : 0;
+        cnt[k] = (t >> 12) == want ? (t & 0xFFFu) : 0u;
+        sum += cnt[k];
+      }
       uint32_t tot;
-      const uint32_t off = base + tail_scan(cnt, s_w, tot);
-      for (uint32_t i = 0; i < cnt; ++i)
-        if (off + i < TAIL_QCAP) cur.put(off + i, g.tl_buf[(uint64_t)b * BLK_SLOTS + i]);
+      uint32_t off = base + tail_scan(sum, s_w, tot);
+#pragma unroll
+      for (int k = 0; k < TG; ++k) {
+        const uint32_t b = b0 + k * TAIL_THREADS + threadIdx.x;
+        for (uint32_t i = 0; i < cnt[k]; ++i)
+          if (off + i < TAIL_QCAP) cur.put(off + i, g.tl_buf[(uint64_t)b * BLK_SLOTS + i]);
+        off += cnt[k];
+      }
       base += tot;
     }
   }
@@ -1020,23 +1124,28 @@ __global__ __launch_bounds__(256) void k_sweep(DevGraph g, int should_kill) {
     const uint32_t word = g.vis[(uint64_t)blk * 64 + lane];
     const uint4 f4[2] = {*(const uint4 *)(g.flags + base), *(const uint4 *)(g.flags + base + 16)};
     const uint8_t *fb = (const uint8_t *)f4;
-    uint32_t alive = 0, kill = 0, req = 0, prox = 0, halted = 0;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      alive |= ((fb[j] & (FL_ALIVE | FL_PROXY)) == FL_ALIVE) ? (1u << j) : 0u;
-      prox |= ((fb[j] & (FL_ALIVE | FL_PROXY)) == (FL_ALIVE | FL_PROXY)) ? (1u << j) : 0u;
-      halted |= (fb[j] & FL_HALTED) ? (1u << j) : 0u;
-    }
+    const uint32_t fa = flag_bits(f4, FL_ALIVE), fp = flag_bits(f4, FL_PROXY);
+    const uint32_t alive = fa & ~fp, prox = fa & fp;
+    const uint32_t halted = flag_bits(f4, FL_HALTED), local = flag_bits(f4, FL_LOCAL);
+    uint32_t kill = 0, req = 0;
     // traced edges (:231): the nonzero out-counts of the marked, unhalted shadows
-    if (const uint32_t ex = alive & word & ~halted) {
-      // (loading these with the flags instead, unconditionally: k_sweep 35 -> 45 us, profiles/r3d)
+    // Coalesced: load q of lane l holds slots q*256 + 4l .. +3, whose bits come
+    // from lane q*8 + l/8 by one shuffle (a 128-B run per lane touched 64 lines
+    // per load instruction).
+    const uint32_t ex = alive & word & ~halted;
+    if (__ballot(ex != 0)) {
+      const uint4 *zp = (const uint4 *)(g.nzdeg + (uint64_t)blk * BLK_SLOTS);
+      uint32_t b4[8];
       uint4 z[8];
-      const uint4 *zp = (const uint4 *)(g.nzdeg + base);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) z[q] = zp[q];
-      const uint32_t *zs = (const uint32_t *)z;
+      for (int q = 0; q < 8; ++q) {
+        b4[q] = (__shfl(ex, q * 8 + (lane >> 3)) >> ((lane & 7) * 4)) & 0xFu;
+        z[q] = b4[q] ? zp[q * 64 + lane] : make_uint4(0, 0, 0, 0);
+      }
 #pragma unroll
-      for (int j = 0; j < 32; ++j) n_edges += ((ex >> j) & 1u) ? zs[j] : 0u;
+      for (int q = 0; q < 8; ++q)
+        n_edges += (uint64_t)((b4[q] & 1u) ? z[q].x : 0u) + ((b4[q] & 2u) ? z[q].y : 0u) +
+                   (uint64_t)((b4[q] & 4u) ? z[q].z : 0u) + ((b4[q] & 8u) ? z[q].w : 0u);
     }
     const uint32_t garbage = alive & ~word;
     n_live += __popc(alive & word);
@@ -1045,12 +1154,13 @@ __global__ __launch_bounds__(256) void k_sweep(DevGraph g, int should_kill) {
     while (gm) {
       const int j = __ffs(gm) - 1;
       gm &= gm - 1;
-      const uint8_t f = fb[j];
-      if (f & FL_LOCAL) {
+      // (bit masks, not fb[j]: a runtime index into the flag registers cost
+      // this kernel ~20 VGPRs, and occupancy)
+      if ((local >> j) & 1u) {
         const uint32_t s = g.sup[base + j];
         if (s == SLOT_NONE) {
           n_npe++;
-        } else if (should_kill && !(f & FL_HALTED) && s < 0xFFFFFFF0u) {
+        } else if (should_kill && !((halted >> j) & 1u) && s < 0xFFFFFFF0u) {
           if ((g.vis[s >> 5] >> (s & 31)) & 1u) {
             kill |= 1u << j;
           } else if ((g.flags[s] & (FL_ALIVE | FL_PROXY)) == (FL_ALIVE | FL_PROXY)) {
