@@ -147,20 +147,32 @@ __device__ inline void ep_move(T *pool, uint32_t from, uint32_t len, uint32_t r)
   }
 }
 
+// A distinct pair is handled by the same thread before and after the owners'
+// growth (thread i: plist[i]), so its sum, edge-table bucket and rank stay in
+// that thread's registers; LDS holds the reduction and the owner table.
 struct EpOwnerLds {
   uint64_t key[EP_TAB];   // pair o << 32 | t
   int32_t sum[EP_TAB];
-  uint32_t rank[EP_TAB];  // rank among the owner's new edges, EP_EXIST, or EP_SKIP
-  uint32_t bkt[EP_TAB];   // edge-table bucket
   uint32_t okey[EP_TAB];  // owner table: owner slot (~0: free)
   uint32_t ocnt[EP_TAB];  // new edges of the owner in this round; after the growth, its
                           // segment offset + 1 (0: its new edges were dropped, pool full)
   int32_t onz[EP_TAB];    // change of the owner's nonzero count; after the growth,
                           // the owner's degree before its new edges
+  uint32_t oseg[EP_TAB];  // owners with new edges: segment offset, and degree | log2(capacity)
+  uint32_t oinf[EP_TAB];  // << 27 (ep_pack_inf), loaded by their new pairs' threads beside the
+                          // existing pairs' count updates
   uint32_t plist[EP_CH];  // pair table entries in use
   uint32_t olist[EP_CH];  // owner table entries in use
   uint32_t np, nol, nnew;
 };
+
+// Degree and segment capacity (0 or a power of two >= 4) in one word; a degree
+// of 2^27 or more (never seen) is marked for a reload from the arrays.
+constexpr uint32_t EP_INF_RELOAD = 0xFFFFFFFFu;
+__device__ inline uint32_t ep_pack_inf(uint32_t deg, uint32_t cap) {
+  if (deg >= (1u << 27)) return EP_INF_RELOAD;
+  return deg | ((cap ? (uint32_t)__builtin_ctz(cap) : 31u) << 27);
+}
 
 __device__ inline uint32_t ep_owner_slot(EpOwnerLds &L, uint32_t o) {
   uint32_t h = (uint32_t)mix64(o) & (EP_TAB - 1);
@@ -179,7 +191,7 @@ __device__ inline uint32_t ep_owner_slot(EpOwnerLds &L, uint32_t o) {
 // the owners' segments, degrees and nonzero counts are written without atomics.
 // Workgroup-scope visibility of earlier rounds' global writes (edge-table
 // values, degrees) is the barrier's (one CU, one L1).
-__global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
+__global__ __launch_bounds__(EP_WG) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_ep_owner(DevGraph g, EdgeArgs a) {
   __shared__ EpOwnerLds L;
   const uint32_t b = blockIdx.x;
   const uint64_t a0 = a.hoff[(uint64_t)b * a.nblk], a1 = ep_end(a, b, 0);
@@ -194,13 +206,20 @@ __global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
   Counters *c = g.ctr;
   unsigned long long *const tops[1] = {&c->pool_top};
   const uint32_t tid = threadIdx.x;
+  // this round's atom (one per thread), loaded during the previous round
+  uint64_t nkey = 0;
+  uint32_t nval = 0;
+  if (a0 + tid < a1) {
+    nkey = a.pk[a0 + tid];
+    nval = a.pv[a0 + tid];
+  }
   for (uint64_t c0 = a0; c0 < a1; c0 += EP_CH) {
     const uint32_t m = (uint32_t)min((uint64_t)EP_CH, a1 - c0);
     if (tid == 0) L.np = L.nol = L.nnew = 0;
     __syncthreads();
     // reduce the round's atoms (one per thread) per pair
     if (tid < m) {
-      const uint64_t key = a.pk[c0 + tid];
+      const uint64_t key = nkey;
       uint32_t h = (uint32_t)mix64(key) & (EP_TAB - 1);
       for (;;) {
         const uint64_t k = atomicCAS((unsigned long long *)&L.key[h], (unsigned long long)KEY_EMPTY,
@@ -209,47 +228,57 @@ __global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
         if (k == KEY_EMPTY || k == key) break;
         h = (h + 1) & (EP_TAB - 1);
       }
-      atomicAdd(&L.sum[h], (int32_t)a.pv[c0 + tid]);
+      atomicAdd(&L.sum[h], (int32_t)nval);
     }
     __syncthreads();
+    // the next round's atom, in flight with this round's probes
+    if (c0 + EP_CH + tid < a1) {
+      nkey = a.pk[c0 + EP_CH + tid];
+      nval = a.pv[c0 + EP_CH + tid];
+    }
     // each distinct pair (one per thread): its edge-table key; existing edges take the sum
     const uint32_t np = L.np;
     const uint32_t ph = tid < np ? L.plist[tid] : 0;
-    if (tid < np) {
-      const uint64_t key = L.key[ph];
-      uint32_t rk = EP_SKIP;
-      const int32_t d = L.sum[ph];
-      if (d != 0) {  // absent == 0: a zero sum changes nothing
-        const uint32_t o = (uint32_t)(key >> 32), t = (uint32_t)key;
-        bool ins = false;
-        uint32_t v = 0, rv = 0;
-        // the owner's segment, loaded beside the probe (an existing edge needs it)
-        const uint32_t seg = g.adj[o].x;
-        const uint64_t bk = edge_find_or_insert(g, key, &ins, &v, &rv);
-        if (bk != KEY_EMPTY) {  // else the table is full: ERR_ETAB_FULL is set
-          L.bkt[ph] = (uint32_t)bk;
-          const uint32_t oh = ep_owner_slot(L, o);
-          if (!ins) {
-            int32_t *p = edge_count_ptr(g.pool, (uint64_t)seg + v);
-            const int32_t old = *p;
-            const int32_t now = (int32_t)((uint32_t)old + (uint32_t)d);
-            *p = now;
-            if ((old != 0) != (now != 0)) atomicAdd(&L.onz[oh], now != 0 ? 1 : -1);
-            if ((old > 0) != (now > 0)) {  // the reverse candidate follows the count's sign
-              const uint32_t r = rv;  // loaded with the key: this workgroup owns the pair
-              const uint32_t cand = o | (now > 0 ? RC_POS : 0u);
-              if (r != 0xFFFFFFFFu && (r & EP_PENDING)) a.rv_o[r & ~EP_PENDING] = cand;  // still in the overflow list
-              else if (r < g.rcap[t]) g.rpool[(uint64_t)g.radj[t].x + r] = cand;
-              if (now <= 0 && g.par[t] == o) g.par[t] = SLOT_NONE;  // the pull hint dies with the count
-            }
-            rk = EP_EXIST;
-          } else {
-            rk = atomicAdd(&L.ocnt[oh], 1u);
-            atomicAdd(&L.nnew, 1u);
+    const uint64_t pkey = tid < np ? L.key[ph] : 0;
+    const int32_t psum = tid < np ? L.sum[ph] : 0;
+    uint32_t rk = EP_SKIP, pbk = 0, rcap_t = 0;
+    if (tid < np && psum != 0) {  // absent == 0: a zero sum changes nothing
+      const int32_t d = psum;
+      const uint32_t o = (uint32_t)(pkey >> 32), t = (uint32_t)pkey;
+      bool ins = false;
+      uint32_t v = 0, rv = 0;
+      // the owner's segment, loaded beside the probe (an existing edge needs it)
+      const uint32_t seg = g.adj[o].x;
+      const uint64_t bk = edge_find_or_insert(g, pkey, &ins, &v, &rv);
+      if (bk != KEY_EMPTY) {  // else the table is full: ERR_ETAB_FULL is set
+        pbk = (uint32_t)bk;
+        const uint32_t oh = ep_owner_slot(L, o);
+        if (!ins) {
+          int32_t *p = edge_count_ptr(g.pool, (uint64_t)seg + v);
+          const int32_t old = *p;
+          const int32_t now = (int32_t)((uint32_t)old + (uint32_t)d);
+          *p = now;
+          if ((old != 0) != (now != 0)) atomicAdd(&L.onz[oh], now != 0 ? 1 : -1);
+          if ((old > 0) != (now > 0)) {  // the reverse candidate follows the count's sign
+            const uint32_t r = rv;  // loaded with the key: this workgroup owns the pair
+            const uint32_t cand = o | (now > 0 ? RC_POS : 0u);
+            if (r != 0xFFFFFFFFu && (r & EP_PENDING)) a.rv_o[r & ~EP_PENDING] = cand;  // still in the overflow list
+            else if (r < g.rcap[t]) g.rpool[(uint64_t)g.radj[t].x + r] = cand;
+            if (now <= 0 && g.par[t] == o) g.par[t] = SLOT_NONE;  // the pull hint dies with the count
           }
+          rk = EP_EXIST;
+        } else {
+          // a new edge: its owner's degree / capacity (for the growth) and its
+          // target's candidate capacity, beside the existing pairs' updates
+          const uint2 oad = g.adj[o];
+          const uint32_t cap = g.ecap[o];
+          rcap_t = g.rcap[t];
+          L.oseg[oh] = oad.x;  // every new pair of the owner stores the same values
+          L.oinf[oh] = ep_pack_inf(oad.y, cap);
+          rk = atomicAdd(&L.ocnt[oh], 1u);
+          atomicAdd(&L.nnew, 1u);
         }
       }
-      L.rank[ph] = rk;
     }
     __syncthreads();
     // owners with new edges (one per thread): one growth each, one pool
@@ -262,8 +291,16 @@ __global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
       uint2 ad = make_uint2(0, 0);
       uint32_t want = 0;
       if (nn) {
-        ad = g.adj[o];
-        if (ad.y + nn > g.ecap[o]) want = seg_cap_ep(ad.y + nn);
+        const uint32_t inf = L.oinf[oh];
+        uint32_t cap;
+        if (inf == EP_INF_RELOAD) {
+          ad = g.adj[o];
+          cap = g.ecap[o];
+        } else {
+          ad = make_uint2(L.oseg[oh], inf & ((1u << 27) - 1));
+          cap = (inf >> 27) == 31 ? 0u : (1u << (inf >> 27));
+        }
+        if (ad.y + nn > cap) want = seg_cap_ep(ad.y + nn);
       }
       const uint32_t v1[1] = {want};
       unsigned long long offs[1];
@@ -286,7 +323,7 @@ __global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
         L.ocnt[oh] = add ? ad.x + 1 : 0u;  // (LDS: two 1024-thread workgroups per CU need <= 80 KiB each)
         if (add) g.adj[o] = make_uint2(ad.x, ad.y + add);
         const int32_t dz = L.onz[oh] + (int32_t)add;  // new edges have nonzero counts
-        if (dz) g.nzdeg[o] = (uint32_t)((int32_t)g.nzdeg[o] + dz);
+        if (dz) atomicAdd(&g.nzdeg[o], (uint32_t)dz);  // no return: nothing waits for it
         L.onz[oh] = (int32_t)ad.y;
       }
     }
@@ -294,29 +331,25 @@ __global__ __launch_bounds__(EP_WG) void k_ep_owner(DevGraph g, EdgeArgs a) {
     // the new edges, after their owner's old degree; each appends its reverse
     // candidate to its target's segment (or to the overflow list)
     uint32_t ovf = 0, nt = 0, ridx = 0, cand = 0, nbk = 0, nidx = 0;
-    if (tid < np) {
-      const uint32_t rk = L.rank[ph];
-      const uint64_t key = L.key[ph];
-      if (rk < EP_SKIP) {  // not EP_SKIP / EP_EXIST
-        const uint32_t o = (uint32_t)(key >> 32);
-        nt = (uint32_t)key;
-        const uint32_t oh = ep_owner_slot(L, o);
-        if (L.ocnt[oh]) {  // else the pool is full (error set)
-          nidx = (uint32_t)L.onz[oh] + rk;
-          const int32_t d = L.sum[ph];
-          nbk = L.bkt[ph];
-          g.pool[(uint64_t)(L.ocnt[oh] - 1) + nidx] = pack_edge(nt, d);
-          cand = o | (d > 0 ? RC_POS : 0u);
-          const uint32_t cap = g.rcap[nt];
-          const unsigned long long old = atomicAdd((unsigned long long *)&g.radj[nt], 1ull << 32);
-          ridx = (uint32_t)(old >> 32);
-          if (ridx < cap) {
-            g.rpool[(uint64_t)(uint32_t)old + ridx] = cand;
-            g.etab[nbk].val = nidx;
-            g.etab[nbk].rev = ridx;
-          } else {
-            ovf = 1;
-          }
+    if (tid < np && rk < EP_SKIP) {  // not EP_SKIP / EP_EXIST
+      const uint32_t o = (uint32_t)(pkey >> 32);
+      nt = (uint32_t)pkey;
+      const uint32_t oh = ep_owner_slot(L, o);
+      if (L.ocnt[oh]) {  // else the pool is full (error set)
+        nidx = (uint32_t)L.onz[oh] + rk;
+        const int32_t d = psum;
+        nbk = pbk;
+        g.pool[(uint64_t)(L.ocnt[oh] - 1) + nidx] = pack_edge(nt, d);
+        cand = o | (d > 0 ? RC_POS : 0u);
+        const uint32_t cap = rcap_t;
+        const unsigned long long old = atomicAdd((unsigned long long *)&g.radj[nt], 1ull << 32);
+        ridx = (uint32_t)(old >> 32);
+        if (ridx < cap) {
+          g.rpool[(uint64_t)(uint32_t)old + ridx] = cand;
+          g.etab[nbk].val = nidx;
+          g.etab[nbk].rev = ridx;
+        } else {
+          ovf = 1;
         }
       }
     }

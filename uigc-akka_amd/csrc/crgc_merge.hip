@@ -43,7 +43,7 @@ __device__ inline int id_probe_from(const DevGraph &g, uint64_t id, uint64_t h, 
   return id_probe(g, id, bucket, slot);
 }
 
-__global__ __launch_bounds__(IDS_THREADS) void k_ids(DevGraph g, IdArgs a) {
+__global__ __launch_bounds__(IDS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_ids(DevGraph g, IdArgs a) {
   uint64_t cnt[5], total = 0;
   for (int k = 0; k < 5; ++k) {
     cnt[k] = k < a.nseg ? (a.seg[k].n_dev ? (uint64_t)*a.seg[k].n_dev : a.seg[k].n) : 0;

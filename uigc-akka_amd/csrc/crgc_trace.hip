@@ -423,7 +423,7 @@ __device__ inline void expand_bytes_out(const DevGraph &g, uint32_t nb2) {
   if (threadIdx.x == 0) g.xbytes[blockIdx.x] += s_nb / 2;
 }
 
-__global__ __launch_bounds__(256) void k_expand(DevGraph g, LevelArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_expand(DevGraph g, LevelArgs a) {
   constexpr int U = EXPAND_U;
   __shared__ uint32_t s_start[4][65];
   __shared__ uint32_t s_off[4][64];
