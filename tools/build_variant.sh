@@ -2,7 +2,7 @@
 # Build the working tree's HIP shim with one source edit applied to a copy, into
 # uigc-akka_amd/lib/ab/<name>.so (experiments for tools/gpu_ab2.sh; the tree
 # itself is not touched).  Runs here, on the CPU.
-# usage: bash tools/build_variant.sh <name> <file.hip> <python-replace-script>
+# usage: bash tools/build_variant.sh <name> <file.hip> <python-replace-script | ->
 #   the script reads the source from stdin and writes the edited one to stdout
 set -euo pipefail
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -14,8 +14,9 @@ mkdir -p "$T/a"
 cp -r "$ROOT/uigc-akka_amd/csrc" "$T/a/csrc"  # csrc/../../include is $T/include
 mkdir -p "$T/include" "$T/obj" "$ROOT/uigc-akka_amd/lib/ab"
 cp "$ROOT/include/crgc.h" "$T/include/"
-python3 -c "$EDIT" < "$ROOT/uigc-akka_amd/csrc/$FILE" > "$T/a/csrc/$FILE"
-if cmp -s "$ROOT/uigc-akka_amd/csrc/$FILE" "$T/a/csrc/$FILE"; then
+# EDIT "-": the working tree as it is
+[ "$EDIT" != "-" ] && python3 -c "$EDIT" < "$ROOT/uigc-akka_amd/csrc/$FILE" > "$T/a/csrc/$FILE"
+if [ "$EDIT" != "-" ] && cmp -s "$ROOT/uigc-akka_amd/csrc/$FILE" "$T/a/csrc/$FILE"; then
   echo "edit changed nothing" >&2
   exit 1
 fi

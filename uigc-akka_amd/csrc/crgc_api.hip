@@ -267,6 +267,7 @@ struct crgc_graph {
   // it on C2, profiles/r3f/ab_merge.txt)
   bool use_side = false;
   bool chunk_host = true;  // CRGC_CHUNK_HOST=0: large host batches in one piece
+  uint32_t chunk_max = 4;  // CRGC_CHUNK_MAX: at most this many chunks (2 .. 4)
   // last trace
   uint64_t last_garbage = 0, last_kill = 0, last_live = 0;
   crgc_trace_stats last_stats{};
@@ -559,6 +560,7 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
       if (hipEventCreate(&e) != hipSuccess) rc = CRGC_E_DEVICE;
     if (const char *m = getenv("CRGC_SIDE_STREAM")) h->use_side = atoi(m) != 0;  // A/B switch
     if (const char *m = getenv("CRGC_CHUNK_HOST")) h->chunk_host = atoi(m) != 0;
+    if (const char *m = getenv("CRGC_CHUNK_MAX")) h->chunk_max = std::min<uint32_t>(4, std::max(2, atoi(m)));
     if (hipStreamCreateWithFlags(&h->cpy, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_cstart, hipEventDisableTiming) != hipSuccess)
       rc = CRGC_E_DEVICE;
@@ -1143,11 +1145,11 @@ static int merge_entries_routed(crgc_graph *h, const crgc_entry_batch *b, int vr
   return merge_entries_one(h, &v, Ct, St, Ut);
 }
 
-// A large host batch in K chunks of whole entries: chunk j's arrays are copied
-// on the copy stream while chunks < j merge on the graph's stream, so the
-// hand-off's PCIe time overlaps the merge (pinned buffers registered with
-// crgc_host_register copy by DMA; pageable ones through the driver's staging,
-// which still overlaps the kernels already queued).  Every chunk is a merge of
+// A large pageable host batch in K chunks of whole entries: chunk j's arrays
+// are copied on the copy stream while chunks < j merge on the graph's stream,
+// so the hand-off's PCIe time overlaps the merge (C2: 3.4 ms per wakeup
+// against 4.9 ms in one piece; batches in buffers registered with
+// crgc_host_register are copied whole, host_registered below).  Every chunk is a merge of
 // its own (its own epoch): merges commute, and the last-write-wins fields
 // follow chunk order, then record order — the batch's order.
 // Offsets are rebased on the device (k_rebase).  The caller's buffers are
@@ -1247,6 +1249,31 @@ static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint3
   return rc;
 }
 
+// Whether every record array of a host batch lies in buffers registered with
+// crgc_host_register.  Such batches are copied whole: from registered memory
+// one large copy per array runs at ~57 GB/s but ~1 MB chunk copies at 4.4 GB/s
+// (profiles/r3g/pcie_probe.txt); unchunked, a registered C2 wakeup takes 2.3 ms
+// against 4.5 ms chunked (profiles/r3i/pcie.txt).  Pageable batches keep the chunks.
+static bool host_registered(const crgc_graph *h, const crgc_entry_batch *b, uint64_t C, uint64_t S,
+                            uint64_t U) {
+  if (h->pinned.empty()) return false;
+  const uint64_t n = b->n_entries;
+  const std::pair<const void *, uint64_t> arr[11] = {
+      {b->self, n * 8},          {b->recv_count, n * 2},     {b->flags, n},
+      {b->created_off, (n + 1) * 4}, {b->created_owner, C * 8}, {b->created_target, C * 8},
+      {b->spawned_off, (n + 1) * 4}, {b->spawned, S * 8},      {b->updated_off, (n + 1) * 4},
+      {b->updated_ref, U * 8},   {b->updated_info, U * 2}};
+  for (const auto &a : arr) {
+    if (!a.second) continue;
+    const char *p = (const char *)a.first;
+    bool in = false;
+    for (const auto &r : h->pinned)
+      if (p >= r.first && p + a.second <= r.first + r.second) in = true;
+    if (!in) return false;
+  }
+  return true;
+}
+
 int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
   if (int rc = check_graph(h)) return rc;
   DeviceGuard dg(h->device);
@@ -1254,8 +1281,9 @@ int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
   const int vrc = entry_counts(h, b, h->tp, &C, &S, &U);
   if (!h->tp) {
     if (vrc) return vrc;
-    if (b->memory == CRGC_MEM_HOST && b->n_entries >= 2 * CHUNK_MIN && h->chunk_host)
-      return merge_entries_chunked(h, b, (uint32_t)std::min<uint64_t>(CHUNK_MAX, b->n_entries / CHUNK_MIN));
+    if (b->memory == CRGC_MEM_HOST && b->n_entries >= 2 * CHUNK_MIN && h->chunk_host &&
+        !host_registered(h, b, C, S, U))
+      return merge_entries_chunked(h, b, (uint32_t)std::min<uint64_t>(h->chunk_max, b->n_entries / CHUNK_MIN));
     return merge_entries_one(h, b, C, S, U);
   }
   if (h->route && h->G <= ROUTE_MAX_SHARDS && h->F <= ROUTE_MAX_F)
@@ -2049,6 +2077,19 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
   }
 }
 
+// A host pointer the device can store to (page-locked or registered memory),
+// or nullptr (pageable memory, or not a host pointer the runtime knows).
+static uint64_t *device_view(uint64_t *p) {
+  if (!p) return nullptr;
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: not an error for the caller
+    return nullptr;
+  }
+  if (at.type != hipMemoryTypeHost || !at.devicePointer) return nullptr;
+  return (uint64_t *)at.devicePointer;
+}
+
 static int copy_lists(crgc_graph *h, crgc_trace_out *out, bool sync = true) {
   bool big = false;
   out->n_garbage = h->last_garbage;
@@ -2155,14 +2196,20 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   LevelRun lr;
   uint64_t rounds = 0, ids_sent = 0, x_bytes = 0;
   double ms_x = 0;
+  bool direct = false;  // the lists are in the caller's buffers already
   if (!h->tp) {
     // The sweep is enqueued behind every level chunk and runs only once the
     // mark is done (mark_done), together with the counter read-back, so a
     // steady-state wakeup has one host synchronisation for mark + sweep.
+    // caller buffers the device can write (page-locked / registered): the
+    // lists go there behind the sweep, and the trace needs one host round trip
+    uint64_t *dg = device_view(out->garbage_ids), *dk = device_view(out->kill_ids);
     auto sweep = [&]() -> hipError_t {
       hipError_t e = hipEventRecord(h->ev[1], h->stream);
       if (e == hipSuccess) e = launch_sweep(h->g.d, should_kill ? 1 : 0, top, h->stream);
       if (e == hipSuccess) e = hipEventRecord(h->ev[2], h->stream);
+      if (e == hipSuccess && (dg || dk))
+        e = launch_copy_lists(h->g.d, dg, dg ? out->garbage_cap : 0, dk, dk ? out->kill_cap : 0, h->stream);
       if (e == hipSuccess)
         e = hipMemcpyAsync(h->hctr, h->ctr, offsetof(Counters, ring), hipMemcpyDeviceToHost, h->stream);
       return e;
@@ -2172,6 +2219,9 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
     lr.defer = true;
     if (int rc = run_levels(h, false, 0, top, true, 0, lr, &end, sweep)) return rc;
     absorb_counters(h);  // read back with the last chunk's level counts
+    const Counters &cc = *h->hctr;
+    direct = (dg || dk) && (!out->garbage_ids || (dg && cc.n_garbage <= out->garbage_cap)) &&
+             (!out->kill_ids || (dk && cc.n_kill <= out->kill_cap));
   } else {
     if (int rc = mark_all(h, false, 0, top, lr, &rounds, &ids_sent, &ms_x, &x_bytes)) return rc;
     HIP_TRY(hipEventRecord(h->ev[1], h->stream));
@@ -2186,12 +2236,19 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   h->last_kill = c.n_kill;
   h->last_live = c.n_live;
   // result copies first; the event queries overlap them
-  const int rc = copy_lists(h, out, /*sync=*/false);
+  int rc = CRGC_OK;
+  if (direct) {
+    out->n_garbage = h->last_garbage;
+    out->n_kill = h->last_kill;
+    out->n_live = h->last_live;
+  } else {
+    rc = copy_lists(h, out, /*sync=*/false);
+  }
   if (lr.pending) {
     lr.pending();
     lr.pending = nullptr;
   }
-  HIP_TRY(hsync(h));
+  if (!direct) HIP_TRY(hsync(h));
   crgc_trace_stats st{};
   st.edges_scanned = c.edges_scanned;
   st.sup_edges = c.sup_edges;

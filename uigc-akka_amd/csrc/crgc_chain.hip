@@ -24,7 +24,7 @@
 namespace crgc {
 
 constexpr uint32_t CH_NONE = 0xFFFFFFFFu;
-constexpr int STAT_SUP_SLOT = 1, STAT_EDGES_SLOT = 2;  // crgc_trace.hip STAT_SUP / STAT_EDGES of block 0
+constexpr int STAT_SUP_SLOT = 1;  // crgc_trace.hip STAT_SUP of block 0
 constexpr uint32_t CH_COMPLEX = 0xFFFFFFFEu;
 
 __device__ inline bool bit_of(const uint32_t *bm, uint32_t v) { return (bm[v >> 5] >> (v & 31)) & 1u; }

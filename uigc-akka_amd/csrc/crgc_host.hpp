@@ -220,6 +220,8 @@ hipError_t launch_trace_reset(const DevGraph &g, uint64_t nblk, uint32_t ctr_fro
 hipError_t launch_sweep(const DevGraph &g, int should_kill, uint64_t slot_top, hipStream_t s,
                         int phase = 3);
 int level_grid(uint64_t slot_top);
+hipError_t launch_copy_lists(const DevGraph &g, uint64_t *gdst, uint64_t gcap, uint64_t *kdst, uint64_t kcap,
+                             hipStream_t s);
 // sharded graphs
 hipError_t launch_list(const DevGraph &g, int mode, bool scatter, uint32_t *buf, uint32_t *cnt,
                        uint64_t nblk, uint64_t *send, uint32_t *send_slot, hipStream_t s);

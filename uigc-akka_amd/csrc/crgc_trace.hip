@@ -1123,7 +1123,6 @@ __global__ __launch_bounds__(256) void k_sweep(DevGraph g, int should_kill) {
     const uint64_t base = (uint64_t)blk * BLK_SLOTS + (uint64_t)lane * 32;
     const uint32_t word = g.vis[(uint64_t)blk * 64 + lane];
     const uint4 f4[2] = {*(const uint4 *)(g.flags + base), *(const uint4 *)(g.flags + base + 16)};
-    const uint8_t *fb = (const uint8_t *)f4;
     const uint32_t fa = flag_bits(f4, FL_ALIVE), fp = flag_bits(f4, FL_PROXY);
     const uint32_t alive = fa & ~fp, prox = fa & fp;
     const uint32_t halted = flag_bits(f4, FL_HALTED), local = flag_bits(f4, FL_LOCAL);
@@ -1321,6 +1320,30 @@ __global__ __launch_bounds__(256) void k_sweep_gather(DevGraph g) {
     }
     for (uint32_t i = lane_id(); i < kn; i += 64) g.out_kill[ko + i] = g.vid[ka[i]];
   }
+}
+
+// The garbage / kill ids straight into the caller's device-accessible host
+// buffers (page-locked or registered), behind the sweep on the same stream, so
+// a trace needs one host synchronisation, not two (counters, then copies of
+// their size).  A list longer than its buffer, an NPE or a mark that is not done
+// yet copies nothing; the host then takes the copy path (and its E2BIG).
+__global__ __launch_bounds__(256) void k_copy_lists(DevGraph g, uint64_t *gdst, uint64_t gcap, uint64_t *kdst,
+                                                    uint64_t kcap) {
+  const Counters *c = g.ctr;
+  if (!c->mark_done || c->npe) return;
+  const uint64_t ng = c->n_garbage, nk = c->n_kill;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  const uint64_t t0 = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gdst && ng <= gcap)
+    for (uint64_t i = t0; i < ng; i += stride) gdst[i] = g.out_ids[i];
+  if (kdst && nk <= kcap)
+    for (uint64_t i = t0; i < nk; i += stride) kdst[i] = g.out_kill[i];
+}
+
+hipError_t launch_copy_lists(const DevGraph &g, uint64_t *gdst, uint64_t gcap, uint64_t *kdst, uint64_t kcap,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(k_copy_lists, dim3(64), dim3(256), 0, s, g, gdst, gcap, kdst, kcap);
+  return hipGetLastError();
 }
 
 hipError_t launch_sweep(const DevGraph &g, int should_kill, uint64_t slot_top, hipStream_t s,
