@@ -204,6 +204,7 @@ struct Knobs {
   uint32_t xclosure_after = 8;   // CRGC_XCLOSURE_AFTER
   uint32_t xclosure_narrow = 1024;  // CRGC_XCLOSURE_NARROW
   uint32_t xslices = 1;          // CRGC_XSLICES: push-level target slices (1, 2, 4, 8)
+  bool bin = true;               // CRGC_BIN=0: the pseudo-root level pushes candidate bytes directly
   void read() {
     auto env = [](const char *k) { return getenv(k); };
     if (const char *m = env("CRGC_PULL")) pull = atoi(m) != 0;
@@ -229,6 +230,7 @@ struct Knobs {
       buckets_log2 = std::min(10, std::max(1, atoi(m)));
     if (const char *m = env("CRGC_XCLOSURE_AFTER")) xclosure_after = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_XCLOSURE_NARROW")) xclosure_narrow = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_BIN")) bin = atoi(m) != 0;
     if (const char *m = env("CRGC_XSLICES")) {
       const uint32_t v = (uint32_t)strtoul(m, nullptr, 10);
       xslices = v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
@@ -285,6 +287,8 @@ struct crgc_graph {
   Scratch x_route, x_route_send, x_cat;  // routed entry merges
   Scratch x_dg, x_dg_out;    // DeltaGraph production
   Scratch x_chain;           // chain mode (crgc_chain.hip)
+  Scratch x_bin;             // the pseudo-root level's binned push: counters, then bin regions
+  void *x_bin_zeroed = nullptr;  // x_bin allocation whose counters were zeroed
   Scratch x_gc, x_gc_list;   // replicated chain closure of sharded marks (crgc_xchain.hip)
   uint64_t *h_small = nullptr;       // pinned host staging for small all-gathers
   char *h_route = nullptr;           // pinned RoutePart / ConcatPart tables
@@ -613,7 +617,7 @@ void crgc_destroy(crgc_graph *h) {
   h->work.release();
   for (Scratch *x : {&h->x_send, &h->x_slot, &h->x_recv, &h->x_ans, &h->x_ans_back, &h->x_small,
                      &h->x_pack, &h->x_pack_recv, &h->x_route, &h->x_route_send, &h->x_cat,
-                     &h->x_dg, &h->x_dg_out, &h->x_chain, &h->x_gc, &h->x_gc_list})
+                     &h->x_dg, &h->x_dg_out, &h->x_chain, &h->x_gc, &h->x_gc_list, &h->x_bin})
     x->release();
   if (h->ctr) hipFree(h->ctr);
   if (h->hctr) hipHostFree(h->hctr);
@@ -1643,6 +1647,30 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   la.xslices = kn.xslices;
   la.tail_start = std::min<uint32_t>(kn.tail_start, TAIL_QCAP);
   la.tail_max = std::min<uint32_t>(std::max(kn.tail_max, 1u), TAIL_QCAP);
+  // The pseudo-root level's binned push (crgc_trace.hip k_expand_bin): up to 256
+  // bins of >= 65536 slots (an LDS bitmap of <= 128 KiB each), regions for half
+  // the graph's edge keys; counters zeroed once, then reset by k_bin_apply.
+  if (roots && kn.bin && !kn.alpha && top > 0) {
+    uint32_t lg = 0;
+    while (lg < 63 && (1ull << lg) < top) ++lg;
+    const uint32_t shift = std::max<uint32_t>(16, lg > 8 ? lg - 8 : 0);
+    const uint64_t nb = (top + (1ull << shift) - 1) >> shift;
+    if (shift <= 20 && nb <= BIN_MAX) {
+      // BIN_SHARDS regions per bin; a full region falls back to direct stores
+      const uint64_t cap = std::max<uint64_t>(4096, (h->etab_used + h->atoms_since) / 2 / (nb * BIN_SHARDS));
+      const size_t cur_bytes = (size_t)(BIN_MAX * BIN_SHARDS + 4) * 4;
+      HIP_TRY(h->x_bin.ensure(cur_bytes + nb * BIN_SHARDS * cap * 4));
+      if (h->x_bin_zeroed != h->x_bin.ptr) {
+        HIP_TRY(hipMemsetAsync(h->x_bin.ptr, 0, cur_bytes, h->stream));
+        h->x_bin_zeroed = h->x_bin.ptr;
+      }
+      la.bin_cur = (uint32_t *)h->x_bin.ptr;
+      la.bins = (uint32_t *)((char *)h->x_bin.ptr + cur_bytes);
+      la.bin_shift = shift;
+      la.nbins = (uint32_t)nb;
+      la.bin_cap = (uint32_t)cap;
+    }
+  }
   // Device times, from timing-only events (no system-scope fence):
   //   every chunk of levels: an event pair around it (ms_mark, dispatch gaps included);
   //   CRGC_KERNEL_TIMING=1 (default): k_expand's start / stop carried by its dispatch;

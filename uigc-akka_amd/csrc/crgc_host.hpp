@@ -181,7 +181,16 @@ struct LevelArgs {
   uint32_t chain_after;    // k_tail hands a deep mark to chain mode after this many rounds (0: never)
   uint32_t xslices;        // push levels: 1, 2, 4 or 8 target slices (k_expand: XCD-local candidate stores)
   uint16_t location;
+  // the pseudo-root level's binned push (k_expand_bin / k_bin_apply), nbins == 0: off
+  uint32_t *bins;          // nbins x BIN_SHARDS regions of bin_cap target slots
+  uint32_t *bin_cur;       // [0] the binned-mode word, [4 ..] the regions' fill counts (zero between traces)
+  uint32_t bin_shift;      // a bin covers slots [b << bin_shift, (b + 1) << bin_shift)
+  uint32_t nbins;
+  uint32_t bin_cap;
 };
+constexpr uint32_t BIN_SHARDS = 8;   // fill counters per bin (workgroup % 8)
+constexpr uint32_t BIN_MAX = 256;    // bins at most (k_expand_bin's LDS staging)
+constexpr uint32_t BIN_SB = 32;      // staged targets per bin per workgroup (a round stages ~19 per bin at C2)
 
 // Chain mode (crgc_chain.hip).
 struct ChainArgs {

@@ -651,6 +651,238 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 
 
 // ---------------------------------------------------------------------------
+// The pseudo-root level's push, binned (round 3).  Level 0 of a wide trace
+// pushes ~1e7 candidate bytes to random slots of a ~10 MB byte map that no
+// XCD's 4 MB L2 holds: the edge stream takes ~22 us, the random byte stores
+// ~215 us (C2, profiles/r3g/lv1).  Binned, the stores become sequential:
+//   k_expand_bin   the level's edges as in k_expand, each target appended to
+//                  an LDS bin of its slot range (nbins <= 256 ranges of
+//                  2^bin_shift slots); the workgroups walk their units (light
+//                  chunks, hub pieces) in lock-step rounds of 4 (a unit per
+//                  wave), and after a round every bin holding >= BIN_SB / 2
+//                  targets is flushed to its global region (one atomic per bin
+//                  and workgroup, on one of BIN_SHARDS counters); a full LDS
+//                  bin or region falls back to the direct byte store, so
+//                  nothing is ever dropped.
+//   k_bin_apply    one workgroup per bin: its targets into an LDS bitmap of
+//                  the bin's slot range (8 loads in flight per thread), then the
+//                  range's candidate bytes OR-ed with it in 16-B groups
+//                  (sequential), counters reset.
+// (A slice per bin and workgroup, filled without atomics, two units per wave
+// and round: level 0 320 us against 202 us — profiles/r3g/ab10.)
+// Used only when the level-0 frontier is >= 1/32 of the slots (both kernels
+// derive the same answer; the mode word tells k_bin_apply).
+// ---------------------------------------------------------------------------
+__device__ inline bool bin_mode(const Counters *c, const LevelArgs &a) {
+  return a.nbins > 0 && a.nbins <= BIN_MAX && c->ring[0] * 32 >= c->slot_top;
+}
+
+
+__global__ __launch_bounds__(256) void k_expand_bin(DevGraph g, LevelArgs a) {
+  constexpr int U = EXPAND_U;
+  extern __shared__ __attribute__((aligned(16))) uint32_t bl[];
+  __shared__ uint32_t s_start[4][65];
+  __shared__ uint32_t s_off[4][64];
+  __shared__ uint32_t s_ulist[256], s_utag[256], s_wcnt[4], s_nact;
+  Counters *c = g.ctr;
+  if (c->tail_state) return;
+  const uint32_t NB = a.nbins;
+  uint32_t *lcnt = bl;                  // [NB] staged targets
+  uint32_t *fbase = bl + BIN_MAX;       // [NB] flush: region offset
+  uint32_t *fn = bl + 2 * BIN_MAX;      // [NB] flush: targets taken
+  uint32_t *lbuf = bl + 3 * BIN_MAX;    // [NB][BIN_SB]
+  const bool binned = bin_mode(c, a);
+  uint8_t *Fn = g.front[1];
+  const int wv = threadIdx.x >> 6, lane = lane_id(), tid = threadIdx.x;
+  const uint64_t G = gridDim.x, wg = blockIdx.x;
+  const uint32_t shard = (uint32_t)(wg % BIN_SHARDS);
+  const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
+  const uint64_t ncid = nblk * 32;
+  const uint64_t nh = min(c->qh[0], (unsigned long long)g.qh_cap);
+  const uint64_t nunits = ncid + nh;
+  uint32_t nb2 = 0;
+  for (uint32_t b = tid; b < BIN_MAX; b += 256) lcnt[b] = 0;
+  uint32_t *cur = a.bin_cur + 4;  // bin_cur[0]: the binned-mode word
+  if (binned && wg == 0 && tid == 0) a.bin_cur[0] = 1;
+  __syncthreads();
+
+  // one target: its bin, or (not binned / bin full) the byte at once
+  auto put = [&](uint32_t t) {
+    if (binned) {
+      const uint32_t b = t >> a.bin_shift;
+      const uint32_t pos = atomicAdd(&lcnt[b], 1u);
+      if (pos < BIN_SB) {
+        lbuf[b * BIN_SB + pos] = t;
+        return;
+      }
+    }
+    Fn[t] = 1;
+  };
+  // bins with >= thr targets to their regions: one atomic per bin (thread b
+  // of the workgroup, all in flight together), then every wave copies its bins'
+  // targets
+  auto flush = [&](uint32_t thr) {
+    if (tid < NB) {
+      const uint32_t n = min(lcnt[tid], BIN_SB);
+      const uint32_t take = n >= thr ? n : 0u;
+      fn[tid] = take;
+      fbase[tid] = take ? atomicAdd(&cur[tid * BIN_SHARDS + shard], take) : 0u;
+    }
+    __syncthreads();
+    for (uint32_t b = wv; b < NB; b += 4) {
+      const uint32_t n = fn[b];
+      if (lane < n) {
+        const uint32_t t = lbuf[b * BIN_SB + lane];
+        const uint32_t pos = fbase[b] + lane;
+        if (pos < a.bin_cap) a.bins[((uint64_t)b * BIN_SHARDS + shard) * a.bin_cap + pos] = t;
+        else Fn[t] = 1;  // region full: the byte at once
+        nb2 += 8;
+      }
+    }
+    __syncthreads();
+    if (tid < NB && fn[tid]) lcnt[tid] = 0;
+    __syncthreads();
+  };
+  auto edges = [&](const uint64_t (&ed)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (edge_count(ed[u]) > 0) put(edge_target(ed[u]));
+  };
+  auto unit = [&](uint64_t un, uint32_t tag) {
+    if (un < ncid) {  // light ranges: chunk (block b, k-th 64)
+      const uint64_t b = un % nblk;
+      const uint32_t k = (uint32_t)(un / nblk);
+      const uint32_t cnt = tag & 0xFFFu;
+      const uint32_t qi = k * 64 + lane;
+      const uint2 rr = qi < cnt ? g.qn_buf[b * BLK_SLOTS + qi] : make_uint2(0, 0);
+      nb2 += qi < cnt ? 16 : 0;
+      const uint32_t incl = wave_incl_scan(rr.y);
+      const uint32_t dtot = __shfl(incl, 63);
+      s_start[wv][lane] = incl - rr.y;
+      s_off[wv][lane] = rr.x;
+      wave_lds_fence();
+      for (uint32_t e0 = 0; e0 < dtot; e0 += 64 * U) {
+        uint64_t ed[U];
+#pragma unroll
+        for (int uu = 0; uu < U; ++uu) {
+          const uint32_t e = e0 + uu * 64 + lane;
+          ed[uu] = 0;
+          if (e < dtot) {
+            int lo = 0, hi = 63;
+            while (lo < hi) {
+              const int mid = (lo + hi + 1) >> 1;
+              if (s_start[wv][mid] <= e) lo = mid;
+              else hi = mid - 1;
+            }
+            ed[uu] = pool_load(&g.pool[(uint64_t)s_off[wv][lo] + (e - s_start[wv][lo])]);
+            nb2 += 16;
+          }
+        }
+        edges(ed);
+      }
+      wave_lds_fence();
+    } else {  // a hub piece
+      const uint2 rr = g.qh_buf[un - ncid];
+      nb2 += lane == 0 ? 16 : 0;
+      for (uint32_t e0 = 0; e0 < rr.y; e0 += 64 * U) {
+        uint64_t ed[U];
+#pragma unroll
+        for (int uu = 0; uu < U; ++uu) {
+          const uint32_t e = e0 + uu * 64 + lane;
+          ed[uu] = e < rr.y ? pool_load(&g.pool[(uint64_t)rr.x + e]) : 0;
+          nb2 += e < rr.y ? 16 : 0;
+        }
+        edges(ed);
+      }
+    }
+  };
+
+  // Unit ids are dealt round-robin over the workgroups (workgroup w, window i,
+  // thread t: id (256 i + t) G + w): light chunks with work cluster at the
+  // low ids (k = 0 .. 3 of every block at level 0), so consecutive windows
+  // would leave most workgroups idle.
+  for (uint64_t ub = 0; ub * G < nunits; ub += 256) {
+    // this window's units with work, compacted (ballot / popc per wave)
+    const uint64_t u = (ub + tid) * G + wg;
+    uint32_t tag = 0;
+    bool act = false;
+    if (u < ncid) {
+      tag = g.qn_tag[u % nblk];
+      act = (tag >> 12) == 1u && (tag & 0xFFFu) > (uint32_t)(u / nblk) * 64;
+      nb2 += 8;
+    } else if (u < nunits) {
+      act = true;
+    }
+    const uint64_t ball = __ballot(act);
+    if (lane == 0) s_wcnt[wv] = __popcll(ball);
+    __syncthreads();
+    uint32_t off = 0;
+    for (int w = 0; w < wv; ++w) off += s_wcnt[w];
+    if (act) {
+      const uint32_t i = off + __popcll(ball & lanemask_lt());
+      s_ulist[i] = (uint32_t)tid;
+      s_utag[i] = tag;
+    }
+    if (tid == 0) s_nact = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
+    __syncthreads();
+    const uint32_t nact = s_nact;
+    for (uint32_t r0 = 0; r0 < nact; r0 += 4) {
+      if (r0 + wv < nact) unit((ub + s_ulist[r0 + wv]) * G + wg, s_utag[r0 + wv]);
+      __syncthreads();
+      if (binned) flush(BIN_SB / 2);
+    }
+    __syncthreads();  // s_ulist is rewritten by the next window
+  }
+  if (binned) flush(1);
+  expand_bytes_out(g, nb2);
+}
+
+__global__ __launch_bounds__(1024) void k_bin_apply(DevGraph g, LevelArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t bm[];  // 2^bin_shift bits
+  if (!a.bins || a.bin_cur[0] == 0) return;  // level 0 was not binned
+  uint32_t *cur = a.bin_cur + 4;
+  const uint32_t b = blockIdx.x, tid = threadIdx.x;
+  const uint32_t span = 1u << a.bin_shift, words = span / 32;
+  for (uint32_t k = tid; k < words; k += 1024) bm[k] = 0;
+  __syncthreads();
+  uint32_t nb2 = 0;
+  // (8 or 16 loads in flight per thread made this kernel slower, not faster:
+  // 48 -> 79 us at C2, profiles/r3g/README.md)
+  for (uint32_t sh = 0; sh < BIN_SHARDS; ++sh) {
+    const uint32_t n = min(cur[b * BIN_SHARDS + sh], a.bin_cap);
+    const uint32_t *src = a.bins + ((uint64_t)b * BIN_SHARDS + sh) * a.bin_cap;
+    for (uint32_t i = tid; i < n; i += 1024) {
+      const uint32_t t = src[i] - (b << a.bin_shift);
+      atomicOr(&bm[t >> 5], 1u << (t & 31));
+      nb2 += 8;
+    }
+  }
+  __syncthreads();
+  uint8_t *Fn = g.front[1];
+  const uint64_t lo = (uint64_t)b << a.bin_shift;
+  const uint64_t top = g.ctr->slot_top;
+  const uint64_t hi = min(lo + span, (top + 15) & ~15ull);  // Fn holds scap >= this (a multiple of 2048)
+  for (uint64_t q = lo + (uint64_t)tid * 16; q < hi; q += 1024 * 16) {
+    const uint32_t rel = (uint32_t)(q - lo);
+    const uint32_t bits = (bm[rel >> 5] >> (rel & 31)) & 0xFFFFu;
+    if (!bits) continue;
+    uint4 v = *(const uint4 *)(Fn + q);
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if ((bits >> j) & 1u) w[j >> 2] |= 1u << (8 * (j & 3));
+    *(uint4 *)(Fn + q) = make_uint4(w[0], w[1], w[2], w[3]);
+    nb2 += 64;  // 16 B read + 16 B written
+  }
+  __syncthreads();
+  // every workgroup has read its counters: reset them (and the mode word) for the next trace
+  if (tid < BIN_SHARDS) cur[b * BIN_SHARDS + tid] = 0;
+  if (b == 0 && tid == 0) a.bin_cur[0] = 0;
+  const uint32_t ws = wave_sum(nb2);
+  if (lane_id() == 0 && ws) atomicAdd((unsigned long long *)&g.xbytes[b], (unsigned long long)(ws / 2));
+}
+
+// ---------------------------------------------------------------------------
 // k_tail: one workgroup finishes the mark once a sparse level's frontier is
 // narrow (deep chains and rings, the last levels of a wide trace): rounds over
 // a queue in place of level-kernel triples.  It replaces k_expand of the level
@@ -1064,6 +1296,17 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
   // level controller: the level count, and the narrow-frontier takeover
   hipExtLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, e[2], e[3], 0, g, a);
   // 8 WGs of 4 waves per CU
+  if (roots && a.nbins) {
+    // the pseudo-root level, binned when it is wide: both kernels timed as its expand
+    const size_t lds = (size_t)(3 * BIN_MAX + a.nbins * BIN_SB) * 4;
+    // as many workgroups as are resident at once (LDS-bound: ~4 KiB static besides)
+    const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, (uint32_t)((160u << 10) / (lds + 4608))));
+    const uint32_t bgrid = std::min<uint32_t>(STAT_WG, 256 * per_cu);
+    hipExtLaunchKernelGGL(k_expand_bin, dim3(bgrid), dim3(256), lds, s, e[4], nullptr, 0, g, a);
+    hipExtLaunchKernelGGL(k_bin_apply, dim3(a.nbins), dim3(1024), (size_t)(1u << a.bin_shift) / 8, s, nullptr,
+                          e[5], 0, g, a);
+    return hipGetLastError();
+  }
   auto expand = [&](auto kern) {
     hipExtLaunchKernelGGL(kern, dim3(STAT_WG), dim3(256), 0, s, e[4], e[5], 0, g, a);
   };
