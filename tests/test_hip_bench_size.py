@@ -152,3 +152,36 @@ def test_c3_chains_eight_shards(hip_mod, oracle_mod):
         assert g.export() == o.export()
     finally:
         g.close()
+
+
+def test_large_host_batches_chunked_and_registered(hip_mod, oracle_mod):
+    """Host batches of >= 2^19 entries take the merge's host paths (crgc_api.hip
+    crgc_merge_entries): a pageable batch is copied and merged in chunks, one
+    merge per chunk with its own epoch (merge_entries_chunked); a batch in a
+    buffer registered with crgc_host_register is copied whole.  Both graphs must
+    equal the oracle's after every merge, and their traces too
+    (ShadowGraph.java:64-156, 205-289)."""
+    from crgc_hip import HostArena
+    w = world.World(seed=0x5EED + 7)
+    w.bulk_graph(200_000, 2_000_000)
+    hp, hr, o = hip_mod.ShadowGraph(), hip_mod.ShadowGraph(), oracle_mod.OracleGraph()
+    loads = list(w.batches(1 << 20))
+    for b in loads:
+        hp.merge_entries(b.to_device())
+        hr.merge_entries(b.to_device())
+        o.merge_entries(b)
+    big = [w.wakeup(600_000, busy=18_000, pending=2_000) for _ in range(2)]
+    assert all(len(b.self) >= 1 << 19 for b in big)
+    arena = HostArena(max(b.nbytes() for b in big) * 1.1 + (1 << 20))
+    hr.register_host(arena.buf)
+    for b in big:
+        hp.merge_entries(b)                # pageable: chunked
+        hr.merge_entries(arena.pack(b))    # registered: whole
+        o.merge_entries(b)
+        want = o.export()
+        assert hp.export() == want
+        assert hr.export() == want
+        ro = o.trace(True)
+        _same(hp.trace(True), ro)
+        _same(hr.trace(True), ro)
+    hr.unregister_host(arena.buf)
