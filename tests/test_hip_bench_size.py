@@ -154,7 +154,7 @@ def test_c3_chains_eight_shards(hip_mod, oracle_mod):
         g.close()
 
 
-def test_large_host_batches_chunked_and_registered(hip_mod, oracle_mod):
+def test_large_host_batches_chunked_and_registered(hip_mod, oracle_mod, monkeypatch):
     """Host batches of >= 2^19 entries take the merge's host paths (crgc_api.hip
     crgc_merge_entries): a pageable batch is copied and merged in chunks, one
     merge per chunk with its own epoch (merge_entries_chunked); a batch in a
@@ -162,6 +162,7 @@ def test_large_host_batches_chunked_and_registered(hip_mod, oracle_mod):
     equal the oracle's after every merge, and their traces too
     (ShadowGraph.java:64-156, 205-289)."""
     from crgc_hip import HostArena
+    monkeypatch.setenv("CRGC_BIN_MIN_SLOTS", "0")  # and the pseudo-root level binned at this size
     w = world.World(seed=0x5EED + 7)
     w.bulk_graph(200_000, 2_000_000)
     hp, hr, o = hip_mod.ShadowGraph(), hip_mod.ShadowGraph(), oracle_mod.OracleGraph()

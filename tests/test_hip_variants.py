@@ -23,6 +23,8 @@ VARIANTS = [
     {"CRGC_PULL": "0"},                   # push only
     {"CRGC_TAIL": "0"},                   # no narrow-frontier takeover
     {"CRGC_TAIL_START": "1000000", "CRGC_TAIL_MAX": "64"},  # early takeover, frequent bails
+    {"CRGC_BIN_MIN_SLOTS": "0"},          # the pseudo-root level binned at this size too
+    {"CRGC_BIN": "0"},                    # the pseudo-root level's direct push
 ]
 
 

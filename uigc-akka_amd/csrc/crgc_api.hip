@@ -205,6 +205,8 @@ struct Knobs {
   uint32_t xclosure_narrow = 1024;  // CRGC_XCLOSURE_NARROW
   uint32_t xslices = 1;          // CRGC_XSLICES: push-level target slices (1, 2, 4, 8)
   bool bin = true;               // CRGC_BIN=0: the pseudo-root level pushes candidate bytes directly
+  uint64_t bin_min = 1ull << 22; // CRGC_BIN_MIN_SLOTS: binned only above this many slots (a smaller
+                                 // candidate byte map stays in the L2: C1 mark +10 us binned)
   void read() {
     auto env = [](const char *k) { return getenv(k); };
     if (const char *m = env("CRGC_PULL")) pull = atoi(m) != 0;
@@ -231,6 +233,7 @@ struct Knobs {
     if (const char *m = env("CRGC_XCLOSURE_AFTER")) xclosure_after = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_XCLOSURE_NARROW")) xclosure_narrow = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_BIN")) bin = atoi(m) != 0;
+    if (const char *m = env("CRGC_BIN_MIN_SLOTS")) bin_min = strtoull(m, nullptr, 10);
     if (const char *m = env("CRGC_XSLICES")) {
       const uint32_t v = (uint32_t)strtoul(m, nullptr, 10);
       xslices = v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
@@ -1650,7 +1653,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   // The pseudo-root level's binned push (crgc_trace.hip k_expand_bin): up to 256
   // bins of >= 65536 slots (an LDS bitmap of <= 128 KiB each), regions for half
   // the graph's edge keys; counters zeroed once, then reset by k_bin_apply.
-  if (roots && kn.bin && !kn.alpha && top > 0) {
+  if (roots && kn.bin && !kn.alpha && top > 0 && top >= kn.bin_min) {
     uint32_t lg = 0;
     while (lg < 63 && (1ull << lg) < top) ++lg;
     const uint32_t shift = std::max<uint32_t>(16, lg > 8 ? lg - 8 : 0);
