@@ -444,14 +444,15 @@ int ensure_capacity(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   auto fits = [&](uint64_t st, uint64_t pt, uint64_t rt, uint64_t eu) {
     const Caps &c = h->g.caps;
     return st + ids <= c.scap && (st + ids) * 10 <= c.hcap * 7 &&
-           pt + 2 * eu + 6 * atoms <= c.pcap && rt + 2 * eu + 6 * atoms <= c.pcap &&
+           pt + 2 * eu + 6 * atoms <= c.pcap && rt + 2 * eu + 6 * atoms + 4 * ids <= c.pcap &&
            (eu + atoms) * 10 <= c.ecap * 7;
   };
   // upper bounds since the last sync
   const uint64_t st = h->slot_top + h->ids_since;
   const uint64_t eu = h->etab_used + h->atoms_since;
   const uint64_t grow = 2 * (h->etab_used + h->atoms_since) + 6 * h->atoms_since;
-  if (fits(st, h->pool_top + grow, h->rpool_top + grow, eu)) return CRGC_OK;
+  // (+ 4 reverse-candidate entries per new shadow: k_ids' first segments)
+  if (fits(st, h->pool_top + grow, h->rpool_top + grow + 4 * h->ids_since, eu)) return CRGC_OK;
   HIP_TRY(sync_counters(h));
   if (int rc = device_error(h)) return rc;
   if (fits(h->slot_top, h->pool_top, h->rpool_top, h->etab_used)) return CRGC_OK;

@@ -29,6 +29,7 @@ constexpr int IDS_THREADS = 1024;
 #ifndef CRGC_IDS_K
 #define CRGC_IDS_K 1
 #endif
+constexpr uint32_t IDS_RCAP = 4;  // reverse-candidate entries a new shadow starts with
 constexpr int IDS_K = CRGC_IDS_K;  // ids per thread per round (4: merge +20 us on C2, profiles/r3f/ab_merge.txt)
 
 // Continues a probe whose first bucket `b` (at h) was already loaded.
@@ -110,11 +111,15 @@ __global__ __launch_bounds__(IDS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 
           ++nins;
           nhome += is_home(g, id[j]) ? 1u : 0u;
         }
-      unsigned long long *const ctrs[2] = {&g.ctr->slot_top, &g.ctr->inserted};
-      const uint32_t v[2] = {nins, nhome};
-      unsigned long long base[2];
-      block_append<2>(ctrs, v, base);
-      unsigned long long s = base[0];
+      // A new shadow starts with a reverse-candidate segment of IDS_RCAP
+      // entries: most take their first in-edges in this same merge, which would
+      // otherwise all go through k_rv_grow's overflow path (crgc_edges.hip §3).
+      unsigned long long *const ctrs[3] = {&g.ctr->slot_top, &g.ctr->inserted, &g.ctr->rpool_top};
+      const uint32_t v[3] = {nins, nhome, nins * IDS_RCAP};
+      unsigned long long base[3];
+      block_append<3>(ctrs, v, base);
+      unsigned long long s = base[0], ro = base[2];
+      const bool rfit = ro + (uint64_t)nins * IDS_RCAP <= g.rpcap;
 #pragma unroll
       for (int j = 0; j < IDS_K; ++j) {
         if (st[j] != RS_INSERTED) continue;
@@ -126,8 +131,13 @@ __global__ __launch_bounds__(IDS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 
           slot[j] = (uint32_t)s;
           g.vid[s] = id[j];
           g.flags[s] = home ? FL_ALIVE : (FL_ALIVE | FL_PROXY);
+          if (rfit) {
+            g.radj[s] = make_uint2((uint32_t)ro, 0u);
+            g.rcap[s] = IDS_RCAP;
+          }
         }
         ++s;
+        ro += IDS_RCAP;
         atomicExch(&g.htab[bucket[j]].val, slot[j]);
       }
 #pragma unroll
