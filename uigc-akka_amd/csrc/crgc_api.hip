@@ -250,6 +250,7 @@ struct crgc_graph {
   Arrays g;
   Counters *ctr = nullptr;   // device
   Counters *hctr = nullptr;  // pinned host mirror
+  Counters *hctr_dev = nullptr;  // its device view (k_publish stores the level loop's counters there)
   unsigned long long epoch = 0;
   bool poisoned = false;
   // exact values as of the last synchronisation + upper-bound increments since
@@ -320,9 +321,13 @@ int map_hip(hipError_t e) {
     if (_e != hipSuccess) return map_hip(_e);       \
   } while (0)
 
+// Every API entry point takes one.  It also drops a stale "last error" of this
+// thread: the launch helpers report hipGetLastError(), which must not pick up
+// an error an earlier call left behind (each call checks its own results).
 struct DeviceGuard {
   int prev = -1;
   explicit DeviceGuard(int dev) {
+    (void)hipGetLastError();
     hipGetDevice(&prev);
     if (prev != dev) hipSetDevice(dev);
   }
@@ -595,6 +600,10 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     }
     hipMemsetAsync(h->ctr, 0, sizeof(Counters), h->stream);
     memset(h->hctr, 0, sizeof(Counters));
+    if (hipHostGetDevicePointer((void **)&h->hctr_dev, h->hctr, 0) != hipSuccess || !h->hctr_dev) {
+      rc = CRGC_E_DEVICE;
+      break;
+    }
     const uint64_t v0 = cfg && cfg->vertex_capacity ? cfg->vertex_capacity : (1u << 16);
     const uint64_t e0 = cfg && cfg->edge_capacity ? cfg->edge_capacity : 8 * v0;
     Caps c = caps_for(v0, e0, v0, e0);
@@ -1734,24 +1743,27 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
     if (after_chunk) HIP_TRY(after_chunk());
     // counts of levels L-1 .. L+chunk-1
     const int first = L - 1, last = L + chunk - 1;
-    for (int lv = first; lv <= last;) {
-      const int i0 = lv % LEVEL_RING;
-      const int cnt = std::min(last - lv + 1, LEVEL_RING - i0);
-      HIP_TRY(hipMemcpyAsync(&ring[i0], (char *)h->ctr + CTR_OFF(ring) + i0 * 8, cnt * 8,
-                             hipMemcpyDeviceToHost, h->stream));
-      lv += cnt;
-    }
-    HIP_TRY(hipMemcpyAsync(tail, (char *)h->ctr + CTR_OFF(tail_state), 24, hipMemcpyDeviceToHost,
-                           h->stream));
+    const uint32_t nring = (uint32_t)std::min(last - first + 1, LEVEL_RING);
+    HIP_TRY(launch_publish(h->ctr, h->hctr_dev, (uint32_t)first, nring, h->stream));
     HIP_TRY(hsync(h));
+    for (uint32_t i = 0; i < nring; ++i) {
+      const int k = (first + (int)i) % LEVEL_RING;
+      ring[k] = h->hctr->ring[k];
+    }
+    tail[0] = h->hctr->tail_state;
+    tail[1] = h->hctr->tail_level;
+    tail[2] = h->hctr->tail_from;
     if (roots && first == 0) lr.roots = ring[0];
     if (tail[0] == TAIL_CHAINS) {  // k_tail handed a deep mark to chain mode, which finishes it
       HIP_TRY(chunk_event());  // chain mode's device time counts as mark time
       if (int rc = run_chains(h, investigate, top)) return rc;
       HIP_TRY(chunk_event());
       if (after_chunk) HIP_TRY(after_chunk());
-      HIP_TRY(hipMemcpyAsync(tail, (char *)h->ctr + CTR_OFF(tail_state), 24, hipMemcpyDeviceToHost, h->stream));
+      HIP_TRY(launch_publish(h->ctr, h->hctr_dev, 0, 0, h->stream));
       HIP_TRY(hsync(h));
+      tail[0] = h->hctr->tail_state;
+      tail[1] = h->hctr->tail_level;
+      tail[2] = h->hctr->tail_from;
     }
     if (tail[0] == TAIL_BAILED) {  // k_tail handed a wide frontier back: resume there
       if ((int)tail[1] <= last_bail || (uint64_t)tail[1] > (1ull << 19)) {
@@ -1790,19 +1802,29 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   }
 }
 
+// Event-pair time in ms, 0 when the runtime cannot give it (e.g. a timestamp
+// not yet written back): statistics only, and no error is left behind for the
+// next launch helper's hipGetLastError() to report.
+static float elapsed_ms(hipEvent_t a, hipEvent_t b) {
+  float t = 0;
+  if (hipEventElapsedTime(&t, a, b) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0.f;
+  }
+  return t;
+}
+
 // Device times of one run_levels call, from its events (host-side queries,
 // deferred by crgc_trace until the result copies are in flight).
 static void collect_times(crgc_graph *h, LevelRun &lr, size_t nl, size_t nc, int timing, bool log,
                           size_t first_level, size_t last, const std::vector<unsigned long long> &ring) {
   for (size_t i = 0; i + 1 < nc; i += 2) {
-    float t = 0;
-    hipEventElapsedTime(&t, h->chunk_ev[i], h->chunk_ev[i + 1]);
-    lr.ms += t;
+    lr.ms += elapsed_ms(h->chunk_ev[i], h->chunk_ev[i + 1]);
   }
   for (size_t i = 0; i < (timing ? nl : 0); ++i) {
     float t[3] = {0, 0, 0};
     for (int k = timing >= 2 ? 0 : 2; k < 3; ++k)
-      hipEventElapsedTime(&t[k], h->lvl_ev[6 * i + 2 * k], h->lvl_ev[6 * i + 2 * k + 1]);
+      t[k] = elapsed_ms(h->lvl_ev[6 * i + 2 * k], h->lvl_ev[6 * i + 2 * k + 1]);
     lr.ms_f += t[0];
     lr.ms_t += t[1];
     lr.ms_e += t[2];
@@ -2242,9 +2264,7 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
       if (e == hipSuccess) e = hipEventRecord(h->ev[2], h->stream);
       if (e == hipSuccess && (dg || dk))
         e = launch_copy_lists(h->g.d, dg, dg ? out->garbage_cap : 0, dk, dk ? out->kill_cap : 0, h->stream);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(h->hctr, h->ctr, offsetof(Counters, ring), hipMemcpyDeviceToHost, h->stream);
-      return e;
+      return e;  // the counters come back with the chunk's k_publish
     };
     int end = 0;
     rounds = 1;
@@ -2296,9 +2316,7 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   st.ids_sent = ids_sent;
   st.exchange_bytes = x_bytes;
   st.ms_exchange = ms_x;
-  float ms = 0;
-  hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
-  st.ms_sweep = ms;
+  st.ms_sweep = elapsed_ms(h->ev[1], h->ev[2]);
   st.pseudo_roots = lr.roots;
   h->live = c.n_live;
   h->n_proxy = c.n_proxy;

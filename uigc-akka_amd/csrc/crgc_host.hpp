@@ -229,6 +229,7 @@ hipError_t launch_trace_reset(const DevGraph &g, uint64_t nblk, uint32_t ctr_fro
 hipError_t launch_sweep(const DevGraph &g, int should_kill, uint64_t slot_top, hipStream_t s,
                         int phase = 3);
 int level_grid(uint64_t slot_top);
+hipError_t launch_publish(const Counters *c, Counters *hdst, uint32_t r0, uint32_t rn, hipStream_t s);
 hipError_t launch_copy_lists(const DevGraph &g, uint64_t *gdst, uint64_t gcap, uint64_t *kdst, uint64_t kcap,
                              hipStream_t s);
 // sharded graphs

@@ -1589,6 +1589,26 @@ hipError_t launch_copy_lists(const DevGraph &g, uint64_t *gdst, uint64_t gcap, u
   return hipGetLastError();
 }
 
+// The counters the host loop reads after a level chunk (everything before the
+// level ring, and ring[r0 .. r0 + rn) mod LEVEL_RING) stored by the device into
+// the pinned host mirror: one small kernel instead of D2H copies into pageable
+// vectors, each of which waited for the stream and went through a staging buffer.
+__global__ __launch_bounds__(256) void k_publish(const Counters *c, Counters *hdst, uint32_t r0, uint32_t rn) {
+  constexpr uint32_t PRE = (uint32_t)(offsetof(Counters, ring) / 8);
+  const unsigned long long *src = (const unsigned long long *)c;
+  unsigned long long *dst = (unsigned long long *)hdst;
+  for (uint32_t i = threadIdx.x; i < PRE; i += 256) dst[i] = src[i];
+  for (uint32_t i = threadIdx.x; i < rn; i += 256) {
+    const uint32_t k = (r0 + i) % LEVEL_RING;
+    hdst->ring[k] = c->ring[k];
+  }
+}
+
+hipError_t launch_publish(const Counters *c, Counters *hdst, uint32_t r0, uint32_t rn, hipStream_t s) {
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, c, hdst, r0, rn);
+  return hipGetLastError();
+}
+
 hipError_t launch_sweep(const DevGraph &g, int should_kill, uint64_t slot_top, hipStream_t s,
                         int phase) {
   const int grid = level_grid(slot_top);
