@@ -39,7 +39,8 @@
 extern "C" {
 #endif
 
-#define CRGC_ABI_VERSION 3u  /* 2: crgc_trace_stats.expand_launches / expand_bytes; 3: exchange_bytes */
+#define CRGC_ABI_VERSION 4u  /* 2: crgc_trace_stats.expand_launches / expand_bytes; 3: exchange_bytes;
+                                 4: time_query_failures, direct_lists */
 
 /* ---- status codes ------------------------------------------------------- */
 #define CRGC_OK 0
@@ -109,7 +110,7 @@ uint32_t crgc_shard_of(uint64_t id, uint32_t n_shards);
 typedef struct crgc_config {
   uint32_t abi_version;        /* CRGC_ABI_VERSION                          */
   int32_t device;              /* HIP device ordinal                        */
-  uint32_t entry_field_size;   /* F, uigc.crgc.entry-field-size (default 4; at most 255) */
+  uint32_t entry_field_size;   /* F, uigc.crgc.entry-field-size (default 4)  */
   uint32_t delta_graph_size;   /* uigc.crgc.delta-graph-size (default 64)   */
   uint64_t vertex_capacity;    /* hint: expected live shadows (this shard)  */
   uint64_t edge_capacity;      /* hint: expected live (owner,target) pairs  */
@@ -197,6 +198,12 @@ typedef struct crgc_trace_stats {
   /* sharded graphs: bytes this shard sent in mark rounds (ids, home slots,
      frontier bitmaps) and in the home-slot resolution before them */
   uint64_t exchange_bytes;
+  /* device-time queries (event pairs) the runtime could not answer; their ms
+     count as 0, so a nonzero value means the ms_* fields above are short */
+  uint64_t time_query_failures;
+  /* 1: the garbage / kill ids were stored by the device straight into the
+     caller's page-locked buffers (no copy-back round trip) */
+  uint64_t direct_lists;
 } crgc_trace_stats;
 
 typedef struct crgc_trace_out {

@@ -15,8 +15,10 @@
 //          supervisor edges, halted shadows marked but not expanded; sweep.
 // Collected slots are never reused (the incarnation rule E9 holds as in the
 // HIP graph: edges to them have count <= 0 or come from halted owners).
-// Not a checker and not the product: tests/test_omp_graph_cpu.py compares its
-// garbage / kill counts with the oracle's, bench.py times it.
+// Not the product.  tests/test_omp_graph_cpu.py pins its garbage / kill sets to
+// the oracle's; bench.py times it; the full-size GPU parity tests
+// (tests/test_hip_full_size.py) use it as the checker where the single-thread
+// oracle would take too long.
 #include <omp.h>
 #include <parallel/algorithm>
 
@@ -240,9 +242,12 @@ int omp_graph_merge(void *h, const crgc_entry_batch *b, int threads) {
 }
 
 // ShadowGraph.trace(shouldKill).  Returns 0 or CRGC_E_NULL_SUPERVISOR (graph
-// unchanged).  Counts only; *edges = traced (nonzero) out-edges.
+// unchanged).  *edges = traced (nonzero) out-edges.  With id buffers the
+// garbage / kill ids are written too (order unspecified; CRGC_E2BIG, after the
+// trace, when a capacity is short — the counts are exact either way).
 int omp_graph_trace(void *h, int should_kill, int threads, uint64_t *n_garbage, uint64_t *n_kill, uint64_t *n_live,
-                    uint64_t *edges, uint64_t *pseudo_roots) {
+                    uint64_t *edges, uint64_t *pseudo_roots, uint64_t *garbage_ids, uint64_t garbage_cap,
+                    uint64_t *kill_ids, uint64_t kill_cap) {
   Graph &g = *(Graph *)h;
   if (threads > 0) omp_set_num_threads(threads);
   const uint64_t top = g.slot_top;
@@ -291,19 +296,36 @@ int omp_graph_trace(void *h, int should_kill, int threads, uint64_t *n_garbage, 
     front.swap(next);
   }
   uint64_t ng = 0, nk = 0, nl = 0, npe = 0;
-#pragma omp parallel for schedule(static) reduction(+ : ng, nk, nl, npe)
-  for (uint64_t v = 0; v < top; ++v) {
-    const uint8_t f = g.flags[v];
-    if (!(f & ALIVE)) continue;
-    if (g.mark[v]) {
-      ++nl;
-      continue;
+  const bool want_ids = garbage_ids || kill_ids;
+  std::vector<uint64_t> gl, kl;
+#pragma omp parallel
+  {
+    std::vector<uint64_t> mg, mk;
+#pragma omp for schedule(static) reduction(+ : ng, nk, nl, npe)
+    for (uint64_t v = 0; v < top; ++v) {
+      const uint8_t f = g.flags[v];
+      if (!(f & ALIVE)) continue;
+      if (g.mark[v]) {
+        ++nl;
+        continue;
+      }
+      ++ng;
+      if (want_ids) mg.push_back(g.vid[v]);
+      if (f & LOCAL) {
+        const uint32_t s = g.sup[v];
+        if (s == NONE) ++npe;
+        else if (should_kill && !(f & HALTED) && g.mark[s] && (g.flags[s] & ALIVE)) {
+          ++nk;
+          if (want_ids) mk.push_back(g.vid[v]);
+        }
+      }
     }
-    ++ng;
-    if (f & LOCAL) {
-      const uint32_t s = g.sup[v];
-      if (s == NONE) ++npe;
-      else if (should_kill && !(f & HALTED) && g.mark[s] && (g.flags[s] & ALIVE)) ++nk;
+    if (want_ids) {
+#pragma omp critical
+      {
+        gl.insert(gl.end(), mg.begin(), mg.end());
+        kl.insert(kl.end(), mk.begin(), mk.end());
+      }
     }
   }
   if (npe) return CRGC_E_NULL_SUPERVISOR;
@@ -316,13 +338,22 @@ int omp_graph_trace(void *h, int should_kill, int threads, uint64_t *n_garbage, 
     g.flags[v] = 0;
     std::vector<Edge>().swap(g.out[v]);
   }
+  bool big = false;
+  if (garbage_ids) {
+    if (gl.size() <= garbage_cap) std::copy(gl.begin(), gl.end(), garbage_ids);
+    else big = true;
+  }
+  if (kill_ids) {
+    if (kl.size() <= kill_cap) std::copy(kl.begin(), kl.end(), kill_ids);
+    else big = true;
+  }
   g.n_live = nl;
   *n_garbage = ng;
   *n_kill = nk;
   *n_live = nl;
   *edges = ed;
   *pseudo_roots = pr;
-  return 0;
+  return big ? CRGC_E2BIG : 0;
 }
 
 }  // extern "C"

@@ -33,7 +33,9 @@ OMP_LIB_PATH = os.path.join(_HERE, "_build", "libcrgc_omp.so")
 
 def build(force: bool = False) -> str:
     """Compile the oracle (and the OpenMP bench baseline) with g++ (oracle/Makefile)."""
-    fresh = all(os.path.exists(lib) and os.path.getmtime(lib) >= os.path.getmtime(os.path.join(_HERE, src))
+    hdrs = [os.path.join(_REPO, "include", "crgc.h"), os.path.join(_HERE, "crgc_oracle.h")]
+    fresh = all(os.path.exists(lib) and
+                all(os.path.getmtime(lib) >= os.path.getmtime(f) for f in [os.path.join(_HERE, src)] + hdrs)
                 for lib, src in ((LIB_PATH, "crgc_oracle.cpp"), (OMP_LIB_PATH, "omp_graph.cpp")))
     if not force and fresh:
         return LIB_PATH
@@ -131,8 +133,10 @@ class OracleGraph:
 
 
 class OmpGraph:
-    """BENCH ONLY: the strong CPU baseline (oracle/omp_graph.cpp), a parallel
-    OpenMP merge + trace over the same entry batches.  Counts only."""
+    """The strong CPU baseline (oracle/omp_graph.cpp), a parallel OpenMP merge +
+    trace over the same entry batches: bench.py times it, and the full-size
+    GPU parity tests check the HIP graph against it (its sets are pinned to the
+    oracle's by tests/test_omp_graph_cpu.py)."""
 
     def __init__(self, F: int = 4, vertex_hint: int = 1 << 16, threads: int = 0):
         build()
@@ -141,9 +145,11 @@ class OmpGraph:
         lib.omp_graph_create.argtypes = [C.c_uint32, C.c_uint64]
         lib.omp_graph_destroy.argtypes = [C.c_void_p]
         lib.omp_graph_merge.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
-        lib.omp_graph_trace.argtypes = [C.c_void_p, C.c_int, C.c_int] + [C.POINTER(C.c_uint64)] * 5
+        lib.omp_graph_trace.argtypes = ([C.c_void_p, C.c_int, C.c_int] + [C.POINTER(C.c_uint64)] * 5 +
+                                        [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64])
         self.lib, self.threads = lib, threads
         self.h = lib.omp_graph_create(F, vertex_hint)
+        self._ids = None
 
     def close(self):
         if self.h:
@@ -161,9 +167,28 @@ class OmpGraph:
         if rc:
             raise abi.CrgcError(rc, "omp_graph_merge")
 
-    def trace(self, should_kill: bool = True) -> dict:
+    def trace(self, should_kill: bool = True, ids: bool = False) -> dict:
+        """Counts; with ids=True also 'garbage_ids' / 'kill_ids' (unsorted)."""
         v = [C.c_uint64() for _ in range(5)]
-        rc = self.lib.omp_graph_trace(self.h, int(should_kill), self.threads, *[C.byref(x) for x in v])
+        g = k = None
+        if ids:
+            if self._ids is None:
+                self.reserve_ids(1 << 16)
+            g, k = self._ids
+        rc = self.lib.omp_graph_trace(self.h, int(should_kill), self.threads, *[C.byref(x) for x in v],
+                                      g.ctypes.data if ids else None, len(g) if ids else 0,
+                                      k.ctypes.data if ids else None, len(k) if ids else 0)
+        if rc == abi.E2BIG:  # the trace happened (counts exact): the ids of this one are lost
+            self.reserve_ids(2 * int(max(v[0].value, v[1].value)) + 1024)
+            raise abi.CrgcError(rc, "omp_graph_trace: id buffers too small (grown for the next trace)")
         if rc:
             raise abi.CrgcError(rc, "omp_graph_trace")
-        return dict(zip(("garbage", "kill", "live", "edges_scanned", "pseudo_roots"), (x.value for x in v)))
+        out = dict(zip(("garbage", "kill", "live", "edges_scanned", "pseudo_roots"), (x.value for x in v)))
+        if ids:
+            out["garbage_ids"] = g[:out["garbage"]].copy()
+            out["kill_ids"] = k[:out["kill"]].copy()
+        return out
+
+    def reserve_ids(self, n: int):
+        """Id buffers for traces of up to n garbage shadows."""
+        self._ids = (np.zeros(n, np.uint64), np.zeros(n, np.uint64))

@@ -9,6 +9,11 @@ for sub in ("uigc-akka_amd", "workload", "oracle", "tests"):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# The tests drive the A/B variants and test hooks (CRGC_ALPHA, CRGC_XBITS, ...),
+# which the library reads only under this gate (crgc_api.hip Knobs); with no
+# hook variable set, every default is the production one.
+os.environ["CRGC_TEST_HOOKS"] = "1"
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")

@@ -1,7 +1,9 @@
-"""The strong CPU baseline (oracle/omp_graph.cpp, bench only) computes what the
-oracle computes: per wakeup, the same garbage / kill / live / pseudo-root /
-traced-edge counts on the C1 stream and a C2-shaped one (so bench.py's
-cpu_baseline times the same work as the GPU line)."""
+"""The strong CPU baseline (oracle/omp_graph.cpp) computes what the oracle
+computes: per wakeup, the same garbage and kill SETS and the same live /
+pseudo-root / traced-edge counts on the C1 stream and a C2-shaped one.  This
+pins it, so bench.py's cpu_baseline times the same work as the GPU line and the
+full-size GPU parity tests (tests/test_hip_full_size.py) may use it as the
+checker where the single-thread oracle would take too long."""
 import pytest
 
 import world
@@ -32,6 +34,8 @@ def test_omp_graph_matches_oracle(oracle_mod, make):
             b = w.wakeup(V // 10, busy=V * 9 // 100, pending=V // 100)
             o.merge_entries(b)
             p.merge_entries(b)
-        ro, rp = o.trace(True), p.trace(True)
+        ro, rp = o.trace(True), p.trace(True, ids=True)
         assert (len(ro.garbage), len(ro.kill), ro.n_live, ro.pseudo_roots, ro.edges_scanned) == \
             (rp["garbage"], rp["kill"], rp["live"], rp["pseudo_roots"], rp["edges_scanned"]), k
+        assert ro.garbage_set() == set(rp["garbage_ids"].tolist()), k
+        assert ro.kill_set() == set(rp["kill_ids"].tolist()), k

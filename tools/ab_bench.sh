@@ -2,6 +2,7 @@
 # Interleaved bench A/B over environment variants (each "K=V,K2=V2" or BASE),
 # two passes; ms_per_step, merge and mark per variant into summary.txt.
 # usage: bash tools/ab_bench.sh <tag> <variant>...
+export CRGC_TEST_HOOKS=1  # the env variants below are test hooks (crgc_api.hip Knobs)
 set -euo pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$ROOT/gpurun_out/${1:-abb}

@@ -2,6 +2,7 @@
 # Env-variant A/B over workloads, two interleaved passes:
 #   bash tools/ab_env_wl.sh <tag> "<workloads>" <variant>...   (variant: BASE or K=V[,K2=V2])
 # summary.txt: workload, variant, ms per wakeup (C3: per trace), mark-kernel ms
+export CRGC_TEST_HOOKS=1  # the env variants below are test hooks (crgc_api.hip Knobs)
 set -euo pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$ROOT/gpurun_out/$1

@@ -9,6 +9,8 @@ crgc_api.hip); results must be identical, only timings differ.
 import argparse
 import json
 import os
+
+os.environ.setdefault("CRGC_TEST_HOOKS", "1")  # the variants are test hooks (crgc_api.hip Knobs)
 import statistics
 import sys
 import time

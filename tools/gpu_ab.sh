@@ -1,5 +1,6 @@
 #!/bin/bash
 # Trace A/B (tools/ab_trace.py) + level log + quick bench; usage: bash tools/gpu_ab.sh <tag> [tests]
+export CRGC_TEST_HOOKS=1  # the env variants below are test hooks (crgc_api.hip Knobs)
 set -euo pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$ROOT/gpurun_out/${1:-ab}

@@ -1,0 +1,43 @@
+#!/bin/bash
+# Round-4 GPU driver (run through gpurun from the repo root):
+#   bash tools/gpu_r4.sh <tag> <steps...>
+# steps (each under its own time limit, chained: the first failure ends the call):
+#   tests[:-k expr]  pytest -m gpu (optionally -k)        smoke   __graft_entry__.smoke()
+#   c2 c1 c3 c5      bench.py lines                        levels  C2 level log (CRGC_LEVEL_LOG)
+#   kt               rocprofv3 --kernel-trace --stats of the timed C2 wakeups only (--no-pcie)
+#   pmc              FETCH_SIZE and WRITE_SIZE passes of the same command, one run each
+#   probe            tools/hip_probe.hip: HIP last-error / event / pointer-range semantics
+set -euo pipefail
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=$1; shift
+O=$ROOT/gpurun_out/$TAG
+mkdir -p "$O"
+export TMPDIR=/tmp
+B="python3 $ROOT/bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-pcie"
+for step in "$@"; do
+  echo "[gpu_r4] $step $(date +%T)"
+  case "$step" in
+    tests|tests:*)
+      K=()
+      [ "$step" != tests ] && K=(-k "${step#tests:}")
+      (cd "$ROOT" && timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 150 \
+        --timeout-method thread "${K[@]}" > "$O/gpu_tests.log" 2>&1) ;;
+    smoke) (cd "$ROOT" && timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1) ;;
+    c2) (cd /tmp && timeout -k 10 480 python3 "$ROOT/bench.py" > "$O/bench_c2.json" 2> "$O/bench_c2.err") ;;
+    c2q) (cd /tmp && timeout -k 10 300 python3 "$ROOT/bench.py" --no-cpu-baseline > "$O/bench_c2q.json" 2> "$O/bench_c2q.err") ;;
+    c1) (cd /tmp && timeout -k 10 300 python3 "$ROOT/bench.py" --workload c1 > "$O/bench_c1.json" 2> "$O/bench_c1.err") ;;
+    c3) (cd /tmp && timeout -k 10 300 python3 "$ROOT/bench.py" --workload c3 > "$O/bench_c3.json" 2> "$O/bench_c3.err") ;;
+    c5) (cd /tmp && timeout -k 10 420 python3 "$ROOT/bench.py" --workload c5 --steps 5 --warmup 2 --no-cpu-baseline \
+          > "$O/bench_c5.json" 2> "$O/bench_c5.err") ;;
+    levels) (cd /tmp && CRGC_LEVEL_LOG=1 CRGC_KERNEL_TIMING=2 timeout -k 10 420 $B > "$O/levels.json" 2> "$O/levels.err") ;;
+    kt) (cd /tmp && timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o kt -- $B \
+          > "$O/bench_kt.json" 2> "$O/bench_kt.err") ;;
+    pmc) (cd /tmp && timeout -k 10 420 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o pmc -- $B \
+            > "$O/bench_fetch.json" 2> "$O/bench_fetch.err" &&
+          timeout -k 10 420 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o pmc -- $B \
+            > "$O/bench_write.json" 2> "$O/bench_write.err") ;;
+    probe) (cd "$ROOT" && timeout -k 10 60 ./tools/_build/hip_probe > "$O/hip_probe.txt" 2>&1) ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[gpu_r4] done $(date +%T)"

@@ -2,6 +2,8 @@
 on a C4-shaped graph: G logical shards on one GPU (in-process transport)."""
 import json
 import os
+
+os.environ.setdefault("CRGC_TEST_HOOKS", "1")  # the variants are test hooks (crgc_api.hip Knobs)
 import sys
 import time
 

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 OK = 0
 E_INVAL = -1
@@ -123,6 +123,8 @@ class CrgcTraceStats(C.Structure):
         ("expand_launches", _U64),
         ("expand_bytes", _U64),
         ("exchange_bytes", _U64),
+        ("time_query_failures", _U64),
+        ("direct_lists", _U64),
     ]
 
 

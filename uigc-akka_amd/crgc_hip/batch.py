@@ -165,6 +165,32 @@ class EntryBatch:
             (uo[lo:hi + 1] - uo[lo]).astype(np.uint32),
             self.updated_ref[uo[lo]:uo[hi]].copy(), self.updated_info[uo[lo]:uo[hi]].copy())
 
+    @staticmethod
+    def concat(batches: Sequence["EntryBatch"]) -> "EntryBatch":
+        """Host batches back to back, in order (offsets rebased): the queue of
+        several producers drained one after the other."""
+        bs = [b for b in batches if b.n_entries]
+        if not bs:
+            return EntryBatch.empty()
+        if len(bs) == 1:
+            return bs[0]
+        assert all(b.memory == abi.MEM_HOST for b in bs)
+
+        def offs(name):
+            parts, base = [np.zeros(1, np.uint64)], 0
+            for b in bs:
+                o = getattr(b, name).astype(np.uint64)
+                parts.append(o[1:] + base)
+                base += int(o[-1])
+            out = np.concatenate(parts)
+            assert out[-1] < (1 << 32)
+            return out.astype(np.uint32)
+
+        cat = lambda k: np.concatenate([getattr(b, k) for b in bs])  # noqa: E731
+        return EntryBatch(cat("self"), cat("recv_count"), cat("flags"), offs("created_off"),
+                          cat("created_owner"), cat("created_target"), offs("spawned_off"),
+                          cat("spawned"), offs("updated_off"), cat("updated_ref"), cat("updated_info"))
+
     def split(self, k: int) -> List["EntryBatch"]:
         """k consecutive host parts (part r = entries [n*r/k, n*(r+1)/k))."""
         n = self.n_entries
@@ -355,6 +381,8 @@ class TraceResult:
     expand_launches: int = 0
     expand_bytes: int = 0
     exchange_bytes: int = 0
+    time_query_failures: int = 0
+    direct_lists: int = 0
 
     def garbage_set(self):
         return set(int(x) for x in self.garbage)

@@ -151,7 +151,8 @@ class ShadowGraph:
                            int(st.sup_edges), int(st.levels), int(st.launches), st.ms_mark,
                            st.ms_sweep, st.ms_total, st.ms_frontier, st.ms_tail, st.ms_expand,
                            int(st.rounds), int(st.ids_sent), st.ms_exchange,
-                           int(st.expand_launches), int(st.expand_bytes), int(st.exchange_bytes))
+                           int(st.expand_launches), int(st.expand_bytes), int(st.exchange_bytes),
+                           int(st.time_query_failures), int(st.direct_lists))
 
     def _trace_into(self, shouldKill, g, k):
         out = abi.CrgcTraceOut()
@@ -165,25 +166,40 @@ class ShadowGraph:
         r, ng, nk = self.trace_kill_ids(shouldKill)
         return dataclasses.replace(r, garbage=r.garbage[:ng].copy(), kill=r.kill[:nk].copy())
 
-    def trace_kill_ids(self, shouldKill: bool = True):
-        """trace() into reusable host buffers: (result with buffer views, n_garbage, n_kill)."""
+    @staticmethod
+    def id_buffers(n: int = 1 << 16):
+        """A (garbage, kill) pair of host id buffers for trace_kill_ids(bufs=...):
+        page-locked when the process uses torch (the device stores into them)."""
+        return _host_ids(n), _host_ids(n)
+
+    def trace_kill_ids(self, shouldKill: bool = True, bufs=None):
+        """trace() into reusable host buffers: (result with buffer views, n_garbage, n_kill).
+        bufs: the caller's (garbage, kill) buffers (id_buffers()) instead of the
+        graph's own, for results that must outlive the next trace (a list that
+        does not fit comes back in a fresh buffer instead)."""
         self.flush()
-        if getattr(self, "_gbuf", None) is None:
-            self._gbuf = _host_ids(1 << 16)
-            self._kbuf = _host_ids(1 << 16)
-        rc, out = self._trace_into(shouldKill, self._gbuf, self._kbuf)
+        if bufs is None:
+            if getattr(self, "_gbuf", None) is None:
+                self._gbuf = _host_ids(1 << 16)
+                self._kbuf = _host_ids(1 << 16)
+            gb, kb = self._gbuf, self._kbuf
+        else:
+            gb, kb = bufs
+        rc, out = self._trace_into(shouldKill, gb, kb)
         if rc == abi.E2BIG:
-            if out.n_garbage > len(self._gbuf):
-                self._gbuf = _host_ids(int(out.n_garbage) * 2)
-            if out.n_kill > len(self._kbuf):
-                self._kbuf = _host_ids(int(out.n_kill) * 2)
-            out.garbage_ids, out.garbage_cap = _ptr(self._gbuf), len(self._gbuf)
-            out.kill_ids, out.kill_cap = _ptr(self._kbuf), len(self._kbuf)
+            if out.n_garbage > len(gb):
+                gb = _host_ids(int(out.n_garbage) * 2)
+            if out.n_kill > len(kb):
+                kb = _host_ids(int(out.n_kill) * 2)
+            if bufs is None:
+                self._gbuf, self._kbuf = gb, kb
+            out.garbage_ids, out.garbage_cap = _ptr(gb), len(gb)
+            out.kill_ids, out.kill_cap = _ptr(kb), len(kb)
             rc = self.lib.crgc_last_trace(self.h, C.byref(out))
         self._synced()
         self._chk(rc, "crgc_trace")
         ng, nk = int(out.n_garbage), int(out.n_kill)
-        return self._result(out, self._gbuf[:ng], self._kbuf[:nk]), ng, nk
+        return self._result(out, gb[:ng], kb[:nk]), ng, nk
 
     def trace_counts(self, shouldKill: bool = True):
         """trace() without copying the id lists back (counts and timings only)."""
@@ -486,7 +502,8 @@ class ShardedShadowGraph:
             max(r.ms_expand for r in rs), max(r.rounds for r in rs),
             sum(r.ids_sent for r in rs), max(r.ms_exchange for r in rs),
             sum(r.expand_launches for r in rs), sum(r.expand_bytes for r in rs),
-            sum(r.exchange_bytes for r in rs))
+            sum(r.exchange_bytes for r in rs), sum(r.time_query_failures for r in rs),
+            min(r.direct_lists for r in rs))
 
     def count_reachable_from(self, location: int) -> int:
         vals = self._all(lambda s: s.count_reachable_from(location))

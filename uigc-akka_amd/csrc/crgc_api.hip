@@ -132,36 +132,45 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   }
 #undef A
   a.allocated = true;
-  // Default state of every unused slot / bucket.
-  hipMemsetAsync(d.htab, 0xFF, c.hcap * sizeof(IdBucket), s);
-  hipMemsetAsync(d.recv, 0, c.scap * 4, s);
-  hipMemsetAsync(d.flags, 0, c.scap, s);
-  hipMemsetAsync(d.sup, 0xFF, c.scap * 4, s);
-  hipMemsetAsync(d.adj, 0, c.scap * 8, s);
-  hipMemsetAsync(d.ecap, 0, c.scap * 4, s);
-  hipMemsetAsync(d.vseq, 0, c.scap * 8, s);
-  hipMemsetAsync(d.sseq, 0, c.scap * 8, s);
-  hipMemsetAsync(d.etab, 0xFF, c.ecap * sizeof(EdgeBucket), s);
-  hipMemsetAsync(d.vis, 0, c.scap / 8, s);
-  hipMemsetAsync(d.front[0], 0, c.scap, s);
-  hipMemsetAsync(d.front[1], 0, c.scap, s);
-  hipMemsetAsync(d.dirty[0], 0, c.scap / BLK_SLOTS, s);
-  hipMemsetAsync(d.dirty[1], 0, c.scap / BLK_SLOTS, s);
-  hipMemsetAsync(d.nzdeg, 0, c.scap * 4, s);
-  hipMemsetAsync(d.radj, 0, c.scap * 8, s);
-  hipMemsetAsync(d.rcap, 0, c.scap * 4, s);
-  hipMemsetAsync(d.rnew, 0, c.scap * 4, s);
-  hipMemsetAsync(d.par, 0xFF, c.scap * 4, s);  // no hints in a new generation
-  hipMemsetAsync(d.fx, 0, c.scap / 8, s);
-  hipMemsetAsync(d.cm, 0, c.scap / 8, s);
-  hipMemsetAsync(d.pb[0], 0, c.scap / 8, s);
-  hipMemsetAsync(d.pb[1], 0, c.scap / 8, s);
+  // Default state of every unused slot / bucket (each memset's own status:
+  // hipGetLastError would also report a soft failure of an earlier call).
+  hipError_t ms = hipSuccess;
+#define M(p, v, n)                                  \
+  do {                                              \
+    const hipError_t r = hipMemsetAsync(p, v, n, s); \
+    if (ms == hipSuccess) ms = r;                   \
+  } while (0)
+  M(d.htab, 0xFF, c.hcap * sizeof(IdBucket));
+  M(d.recv, 0, c.scap * 4);
+  M(d.flags, 0, c.scap);
+  M(d.sup, 0xFF, c.scap * 4);
+  M(d.adj, 0, c.scap * 8);
+  M(d.ecap, 0, c.scap * 4);
+  M(d.vseq, 0, c.scap * 8);
+  M(d.sseq, 0, c.scap * 8);
+  M(d.etab, 0xFF, c.ecap * sizeof(EdgeBucket));
+  M(d.vis, 0, c.scap / 8);
+  M(d.front[0], 0, c.scap);
+  M(d.front[1], 0, c.scap);
+  M(d.dirty[0], 0, c.scap / BLK_SLOTS);
+  M(d.dirty[1], 0, c.scap / BLK_SLOTS);
+  M(d.nzdeg, 0, c.scap * 4);
+  M(d.radj, 0, c.scap * 8);
+  M(d.rcap, 0, c.scap * 4);
+  M(d.rnew, 0, c.scap * 4);
+  M(d.par, 0xFF, c.scap * 4);  // no hints in a new generation
+  M(d.fx, 0, c.scap / 8);
+  M(d.cm, 0, c.scap / 8);
+  M(d.pb[0], 0, c.scap / 8);
+  M(d.pb[1], 0, c.scap / 8);
   if (sharded) {
-    hipMemsetAsync(d.phs, 0xFF, c.scap * 4, s);  // PHS_NONE: a new generation resolves again
-    hipMemsetAsync(d.xp_cnt, 0, c.scap / BLK_SLOTS * 4, s);
-    hipMemsetAsync(d.rq_cnt, 0, c.scap / BLK_SLOTS * 4, s);
+    M(d.phs, 0xFF, c.scap * 4);  // PHS_NONE: a new generation resolves again
+    M(d.xp_cnt, 0, c.scap / BLK_SLOTS * 4);
+    M(d.rq_cnt, 0, c.scap / BLK_SLOTS * 4);
   }
-  return hipGetLastError();
+#undef M
+  if (ms != hipSuccess) free_arrays(a);
+  return ms;
 }
 
 Caps caps_for(uint64_t live, uint64_t edges, uint64_t ids_pending, uint64_t atoms_pending) {
@@ -179,8 +188,17 @@ Caps caps_for(uint64_t live, uint64_t edges, uint64_t ids_pending, uint64_t atom
 
 }  // namespace
 
-// Tuning and test switches, read once when the handle is created (not per
-// call): the A/B variants and test hooks of DESIGN.md §4 / tests/.
+// Switches, read once when the handle is created (not per call).
+//
+// Production reads only the documented keys:
+//   CRGC_LEVEL_TIMEOUT_S  wall bound of one trace's level loop (default 300 s)
+//   CRGC_KERNEL_TIMING    0: chunk events only, 1 (default): k_expand's dispatch
+//                         events too (the roofline's live timing), 2: every level kernel
+//   CRGC_LEVEL_LOG        per-level device times on stderr (diagnostics)
+// (and, in the transports, CRGC_RCCL_TIMEOUT_S / CRGC_LOCAL_BARRIER_S).
+// Everything else — the A/B variants of DESIGN.md §4 and the test hooks of
+// tests/ — is read only when CRGC_TEST_HOOKS=1, so a JVM host that inherits a
+// stray environment variable cannot change the kernels it runs.
 struct Knobs {
   bool pull = true;              // CRGC_PULL=0: push only
   uint64_t pull_div = 16;        // CRGC_PULL_DIV: pull after a frontier of >= slots / div
@@ -196,6 +214,7 @@ struct Knobs {
   uint32_t chain_after = 64;     // CRGC_CHAIN_AFTER
   int kernel_timing = 1;         // CRGC_KERNEL_TIMING: 0 chunks, 1 k_expand, 2 all level kernels
   bool level_log = false;        // CRGC_LEVEL_LOG
+  uint64_t level_timeout_s = 300;  // CRGC_LEVEL_TIMEOUT_S
   int xbits = 1;                 // CRGC_XBITS: sharded mark form (0 ids, 1 cheaper, 2 bitmaps)
   int buckets_log2 = 0;          // CRGC_BUCKETS_LOG2: edge-pipeline buckets (test hook; 0 = by size)
   // Sharded deep marks switch to the replicated chain closure (crgc_xchain.hip)
@@ -207,8 +226,18 @@ struct Knobs {
   bool bin = true;               // CRGC_BIN=0: the pseudo-root level pushes candidate bytes directly
   uint64_t bin_min = 1ull << 22; // CRGC_BIN_MIN_SLOTS: binned only above this many slots (a smaller
                                  // candidate byte map stays in the L2: C1 mark +10 us binned)
+  bool route = true;             // CRGC_ROUTE=0: sharded entry merges all-gather every batch
+  bool side_stream = false;      // CRGC_SIDE_STREAM=1: edge pipeline beside the vertex updates
+  bool side_prio = false;        // CRGC_SIDE_PRIO=1: that side stream at the highest priority
+  bool chunk_host = true;        // CRGC_CHUNK_HOST=0: large pageable host batches in one piece
+  uint32_t chunk_max = 4;        // CRGC_CHUNK_MAX: at most this many chunks (2 .. 4)
   void read() {
     auto env = [](const char *k) { return getenv(k); };
+    if (const char *m = env("CRGC_KERNEL_TIMING")) kernel_timing = atoi(m);
+    level_log = env("CRGC_LEVEL_LOG") != nullptr;
+    if (const char *m = env("CRGC_LEVEL_TIMEOUT_S")) level_timeout_s = std::max<uint64_t>(1, strtoull(m, nullptr, 10));
+    const char *hooks = env("CRGC_TEST_HOOKS");
+    if (!hooks || atoi(hooks) != 1) return;
     if (const char *m = env("CRGC_PULL")) pull = atoi(m) != 0;
     if (const char *m = env("CRGC_PULL_DIV")) pull_div = std::max<uint64_t>(1, strtoull(m, nullptr, 10));
     if (const char *m = env("CRGC_PULL_CUR_DIV")) pull_cur_div = (uint32_t)strtoul(m, nullptr, 10);
@@ -225,8 +254,6 @@ struct Knobs {
     if (const char *m = env("CRGC_TAIL_START")) tail_start = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_TAIL_MAX")) tail_max = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_CHAIN_AFTER")) chain_after = (uint32_t)strtoul(m, nullptr, 10);
-    if (const char *m = env("CRGC_KERNEL_TIMING")) kernel_timing = atoi(m);
-    level_log = env("CRGC_LEVEL_LOG") != nullptr;
     if (const char *m = env("CRGC_XBITS")) xbits = atoi(m);
     if (const char *m = env("CRGC_BUCKETS_LOG2"))
       buckets_log2 = std::min(10, std::max(1, atoi(m)));
@@ -238,6 +265,11 @@ struct Knobs {
       const uint32_t v = (uint32_t)strtoul(m, nullptr, 10);
       xslices = v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
     }
+    if (const char *m = env("CRGC_ROUTE")) route = atoi(m) != 0;
+    if (const char *m = env("CRGC_SIDE_STREAM")) side_stream = atoi(m) != 0;
+    if (const char *m = env("CRGC_SIDE_PRIO")) side_prio = atoi(m) != 0;
+    if (const char *m = env("CRGC_CHUNK_HOST")) chunk_host = atoi(m) != 0;
+    if (const char *m = env("CRGC_CHUNK_MAX")) chunk_max = std::min<uint32_t>(4, std::max(2, atoi(m)));
   }
 };
 
@@ -292,7 +324,7 @@ struct crgc_graph {
   Scratch x_dg, x_dg_out;    // DeltaGraph production
   Scratch x_chain;           // chain mode (crgc_chain.hip)
   Scratch x_bin;             // the pseudo-root level's binned push: counters, then bin regions
-  void *x_bin_zeroed = nullptr;  // x_bin allocation whose counters were zeroed
+  uint64_t x_bin_zeroed = 0;  // x_bin allocation (Scratch::gen) whose counters were zeroed
   Scratch x_gc, x_gc_list;   // replicated chain closure of sharded marks (crgc_xchain.hip)
   uint64_t *h_small = nullptr;       // pinned host staging for small all-gathers
   char *h_route = nullptr;           // pinned RoutePart / ConcatPart tables
@@ -537,10 +569,6 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
   if (!h) return CRGC_E_NOMEM;
   h->device = cfg ? cfg->device : 0;
   h->F = (cfg && cfg->entry_field_size) ? cfg->entry_field_size : 4;
-  if (h->F > 255) {  // reference.conf:40 is 4; per-block record counts are packed in 16 bits
-    delete h;
-    return CRGC_E_INVAL;
-  }
   h->DGS = (cfg && cfg->delta_graph_size) ? cfg->delta_graph_size : 64;
   h->knobs.read();
   // A transport makes the handle a shard (a transport with n_shards == 1 runs
@@ -555,7 +583,7 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     h->G = cfg->n_shards;
     h->shard = cfg->shard;
     h->tp = cfg->transport;
-    if (const char *m = getenv("CRGC_ROUTE")) h->route = atoi(m) != 0;
+    h->route = h->knobs.route;
   }
   DeviceGuard dg(h->device);
   int rc = CRGC_OK;
@@ -571,9 +599,9 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     }
     for (auto &e : h->ev)
       if (hipEventCreate(&e) != hipSuccess) rc = CRGC_E_DEVICE;
-    if (const char *m = getenv("CRGC_SIDE_STREAM")) h->use_side = atoi(m) != 0;  // A/B switch
-    if (const char *m = getenv("CRGC_CHUNK_HOST")) h->chunk_host = atoi(m) != 0;
-    if (const char *m = getenv("CRGC_CHUNK_MAX")) h->chunk_max = std::min<uint32_t>(4, std::max(2, atoi(m)));
+    h->use_side = h->knobs.side_stream;  // A/B switch
+    h->chunk_host = h->knobs.chunk_host;
+    h->chunk_max = h->knobs.chunk_max;
     if (hipStreamCreateWithFlags(&h->cpy, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_cstart, hipEventDisableTiming) != hipSuccess)
       rc = CRGC_E_DEVICE;
@@ -583,8 +611,7 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     // device's highest priority, so its workgroups dispatch first
     int prio_lo = 0, prio_hi = 0;
     hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    const char *sp = getenv("CRGC_SIDE_PRIO");
-    const int side_prio = (sp && atoi(sp)) ? prio_hi : 0;
+    const int side_prio = h->knobs.side_prio ? prio_hi : 0;
     if (hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, side_prio) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess)
@@ -942,7 +969,7 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   const uint64_t nb256 = (n + 255) / 256;
   const size_t work_bytes =
       Carver::need({n * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4, n * h->F * 4, sh ? n : 0,
-                    sh ? n * h->F * 8 : 0, 8, nb256 * 256 * 4, nb256 * 256 * h->F * 4, nb256 * 4}) +
+                    sh ? n * h->F * 8 : 0, 8, nb256 * 256 * 4, nb256 * 256 * h->F * 4, nb256 * 8}) +
       edge_scratch(h, max_atoms);
   if (h->stage.ensure(host_bytes + 256) != hipSuccess || h->work.ensure(work_bytes) != hipSuccess)
     return CRGC_E_NOMEM;
@@ -979,7 +1006,7 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   a.n_atoms = wc.take<uint64_t>(1);
   a.conf_v = wc.take<uint32_t>(nb256 * 256);
   a.conf_s = wc.take<uint32_t>(nb256 * 256 * h->F);
-  a.conf_n = wc.take<uint32_t>(nb256);
+  a.conf_n = wc.take<uint32_t>(2 * nb256);
   // a batch refused for its offsets writes no atoms and the edge pipeline
   // skips it (EdgeArgs::err), so the atom arrays need no clearing
   HIP_TRY(launch_entries(h->g.d, a, h->stream, 0));
@@ -1605,6 +1632,7 @@ struct LevelRun {
   uint64_t levels = 0, roots = 0, launches = 0, depth = 0;
   uint64_t first_chunk = 0;  // level launches after level 0 that this trace needed
   double ms = 0, ms_f = 0, ms_t = 0, ms_e = 0;
+  uint64_t time_fail = 0;              // event pairs the runtime could not time
   bool defer = false;                  // leave the event queries to the caller (pending)
   std::function<void()> pending;
 };
@@ -1673,9 +1701,11 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
       const uint64_t cap = std::max<uint64_t>(4096, (h->etab_used + h->atoms_since) / 2 / (nb * BIN_SHARDS));
       const size_t cur_bytes = (size_t)(BIN_MAX * BIN_SHARDS + 4) * 4;
       HIP_TRY(h->x_bin.ensure(cur_bytes + nb * BIN_SHARDS * cap * 4));
-      if (h->x_bin_zeroed != h->x_bin.ptr) {
+      // a fresh allocation (compared by generation: a reallocation may return
+      // the same base address) starts with zero counters
+      if (h->x_bin_zeroed != h->x_bin.gen) {
         HIP_TRY(hipMemsetAsync(h->x_bin.ptr, 0, cur_bytes, h->stream));
-        h->x_bin_zeroed = h->x_bin.ptr;
+        h->x_bin_zeroed = h->x_bin.gen;
       }
       la.bin_cur = (uint32_t *)h->x_bin.ptr;
       la.bins = (uint32_t *)((char *)h->x_bin.ptr + cur_bytes);
@@ -1732,7 +1762,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   const auto loop_t0 = std::chrono::steady_clock::now();
   int last_bail = -1;
   for (uint64_t pass = 0;; ++pass) {
-    if (pass > 4096 || std::chrono::steady_clock::now() - loop_t0 > std::chrono::seconds(300)) {
+    if (pass > 4096 || std::chrono::steady_clock::now() - loop_t0 > std::chrono::seconds(kn.level_timeout_s)) {
       h->poisoned = true;
       return CRGC_E_TIMEOUT;
     }
@@ -1802,13 +1832,15 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   }
 }
 
-// Event-pair time in ms, 0 when the runtime cannot give it (e.g. a timestamp
-// not yet written back): statistics only, and no error is left behind for the
-// next launch helper's hipGetLastError() to report.
-static float elapsed_ms(hipEvent_t a, hipEvent_t b) {
+// Event-pair time in ms.  A pair the runtime cannot time counts as 0 ms and is
+// counted in *fails (crgc_trace_stats.time_query_failures: the ms_* fields are
+// then short, and bench.py refuses to print a roofline from them); the failed
+// query's status is read here so that no later call reports it.
+static float elapsed_ms(hipEvent_t a, hipEvent_t b, uint64_t *fails) {
   float t = 0;
   if (hipEventElapsedTime(&t, a, b) != hipSuccess) {
     (void)hipGetLastError();
+    ++*fails;
     return 0.f;
   }
   return t;
@@ -1819,12 +1851,12 @@ static float elapsed_ms(hipEvent_t a, hipEvent_t b) {
 static void collect_times(crgc_graph *h, LevelRun &lr, size_t nl, size_t nc, int timing, bool log,
                           size_t first_level, size_t last, const std::vector<unsigned long long> &ring) {
   for (size_t i = 0; i + 1 < nc; i += 2) {
-    lr.ms += elapsed_ms(h->chunk_ev[i], h->chunk_ev[i + 1]);
+    lr.ms += elapsed_ms(h->chunk_ev[i], h->chunk_ev[i + 1], &lr.time_fail);
   }
   for (size_t i = 0; i < (timing ? nl : 0); ++i) {
     float t[3] = {0, 0, 0};
     for (int k = timing >= 2 ? 0 : 2; k < 3; ++k)
-      t[k] = elapsed_ms(h->lvl_ev[6 * i + 2 * k], h->lvl_ev[6 * i + 2 * k + 1]);
+      t[k] = elapsed_ms(h->lvl_ev[6 * i + 2 * k], h->lvl_ev[6 * i + 2 * k + 1], &lr.time_fail);
     lr.ms_f += t[0];
     lr.ms_t += t[1];
     lr.ms_e += t[2];
@@ -2131,17 +2163,35 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
   }
 }
 
-// A host pointer the device can store to (page-locked or registered memory),
-// or nullptr (pageable memory, or not a host pointer the runtime knows).
-static uint64_t *device_view(uint64_t *p) {
-  if (!p) return nullptr;
+// The device view of a caller's host buffer of `bytes` bytes that the device
+// may store to directly: the whole range must lie in ONE page-locked
+// allocation — a range of this handle's crgc_host_register, or an allocation
+// whose extent the runtime reports (hipHostMalloc) — else nullptr (pageable
+// memory, or a buffer that runs past its pinned allocation: the lists then
+// come back by a stream copy, copy_lists).
+static uint64_t *device_view(crgc_graph *h, uint64_t *p, uint64_t bytes) {
+  if (!p || !bytes) return nullptr;
   hipPointerAttribute_t at{};
   if (hipPointerGetAttributes(&at, p) != hipSuccess) {
     (void)hipGetLastError();  // pageable memory: not an error for the caller
     return nullptr;
   }
   if (at.type != hipMemoryTypeHost || !at.devicePointer) return nullptr;
-  return (uint64_t *)at.devicePointer;
+  const char *c = (const char *)p;
+  for (const auto &r : h->pinned)
+    if (c >= r.first && c + bytes <= r.first + r.second) return (uint64_t *)at.devicePointer;
+  void *base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange((hipDeviceptr_t *)&base, &size, (hipDeviceptr_t)p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  const char *b = (const char *)base;
+  const char *dv = (const char *)at.devicePointer;
+  // the runtime reports the allocation in host or device addresses (one VA on gfx950)
+  const bool in_host = c >= b && c + bytes <= b + size;
+  const bool in_dev = dv >= b && dv + bytes <= b + size;
+  return (in_host || in_dev) ? (uint64_t *)at.devicePointer : nullptr;
 }
 
 static int copy_lists(crgc_graph *h, crgc_trace_out *out, bool sync = true) {
@@ -2257,7 +2307,8 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
     // steady-state wakeup has one host synchronisation for mark + sweep.
     // caller buffers the device can write (page-locked / registered): the
     // lists go there behind the sweep, and the trace needs one host round trip
-    uint64_t *dg = device_view(out->garbage_ids), *dk = device_view(out->kill_ids);
+    uint64_t *dg = device_view(h, out->garbage_ids, out->garbage_cap * 8),
+             *dk = device_view(h, out->kill_ids, out->kill_cap * 8);
     auto sweep = [&]() -> hipError_t {
       hipError_t e = hipEventRecord(h->ev[1], h->stream);
       if (e == hipSuccess) e = launch_sweep(h->g.d, should_kill ? 1 : 0, top, h->stream);
@@ -2316,7 +2367,9 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   st.ids_sent = ids_sent;
   st.exchange_bytes = x_bytes;
   st.ms_exchange = ms_x;
-  st.ms_sweep = elapsed_ms(h->ev[1], h->ev[2]);
+  st.ms_sweep = elapsed_ms(h->ev[1], h->ev[2], &lr.time_fail);
+  st.time_query_failures = lr.time_fail;
+  st.direct_lists = direct ? 1 : 0;
   st.pseudo_roots = lr.roots;
   h->live = c.n_live;
   h->n_proxy = c.n_proxy;

@@ -174,6 +174,7 @@ __global__ void k_chain_done(DevGraph g, ChainArgs ca, uint32_t rounds) {
 
 hipError_t launch_chain(const DevGraph &g, const ChainArgs &ca, int step, const uint32_t *src, uint32_t *dst,
                         uint64_t top, uint32_t fi, int first, uint32_t rounds, hipStream_t s) {
+  launch_begin();
   const uint64_t words = (top + 31) / 32;
   const int wgrid = grid_for((top + 63) / 64, 4, 4096);
   switch (step) {

@@ -587,6 +587,7 @@ hipError_t run_scan(ScanSet q, hipStream_t s) {
 static int dg_grid(uint64_t n) { return (int)std::min<uint64_t>((n + 255) / 256, 8192); }
 
 hipError_t launch_dg_chain(const DgArgs &a, int phase, hipStream_t s) {
+  launch_begin();
   const uint64_t N = a.n + 1;
   if (phase == 0) {
     hipLaunchKernelGGL(k_dg_span, dim3((N + 4 * SPAN_S - 1) / (4 * SPAN_S)), dim3(256), 0, s, a);
@@ -976,6 +977,7 @@ __global__ __launch_bounds__(256) void k_dg_compact(DgArgs a, uint64_t ng, DgOut
 }
 
 hipError_t launch_dg_write(const DgArgs &a, uint64_t ng, const DgOut &t, hipStream_t s) {
+  launch_begin();
   if (ng == 0) return hipSuccess;
   const uint64_t bound = ng == DG_NG_DEVICE ? a.n + 1 : ng;
   hipLaunchKernelGGL(k_dg_bounds, dim3(dg_grid(bound)), dim3(256), 0, s, a, ng);
@@ -998,10 +1000,12 @@ hipError_t launch_dg_write(const DgArgs &a, uint64_t ng, const DgOut &t, hipStre
     hipLaunchKernelGGL(k_scan_one, dim3(1), dim3(SCAN_B), 0, s, q, &a.ctr->n_graphs, &a.ctr->first_long);
   }
   hipLaunchKernelGGL(k_dg_write, dim3((unsigned)std::min<uint64_t>(bound, 4096)), dim3(64), 0, s, a, ng, t);
+  if (hipError_t e = hipGetLastError()) return e;  // before the nested helper drops it
   return launch_dg_scans(a, ng, s);
 }
 
 hipError_t launch_dg_compact(const DgArgs &a, uint64_t ng, const DgOut &t, const DgOut &o, hipStream_t s) {
+  launch_begin();
   if (ng == 0) return hipSuccess;
   const uint64_t bound = ng == DG_NG_DEVICE ? a.n + 1 : ng;
   hipLaunchKernelGGL(k_dg_compact, dim3((unsigned)std::min<uint64_t>((bound + 3) / 4, 4096)), dim3(256), 0, s, a,
@@ -1010,6 +1014,7 @@ hipError_t launch_dg_compact(const DgArgs &a, uint64_t ng, const DgOut &t, const
 }
 
 hipError_t launch_dg_scans(const DgArgs &a, uint64_t ng, hipStream_t s) {
+  launch_begin();
   ScanSet q{};
   q.n = ng;
   q.bsum = a.bsum;
@@ -1048,6 +1053,7 @@ __global__ __launch_bounds__(256) void k_dg_offsets(DgArgs a, uint64_t ng, DgOut
 }
 
 hipError_t launch_dg_offsets(const DgArgs &a, uint64_t ng, const DgOut &o, hipStream_t s) {
+  launch_begin();
   hipLaunchKernelGGL(k_dg_offsets, dim3(dg_grid((ng == DG_NG_DEVICE ? a.n + 1 : ng) + 1)), dim3(256), 0, s, a, ng,
                      o);
   return hipGetLastError();

@@ -437,6 +437,7 @@ __global__ __launch_bounds__(RV_THREADS) void k_rv_place(DevGraph g, EdgeArgs a)
 
 // ---- driver --------------------------------------------------------------------
 hipError_t launch_edges(const DevGraph &g, const EdgeArgs &a, hipStream_t s) {
+  launch_begin();
   if (a.max_atoms == 0) return hipSuccess;
   const size_t lds_hist = (size_t)a.nbk * 4;
   const dim3 pgrid((unsigned)a.nblk);

@@ -16,6 +16,7 @@ namespace crgc {
 struct Scratch {
   void *ptr = nullptr;
   size_t bytes = 0;
+  uint64_t gen = 0;  // bumped by every allocation (the allocator may return the same base)
   hipError_t ensure(size_t need) {
     if (need <= bytes) return hipSuccess;
     if (ptr) hipFree(ptr);
@@ -23,7 +24,10 @@ struct Scratch {
     bytes = 0;
     size_t sz = need + need / 4 + 4096;
     hipError_t e = hipMalloc(&ptr, sz);
-    if (e == hipSuccess) bytes = sz;
+    if (e == hipSuccess) {
+      bytes = sz;
+      ++gen;
+    }
     return e;
   }
   void release() {
@@ -96,7 +100,7 @@ struct EntryArgs {
   // last-write-wins conflicts, per block of 256 entries (k_entries_vertex -> k_entries_lww)
   uint32_t *conf_v;      // [n rounded to 256] slots whose busy/root several entries tagged
   uint32_t *conf_s;      // [same * F] children whose supervisor several entries tagged
-  uint32_t *conf_n;      // [blocks] counts: self | spawn << 16
+  uint32_t *conf_n;      // [2 * blocks] counts: self slots, spawned children
   uint32_t *atom_o;      // [2*n*F]: created atoms, then updated atoms
   uint32_t *atom_t;
   int32_t *atom_d;

@@ -22,6 +22,14 @@
 
 namespace crgc {
 
+// Every launch_* helper reports hipGetLastError() after its launches.  The
+// runtime keeps the last failing status of ANY call on the thread until it is
+// read — soft failures included (a stream query's hipErrorNotReady, an event
+// query, a pointer query on pageable memory; tools/hip_probe.hip,
+// profiles/r4a/README.md) — so each helper first drops whatever an earlier
+// call left behind and reports only its own launches.
+inline void launch_begin() { (void)hipGetLastError(); }
+
 constexpr uint64_t KEY_EMPTY = 0xFFFFFFFFFFFFFFFFull;
 constexpr uint32_t PHS_NONE = 0xFFFFFFFFu;    // proxy's home slot not resolved yet
 constexpr uint32_t PHS_ABSENT = 0xFFFFFFFEu;  // the home shard has no live shadow of the id

@@ -169,6 +169,7 @@ __global__ __launch_bounds__(IDS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 
 }
 
 hipError_t launch_ids(const DevGraph &g, const IdArgs &a, hipStream_t s) {
+  launch_begin();
   uint64_t n = 0;
   for (int k = 0; k < a.nseg; ++k) n += a.seg[k].n;
   if (n == 0) return hipSuccess;
@@ -297,14 +298,16 @@ __global__ __launch_bounds__(256) void k_entries_vertex(DevGraph g, EntryArgs a)
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) a.conf_n[blockIdx.x] = s_nv | (s_ns << 16);  // <= 256, <= 256 * F (F <= 255)
+  if (threadIdx.x == 0) {  // <= 256 slots, <= 256 * F children
+    a.conf_n[2 * blockIdx.x] = s_nv;
+    a.conf_n[2 * blockIdx.x + 1] = s_ns;
+  }
 }
 
 // The slots several entries of this merge tagged: the tag's entry (the last
 // in batch order) writes the field.  One block per k_entries_vertex block.
 __global__ __launch_bounds__(256) void k_entries_lww(DevGraph g, EntryArgs a) {
-  const uint32_t cn = a.conf_n[blockIdx.x];
-  const uint32_t nv = cn & 0xFFFFu, ns = cn >> 16;
+  const uint32_t nv = a.conf_n[2 * blockIdx.x], ns = a.conf_n[2 * blockIdx.x + 1];
   const uint32_t *cv = a.conf_v + (uint64_t)blockIdx.x * 256;
   const uint32_t *cs_ = a.conf_s + (uint64_t)blockIdx.x * 256 * a.F;
   for (uint32_t k = threadIdx.x; k < nv; k += 256) {
@@ -339,6 +342,7 @@ __global__ __launch_bounds__(256) void k_entries_shard_prep(DevGraph g, EntryArg
 // phase 0: (sharded prep) ids, atoms — the edge pipeline may start after it;
 // phase 1: vertex updates, LWW winners.
 hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s, int phase) {
+  launch_begin();
   if (a.n == 0) return hipSuccess;
   const uint64_t nf = a.n * a.F;
   const int blocks = (int)((a.n + 255) / 256);
@@ -357,6 +361,7 @@ hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s, 
   ia.seg[3] = IdSeg{a.spawned, a.spawn_slot, nf, a.s_off + a.n, false, nullptr, nullptr};
   ia.seg[4] = IdSeg{a.u_ref, a.u_slot, nf, a.u_off + a.n, false, sh ? a.u_partner : nullptr,
                     nullptr};
+  if (hipError_t e = hipGetLastError()) return e;  // before the nested helper drops it
   if (hipError_t e = launch_ids(g, ia, s)) return e;
   hipLaunchKernelGGL(k_entries_atoms, dim3(blocks), dim3(256), 0, s, g, a);
   return hipGetLastError();
@@ -429,6 +434,7 @@ __global__ __launch_bounds__(256) void k_deltas_shard_prep(DeltaArgs a, uint64_t
 // phase 0: (sharded prep) ids, apply — the edge pipeline may start after it;
 // phase 1: LWW winners.
 hipError_t launch_deltas(const DevGraph &g, const DeltaArgs &a, uint64_t n_out, hipStream_t s, int phase) {
+  launch_begin();
   if (a.n == 0) return hipSuccess;
   const int blocks = (int)((a.n + 255) / 256);
   if (phase == 1) {
@@ -446,6 +452,7 @@ hipError_t launch_deltas(const DevGraph &g, const DeltaArgs &a, uint64_t n_out, 
   ia.seg[1] = IdSeg{a.sup, a.sup_slot, a.n, nullptr, true, a.id, nullptr};
   ia.seg[2] = IdSeg{a.out_target, a.ot_slot, n_out, a.out_off + a.n, false,
                     sh ? a.o_partner : nullptr, nullptr};
+  if (hipError_t e = hipGetLastError()) return e;  // before the nested helper drops it
   if (hipError_t e = launch_ids(g, ia, s)) return e;
   hipLaunchKernelGGL(k_deltas_apply, dim3(blocks), dim3(256), 0, s, g, a);
   return hipGetLastError();
@@ -499,6 +506,7 @@ __global__ __launch_bounds__(256) void k_undo_edges(DevGraph g, UndoArgs a) {
 }
 
 hipError_t launch_undo_check(const DevGraph &g, const UndoArgs &a, hipStream_t s) {
+  launch_begin();
   if (a.n + a.nc == 0) return hipSuccess;
   hipLaunchKernelGGL(k_undo_exist, dim3((a.n + a.nc + 255) / 256), dim3(256), 0, s, g, a);
   return hipGetLastError();
@@ -506,6 +514,7 @@ hipError_t launch_undo_check(const DevGraph &g, const UndoArgs &a, hipStream_t s
 
 hipError_t launch_undo_apply(const DevGraph &g, const UndoArgs &a, uint64_t slot_top,
                              hipStream_t s) {
+  launch_begin();
   if (slot_top)
     hipLaunchKernelGGL(k_undo_halt, dim3((slot_top + 255) / 256), dim3(256), 0, s, g,
                        a.location, slot_top);
@@ -528,6 +537,7 @@ __global__ __launch_bounds__(256) void k_rebase(uint32_t *c_off, uint32_t *s_off
 
 hipError_t launch_rebase(uint32_t *c_off, uint32_t *s_off, uint32_t *u_off, uint64_t n, uint32_t c0, uint32_t s0,
                          uint32_t u0, hipStream_t s) {
+  launch_begin();
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_rebase, dim3((n + 255) / 256), dim3(256), 0, s, c_off, s_off, u_off, n, c0, s0, u0);
   return hipGetLastError();

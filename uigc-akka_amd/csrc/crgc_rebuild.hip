@@ -238,6 +238,7 @@ __global__ __launch_bounds__(256) void k_rb_rfill(DevGraph dst) {
 
 hipError_t launch_rebuild(const DevGraph &src, uint64_t src_top, const DevGraph &dst, uint32_t *map,
                           uint32_t *newdeg, uint64_t *offs, void *scan_tmp, hipStream_t s) {
+  launch_begin();
   (void)newdeg;
   const int grid = grid_for(src_top, 256, 8192);
   hipLaunchKernelGGL(k_rb_vertices, dim3(grid), dim3(256), 0, s, src, src_top, dst, map);

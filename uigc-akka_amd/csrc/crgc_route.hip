@@ -204,6 +204,7 @@ __global__ __launch_bounds__(RT_THREADS) void k_route_scatter(RouteArgs a, const
 }
 
 hipError_t launch_route(const RouteArgs &a, int phase, const RoutePart *parts, hipStream_t s) {
+  launch_begin();
   if (a.n == 0) return hipSuccess;
   const int blocks = (int)a.nblk;
   if (phase == 0) {
@@ -269,6 +270,7 @@ __global__ __launch_bounds__(256) void k_concat(const ConcatPart *parts, uint32_
 
 hipError_t launch_concat(const ConcatPart *parts, uint32_t G, const RoutePart &dst, uint64_t N, uint64_t C,
                          uint64_t S, uint64_t U, hipStream_t s) {
+  launch_begin();
   const uint64_t work = std::max(std::max(N, C), std::max(S, U));
   hipLaunchKernelGGL(k_concat, dim3(grid_for(work, 256, 4096)), dim3(256), 0, s, parts, G, dst, N, C, S, U);
   return hipGetLastError();

@@ -1276,6 +1276,7 @@ int level_grid(uint64_t slot_top) {
 
 hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool investigate,
                         uint64_t slot_top, hipStream_t s, hipEvent_t *ev) {
+  launch_begin();
   LevelArgs a = a0;
   const int grid = level_grid(slot_top);
   a.frontier_grid = grid;
@@ -1336,6 +1337,7 @@ __global__ __launch_bounds__(256) void k_trace_reset(DevGraph g, uint64_t nblk, 
 
 hipError_t launch_trace_reset(const DevGraph &g, uint64_t nblk, uint32_t ctr_from, uint32_t ctr_words,
                               hipStream_t s) {
+  launch_begin();
   hipLaunchKernelGGL(k_trace_reset, dim3(grid_for(std::max<uint64_t>(nblk * 16, ctr_words), 256, 2048)),
                      dim3(256), 0, s, g, nblk, ctr_from, ctr_words);
   return hipGetLastError();
@@ -1585,6 +1587,7 @@ __global__ __launch_bounds__(256) void k_copy_lists(DevGraph g, uint64_t *gdst, 
 
 hipError_t launch_copy_lists(const DevGraph &g, uint64_t *gdst, uint64_t gcap, uint64_t *kdst, uint64_t kcap,
                              hipStream_t s) {
+  launch_begin();
   hipLaunchKernelGGL(k_copy_lists, dim3(64), dim3(256), 0, s, g, gdst, gcap, kdst, kcap);
   return hipGetLastError();
 }
@@ -1605,12 +1608,14 @@ __global__ __launch_bounds__(256) void k_publish(const Counters *c, Counters *hd
 }
 
 hipError_t launch_publish(const Counters *c, Counters *hdst, uint32_t r0, uint32_t rn, hipStream_t s) {
+  launch_begin();
   hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, c, hdst, r0, rn);
   return hipGetLastError();
 }
 
 hipError_t launch_sweep(const DevGraph &g, int should_kill, uint64_t slot_top, hipStream_t s,
                         int phase) {
+  launch_begin();
   const int grid = level_grid(slot_top);
   if (phase & 1) {
     hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(256), 0, s, g, should_kill);
@@ -1692,6 +1697,7 @@ __global__ __launch_bounds__(256) void k_list_scatter(DevGraph g, uint32_t *buf,
 
 hipError_t launch_list(const DevGraph &g, int mode, bool scatter, uint32_t *buf, uint32_t *cnt,
                        uint64_t nblk, uint64_t *send, uint32_t *send_slot, hipStream_t s) {
+  launch_begin();
   if (nblk == 0) return hipSuccess;
   const int grid = (int)((nblk + 3) / 4);
   if (!scatter) {
@@ -1777,6 +1783,7 @@ __global__ __launch_bounds__(256) void k_phs_set(DevGraph g, const uint32_t *slo
 
 hipError_t launch_resolve(const DevGraph &g, int step, uint64_t mask, uint64_t *send, uint32_t *slots,
                           const uint64_t *ids, uint64_t n, uint32_t *ans, uint64_t slot_top, hipStream_t s) {
+  launch_begin();
   const int vgrid = grid_for(slot_top, 256, 4096);
   switch (step) {
     case 0: hipLaunchKernelGGL(k_phs_reset, dim3(vgrid), dim3(256), 0, s, g, mask); break;
@@ -1848,6 +1855,7 @@ __global__ __launch_bounds__(256) void k_xlist(DevGraph g, const uint32_t *buf, 
 
 hipError_t launch_xlist(const DevGraph &g, bool scatter, uint64_t nblk, char *send, const XSend &x,
                         hipStream_t s) {
+  launch_begin();
   if (nblk == 0) return hipSuccess;
   const int grid = (int)((nblk + 3) / 4);
   if (scatter)
@@ -1899,6 +1907,7 @@ __global__ __launch_bounds__(256) void k_ximport(DevGraph g, const char *recv, X
 }
 
 hipError_t launch_ximport(const DevGraph &g, const char *recv, const XRecv &x, int level, hipStream_t s) {
+  launch_begin();
   const uint64_t n = x.start[x.G];
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_ximport, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, g, recv, x, level);
@@ -1929,6 +1938,7 @@ __global__ __launch_bounds__(256) void k_kill_fix(DevGraph g, const uint32_t *sl
 
 hipError_t launch_requests(const DevGraph &g, int phase, const uint64_t *ids, uint64_t n, uint8_t *ans,
                            const uint32_t *slots, hipStream_t s) {
+  launch_begin();
   if (n == 0) return hipSuccess;
   const int grid = grid_for(n, 256, 4096);
   if (phase == 0) hipLaunchKernelGGL(k_req_answer, dim3(grid), dim3(256), 0, s, g, ids, n, ans);
@@ -1951,6 +1961,7 @@ __global__ __launch_bounds__(256) void k_invalidate(DevGraph g, const uint64_t *
 }
 
 hipError_t launch_invalidate(const DevGraph &g, const uint64_t *ids, uint64_t n, hipStream_t s) {
+  launch_begin();
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_invalidate, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, g, ids, n);
   return hipGetLastError();
@@ -1977,6 +1988,7 @@ __global__ __launch_bounds__(256) void k_count_marked(DevGraph g) {
 }
 
 hipError_t launch_count_marked(const DevGraph &g, uint64_t slot_top, hipStream_t s) {
+  launch_begin();
   hipLaunchKernelGGL(k_count_marked, dim3(level_grid(slot_top)), dim3(256), 0, s, g);
   return hipGetLastError();
 }
@@ -2000,6 +2012,7 @@ __global__ __launch_bounds__(256) void k_local_roots(DevGraph g) {
 }
 
 hipError_t launch_local_roots(const DevGraph &g, uint64_t slot_top, hipStream_t s) {
+  launch_begin();
   hipLaunchKernelGGL(k_local_roots, dim3(grid_for(slot_top, 256, 8192)), dim3(256), 0, s, g);
   return hipGetLastError();
 }

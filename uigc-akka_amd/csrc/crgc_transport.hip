@@ -126,6 +126,7 @@ struct RcclTransport final : crgc_transport {
       hipStream_t s;
       int query() {
         const hipError_t e = hipStreamQuery(s);
+        if (e == hipErrorNotReady) (void)hipGetLastError();  // a soft status: not the caller's error
         return e == hipSuccess ? 0 : (e == hipErrorNotReady ? 1 : -1);
       }
       bool async_error() {

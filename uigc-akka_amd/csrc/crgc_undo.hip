@@ -95,12 +95,14 @@ __global__ __launch_bounds__(256) void k_ua_fold_fields(UndoAccDev u, UaFieldArg
 }
 
 hipError_t launch_ua_fold_deltas(const UndoAccDev &u, const UaDeltaArgs &a, hipStream_t s) {
+  launch_begin();
   if (a.n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_ua_fold_deltas, dim3((a.n + 255) / 256), dim3(256), 0, s, u, a);
   return hipGetLastError();
 }
 
 hipError_t launch_ua_fold_fields(const UndoAccDev &u, const UaFieldArgs &a, hipStream_t s) {
+  launch_begin();
   if (a.n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_ua_fold_fields, dim3((a.n + 255) / 256), dim3(256), 0, s, u, a);
   return hipGetLastError();
@@ -146,12 +148,14 @@ __global__ __launch_bounds__(256) void k_ua_rehash_pairs(UndoAccDev o, UndoAccDe
 }
 
 hipError_t launch_ua_init(const UndoAccDev &u, hipStream_t s) {
+  launch_begin();
   hipLaunchKernelGGL(k_ua_init, dim3(grid_for(std::max(u.cap, u.pcap), 256, 4096)), dim3(256), 0, s, u);
   return hipGetLastError();
 }
 
 // ids too (map != null: old id bucket -> new) or pairs only
 hipError_t launch_ua_rehash(const UndoAccDev &o, const UndoAccDev &n, uint32_t *map, bool ids, hipStream_t s) {
+  launch_begin();
   if (ids)
     hipLaunchKernelGGL(k_ua_rehash_ids, dim3(grid_for(o.cap, 256, 4096)), dim3(256), 0, s, o, n, map);
   hipLaunchKernelGGL(k_ua_rehash_pairs, dim3(grid_for(o.pcap, 256, 4096)), dim3(256), 0, s, o, n,
@@ -203,6 +207,7 @@ __global__ __launch_bounds__(256) void k_ua_created(UndoAccDev u, UaExportArgs x
 }
 
 hipError_t launch_ua_export(const UndoAccDev &u, const UaExportArgs &x, int phase, hipStream_t s) {
+  launch_begin();
   const int gi = grid_for(u.cap, 256, 4096), gp = grid_for(u.pcap, 256, 4096);
   if (phase == 0) {  // counts: admitted fields, created refs per field, and their scans
     hipLaunchKernelGGL(k_ua_prep, dim3(gi), dim3(256), 0, s, u, x);

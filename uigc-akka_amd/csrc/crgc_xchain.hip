@@ -254,6 +254,7 @@ __global__ __launch_bounds__(256) void k_xc_finish(DevGraph g, XcArgs x) {
 
 hipError_t launch_xclosure(const DevGraph &g, const XcArgs &x, int step, const void *p0, uint32_t *p1, uint64_t n,
                            uint32_t fi, int first, hipStream_t s) {
+  launch_begin();
   switch (step) {
     case 0: {  // import this round's received marks
       const XRecv *r = (const XRecv *)p1;

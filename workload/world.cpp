@@ -120,9 +120,25 @@ struct wl_world {
   double p_send = 0.40, p_share = 0.20, p_release = 0.20, p_spawn = 0.10;
   double actions_per_msg = 1.5;
   uint64_t n_entries_emitted = 0;
+  uint32_t id_space = 0;  // 0: the historical id map (C1-C3, C5 streams); k: mix48(k << 32 | index)
 };
 
+// A bijection of the 48-bit integers (xor-shifts and odd multipliers mod 2^48).
+static uint64_t mix48(uint64_t x) {
+  const uint64_t M = 0xFFFFFFFFFFFFull;
+  x &= M;
+  x ^= x >> 23;
+  x = (x * 0x9E3779B97F4A7C15ull) & M;
+  x ^= x >> 25;
+  x = (x * 0xBF58476D1CE4E5B9ull) & M;
+  x ^= x >> 21;
+  return x;
+}
+
 static uint64_t make_id(wl_world *w, uint64_t idx) {
+  // Id space k > 0 (C4's components, wl_set_id_space): a bijection of
+  // (k, actor index), so several simulated producers of one node never share an id.
+  if (w->id_space) return ((uint64_t)w->location << 48) | mix48(((uint64_t)w->id_space << 32) | idx);
   // random-looking 48-bit local part so hash placement is uniform
   uint64_t x = (idx + 1) * 0x9E3779B97F4A7C15ull;
   x ^= x >> 29;
@@ -282,6 +298,13 @@ wl_world *wl_create(uint64_t seed, uint32_t F, uint16_t location) {
 }
 
 void wl_destroy(wl_world *w) { delete w; }
+
+// Before any actor exists: ids from the injective map of space k (1..65535).
+int wl_set_id_space(wl_world *w, uint32_t k) {
+  if (!w->actors.empty() || k > 0xFFFF) return -1;
+  w->id_space = k;
+  return 0;
+}
 
 void wl_set_mix(wl_world *w, double p_send, double p_share, double p_release, double p_spawn,
                 double actions_per_msg) {

@@ -49,6 +49,7 @@ def _load():
         lib.wl_create.argtypes = [C.c_uint64, C.c_uint32, C.c_uint16]
         lib.wl_destroy.argtypes = [C.c_void_p]
         lib.wl_set_mix.argtypes = [C.c_void_p] + [C.c_double] * 5
+        lib.wl_set_id_space.argtypes = [C.c_void_p, C.c_uint32]
         lib.wl_bulk_graph.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_double,
                                       C.c_uint32, C.c_uint64]
         lib.wl_chain_graph.argtypes = [C.c_void_p] + [C.c_uint32] * 6
@@ -93,6 +94,12 @@ class World:
             self.close()
         except Exception:
             pass
+
+    def set_id_space(self, k: int):
+        """Ids from an injective map of (k, actor index): producers with different
+        k never share an id (C4's components).  Call before any graph is built."""
+        if self.lib.wl_set_id_space(self.h, k) != 0:
+            raise ValueError("wl_set_id_space: actors exist already or k > 65535")
 
     def set_mix(self, send=0.4, share=0.2, release=0.2, spawn=0.1, actions_per_msg=1.5):
         self.lib.wl_set_mix(self.h, send, share, release, spawn, actions_per_msg)
