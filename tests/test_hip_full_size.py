@@ -1,0 +1,90 @@
+"""Garbage-set parity at the sizes the bench numbers are quoted on.
+
+The checker is the OpenMP engine (oracle/omp_graph.cpp): its garbage and kill
+sets, live / pseudo-root / traced-edge counts are pinned to the single-thread
+oracle's by tests/test_omp_graph_cpu.py, and it finishes a 1e8-edge wakeup in
+a fraction of a second on the box's cores where the oracle would take minutes.
+
+  * C2 at full size, the bench's own stream (bench.py: seed 0x5EED + 2,
+    location 1, 1e7 actors / 1e8 edges, 1e6-entry wakeups with 9 % busy and
+    1 % in flight): every trace compared, sets and counts.
+  * C4's construction (8 producers of one node, workload/world.py
+    c4_producer) at 2e6 actors / 2e7 edges on G = 8 logical shards of one
+    MI355X (the 8-GPU layout; in-process transport), against the unsharded
+    OpenMP engine: the sharded protocol at the largest size that fits the
+    test budget.
+
+Reference semantics: ShadowGraph.java:205-289 (trace), :75-125 (mergeEntry).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import world
+
+pytestmark = pytest.mark.gpu
+
+THREADS = int(os.environ.get("OMP_NUM_THREADS") or min(16, os.cpu_count() or 1))
+
+
+def _same(rh, ro, what):
+    assert rh.n_live == ro["live"], what
+    assert rh.pseudo_roots == ro["pseudo_roots"], what
+    assert rh.edges_scanned == ro["edges_scanned"], what
+    assert len(rh.garbage) == ro["garbage"] and len(rh.kill) == ro["kill"], what
+    assert np.array_equal(np.sort(rh.garbage), np.sort(ro["garbage_ids"])), what
+    assert np.array_equal(np.sort(rh.kill), np.sort(ro["kill_ids"])), what
+
+
+def test_c2_full_size_garbage_sets_match_openmp(hip_mod, oracle_mod):
+    V, E, B = 10_000_000, 100_000_000, 1_000_000
+    w = world.World(seed=0x5EED + 2, location=1)      # bench.py's rank-0 C2 node
+    w.bulk_graph(V, E, alpha=2.1, n_roots=V // 1000, cap=100000)
+    h = hip_mod.ShadowGraph(vertex_capacity=int(V * 1.2), edge_capacity=int(E * 1.2))
+    p = oracle_mod.OmpGraph(threads=THREADS, vertex_hint=int(V * 1.5))
+    p.reserve_ids(1 << 20)
+    for b in w.batches(1 << 20):
+        h.merge_entries(b.to_device())
+        p.merge_entries(b)
+    rh, rp = h.trace(True), p.trace(True, ids=True)
+    _same(rh, rp, "after the load")
+    assert rh.n_live > 0.99 * V
+    for k in range(2):
+        b = w.wakeup(B, busy=V * 9 // 100, pending=V // 100)
+        h.merge_entries(b.to_device())
+        p.merge_entries(b)
+        rh, rp = h.trace(True), p.trace(True, ids=True)
+        _same(rh, rp, f"wakeup {k}")
+        assert rh.pseudo_roots > 0.07 * rh.n_live          # the §8d cut: ~10 % busy / in flight
+        assert rh.edges_scanned > 0.9 * E
+        assert len(rh.garbage) > 0 and len(rh.kill) > 0
+
+
+def test_c4_construction_eight_logical_shards_match_openmp(hip_mod, oracle_mod):
+    V, E = 2_000_000, 20_000_000                       # C4's construction at 1/50 scale
+    P = world.C4_PRODUCERS
+    ws = [world.c4_producer(k, V // P, E // P) for k in range(P)]
+    h = hip_mod.ShardedShadowGraph(8, vertex_capacity=V // 8 * 3, edge_capacity=E // 8 * 2)
+    p = oracle_mod.OmpGraph(threads=THREADS, vertex_hint=int(V * 1.5))
+    p.reserve_ids(1 << 20)
+    try:
+        for w in ws:
+            for b in w.batches(1 << 18):
+                h.merge_entries(b, split=True)          # every shard contributes a part
+                p.merge_entries(b)
+        rh, rp = h.trace(True), p.trace(True, ids=True)
+        _same(rh, rp, "after the load")
+        for k in range(2):
+            from crgc_hip.batch import EntryBatch
+            b = EntryBatch.concat([w.wakeup(V // 10 // P, busy=V // P * 9 // 100, pending=V // P // 100)
+                                   for w in ws])
+            h.merge_entries(b, split=True)
+            p.merge_entries(b)
+            rh, rp = h.trace(True), p.trace(True, ids=True)
+            _same(rh, rp, f"wakeup {k}")
+            assert rh.rounds >= 2 and rh.ids_sent > 0      # marks crossed shards
+            assert rh.pseudo_roots > 0.07 * rh.n_live
+        assert h.total_actors_seen() >= V
+    finally:
+        h.close()

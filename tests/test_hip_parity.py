@@ -280,3 +280,74 @@ def test_fan_in_candidate_overflow(hip_mod, oracle_mod, monkeypatch, pull):
         h.merge_entries(b); o.merge_entries(b)
         assert h.export() == o.export()
         _same_trace(h.trace(True), o.trace(True))
+
+
+def test_entry_field_size_above_255(hip_mod, oracle_mod):
+    """uigc.crgc.entry-field-size is any int in the reference (Context.java:14):
+    F = 300, and 512 root entries that all spawn the same 300 children — about
+    76 500 last-write-wins supervisor conflicts in the first 256-entry block,
+    more than round 3's 16-bit per-block count could hold.  Every
+    child's supervisor must be the last spawner in batch order (:101-102)."""
+    from crgc_hip import Entry, EntryBatch
+    F = 300
+    h = hip_mod.ShadowGraph(entry_field_size=F)
+    o = oracle_mod.OracleGraph(entry_field_size=F)
+    loc = 1 << 48
+    root = loc | 1
+    parents = [loc | (10 + i) for i in range(512)]
+    kids = [loc | (10_000 + j) for j in range(F)]
+    es = [Entry(self=root, isRoot=True, spawnedActors=parents[:F]),      # supervisor of the parents
+          Entry(self=root, isRoot=True, spawnedActors=parents[F:])]
+    es += [Entry(self=p, isRoot=True, spawnedActors=kids, createdOwners=[p], createdTargets=[kids[i % F]])
+           for i, p in enumerate(parents)]
+    b = EntryBatch.from_entries(es)
+    h.merge_entries(b)
+    o.merge_entries(b)
+    st = h.export()
+    assert st == o.export()
+    assert {st.vertices[k][2] for k in kids} == {parents[-1]}  # (recv, flags, supervisor)
+    _same_trace(h.trace(True), o.trace(True))
+    # the parents stop being roots and release their refs: only the last one stays
+    # live (the kids' supervisor); the others are garbage, killed (their supervisor is live)
+    es = [Entry(self=p, updatedRefs=[kids[i % F]], updatedInfos=[1]) for i, p in enumerate(parents)]
+    b = EntryBatch.from_entries(es)
+    h.merge_entries(b)
+    o.merge_entries(b)
+    assert h.export() == o.export()
+    rh, ro = h.trace(True), o.trace(True)
+    _same_trace(rh, ro)
+    assert rh.kill_set() == set(parents[:-1])
+
+
+def test_trace_ids_into_partly_registered_buffer(hip_mod, oracle_mod):
+    """the device stores trace ids straight into a caller buffer only
+    when the whole capacity lies in one pinned range.  A garbage buffer that
+    starts inside a crgc_host_register range and runs past its end gets the ids
+    by a stream copy (direct_lists = 0) — a device store there would fault — and
+    buffers wholly inside the range get them from the device (direct_lists = 1)."""
+    h, o = _pair(hip_mod, oracle_mod)
+    arena = np.zeros(1 << 20, np.uint64)        # 8 MiB; the first half is registered
+    half = 1 << 19
+    h.register_host(arena[:half])
+    fz = fuzz.Fuzz(29)
+    try:
+        for step in range(6):
+            eb = fz.entries(3000)
+            h.merge_entries(eb)
+            o.merge_entries(eb)
+            if step % 2 == 0:
+                g, want_direct = arena[half - 64:half + 8192], 0   # runs past the pinned half
+            else:
+                g, want_direct = arena[8192:8192 + 16384], 1      # wholly pinned
+            k = arena[:8192]
+            rc, out = h._trace_into(True, g, k)
+            assert rc == abi.OK
+            ro = o.trace(True)
+            assert set(g[:out.n_garbage].tolist()) == ro.garbage_set()
+            assert set(k[:out.n_kill].tolist()) == ro.kill_set()
+            assert out.n_live == ro.n_live
+            assert out.stats.direct_lists == want_direct, step
+            assert out.stats.time_query_failures == 0
+            fz.sync(o.export())
+    finally:
+        h.unregister_host(arena[:half])

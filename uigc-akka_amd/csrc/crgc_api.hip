@@ -43,11 +43,11 @@ hipError_t dmalloc(T **p, uint64_t n) {
 void free_arrays(Arrays &a) {
   if (!a.allocated) return;
   DevGraph &d = a.d;
-  void *ps[] = {d.htab, d.vid, d.recv, d.flags, d.sup, d.adj, d.ecap, d.vseq, d.sseq,
+  void *ps[] = {d.htab, d.vid, d.recv, d.flags, d.sup, d.adj, d.vseq, d.sseq,
                 d.pool, d.etab, d.vis, d.front[0], d.front[1],
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat, d.xbytes,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill,
-                d.nzdeg, d.radj, d.rcap, d.rnew, d.rpool, d.par, d.fx, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
+                d.nzdeg, d.radj, d.rnew, d.rpool, d.par, d.fx, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
                 d.xp_buf, d.xp_cnt, d.rq_buf, d.rq_cnt, d.phs};
   for (void *p : ps)
     if (p) hipFree(p);
@@ -86,7 +86,6 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   A(dmalloc(&d.flags, c.scap));
   A(dmalloc(&d.sup, c.scap));
   A(dmalloc(&d.adj, c.scap));
-  A(dmalloc(&d.ecap, c.scap));
   A(dmalloc(&d.vseq, c.scap));
   A(dmalloc(&d.sseq, c.scap));
   A(dmalloc(&d.pool, c.pcap));
@@ -112,7 +111,6 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   d.rpcap = c.pcap;
   A(dmalloc(&d.nzdeg, c.scap));
   A(dmalloc(&d.radj, c.scap));
-  A(dmalloc(&d.rcap, c.scap));
   A(dmalloc(&d.rnew, c.scap));
   A(dmalloc(&d.rpool, d.rpcap));
   A(dmalloc(&d.par, c.scap));
@@ -145,7 +143,6 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   M(d.flags, 0, c.scap);
   M(d.sup, 0xFF, c.scap * 4);
   M(d.adj, 0, c.scap * 8);
-  M(d.ecap, 0, c.scap * 4);
   M(d.vseq, 0, c.scap * 8);
   M(d.sseq, 0, c.scap * 8);
   M(d.etab, 0xFF, c.ecap * sizeof(EdgeBucket));
@@ -156,7 +153,6 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   M(d.dirty[1], 0, c.scap / BLK_SLOTS);
   M(d.nzdeg, 0, c.scap * 4);
   M(d.radj, 0, c.scap * 8);
-  M(d.rcap, 0, c.scap * 4);
   M(d.rnew, 0, c.scap * 4);
   M(d.par, 0xFF, c.scap * 4);  // no hints in a new generation
   M(d.fx, 0, c.scap / 8);
@@ -181,6 +177,22 @@ Caps caps_for(uint64_t live, uint64_t edges, uint64_t ids_pending, uint64_t atom
   uint64_t pc = 4 * edges + 8 * atoms_pending + 4 * c.scap + 65536;
   c.pcap = std::min<uint64_t>(pc, 0xFFFFFFF0ull);
   c.ecap = pow2ceil((edges + 2 * atoms_pending) * 3 / 2 + 65536);
+  return c;
+}
+
+// A new graph's capacities from the caller's hints (expected live shadows v0
+// and live (owner, target) pairs e0): slots for twice the live shadows (a trace
+// compacts once dead slots outnumber live ones), the id table at load <= 1/3,
+// the edge table at load <= 2/3 of e0, the pools for power-of-two segments with
+// room to move.  (caps_for sizes a rebuild, which also reserves for the
+// pending merge.)  At C4 on one GPU (1.1e8 / 1.1e9 hints) this is ~130 GB of
+// the 288 GB: caps_for(v0, e0, v0, e0) asked for ~250 GB there.
+Caps caps_create(uint64_t v0, uint64_t e0) {
+  Caps c;
+  c.scap = round_up(2 * v0 + v0 / 4 + 8192, BLK_SLOTS);
+  c.hcap = pow2ceil(c.scap * 3 / 2 + 1024);
+  c.pcap = std::min<uint64_t>(4 * e0 + 4 * c.scap + 65536, 0xFFFFFFF0ull);
+  c.ecap = pow2ceil(e0 * 3 / 2 + 65536);
   return c;
 }
 
@@ -423,6 +435,13 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   const uint64_t live_ub =
       std::min<uint64_t>(src_top, h->live + (h->hctr->inserted - h->inserted_at_trace));
   Caps c = caps_for(std::max<uint64_t>(live_ub, 1), h->etab_used, ids, atoms);
+  if (h->knobs.level_log)
+    fprintf(stderr, "[crgc] rebuild: slots %llu (live <= %llu) pool %llu / %llu rpool %llu edge keys %llu / %llu "
+                    "-> slots %llu pool %llu edge table %llu\n",
+            (unsigned long long)src_top, (unsigned long long)live_ub, (unsigned long long)h->pool_top,
+            (unsigned long long)h->g.caps.pcap, (unsigned long long)h->rpool_top,
+            (unsigned long long)h->etab_used, (unsigned long long)h->g.caps.ecap, (unsigned long long)c.scap,
+            (unsigned long long)c.pcap, (unsigned long long)c.ecap);
   Arrays dst;
   HIP_TRY(alloc_arrays(dst, c, h->ctr, h->stream, h->G, h->shard, h->tp != nullptr));
   Scratch tmp;
@@ -633,7 +652,7 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     }
     const uint64_t v0 = cfg && cfg->vertex_capacity ? cfg->vertex_capacity : (1u << 16);
     const uint64_t e0 = cfg && cfg->edge_capacity ? cfg->edge_capacity : 8 * v0;
-    Caps c = caps_for(v0, e0, v0, e0);
+    Caps c = caps_create(v0, e0);
     if (hipError_t e = alloc_arrays(h->g, c, h->ctr, h->stream, h->G, h->shard, h->tp != nullptr)) {
       rc = map_hip(e);
       break;

@@ -241,7 +241,7 @@ __global__ __launch_bounds__(EP_WG) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const uint32_t ph = tid < np ? L.plist[tid] : 0;
     const uint64_t pkey = tid < np ? L.key[ph] : 0;
     const int32_t psum = tid < np ? L.sum[ph] : 0;
-    uint32_t rk = EP_SKIP, pbk = 0, rcap_t = 0;
+    uint32_t rk = EP_SKIP, pbk = 0;
     if (tid < np && psum != 0) {  // absent == 0: a zero sum changes nothing
       const int32_t d = psum;
       const uint32_t o = (uint32_t)(pkey >> 32), t = (uint32_t)pkey;
@@ -262,19 +262,21 @@ __global__ __launch_bounds__(EP_WG) __attribute__((amdgpu_waves_per_eu(8, 8))) v
           if ((old > 0) != (now > 0)) {  // the reverse candidate follows the count's sign
             const uint32_t r = rv;  // loaded with the key: this workgroup owns the pair
             const uint32_t cand = o | (now > 0 ? RC_POS : 0u);
-            if (r != 0xFFFFFFFFu && (r & EP_PENDING)) a.rv_o[r & ~EP_PENDING] = cand;  // still in the overflow list
-            else if (r < g.rcap[t]) g.rpool[(uint64_t)g.radj[t].x + r] = cand;
+            if (r != 0xFFFFFFFFu && (r & EP_PENDING)) {
+              a.rv_o[r & ~EP_PENDING] = cand;  // still in the overflow list
+            } else {
+              const uint2 rd = g.radj[t];  // offset and capacity in one load
+              if (r < rseg_cap(rd.y)) g.rpool[(uint64_t)rd.x + r] = cand;
+            }
             if (now <= 0 && g.par[t] == o) g.par[t] = SLOT_NONE;  // the pull hint dies with the count
           }
           rk = EP_EXIST;
         } else {
-          // a new edge: its owner's degree / capacity (for the growth) and its
-          // target's candidate capacity, beside the existing pairs' updates
+          // a new edge: its owner's segment and degree (for the growth; the
+          // capacity follows from the degree), beside the existing pairs' updates
           const uint2 oad = g.adj[o];
-          const uint32_t cap = g.ecap[o];
-          rcap_t = g.rcap[t];
           L.oseg[oh] = oad.x;  // every new pair of the owner stores the same values
-          L.oinf[oh] = ep_pack_inf(oad.y, cap);
+          L.oinf[oh] = ep_pack_inf(oad.y, seg_cap(oad.y));
           rk = atomicAdd(&L.ocnt[oh], 1u);
           atomicAdd(&L.nnew, 1u);
         }
@@ -295,7 +297,7 @@ __global__ __launch_bounds__(EP_WG) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         uint32_t cap;
         if (inf == EP_INF_RELOAD) {
           ad = g.adj[o];
-          cap = g.ecap[o];
+          cap = seg_cap(ad.y);
         } else {
           ad = make_uint2(L.oseg[oh], inf & ((1u << 27) - 1));
           cap = (inf >> 27) == 31 ? 0u : (1u << (inf >> 27));
@@ -316,10 +318,7 @@ __global__ __launch_bounds__(EP_WG) __attribute__((amdgpu_waves_per_eu(8, 8))) v
       }
       ep_move(g.pool, ad.x, ad.y, r);
       if (tid < nol) {
-        if (r != 0xFFFFFFFFu) {
-          ad.x = r;
-          g.ecap[o] = want;
-        }
+        if (r != 0xFFFFFFFFu) ad.x = r;  // capacity: seg_cap of the new degree (= want)
         L.ocnt[oh] = add ? ad.x + 1 : 0u;  // (LDS: two 1024-thread workgroups per CU need <= 80 KiB each)
         if (add) g.adj[o] = make_uint2(ad.x, ad.y + add);
         const int32_t dz = L.onz[oh] + (int32_t)add;  // new edges have nonzero counts
@@ -341,10 +340,12 @@ __global__ __launch_bounds__(EP_WG) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         nbk = pbk;
         g.pool[(uint64_t)(L.ocnt[oh] - 1) + nidx] = pack_edge(nt, d);
         cand = o | (d > 0 ? RC_POS : 0u);
-        const uint32_t cap = rcap_t;
+        // the append returns the segment's offset, length and capacity at once
         const unsigned long long old = atomicAdd((unsigned long long *)&g.radj[nt], 1ull << 32);
-        ridx = (uint32_t)(old >> 32);
-        if (ridx < cap) {
+        const uint32_t ry = (uint32_t)(old >> 32);
+        ridx = rseg_len(ry);
+        if (ridx >= RLEN_MASK) set_err(c, ERR_POOL_FULL);  // 2^27 candidates on one shadow: unsupported
+        if (ridx < rseg_cap(ry)) {
           g.rpool[(uint64_t)(uint32_t)old + ridx] = cand;
           g.etab[nbk].val = nidx;
           g.etab[nbk].rev = ridx;
@@ -398,15 +399,14 @@ __global__ __launch_bounds__(RV_THREADS) void k_rv_grow(DevGraph g, EdgeArgs a) 
   const uint64_t stride = (uint64_t)gridDim.x * RV_THREADS;
   for (uint64_t b0 = (uint64_t)blockIdx.x * RV_THREADS; b0 < n; b0 += stride) {  // uniform per block
     const uint64_t q = b0 + threadIdx.x;
-    uint32_t t = 0, cap = 0, want = 0;
+    uint32_t t = 0, cap = 0, want = 0, len = 0;
     uint2 rd = make_uint2(0, 0);
     if (q < n) {
       t = a.rv_t[q];
-      cap = g.rcap[t];
-      if (a.rv_i[q] == cap) {  // the first overflow of t
-        rd = g.radj[t];        // final length: every append of the merge is done
-        want = seg_cap_ep(rd.y);
-      }
+      rd = g.radj[t];  // final length: every append of the merge is done
+      cap = rseg_cap(rd.y);
+      len = rseg_len(rd.y);
+      if (a.rv_i[q] == cap) want = seg_cap_ep(len);  // the first overflow of t
     }
     const uint32_t v1[1] = {want};
     unsigned long long offs[1];
@@ -417,10 +417,7 @@ __global__ __launch_bounds__(RV_THREADS) void k_rv_grow(DevGraph g, EdgeArgs a) 
       else r = (uint32_t)offs[0];
     }
     ep_move(g.rpool, rd.x, cap, r);  // the candidates that fitted
-    if (r != 0xFFFFFFFFu) {
-      g.radj[t].x = r;
-      g.rcap[t] = want;
-    }
+    if (r != 0xFFFFFFFFu) g.radj[t] = make_uint2(r, rseg_pack(len, want));
   }
 }
 
@@ -429,8 +426,9 @@ __global__ __launch_bounds__(RV_THREADS) void k_rv_place(DevGraph g, EdgeArgs a)
   const uint64_t stride = (uint64_t)gridDim.x * RV_THREADS;
   for (uint64_t q = (uint64_t)blockIdx.x * RV_THREADS + threadIdx.x; q < n; q += stride) {
     const uint32_t t = a.rv_t[q], i = a.rv_i[q];
-    if (i >= g.rcap[t]) continue;  // its growth failed (ERR_POOL_FULL)
-    g.rpool[(uint64_t)g.radj[t].x + i] = a.rv_o[q];
+    const uint2 rd = g.radj[t];
+    if (i >= rseg_cap(rd.y)) continue;  // its growth failed (ERR_POOL_FULL)
+    g.rpool[(uint64_t)rd.x + i] = a.rv_o[q];
     g.etab[a.rv_b[q]].rev = i;
   }
 }

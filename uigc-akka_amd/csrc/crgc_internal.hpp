@@ -10,7 +10,7 @@
 //     flags[u8]   ALIVE|INTERNED|LOCAL|BUSY|ROOT|HALTED
 //     sup[u32]    Shadow.supervisor as a slot (NONE = null, DEAD = collected)
 //     adj[uint2]  {offset, degree} of the slot's out-edge segment in the pool
-//     ecap[u32]   segment capacity
+//                 (capacity seg_cap(degree))
 //   edge pool   pool[u64] = target slot (lo 32) | count (hi 32): Shadow.outgoing
 //   edge table  etab[{key u64 = owner<<32|target, val u32 = index inside the
 //               segment, rev u32 = index of its reverse candidate}] 16-B buckets
@@ -134,15 +134,13 @@ struct DevGraph {
   int32_t *recv;
   uint8_t *flags;
   uint32_t *sup;
-  uint2 *adj;
-  uint32_t *ecap;
+  uint2 *adj;                // {segment offset, degree}; the segment's capacity is seg_cap(degree)
   unsigned long long *vseq;  // last-write-wins tag for busy/root
   unsigned long long *sseq;  // last-write-wins tag for supervisor
   uint32_t *nzdeg;           // out-edges with count != 0 (reference `outgoing.size()`)
   // reverse candidates (pull BFS): owners that ever created an edge key to the
   // slot; a candidate is verified against the forward count when used
-  uint2 *radj;               // {offset, length} into rpool
-  uint32_t *rcap;
+  uint2 *radj;               // {offset, rlen | log2(capacity) << RLEN_BITS} into rpool (rseg_*)
   uint32_t *rnew;            // rebuild scratch: in-degree per target
   uint32_t *rpool;           // owner slot | RC_POS while count(owner -> slot) > 0
   uint32_t *par;             // pull hint per slot: an owner whose edge to it has a positive count
@@ -186,6 +184,32 @@ struct DevGraph {
   uint32_t *phs;      // per proxy slot: its slot at the home shard (PHS_NONE / PHS_ABSENT)
   Counters *ctr;
 };
+
+// Segment capacities are powers of two >= 4 (0: no segment).  An owner's
+// out-edge segment always has capacity seg_cap(degree): it grows to that when
+// its degree passes the old capacity, a rebuild sizes it the same way, and the
+// degree only grows in between — so no capacity array is read (one random line
+// less per new edge in k_ep_owner).
+__host__ __device__ inline uint32_t seg_cap(uint32_t deg) {
+  if (deg == 0) return 0;
+  uint32_t c = 4;
+  while (c < deg) c <<= 1;
+  return c;
+}
+// A reverse-candidate segment's length and capacity share radj[t].y, so the one
+// returning 64-bit atomic that appends a candidate also tells whether it fits:
+// length in the low RLEN_BITS bits (at most 2^27 - 1 candidates per shadow;
+// more sets ERR_POOL_FULL), log2(capacity) above them (0: no segment).
+constexpr uint32_t RLEN_BITS = 27;
+constexpr uint32_t RLEN_MASK = (1u << RLEN_BITS) - 1;
+__host__ __device__ inline uint32_t rseg_len(uint32_t y) { return y & RLEN_MASK; }
+__host__ __device__ inline uint32_t rseg_cap(uint32_t y) {
+  const uint32_t lc = y >> RLEN_BITS;
+  return lc ? (1u << lc) : 0u;
+}
+__host__ __device__ inline uint32_t rseg_pack(uint32_t len, uint32_t cap) {
+  return len | ((cap ? (uint32_t)__builtin_ctz(cap) : 0u) << RLEN_BITS);
+}
 
 // splitmix64 finaliser
 __host__ __device__ inline uint64_t mix64(uint64_t x) {

@@ -132,8 +132,7 @@ __global__ __launch_bounds__(IDS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 
           g.vid[s] = id[j];
           g.flags[s] = home ? FL_ALIVE : (FL_ALIVE | FL_PROXY);
           if (rfit) {
-            g.radj[s] = make_uint2((uint32_t)ro, 0u);
-            g.rcap[s] = IDS_RCAP;
+            g.radj[s] = make_uint2((uint32_t)ro, rseg_pack(0, IDS_RCAP));
           }
         }
         ++s;

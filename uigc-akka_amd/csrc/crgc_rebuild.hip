@@ -102,7 +102,6 @@ __global__ __launch_bounds__(256) void k_rb_edges(DevGraph src, uint64_t src_top
           ++kept;
         }
         dst.adj[ns] = make_uint2((uint32_t)off, kept);
-        dst.ecap[ns] = rb_cap(kept);
         // The reference keeps nonzero counts toward collected shadows in
         // `outgoing` (their Shadow objects stay keys there), so they still
         // count in outgoing.size(): carry the owner's count over unchanged.
@@ -211,8 +210,7 @@ __global__ __launch_bounds__(256) void k_rb_rsetup(DevGraph dst, const uint64_t 
   const uint64_t n = dst.ctr->slot_top;
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < n; v += stride) {
-    dst.rcap[v] = rb_cap(dst.rnew[v]);
-    dst.radj[v] = make_uint2((uint32_t)offs[v], 0);
+    dst.radj[v] = make_uint2((uint32_t)offs[v], rseg_pack(0, rb_cap(dst.rnew[v])));
     dst.rnew[v] = 0;
   }
 }
@@ -225,7 +223,7 @@ __global__ __launch_bounds__(256) void k_rb_rfill(DevGraph dst) {
     for (uint32_t e = 0; e < ad.y; ++e) {
       const uint64_t ed = dst.pool[(uint64_t)ad.x + e];
       const uint32_t t = edge_target(ed);
-      const uint32_t pos = atomicAdd(&dst.radj[t].y, 1u);
+      const uint32_t pos = rseg_len(atomicAdd(&dst.radj[t].y, 1u));
       dst.rpool[(uint64_t)dst.radj[t].x + pos] = (uint32_t)o | (edge_count(ed) > 0 ? RC_POS : 0u);
       // the edge's bucket, for its candidate index
       const uint64_t key = edge_key((uint32_t)o, t);

@@ -496,7 +496,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       const uint4 r01 = *(const uint4 *)(g.radj + v0);
       const uint4 r23 = *(const uint4 *)(g.radj + v0 + 2);
       const uint32_t ro[4] = {r01.x, r01.z, r23.x, r23.z};
-      const uint32_t rl[4] = {r01.y, r01.w, r23.y, r23.w};
+      const uint32_t rl[4] = {rseg_len(r01.y), rseg_len(r01.w), rseg_len(r23.y), rseg_len(r23.w)};
       nb2 += 64;  // four in-candidate ranges
       // The thread's (up to) 4 lists are walked together, one round trip for
       // the candidates and one for their frontier bits per round, until every

@@ -174,6 +174,20 @@ class World:
         return self.take(n_entries)
 
 
+C4_PRODUCERS = 8
+
+
+def c4_producer(k: int, n_actors: int, n_edges: int) -> World:
+    """Producer k (0..7) of BASELINE.json's C4 node: 1/8 of the actors and edges
+    of one power-law shadow graph (C2's distribution), location 1,
+    id space k + 1 (disjoint from every other producer's).  The union of the 8
+    producers' streams is one graph whatever the GPU count that holds it."""
+    w = World(seed=0x5EED + 4 + 1000 * k, location=1)
+    w.set_id_space(k + 1)
+    w.bulk_graph(n_actors, n_edges, alpha=2.1, n_roots=max(1, n_actors // 1000), cap=100000)
+    return w
+
+
 def deltas_of(batch: EntryBatch, F: int = 4, dgs: int = 64):
     """A remote node's drained entries folded into DeltaGraphs
     (LocalGC.scala:159-177 over DeltaGraph.java:73-180; workload/deltas.cpp):
