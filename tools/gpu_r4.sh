@@ -7,6 +7,8 @@
 #   kt               rocprofv3 --kernel-trace --stats of the timed C2 wakeups only (--no-pcie)
 #   pmc              FETCH_SIZE and WRITE_SIZE passes of the same command, one run each
 #   probe            tools/hip_probe.hip: HIP last-error / event / pointer-range semantics
+#   c4               C4 unsharded on one GPU (1e8 actors / 1e9 edges, the scaling anchor)
+#   c4l8 c2l8        C4 / C2 over 8 logical shards on the one GPU (the sharded protocol at full size)
 set -euo pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1; shift
@@ -37,6 +39,12 @@ for step in "$@"; do
           timeout -k 10 420 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o pmc -- $B \
             > "$O/bench_write.json" 2> "$O/bench_write.err") ;;
     probe) (cd "$ROOT" && timeout -k 10 60 ./tools/_build/hip_probe > "$O/hip_probe.txt" 2>&1) ;;
+    c4) (cd /tmp && CRGC_LEVEL_LOG=1 timeout -k 10 1000 python3 -u "$ROOT/bench.py" --workload c4 --steps 5 \
+          --warmup 2 --no-pcie > "$O/bench_c4.json" 2> "$O/bench_c4.err") ;;
+    c4l8) (cd /tmp && timeout -k 10 1000 python3 -u "$ROOT/bench.py" --workload c4 --logical-shards 8 \
+          --steps 3 --warmup 1 > "$O/bench_c4l8.json" 2> "$O/bench_c4l8.err") ;;
+    c2l8) (cd /tmp && timeout -k 10 600 python3 -u "$ROOT/bench.py" --workload c2 --logical-shards 8 \
+          --steps 5 --warmup 2 > "$O/bench_c2l8.json" 2> "$O/bench_c2l8.err") ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

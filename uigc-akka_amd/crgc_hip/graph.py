@@ -483,6 +483,13 @@ class ShardedShadowGraph:
         self._all(lambda s, b: s.merge_entries(b if b is not None else EntryBatch.empty()),
                   [(p,) for p in parts])
 
+    def merge_parts(self, parts):
+        """Merge one batch given as G per-shard parts (host or device batches; part r
+        contributed by shard r), applied in shard order."""
+        assert len(parts) == self.G
+        self._all(lambda s, b: s.merge_entries(b if b is not None else EntryBatch.empty()),
+                  [(p,) for p in parts])
+
     def merge_deltas(self, batch):
         self._all(lambda s, b: s.merge_deltas(b if b is not None else DeltaBatch.empty()),
                   [(batch,)] + [(None,)] * (self.G - 1))

@@ -339,6 +339,8 @@ struct crgc_graph {
   uint64_t x_bin_zeroed = 0;  // x_bin allocation (Scratch::gen) whose counters were zeroed
   Scratch x_gc, x_gc_list;   // replicated chain closure of sharded marks (crgc_xchain.hip)
   uint64_t *h_small = nullptr;       // pinned host staging for small all-gathers
+  uint64_t *h_bounce = nullptr;      // pinned bounce for id lists into partly pinned caller buffers
+  uint64_t h_bounce_bytes = 0;
   char *h_route = nullptr;           // pinned RoutePart / ConcatPart tables
   bool route = true;                 // CRGC_ROUTE=0: all-gather every batch instead
   // mark rounds in home-slot form: this shard's slot numbering generation
@@ -681,6 +683,7 @@ void crgc_destroy(crgc_graph *h) {
   if (h->ctr) hipFree(h->ctr);
   if (h->hctr) hipHostFree(h->hctr);
   if (h->h_small) hipHostFree(h->h_small);
+  if (h->h_bounce) hipHostFree(h->h_bounce);
   if (h->h_route) hipHostFree(h->h_route);
   if (h->roots_buf) hipFree(h->roots_buf);
   if (h->side) {
@@ -1717,7 +1720,8 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
     const uint64_t nb = (top + (1ull << shift) - 1) >> shift;
     if (shift <= 20 && nb <= BIN_MAX) {
       // BIN_SHARDS regions per bin; a full region falls back to direct stores
-      const uint64_t cap = std::max<uint64_t>(4096, (h->etab_used + h->atoms_since) / 2 / (nb * BIN_SHARDS));
+      // (a multiple of 64 entries: k_bin_apply reads the regions in 16-B groups)
+      const uint64_t cap = round_up(std::max<uint64_t>(4096, (h->etab_used + h->atoms_since) / 2 / (nb * BIN_SHARDS)), 64);
       const size_t cur_bytes = (size_t)(BIN_MAX * BIN_SHARDS + 4) * 4;
       HIP_TRY(h->x_bin.ensure(cur_bytes + nb * BIN_SHARDS * cap * 4));
       // a fresh allocation (compared by generation: a reallocation may return
@@ -2182,56 +2186,100 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
   }
 }
 
-// The device view of a caller's host buffer of `bytes` bytes that the device
-// may store to directly: the whole range must lie in ONE page-locked
-// allocation — a range of this handle's crgc_host_register, or an allocation
-// whose extent the runtime reports (hipHostMalloc) — else nullptr (pageable
-// memory, or a buffer that runs past its pinned allocation: the lists then
-// come back by a stream copy, copy_lists).
-static uint64_t *device_view(crgc_graph *h, uint64_t *p, uint64_t bytes) {
-  if (!p || !bytes) return nullptr;
+// How the device can reach a caller's host buffer of `bytes` bytes
+// (tools/hip_probe.hip, profiles/r4a/README.md):
+//   HOST_PAGEABLE  unknown to the runtime: stream copies stage it
+//   HOST_PINNED    wholly inside one page-locked allocation — a range of this
+//                  handle's crgc_host_register, or a hipHostMalloc block (whose
+//                  extent hipMemGetAddressRange reports; for registered memory it
+//                  reports no base): device stores or copies; *dview = device view
+//   HOST_PARTIAL   page-locked at its start but running past that allocation: the
+//                  runtime refuses a copy into it and a device store past the
+//                  range would fault, so its ids go through a bounce buffer
+enum HostKind { HOST_PAGEABLE, HOST_PINNED, HOST_PARTIAL };
+
+static HostKind host_kind(crgc_graph *h, const void *p, uint64_t bytes, uint64_t **dview) {
+  *dview = nullptr;
+  if (!p || !bytes) return HOST_PAGEABLE;
   hipPointerAttribute_t at{};
   if (hipPointerGetAttributes(&at, p) != hipSuccess) {
-    (void)hipGetLastError();  // pageable memory: not an error for the caller
-    return nullptr;
+    (void)hipGetLastError();  // a soft status: not the caller's error
+    return HOST_PAGEABLE;
   }
-  if (at.type != hipMemoryTypeHost || !at.devicePointer) return nullptr;
+  if (at.type != hipMemoryTypeHost || !at.devicePointer) return HOST_PAGEABLE;
   const char *c = (const char *)p;
   for (const auto &r : h->pinned)
-    if (c >= r.first && c + bytes <= r.first + r.second) return (uint64_t *)at.devicePointer;
+    if (c >= r.first && c < r.first + r.second) {
+      if (c + bytes > r.first + r.second) return HOST_PARTIAL;
+      *dview = (uint64_t *)at.devicePointer;
+      return HOST_PINNED;
+    }
   void *base = nullptr;
   size_t size = 0;
   if (hipMemGetAddressRange((hipDeviceptr_t *)&base, &size, (hipDeviceptr_t)p) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
+    (void)hipGetLastError();  // sticky otherwise (hipErrorNotFound)
+    return HOST_PARTIAL;
   }
-  const char *b = (const char *)base;
+  const char *bs = (const char *)base;
   const char *dv = (const char *)at.devicePointer;
   // the runtime reports the allocation in host or device addresses (one VA on gfx950)
-  const bool in_host = c >= b && c + bytes <= b + size;
-  const bool in_dev = dv >= b && dv + bytes <= b + size;
-  return (in_host || in_dev) ? (uint64_t *)at.devicePointer : nullptr;
+  const bool in_host = bs && c >= bs && c + bytes <= bs + size;
+  const bool in_dev = bs && dv >= bs && dv + bytes <= bs + size;
+  if (!(in_host || in_dev)) return HOST_PARTIAL;
+  *dview = (uint64_t *)at.devicePointer;
+  return HOST_PINNED;
 }
 
+// The garbage / kill lists of the last trace into the caller's buffers by
+// stream copies (or, for HOST_PARTIAL buffers, through a pinned bounce buffer).
 static int copy_lists(crgc_graph *h, crgc_trace_out *out, bool sync = true) {
   bool big = false;
   out->n_garbage = h->last_garbage;
   out->n_kill = h->last_kill;
   out->n_live = h->last_live;
   out->stats = h->last_stats;
-  if (out->garbage_ids) {
-    if (out->garbage_cap < h->last_garbage) big = true;
-    else if (h->last_garbage)
-      HIP_TRY(hipMemcpyAsync(out->garbage_ids, h->g.d.out_ids, h->last_garbage * 8,
-                             hipMemcpyDeviceToHost, h->stream));
+  struct Job {
+    uint64_t *dst;
+    const uint64_t *src;
+    uint64_t n;
+    bool bounce;
+  } jobs[2] = {{out->garbage_ids, h->g.d.out_ids, h->last_garbage, false},
+               {out->kill_ids, h->g.d.out_kill, h->last_kill, false}};
+  const uint64_t caps[2] = {out->garbage_cap, out->kill_cap};
+  uint64_t bounce_bytes = 0;
+  for (int j = 0; j < 2; ++j) {
+    Job &q = jobs[j];
+    if (!q.dst) continue;
+    if (caps[j] < q.n) {
+      big = true;
+      q.n = 0;
+      continue;
+    }
+    uint64_t *dv;
+    q.bounce = q.n && host_kind(h, q.dst, caps[j] * 8, &dv) == HOST_PARTIAL;
+    if (q.bounce) bounce_bytes += q.n * 8;
   }
-  if (out->kill_ids) {
-    if (out->kill_cap < h->last_kill) big = true;
-    else if (h->last_kill)
-      HIP_TRY(hipMemcpyAsync(out->kill_ids, h->g.d.out_kill, h->last_kill * 8, hipMemcpyDeviceToHost,
-                             h->stream));
+  if (bounce_bytes > h->h_bounce_bytes) {
+    if (h->h_bounce) hipHostFree(h->h_bounce);
+    h->h_bounce = nullptr;
+    h->h_bounce_bytes = 0;
+    HIP_TRY(hipHostMalloc((void **)&h->h_bounce, bounce_bytes, hipHostMallocDefault));
+    h->h_bounce_bytes = bounce_bytes;
   }
-  if (sync) HIP_TRY(hsync(h));
+  uint64_t at = 0;
+  for (Job &q : jobs) {
+    if (!q.dst || !q.n) continue;
+    uint64_t *to = q.bounce ? h->h_bounce + at / 8 : q.dst;
+    HIP_TRY(hipMemcpyAsync(to, q.src, q.n * 8, hipMemcpyDeviceToHost, h->stream));
+    if (q.bounce) at += q.n * 8;
+  }
+  if (sync || bounce_bytes) HIP_TRY(hsync(h));
+  at = 0;
+  for (Job &q : jobs)
+    if (q.dst && q.n && q.bounce) {
+      memcpy(q.dst, h->h_bounce + at / 8, q.n * 8);
+      at += q.n * 8;
+    }
   return big ? CRGC_E2BIG : CRGC_OK;
 }
 
@@ -2326,8 +2374,9 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
     // steady-state wakeup has one host synchronisation for mark + sweep.
     // caller buffers the device can write (page-locked / registered): the
     // lists go there behind the sweep, and the trace needs one host round trip
-    uint64_t *dg = device_view(h, out->garbage_ids, out->garbage_cap * 8),
-             *dk = device_view(h, out->kill_ids, out->kill_cap * 8);
+    uint64_t *dg = nullptr, *dk = nullptr;
+    if (out->garbage_ids) (void)host_kind(h, out->garbage_ids, out->garbage_cap * 8, &dg);
+    if (out->kill_ids) (void)host_kind(h, out->kill_ids, out->kill_cap * 8, &dk);
     auto sweep = [&]() -> hipError_t {
       hipError_t e = hipEventRecord(h->ev[1], h->stream);
       if (e == hipSuccess) e = launch_sweep(h->g.d, should_kill ? 1 : 0, top, h->stream);

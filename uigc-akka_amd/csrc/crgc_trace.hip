@@ -846,15 +846,33 @@ __global__ __launch_bounds__(1024) void k_bin_apply(DevGraph g, LevelArgs a) {
   for (uint32_t k = tid; k < words; k += 1024) bm[k] = 0;
   __syncthreads();
   uint32_t nb2 = 0;
-  // (8 or 16 loads in flight per thread made this kernel slower, not faster:
-  // 48 -> 79 us at C2, profiles/r3g/README.md)
+  // The bin's BIN_SHARDS regions are read together, one 16-B group (4 targets)
+  // of each per thread and step: 8 independent loads in flight instead of a
+  // chain of dependent 4-B loads (the round-3 loop, 48 us at C2, was bound by
+  // that chain: 1024 threads per bin, ~50 dependent loads each).
+  uint32_t n[BIN_SHARDS], nmax = 0;
+#pragma unroll
   for (uint32_t sh = 0; sh < BIN_SHARDS; ++sh) {
-    const uint32_t n = min(cur[b * BIN_SHARDS + sh], a.bin_cap);
-    const uint32_t *src = a.bins + ((uint64_t)b * BIN_SHARDS + sh) * a.bin_cap;
-    for (uint32_t i = tid; i < n; i += 1024) {
-      const uint32_t t = src[i] - (b << a.bin_shift);
-      atomicOr(&bm[t >> 5], 1u << (t & 31));
-      nb2 += 8;
+    n[sh] = min(cur[b * BIN_SHARDS + sh], a.bin_cap);
+    nmax = max(nmax, n[sh]);
+  }
+  const uint32_t base = b << a.bin_shift;
+  for (uint32_t i = tid * 4; i < nmax; i += 1024 * 4) {
+    uint4 q[BIN_SHARDS];
+#pragma unroll
+    for (uint32_t sh = 0; sh < BIN_SHARDS; ++sh)
+      q[sh] = i < n[sh] ? *(const uint4 *)(a.bins + ((uint64_t)b * BIN_SHARDS + sh) * a.bin_cap + i)
+                        : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (uint32_t sh = 0; sh < BIN_SHARDS; ++sh) {
+      const uint32_t v[4] = {q[sh].x, q[sh].y, q[sh].z, q[sh].w};
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j)
+        if (i + j < n[sh]) {
+          const uint32_t t = v[j] - base;
+          atomicOr(&bm[t >> 5], 1u << (t & 31));
+          nb2 += 8;
+        }
     }
   }
   __syncthreads();
