@@ -348,8 +348,13 @@ struct crgc_graph {
   // this shard's last resolution
   uint64_t slot_gen = 0;
   std::vector<uint64_t> peer_gen, peer_top;
-  // host buffers pinned by crgc_host_register: (base, bytes)
-  std::vector<std::pair<char *, uint64_t>> pinned;
+  // host buffers pinned by crgc_host_register: (base, bytes, device view of base)
+  struct Pinned {
+    char *first;
+    uint64_t second;
+    char *dev;
+  };
+  std::vector<Pinned> pinned;
 };
 
 namespace {
@@ -1220,10 +1225,18 @@ static int merge_entries_routed(crgc_graph *h, const crgc_entry_batch *b, int vr
 // follow chunk order, then record order — the batch's order.
 // Offsets are rebased on the device (k_rebase).  The caller's buffers are
 // free when this returns (the last copy is waited for).
+// The device view of a pointer into a crgc_host_register range (nullptr if none).
+static const char *registered_view(const crgc_graph *h, const void *p) {
+  const char *c = (const char *)p;
+  for (const auto &r : h->pinned)
+    if (c >= r.first && c < r.first + r.second) return r.dev + (c - r.first);
+  return nullptr;
+}
+
 constexpr uint64_t CHUNK_MIN = 1u << 18;  // entries per chunk at least
 constexpr uint32_t CHUNK_MAX = 4;
 
-static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint32_t K) {
+static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint32_t K, bool registered) {
   const uint64_t n = b->n_entries;
   struct Part {
     uint64_t lo, hi, c0, c1, s0, s1, u0, u1;
@@ -1233,16 +1246,22 @@ static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint3
   size_t total = 0;
   for (uint32_t j = 0; j < K; ++j) {
     Part &q = p[j];
-    q.lo = n * j / K;
-    q.hi = n * (j + 1) / K;
+    q.lo = (n * j / K) & ~63ull;  // 64-entry boundaries: every per-entry array's chunk is 64-B aligned
+    q.hi = j + 1 == K ? n : (n * (j + 1) / K) & ~63ull;
     q.c0 = b->created_off[q.lo], q.c1 = b->created_off[q.hi];
     q.s0 = b->spawned_off[q.lo], q.s1 = b->spawned_off[q.hi];
     q.u0 = b->updated_off[q.lo], q.u1 = b->updated_off[q.hi];
     if (q.c1 < q.c0 || q.s1 < q.s0 || q.u1 < q.u0) return CRGC_E_INVAL;  // offsets run backwards
     const uint64_t m = q.hi - q.lo, C = q.c1 - q.c0, S = q.s1 - q.s0, U = q.u1 - q.u0;
     const size_t sz[11] = {m * 8, m * 2, m, (m + 1) * 4, C * 8, C * 8, (m + 1) * 4, S * 8, (m + 1) * 4, U * 8, U * 2};
+    const void *src[11] = {b->self + q.lo, b->recv_count + q.lo, b->flags + q.lo, b->created_off + q.lo,
+                           b->created_owner + q.c0, b->created_target + q.c0, b->spawned_off + q.lo,
+                           b->spawned + q.s0, b->updated_off + q.lo, b->updated_ref + q.u0,
+                           b->updated_info + q.u0};
     for (int i = 0; i < 11; ++i) {
       total = (total + 255) & ~(size_t)255;
+      // a kernel copy wants the source's alignment mod 16 (the body in 16-B groups)
+      if (registered) total += (uintptr_t)src[i] & 15;
       q.off[i] = total;
       total += sz[i];
     }
@@ -1261,11 +1280,23 @@ static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint3
                            b->updated_info + q.u0};
     const size_t sz[11] = {m * 8, m * 2, m, (m + 1) * 4, (q.c1 - q.c0) * 8, (q.c1 - q.c0) * 8, (m + 1) * 4,
                            (q.s1 - q.s0) * 8, (m + 1) * 4, (q.u1 - q.u0) * 8, (q.u1 - q.u0) * 2};
-    for (int i = 0; i < 11; ++i)
-      if (sz[i]) {
-        hipError_t e = hipMemcpyAsync(base + q.off[i], src[i], sz[i], hipMemcpyHostToDevice, h->cpy);
-        if (e != hipSuccess) return e;
-      }
+    if (registered) {  // read over PCIe by a kernel (k_copy_ranges): no per-copy runtime overhead
+      HostCopy hc{};
+      for (int i = 0; i < 11; ++i)
+        if (sz[i]) {
+          hc.src[hc.n] = registered_view(h, src[i]);
+          hc.dst[hc.n] = base + q.off[i];
+          hc.bytes[hc.n] = sz[i];
+          ++hc.n;
+        }
+      if (hipError_t e = launch_copy_ranges(hc, h->cpy)) return e;
+    } else {
+      for (int i = 0; i < 11; ++i)
+        if (sz[i]) {
+          hipError_t e = hipMemcpyAsync(base + q.off[i], src[i], sz[i], hipMemcpyHostToDevice, h->cpy);
+          if (e != hipSuccess) return e;
+        }
+    }
     return hipEventRecord(h->ev_chunk[j], h->cpy);
   };
   int rc = CRGC_OK;
@@ -1316,10 +1347,14 @@ static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint3
 }
 
 // Whether every record array of a host batch lies in buffers registered with
-// crgc_host_register.  Such batches are copied whole: from registered memory
-// one large copy per array runs at ~57 GB/s but ~1 MB chunk copies at 4.4 GB/s
-// (profiles/r3g/pcie_probe.txt); unchunked, a registered C2 wakeup takes 2.3 ms
-// against 4.5 ms chunked (profiles/r3i/pcie.txt).  Pageable batches keep the chunks.
+// crgc_host_register.  Such batches are chunked too, but their chunks are read
+// over PCIe by a kernel (k_copy_ranges) rather than copied by the runtime: from
+// registered memory one large runtime copy per array runs at ~57 GB/s but ~1 MB
+// copies at 4.4 GB/s (profiles/r3g/pcie_probe.txt; round 3 therefore copied them
+// whole, 0.9 ms in the merge call, with nothing overlapped).
+static bool host_registered(const crgc_graph *h, const crgc_entry_batch *b, uint64_t C, uint64_t S,
+                            uint64_t U);
+
 static bool host_registered(const crgc_graph *h, const crgc_entry_batch *b, uint64_t C, uint64_t S,
                             uint64_t U) {
   if (h->pinned.empty()) return false;
@@ -1347,9 +1382,9 @@ int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
   const int vrc = entry_counts(h, b, h->tp, &C, &S, &U);
   if (!h->tp) {
     if (vrc) return vrc;
-    if (b->memory == CRGC_MEM_HOST && b->n_entries >= 2 * CHUNK_MIN && h->chunk_host &&
-        !host_registered(h, b, C, S, U))
-      return merge_entries_chunked(h, b, (uint32_t)std::min<uint64_t>(h->chunk_max, b->n_entries / CHUNK_MIN));
+    if (b->memory == CRGC_MEM_HOST && b->n_entries >= 2 * CHUNK_MIN && h->chunk_host)
+      return merge_entries_chunked(h, b, (uint32_t)std::min<uint64_t>(h->chunk_max, b->n_entries / CHUNK_MIN),
+                                   host_registered(h, b, C, S, U));
     return merge_entries_one(h, b, C, S, U);
   }
   if (h->route && h->G <= ROUTE_MAX_SHARDS && h->F <= ROUTE_MAX_F)
@@ -2991,7 +3026,13 @@ int crgc_host_register(crgc_graph *h, void *ptr, uint64_t bytes) {
   DeviceGuard dg(h->device);
   const hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
   if (e != hipSuccess) return e == hipErrorOutOfMemory ? CRGC_E_NOMEM : CRGC_E_INVAL;
-  h->pinned.emplace_back(b, bytes);
+  void *dev = nullptr;  // the device's view, for the chunk copies of registered batches
+  if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess || !dev) {
+    (void)hipGetLastError();
+    hipHostUnregister(ptr);
+    return CRGC_E_DEVICE;
+  }
+  h->pinned.push_back({b, bytes, (char *)dev});
   return CRGC_OK;
 }
 

@@ -215,6 +215,14 @@ hipError_t launch_chain(const DevGraph &g, const ChainArgs &ca, int step, const 
 hipError_t launch_entries(const DevGraph &g, const EntryArgs &a, hipStream_t s, int phase);
 hipError_t launch_deltas(const DevGraph &g, const DeltaArgs &a, uint64_t n_out, hipStream_t s, int phase);
 // the offsets of a chunk of a host batch, rebased to its first entry
+// byte ranges from device-visible host memory into HBM (k_copy_ranges)
+struct HostCopy {
+  const char *src[11];
+  char *dst[11];
+  uint64_t bytes[11];
+  int n;
+};
+hipError_t launch_copy_ranges(const HostCopy &c, hipStream_t s);
 hipError_t launch_rebase(uint32_t *c_off, uint32_t *s_off, uint32_t *u_off, uint64_t n, uint32_t c0, uint32_t s0,
                          uint32_t u0, hipStream_t s);
 hipError_t launch_undo_check(const DevGraph &g, const UndoArgs &a, hipStream_t s);

@@ -542,6 +542,41 @@ hipError_t launch_rebase(uint32_t *c_off, uint32_t *s_off, uint32_t *u_off, uint
   return hipGetLastError();
 }
 
+// Up to 11 byte ranges from page-locked host memory (device-visible pointers)
+// into HBM, read by the shader over PCIe: a registered batch's chunk, copied
+// on the copy stream while the chunk before it merges.  One runtime copy per
+// array from registered memory costs ~0.2 ms of overhead at ~1 MB
+// (profiles/r3g/pcie_probe.txt), so the chunks are copied by this kernel
+// instead.  Source and destination share their alignment mod 16 (the caller
+// places the destination so): the body moves in 16-B groups, the ends by byte.
+__global__ __launch_bounds__(256) void k_copy_ranges(HostCopy c) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  const uint64_t tid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  for (int r = 0; r < c.n; ++r) {
+    const char *s = c.src[r];
+    char *d = c.dst[r];
+    const uint64_t len = c.bytes[r];
+    const uint64_t head = min(len, (uint64_t)((16 - ((uintptr_t)s & 15)) & 15));
+    const uint64_t body = (len - head) & ~15ull;
+    if (tid < head) d[tid] = s[tid];
+    const uint4 *s4 = (const uint4 *)(s + head);
+    uint4 *d4 = (uint4 *)(d + head);
+    for (uint64_t i = tid; i < body / 16; i += stride) d4[i] = s4[i];
+    const uint64_t tail = len - head - body;
+    if (tid < tail) d[head + body + tid] = s[head + body + tid];
+  }
+}
+
+hipError_t launch_copy_ranges(const HostCopy &c, hipStream_t s) {
+  launch_begin();
+  uint64_t tot = 0;
+  for (int r = 0; r < c.n; ++r) tot += c.bytes[r];
+  if (!tot) return hipSuccess;
+  // enough 16-B requests in flight to fill the link, few CUs taken from the merge
+  hipLaunchKernelGGL(k_copy_ranges, dim3(grid_for(tot / 16, 256, 128)), dim3(256), 0, s, c);
+  return hipGetLastError();
+}
+
 int grid_for(uint64_t threads, int block, int cap) {
   uint64_t b = (threads + block - 1) / block;
   if (b < 1) b = 1;
