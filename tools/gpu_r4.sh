@@ -9,6 +9,7 @@
 #   probe            tools/hip_probe.hip: HIP last-error / event / pointer-range semantics
 #   c4               C4 unsharded on one GPU (1e8 actors / 1e9 edges, the scaling anchor)
 #   c4l8 c2l8        C4 / C2 over 8 logical shards on the one GPU (the sharded protocol at full size)
+#   c2rs c4rs        the N>1 bench path itself on one rank (nccl group, RCCL transport, one shard)
 set -euo pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1; shift
@@ -43,6 +44,12 @@ for step in "$@"; do
           --warmup 2 --no-pcie > "$O/bench_c4.json" 2> "$O/bench_c4.err") ;;
     c4l8) (cd /tmp && timeout -k 10 1000 python3 -u "$ROOT/bench.py" --workload c4 --logical-shards 8 \
           --steps 3 --warmup 1 > "$O/bench_c4l8.json" 2> "$O/bench_c4l8.err") ;;
+    c2rs) (cd /tmp && timeout -k 10 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node=1 \
+          --master-addr=127.0.0.1 --master-port=29517 "$ROOT/bench.py" --gpus 1 --workload c2 --rehearse-sharded \
+          --steps 5 --warmup 2 --no-pcie > "$O/bench_c2rs.json" 2> "$O/bench_c2rs.err") ;;
+    c4rs) (cd /tmp && timeout -k 10 1000 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node=1 \
+          --master-addr=127.0.0.1 --master-port=29518 "$ROOT/bench.py" --gpus 1 --workload c4 --rehearse-sharded \
+          --steps 3 --warmup 1 --no-pcie --no-cpu-baseline > "$O/bench_c4rs.json" 2> "$O/bench_c4rs.err") ;;
     c2l8) (cd /tmp && timeout -k 10 600 python3 -u "$ROOT/bench.py" --workload c2 --logical-shards 8 \
           --steps 5 --warmup 2 > "$O/bench_c2l8.json" 2> "$O/bench_c2l8.err") ;;
     *) echo "unknown step $step"; exit 2 ;;
