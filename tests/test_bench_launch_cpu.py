@@ -33,3 +33,14 @@ def test_bench_starts_its_own_ranks():
 def test_bench_refuses_a_world_size_other_than_gpus():
     p = _run(["--gpus", "2", "--dry-run"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode == 2 and "world size 1 != --gpus 2" in p.stderr
+
+
+def test_eight_gpu_default_is_c4_strong_scaling():
+    """--gpus N > 1 quotes BASELINE's C4: one 1e8-actor / 1e9-edge graph sharded
+    over the N ranks (strong scaling), every producer on exactly one rank."""
+    p = _run(["--gpus", "8", "--dry-run", "--steps", "1", "--warmup", "0"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")][0]
+    assert out["config"]["edges"] == 1_000_000_000 and out["config"]["actors"] == 100_000_000
+    assert out["config"]["workload"].startswith("C4") and out["scaling"] == "strong"
+    assert sorted(k for ks in out["producers"] for k in ks) == list(range(8))

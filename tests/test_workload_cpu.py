@@ -70,3 +70,27 @@ def test_c1_generator_has_the_stated_shape(oracle_mod):
         r = o.trace(True)
     assert w.n_busy() == V * 9 // 100
     assert 0.09 * r.n_live < r.pseudo_roots < 0.13 * r.n_live
+
+
+def test_c4_producers_share_no_id_and_concat_keeps_queue_order(oracle_mod):
+    """C4 is one node's graph from 8 producers (workload/world.py c4_producer):
+    their id spaces are disjoint, and EntryBatch.concat of their wakeup parts
+    merges exactly like the parts one after the other (offsets rebased)."""
+    from crgc_hip import EntryBatch
+    ws = [world.c4_producer(k, 4000, 40000) for k in range(world.C4_PRODUCERS)]
+    seen = set()
+    for w in ws:
+        ids = set()
+        for b in w.batches(1 << 20):
+            ids |= set(b.self.tolist()) | set(b.created_target.tolist())
+        assert not (ids & seen)
+        seen |= ids
+        assert all((i >> 48) == 1 for i in ids)      # one node: location 1
+    parts = [w.wakeup(400, busy=360, pending=40) for w in ws]
+    cat = EntryBatch.concat(parts)
+    assert cat.n_entries == sum(p.n_entries for p in parts)
+    a, b = oracle_mod.OracleGraph(), oracle_mod.OracleGraph()
+    a.merge_entries(cat)
+    for p in parts:
+        b.merge_entries(p)
+    assert a.export() == b.export()
