@@ -351,3 +351,30 @@ def test_trace_ids_into_partly_registered_buffer(hip_mod, oracle_mod):
             fz.sync(o.export())
     finally:
         h.unregister_host(arena[:half])
+
+
+@pytest.mark.parametrize("seed,cap", [(17, 0), (18, 64)])
+def test_device_sub_merges_and_pool_repacks(hip_mod, oracle_mod, monkeypatch, seed, cap):
+    """Large device batches merge in sub-merges with rebased offsets (here every
+    300 entries: CRGC_DEV_CHUNK), and the pools are repacked before every merge
+    (CRGC_REPACK_EACH_MERGE: segments move, slots and tables stay) — alongside
+    deltas, undo logs and, at cap 64, rebuilds.  Bit-exact with the oracle."""
+    monkeypatch.setenv("CRGC_DEV_CHUNK", "300")
+    monkeypatch.setenv("CRGC_REPACK_EACH_MERGE", "1")
+    h, o = _pair(hip_mod, oracle_mod, vertex_capacity=cap, edge_capacity=cap)
+    fz = fuzz.Fuzz(seed)
+    for step in range(10):
+        eb = fz.entries(700 + 90 * step)
+        h.merge_entries(eb.to_device())
+        o.merge_entries(eb)
+        if step % 3 == 1:
+            db = fz.deltas(5)
+            h.merge_deltas(db); o.merge_deltas(db)
+        if step == 6:
+            ub = fz.undo(o.export().vertices.keys())
+            h.merge_undo(ub); o.merge_undo(ub)
+        assert h.export() == o.export()
+        rh, ro = h.trace(True), o.trace(True)
+        _same_trace(rh, ro)
+        fz.sync(o.export())
+    assert h.total_actors_seen() == o.total_actors_seen()

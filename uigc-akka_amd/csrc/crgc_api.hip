@@ -243,6 +243,8 @@ struct Knobs {
   bool side_prio = false;        // CRGC_SIDE_PRIO=1: that side stream at the highest priority
   bool chunk_host = true;        // CRGC_CHUNK_HOST=0: large pageable host batches in one piece
   uint32_t chunk_max = 4;        // CRGC_CHUNK_MAX: at most this many chunks (2 .. 4)
+  uint64_t dev_chunk = 0;        // CRGC_DEV_CHUNK: sub-merge size of large device batches (test hook; 0 = 2^20)
+  bool repack_each = false;      // CRGC_REPACK_EACH_MERGE=1: repack the pools before every merge (test hook)
   void read() {
     auto env = [](const char *k) { return getenv(k); };
     if (const char *m = env("CRGC_KERNEL_TIMING")) kernel_timing = atoi(m);
@@ -282,6 +284,8 @@ struct Knobs {
     if (const char *m = env("CRGC_SIDE_PRIO")) side_prio = atoi(m) != 0;
     if (const char *m = env("CRGC_CHUNK_HOST")) chunk_host = atoi(m) != 0;
     if (const char *m = env("CRGC_CHUNK_MAX")) chunk_max = std::min<uint32_t>(4, std::max(2, atoi(m)));
+    if (const char *m = env("CRGC_DEV_CHUNK")) dev_chunk = std::max<uint64_t>(64, strtoull(m, nullptr, 10));
+    if (const char *m = env("CRGC_REPACK_EACH_MERGE")) repack_each = atoi(m) != 0;
   }
 };
 
@@ -335,6 +339,7 @@ struct crgc_graph {
   Scratch x_route, x_route_send, x_cat;  // routed entry merges
   Scratch x_dg, x_dg_out;    // DeltaGraph production
   Scratch x_chain;           // chain mode (crgc_chain.hip)
+  Scratch x_chunk;           // rebased offsets of a large device batch's sub-merges
   Scratch x_bin;             // the pseudo-root level's binned push: counters, then bin regions
   uint64_t x_bin_zeroed = 0;  // x_bin allocation (Scratch::gen) whose counters were zeroed
   Scratch x_gc, x_gc_list;   // replicated chain closure of sharded marks (crgc_xchain.hip)
@@ -500,25 +505,78 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   return CRGC_OK;
 }
 
+// The two pools packed afresh (launch_repack): dead space of relocated
+// segments reclaimed, slots and tables unchanged.  If the new pools cannot be
+// allocated the graph is as before (CRGC_E_NOMEM), so the caller may rebuild.
+int repack(crgc_graph *h) {
+  HIP_TRY(sync_counters(h));
+  if (int rc = device_error(h)) return rc;
+  const Caps &c = h->g.caps;
+  uint64_t *pool2 = nullptr;
+  uint32_t *rpool2 = nullptr;
+  Scratch tmp;
+  const size_t scan = rebuild_scan_tmp_bytes(c.scap);
+  if (dmalloc(&pool2, c.pcap) != hipSuccess || dmalloc(&rpool2, h->g.d.rpcap) != hipSuccess ||
+      tmp.ensure(Carver::need({c.scap * 8, c.scap * 8, 2 * scan})) != hipSuccess) {
+    (void)hipGetLastError();
+    if (pool2) hipFree(pool2);
+    if (rpool2) hipFree(rpool2);
+    return CRGC_E_NOMEM;
+  }
+  Carver cv(tmp.ptr);
+  uint64_t *pp = cv.take<uint64_t>(c.scap), *rp = cv.take<uint64_t>(c.scap);
+  void *st = cv.take<uint64_t>(2 * scan / 8);
+  const uint64_t old_p = h->pool_top, old_r = h->rpool_top;
+  hipError_t e = launch_repack(h->g.d, h->slot_top, pp, rp, st, pool2, rpool2, h->stream);
+  if (e == hipSuccess) e = sync_counters(h);
+  tmp.release();
+  if (e != hipSuccess) {  // the device may have moved part of adj / radj: unusable
+    hipFree(pool2);
+    hipFree(rpool2);
+    h->poisoned = true;
+    return map_hip(e);
+  }
+  hipFree(h->g.d.pool);
+  hipFree(h->g.d.rpool);
+  h->g.d.pool = pool2;
+  h->g.d.rpool = rpool2;
+  if (h->knobs.level_log)
+    fprintf(stderr, "[crgc] repack: pool %llu -> %llu, candidate pool %llu -> %llu (of %llu)\n",
+            (unsigned long long)old_p, (unsigned long long)h->pool_top, (unsigned long long)old_r,
+            (unsigned long long)h->rpool_top, (unsigned long long)c.pcap);
+  return CRGC_OK;
+}
+
 // Make sure `ids` more vertices and `atoms` more edge updates fit.
 int ensure_capacity(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   // A merge's relocations need at most 2*(stored + new) + 4*touched pool
   // entries in either direction (power-of-two segments).
-  auto fits = [&](uint64_t st, uint64_t pt, uint64_t rt, uint64_t eu) {
+  auto pools_fit = [&](uint64_t pt, uint64_t rt, uint64_t eu) {
     const Caps &c = h->g.caps;
-    return st + ids <= c.scap && (st + ids) * 10 <= c.hcap * 7 &&
-           pt + 2 * eu + 6 * atoms <= c.pcap && rt + 2 * eu + 6 * atoms + 4 * ids <= c.pcap &&
-           (eu + atoms) * 10 <= c.ecap * 7;
+    return pt + 2 * eu + 6 * atoms <= c.pcap && rt + 2 * eu + 6 * atoms + 4 * ids <= c.pcap;
+  };
+  auto rest_fits = [&](uint64_t st, uint64_t eu) {
+    const Caps &c = h->g.caps;
+    return st + ids <= c.scap && (st + ids) * 10 <= c.hcap * 7 && (eu + atoms) * 10 <= c.ecap * 7;
   };
   // upper bounds since the last sync
   const uint64_t st = h->slot_top + h->ids_since;
   const uint64_t eu = h->etab_used + h->atoms_since;
   const uint64_t grow = 2 * (h->etab_used + h->atoms_since) + 6 * h->atoms_since;
   // (+ 4 reverse-candidate entries per new shadow: k_ids' first segments)
-  if (fits(st, h->pool_top + grow, h->rpool_top + grow + 4 * h->ids_since, eu)) return CRGC_OK;
+  if (rest_fits(st, eu) && pools_fit(h->pool_top + grow, h->rpool_top + grow + 4 * h->ids_since, eu))
+    return CRGC_OK;
   HIP_TRY(sync_counters(h));
   if (int rc = device_error(h)) return rc;
-  if (fits(h->slot_top, h->pool_top, h->rpool_top, h->etab_used)) return CRGC_OK;
+  const bool rest = rest_fits(h->slot_top, h->etab_used);
+  if (rest && pools_fit(h->pool_top, h->rpool_top, h->etab_used)) return CRGC_OK;
+  // only the pools are short: reclaim their dead space before rebuilding the
+  // whole graph (a rebuild allocates a second graph; a repack, two pools)
+  if (rest) {
+    const int rc = repack(h);
+    if (rc == CRGC_OK && pools_fit(h->pool_top, h->rpool_top, h->etab_used)) return CRGC_OK;
+    if (rc != CRGC_OK && rc != CRGC_E_NOMEM) return rc;
+  }
   return rebuild(h, ids, atoms);
 }
 
@@ -683,7 +741,7 @@ void crgc_destroy(crgc_graph *h) {
   h->work.release();
   for (Scratch *x : {&h->x_send, &h->x_slot, &h->x_recv, &h->x_ans, &h->x_ans_back, &h->x_small,
                      &h->x_pack, &h->x_pack_recv, &h->x_route, &h->x_route_send, &h->x_cat,
-                     &h->x_dg, &h->x_dg_out, &h->x_chain, &h->x_gc, &h->x_gc_list, &h->x_bin})
+                     &h->x_dg, &h->x_dg_out, &h->x_chain, &h->x_gc, &h->x_gc_list, &h->x_bin, &h->x_chunk})
     x->release();
   if (h->ctr) hipFree(h->ctr);
   if (h->hctr) hipHostFree(h->hctr);
@@ -985,6 +1043,8 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   if (n == 0) return CRGC_OK;
   const uint64_t ids = n + 2 * C + S + U;
   const uint64_t max_atoms = n * 2 * (uint64_t)h->F;
+  if (h->knobs.repack_each)
+    if (int rc = repack(h)) return rc;
   if (int rc = ensure_capacity(h, ids, C + U)) return rc;
 
   const size_t host_bytes =
@@ -1375,6 +1435,60 @@ static bool host_registered(const crgc_graph *h, const crgc_entry_batch *b, uint
   return true;
 }
 
+// A large device batch in sub-merges of DEV_CHUNK entries (offsets rebased on
+// the device): each sub-merge checks capacity with its own exact record counts,
+// so the upper bounds of one 1e7-entry wakeup (C4 on one GPU: n + 2C + S + U =
+// 1.7e8 possible new shadows) never force a rebuild the real growth does not
+// need.  Chunks merge in order, each its own epoch: the same result.
+constexpr uint64_t DEV_CHUNK = 1u << 20;
+
+static int merge_entries_dev_chunked(crgc_graph *h, const crgc_entry_batch *b) {
+  const uint64_t n = b->n_entries;
+  const uint64_t CH = h->knobs.dev_chunk ? h->knobs.dev_chunk : DEV_CHUNK;
+  const uint64_t K = (n + CH - 1) / CH;
+  std::vector<uint32_t> bo(3 * (K + 1));
+  for (uint64_t j = 0; j <= K; ++j) {
+    const uint64_t at = std::min(n, j * CH);
+    HIP_TRY(hipMemcpyAsync(&bo[3 * j], b->created_off + at, 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(&bo[3 * j + 1], b->spawned_off + at, 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(&bo[3 * j + 2], b->updated_off + at, 4, hipMemcpyDeviceToHost, h->stream));
+  }
+  HIP_TRY(hsync(h));
+  if (bo[0] || bo[1] || bo[2]) return CRGC_E_INVAL;
+  if (h->x_chunk.ensure(Carver::need({(CH + 1) * 4, (CH + 1) * 4, (CH + 1) * 4})) != hipSuccess)
+    return CRGC_E_NOMEM;
+  Carver cv(h->x_chunk.ptr);
+  uint32_t *co = cv.take<uint32_t>(CH + 1), *so = cv.take<uint32_t>(CH + 1), *uo = cv.take<uint32_t>(CH + 1);
+  for (uint64_t j = 0; j < K; ++j) {
+    const uint64_t lo = j * CH, hi = std::min(n, lo + CH), m = hi - lo;
+    const uint32_t c0 = bo[3 * j], s0 = bo[3 * j + 1], u0 = bo[3 * j + 2];
+    const uint32_t c1 = bo[3 * j + 3], s1 = bo[3 * j + 4], u1 = bo[3 * j + 5];
+    if (c1 < c0 || s1 < s0 || u1 < u0 || c1 - c0 > m * h->F || s1 - s0 > m * h->F || u1 - u0 > m * h->F)
+      return CRGC_E_INVAL;  // offsets run backwards or past F per entry: refused (chunks before it merged)
+    // (stream order: the previous chunk's kernels have read these buffers)
+    HIP_TRY(hipMemcpyAsync(co, b->created_off + lo, (m + 1) * 4, hipMemcpyDeviceToDevice, h->stream));
+    HIP_TRY(hipMemcpyAsync(so, b->spawned_off + lo, (m + 1) * 4, hipMemcpyDeviceToDevice, h->stream));
+    HIP_TRY(hipMemcpyAsync(uo, b->updated_off + lo, (m + 1) * 4, hipMemcpyDeviceToDevice, h->stream));
+    HIP_TRY(launch_rebase(co, so, uo, m + 1, c0, s0, u0, h->stream));
+    crgc_entry_batch v{};
+    v.n_entries = m;
+    v.self = b->self + lo;
+    v.recv_count = b->recv_count + lo;
+    v.flags = b->flags + lo;
+    v.created_off = co;
+    v.created_owner = b->created_owner + c0;
+    v.created_target = b->created_target + c0;
+    v.spawned_off = so;
+    v.spawned = b->spawned + s0;
+    v.updated_off = uo;
+    v.updated_ref = b->updated_ref + u0;
+    v.updated_info = b->updated_info + u0;
+    v.memory = CRGC_MEM_DEVICE;
+    if (int rc = merge_entries_one(h, &v, c1 - c0, s1 - s0, u1 - u0)) return rc;
+  }
+  return CRGC_OK;
+}
+
 int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
   if (int rc = check_graph(h)) return rc;
   DeviceGuard dg(h->device);
@@ -1382,6 +1496,10 @@ int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
   const int vrc = entry_counts(h, b, h->tp, &C, &S, &U);
   if (!h->tp) {
     if (vrc) return vrc;
+    if (b->memory == CRGC_MEM_DEVICE && b->n_entries > (h->knobs.dev_chunk ? h->knobs.dev_chunk : DEV_CHUNK) &&
+        b->created_owner && b->created_target &&
+        b->spawned && b->updated_ref && b->updated_info)
+      return merge_entries_dev_chunked(h, b);
     if (b->memory == CRGC_MEM_HOST && b->n_entries >= 2 * CHUNK_MIN && h->chunk_host)
       return merge_entries_chunked(h, b, (uint32_t)std::min<uint64_t>(h->chunk_max, b->n_entries / CHUNK_MIN),
                                    host_registered(h, b, C, S, U));

@@ -302,6 +302,10 @@ hipError_t launch_rebuild(const DevGraph &src, uint64_t src_slot_top, const DevG
                           uint32_t *map, uint32_t *newdeg, uint64_t *offs, void *scan_tmp,
                           hipStream_t s);
 size_t rebuild_scan_tmp_bytes(uint64_t n);
+// the pools alone, packed into pool2 / rpool2 (pp / rp: scap u64 each; scan_tmp:
+// 2 x rebuild_scan_tmp_bytes(scap)); slots and tables unchanged
+hipError_t launch_repack(const DevGraph &g, uint64_t top, uint64_t *pp, uint64_t *rp, void *scan_tmp, uint64_t *pool2,
+                         uint32_t *rpool2, hipStream_t s);
 
 // routed sharded entry merges (crgc_route.hip)
 constexpr int RT_THREADS = 256;

@@ -234,6 +234,74 @@ __global__ __launch_bounds__(256) void k_rb_rfill(DevGraph dst) {
   }
 }
 
+// ---- repack: the two pools alone ---------------------------------------------
+// Relocated segments leave dead space in the pools (a segment that outgrows its
+// capacity moves to a fresh one).  A repack moves every owner's out-edge segment
+// and every target's candidate segment into new pools, packed in slot order at
+// their current capacities.  Slots, both hash tables and every index inside a
+// segment (edge-table val / rev) stay as they are: only adj.x and radj.x
+// change.  So a merge whose pools would overflow repacks instead of rebuilding
+// the graph — no slot renumbering, and about a third of a rebuild's memory
+// (the C4 graph on one GPU: 51 GB of new pools against a second 130-GB graph).
+__global__ __launch_bounds__(256) void k_rp_sizes(DevGraph g, uint64_t top, uint64_t *pp, uint64_t *rp) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < g.scap; v += stride) {
+    pp[v] = v < top ? seg_cap(g.adj[v].y) : 0;
+    rp[v] = v < top ? rseg_cap(g.radj[v].y) : 0;
+  }
+}
+
+// One slot per lane: its segments' live entries to their new offsets (short
+// ones by the lane, longer ones by the whole wave).
+template <typename T>
+__device__ inline void rp_copy(const T *from, T *to, uint32_t len) {
+  const bool small = len <= 8;
+  if (small)
+    for (uint32_t e = 0; e < len; ++e) to[e] = from[e];
+  uint64_t big = __ballot(!small);
+  while (big) {
+    const int k = __ffsll((unsigned long long)big) - 1;
+    big &= big - 1;
+    const T *fk = (const T *)__shfl((unsigned long long)(uintptr_t)from, k);
+    T *tk = (T *)__shfl((unsigned long long)(uintptr_t)to, k);
+    const uint32_t lk = __shfl(len, k);
+    for (uint32_t e = lane_id(); e < lk; e += 64) tk[e] = fk[e];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rp_move(DevGraph g, uint64_t top, const uint64_t *pp, const uint64_t *rp,
+                                                 uint64_t *pool2, uint32_t *rpool2) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t base = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); base < top; base += stride) {
+    const uint64_t v = base + lane_id();
+    const bool in = v < top;
+    const uint2 ad = in ? g.adj[v] : make_uint2(0, 0);
+    const uint2 rd = in ? g.radj[v] : make_uint2(0, 0);
+    const uint64_t po = in ? pp[v] : 0, ro = in ? rp[v] : 0;
+    rp_copy(g.pool + ad.x, pool2 + po, ad.y);
+    rp_copy(g.rpool + rd.x, rpool2 + ro, rseg_len(rd.y));
+    if (in) {
+      g.adj[v].x = (uint32_t)po;
+      g.radj[v].x = (uint32_t)ro;
+    }
+  }
+}
+
+hipError_t launch_repack(const DevGraph &g, uint64_t top, uint64_t *pp, uint64_t *rp, void *scan_tmp, uint64_t *pool2,
+                         uint32_t *rpool2, hipStream_t s) {
+  launch_begin();
+  const int grid = grid_for(g.scap, 256, 8192);
+  const uint64_t nb = (g.scap + SCAN_TILE - 1) / SCAN_TILE;
+  uint64_t *tp = (uint64_t *)scan_tmp, *tr = tp + nb + 2;
+  hipLaunchKernelGGL(k_rp_sizes, dim3(grid), dim3(256), 0, s, g, top, pp, rp);
+  exclusive_scan(pp, g.scap, tp, s);
+  exclusive_scan(rp, g.scap, tr, s);
+  hipLaunchKernelGGL(k_rb_pool_top, dim3(1), dim3(1), 0, s, g.ctr, tp + nb);
+  hipLaunchKernelGGL(k_rb_rpool_top, dim3(1), dim3(1), 0, s, g.ctr, tr + nb);
+  hipLaunchKernelGGL(k_rp_move, dim3(grid_for(top, 256, 8192)), dim3(256), 0, s, g, top, pp, rp, pool2, rpool2);
+  return hipGetLastError();
+}
+
 hipError_t launch_rebuild(const DevGraph &src, uint64_t src_top, const DevGraph &dst, uint32_t *map,
                           uint32_t *newdeg, uint64_t *offs, void *scan_tmp, hipStream_t s) {
   launch_begin();
