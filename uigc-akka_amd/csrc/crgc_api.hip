@@ -1863,31 +1863,39 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   la.xslices = kn.xslices;
   la.tail_start = std::min<uint32_t>(kn.tail_start, TAIL_QCAP);
   la.tail_max = std::min<uint32_t>(std::max(kn.tail_max, 1u), TAIL_QCAP);
-  // The pseudo-root level's binned push (crgc_trace.hip k_expand_bin): up to 256
-  // bins of >= 65536 slots (an LDS bitmap of <= 128 KiB each), regions for half
-  // the graph's edge keys; counters zeroed once, then reset by k_bin_apply.
+  // The pseudo-root level's binned push (crgc_trace.hip k_bin_walk / k_bin_apply):
+  // up to 256 bins of >= 65536 slots (an LDS bitmap of <= 128 KiB each), a region
+  // for half the graph's edge keys (targets past it are stored at once), the
+  // per-(bin, workgroup) counts and their scan; the mode word is zeroed with a
+  // fresh allocation and reset by k_bin_apply.
   if (roots && kn.bin && !kn.alpha && top > 0 && top >= kn.bin_min) {
     uint32_t lg = 0;
     while (lg < 63 && (1ull << lg) < top) ++lg;
     const uint32_t shift = std::max<uint32_t>(16, lg > 8 ? lg - 8 : 0);
     const uint64_t nb = (top + (1ull << shift) - 1) >> shift;
     if (shift <= 20 && nb <= BIN_MAX) {
-      // BIN_SHARDS regions per bin; a full region falls back to direct stores
-      // (a multiple of 64 entries: k_bin_apply reads the regions in 16-B groups)
-      const uint64_t cap = round_up(std::max<uint64_t>(4096, (h->etab_used + h->atoms_since) / 2 / (nb * BIN_SHARDS)), 64);
-      const size_t cur_bytes = (size_t)(BIN_MAX * BIN_SHARDS + 4) * 4;
-      HIP_TRY(h->x_bin.ensure(cur_bytes + nb * BIN_SHARDS * cap * 4));
+      const uint32_t G = STAT_WG;  // both walk passes (8 workgroups per CU: ~6 KiB of LDS each)
+      const uint64_t nc = nb * G;
+      const uint64_t cap = round_up(std::max<uint64_t>(1u << 16, (h->etab_used + h->atoms_since) / 2), 64);
+      const size_t need = Carver::need({16, 16, nc * 4, nc * 8, ((nc + 1023) / 1024) * 4 * 8 + 64, cap * 4});
+      HIP_TRY(h->x_bin.ensure(need));
+      Carver cv(h->x_bin.ptr);
+      la.bin_mode_w = cv.take<uint32_t>(4);
+      la.bin_tot = cv.take<unsigned long long>(2);
+      la.bin_cnt = cv.take<uint32_t>(nc);
+      la.bin_off = cv.take<uint64_t>(nc);
+      la.bin_bsum = cv.take<uint64_t>(((nc + 1023) / 1024) * 4 + 8);
+      la.bins = cv.take<uint32_t>(cap);
       // a fresh allocation (compared by generation: a reallocation may return
-      // the same base address) starts with zero counters
+      // the same base address) starts with the mode word clear
       if (h->x_bin_zeroed != h->x_bin.gen) {
-        HIP_TRY(hipMemsetAsync(h->x_bin.ptr, 0, cur_bytes, h->stream));
+        HIP_TRY(hipMemsetAsync(la.bin_mode_w, 0, 16, h->stream));
         h->x_bin_zeroed = h->x_bin.gen;
       }
-      la.bin_cur = (uint32_t *)h->x_bin.ptr;
-      la.bins = (uint32_t *)((char *)h->x_bin.ptr + cur_bytes);
       la.bin_shift = shift;
       la.nbins = (uint32_t)nb;
-      la.bin_cap = (uint32_t)cap;
+      la.bin_cap = cap;
+      la.bin_grid = G;
     }
   }
   // Device times, from timing-only events (no system-scope fence):

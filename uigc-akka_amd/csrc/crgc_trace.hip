@@ -651,97 +651,74 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 
 
 // ---------------------------------------------------------------------------
-// The pseudo-root level's push, binned (round 3).  Level 0 of a wide trace
-// pushes ~1e7 candidate bytes to random slots of a ~10 MB byte map that no
-// XCD's 4 MB L2 holds: the edge stream takes ~22 us, the random byte stores
-// ~215 us (C2, profiles/r3g/lv1).  Binned, the stores become sequential:
-//   k_expand_bin   the level's edges as in k_expand, each target appended to
-//                  an LDS bin of its slot range (nbins <= 256 ranges of
-//                  2^bin_shift slots); the workgroups walk their units (light
-//                  chunks, hub pieces) in lock-step rounds of 4 (a unit per
-//                  wave), and after a round every bin holding >= BIN_SB / 2
-//                  targets is flushed to its global region (one atomic per bin
-//                  and workgroup, on one of BIN_SHARDS counters); a full LDS
-//                  bin or region falls back to the direct byte store, so
-//                  nothing is ever dropped.
-//   k_bin_apply    one workgroup per bin: its targets into an LDS bitmap of
-//                  the bin's slot range (8 loads in flight per thread), then the
-//                  range's candidate bytes OR-ed with it in 16-B groups
-//                  (sequential), counters reset.
-// (A slice per bin and workgroup, filled without atomics, two units per wave
-// and round: level 0 320 us against 202 us — profiles/r3g/ab10.)
-// Used only when the level-0 frontier is >= 1/32 of the slots (both kernels
-// derive the same answer; the mode word tells k_bin_apply).
+// The pseudo-root level's push, binned.  Level 0 of a wide trace pushes ~1e7
+// candidate bytes to random slots of a ~10 MB byte map that no XCD's 4 MB L2
+// holds: the edge stream takes ~22 us, the random byte stores ~215 us (C2,
+// profiles/r3g/lv1).  Binned, the stores become sequential.  Round 4 does it
+// as count-then-place (round 3 staged targets in LDS bins flushed in lock-step
+// rounds — four barriers per four units and a returning global atomic per bin
+// and flush: 166 us against the 22-us stream):
+//   k_bin_walk<0>  count: each workgroup walks its units (light chunks, hub
+//                  pieces; the same units in both passes) and counts its
+//                  targets per bin (nbins <= 256 ranges of 2^bin_shift slots)
+//                  in LDS; the counts go out bin-major: no barrier per unit
+//   run_scan       exclusive scan of the (bin, workgroup) counts: every
+//                  workgroup's slice of every bin's region
+//   k_bin_walk<1>  place: the same walk; each target takes the next position of
+//                  its (bin, workgroup) slice from an LDS cursor and is stored
+//                  there (each slice fills front to back, so its lines fill in
+//                  the XCD's L2 before they leave it); no staging, no global
+//                  atomics
+//   k_bin_apply    one workgroup per bin: its region into an LDS bitmap of the
+//                  bin's slot range (16-B loads), then the range's candidate
+//                  bytes OR-ed with it in 16-B groups; the mode word reset.
+// Used only when the level-0 frontier is >= 1/32 of the slots (every kernel
+// derives the same answer; the mode word tells k_bin_apply).  Not binned, the
+// place pass stores the bytes at once.
 // ---------------------------------------------------------------------------
 __device__ inline bool bin_mode(const Counters *c, const LevelArgs &a) {
   return a.nbins > 0 && a.nbins <= BIN_MAX && c->ring[0] * 32 >= c->slot_top;
 }
 
-
-__global__ __launch_bounds__(256) void k_expand_bin(DevGraph g, LevelArgs a) {
+template <int PASS>  // 0: count, 1: place
+__global__ __launch_bounds__(256) void k_bin_walk(DevGraph g, LevelArgs a) {
   constexpr int U = EXPAND_U;
-  extern __shared__ __attribute__((aligned(16))) uint32_t bl[];
   __shared__ uint32_t s_start[4][65];
   __shared__ uint32_t s_off[4][64];
   __shared__ uint32_t s_ulist[256], s_utag[256], s_wcnt[4], s_nact;
+  __shared__ uint32_t lc[BIN_MAX];  // count: targets per bin; place: the next position of each bin's slice
   Counters *c = g.ctr;
   if (c->tail_state) return;
-  const uint32_t NB = a.nbins;
-  uint32_t *lcnt = bl;                  // [NB] staged targets
-  uint32_t *fbase = bl + BIN_MAX;       // [NB] flush: region offset
-  uint32_t *fn = bl + 2 * BIN_MAX;      // [NB] flush: targets taken
-  uint32_t *lbuf = bl + 3 * BIN_MAX;    // [NB][BIN_SB]
   const bool binned = bin_mode(c, a);
+  if (PASS == 0 && !binned) return;  // not binned: the place pass stores the bytes
+  const uint32_t NB = a.nbins;
   uint8_t *Fn = g.front[1];
   const int wv = threadIdx.x >> 6, lane = lane_id(), tid = threadIdx.x;
   const uint64_t G = gridDim.x, wg = blockIdx.x;
-  const uint32_t shard = (uint32_t)(wg % BIN_SHARDS);
   const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
   const uint64_t ncid = nblk * 32;
   const uint64_t nh = min(c->qh[0], (unsigned long long)g.qh_cap);
   const uint64_t nunits = ncid + nh;
   uint32_t nb2 = 0;
-  for (uint32_t b = tid; b < BIN_MAX; b += 256) lcnt[b] = 0;
-  uint32_t *cur = a.bin_cur + 4;  // bin_cur[0]: the binned-mode word
-  if (binned && wg == 0 && tid == 0) a.bin_cur[0] = 1;
+  if (binned)
+    for (uint32_t k = tid; k < NB; k += 256) lc[k] = PASS == 0 ? 0u : (uint32_t)a.bin_off[(uint64_t)k * G + wg];
+  if (PASS == 1 && binned && wg == 0 && tid == 0) a.bin_mode_w[0] = 1;
   __syncthreads();
 
-  // one target: its bin, or (not binned / bin full) the byte at once
   auto put = [&](uint32_t t) {
-    if (binned) {
-      const uint32_t b = t >> a.bin_shift;
-      const uint32_t pos = atomicAdd(&lcnt[b], 1u);
-      if (pos < BIN_SB) {
-        lbuf[b * BIN_SB + pos] = t;
-        return;
-      }
+    if (!binned) {
+      Fn[t] = 1;
+      return;
     }
-    Fn[t] = 1;
-  };
-  // bins with >= thr targets to their regions: one atomic per bin (thread b
-  // of the workgroup, all in flight together), then every wave copies its bins'
-  // targets
-  auto flush = [&](uint32_t thr) {
-    if (tid < NB) {
-      const uint32_t n = min(lcnt[tid], BIN_SB);
-      const uint32_t take = n >= thr ? n : 0u;
-      fn[tid] = take;
-      fbase[tid] = take ? atomicAdd(&cur[tid * BIN_SHARDS + shard], take) : 0u;
+    const uint32_t b = t >> a.bin_shift;
+    if (PASS == 0) {
+      atomicAdd(&lc[b], 1u);
+    } else {
+      const uint32_t pos = atomicAdd(&lc[b], 1u);
+      if (pos < a.bin_cap) a.bins[pos] = t;
+      else Fn[t] = 1;  // past the region: the byte at once
+      nb2 += 8;
     }
-    __syncthreads();
-    for (uint32_t b = wv; b < NB; b += 4) {
-      const uint32_t n = fn[b];
-      if (lane < n) {
-        const uint32_t t = lbuf[b * BIN_SB + lane];
-        const uint32_t pos = fbase[b] + lane;
-        if (pos < a.bin_cap) a.bins[((uint64_t)b * BIN_SHARDS + shard) * a.bin_cap + pos] = t;
-        else Fn[t] = 1;  // region full: the byte at once
-        nb2 += 8;
-      }
-    }
-    __syncthreads();
-    if (tid < NB && fn[tid]) lcnt[tid] = 0;
-    __syncthreads();
   };
   auto edges = [&](const uint64_t (&ed)[U]) {
 #pragma unroll
@@ -800,9 +777,9 @@ __global__ __launch_bounds__(256) void k_expand_bin(DevGraph g, LevelArgs a) {
   // Unit ids are dealt round-robin over the workgroups (workgroup w, window i,
   // thread t: id (256 i + t) G + w): light chunks with work cluster at the
   // low ids (k = 0 .. 3 of every block at level 0), so consecutive windows
-  // would leave most workgroups idle.
+  // would leave most workgroups idle.  Within a window every wave takes every
+  // fourth unit with work, at its own pace: nothing waits on another wave.
   for (uint64_t ub = 0; ub * G < nunits; ub += 256) {
-    // this window's units with work, compacted (ballot / popc per wave)
     const uint64_t u = (ub + tid) * G + wg;
     uint32_t tag = 0;
     bool act = false;
@@ -826,50 +803,43 @@ __global__ __launch_bounds__(256) void k_expand_bin(DevGraph g, LevelArgs a) {
     if (tid == 0) s_nact = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
     __syncthreads();
     const uint32_t nact = s_nact;
-    for (uint32_t r0 = 0; r0 < nact; r0 += 4) {
-      if (r0 + wv < nact) unit((ub + s_ulist[r0 + wv]) * G + wg, s_utag[r0 + wv]);
-      __syncthreads();
-      if (binned) flush(BIN_SB / 2);
-    }
+    for (uint32_t r = wv; r < nact; r += 4) unit((ub + s_ulist[r]) * G + wg, s_utag[r]);
     __syncthreads();  // s_ulist is rewritten by the next window
   }
-  if (binned) flush(1);
+  if (PASS == 0)
+    for (uint32_t k = tid; k < NB; k += 256) a.bin_cnt[(uint64_t)k * G + wg] = lc[k];
   expand_bytes_out(g, nb2);
 }
 
 __global__ __launch_bounds__(1024) void k_bin_apply(DevGraph g, LevelArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t bm[];  // 2^bin_shift bits
-  if (!a.bins || a.bin_cur[0] == 0) return;  // level 0 was not binned
-  uint32_t *cur = a.bin_cur + 4;
+  if (!a.bins || a.bin_mode_w[0] == 0) return;  // level 0 was not binned
   const uint32_t b = blockIdx.x, tid = threadIdx.x;
   const uint32_t span = 1u << a.bin_shift, words = span / 32;
   for (uint32_t k = tid; k < words; k += 1024) bm[k] = 0;
   __syncthreads();
   uint32_t nb2 = 0;
-  // The bin's BIN_SHARDS regions are read together, one 16-B group (4 targets)
-  // of each per thread and step: 8 independent loads in flight instead of a
-  // chain of dependent 4-B loads (the round-3 loop, 48 us at C2, was bound by
-  // that chain: 1024 threads per bin, ~50 dependent loads each).
-  uint32_t n[BIN_SHARDS], nmax = 0;
-#pragma unroll
-  for (uint32_t sh = 0; sh < BIN_SHARDS; ++sh) {
-    n[sh] = min(cur[b * BIN_SHARDS + sh], a.bin_cap);
-    nmax = max(nmax, n[sh]);
-  }
+  // the bin's region [r0, r1) of `bins`, read in aligned 16-B groups, 4 in flight per thread
+  const uint64_t G = a.bin_grid;
+  const uint64_t r0 = min(a.bin_off[(uint64_t)b * G], a.bin_cap);
+  const uint64_t r1 = min(b + 1 < a.nbins ? a.bin_off[(uint64_t)(b + 1) * G] : (uint64_t)*a.bin_tot, a.bin_cap);
   const uint32_t base = b << a.bin_shift;
-  for (uint32_t i = tid * 4; i < nmax; i += 1024 * 4) {
-    uint4 q[BIN_SHARDS];
+  const uint64_t q0 = r0 & ~3ull;
+  for (uint64_t i = q0 + (uint64_t)tid * 4; i < r1; i += 1024 * 4 * 4) {
+    uint4 q[4];
 #pragma unroll
-    for (uint32_t sh = 0; sh < BIN_SHARDS; ++sh)
-      q[sh] = i < n[sh] ? *(const uint4 *)(a.bins + ((uint64_t)b * BIN_SHARDS + sh) * a.bin_cap + i)
-                        : make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t at = i + (uint64_t)j * 1024 * 4;
+      q[j] = at < r1 ? *(const uint4 *)(a.bins + at) : make_uint4(0, 0, 0, 0);
+    }
 #pragma unroll
-    for (uint32_t sh = 0; sh < BIN_SHARDS; ++sh) {
-      const uint32_t v[4] = {q[sh].x, q[sh].y, q[sh].z, q[sh].w};
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t at = i + (uint64_t)j * 1024 * 4;
+      const uint32_t v[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
 #pragma unroll
-      for (uint32_t j = 0; j < 4; ++j)
-        if (i + j < n[sh]) {
-          const uint32_t t = v[j] - base;
+      for (int k = 0; k < 4; ++k)
+        if (at + k >= r0 && at + k < r1) {
+          const uint32_t t = v[k] - base;
           atomicOr(&bm[t >> 5], 1u << (t & 31));
           nb2 += 8;
         }
@@ -893,9 +863,8 @@ __global__ __launch_bounds__(1024) void k_bin_apply(DevGraph g, LevelArgs a) {
     nb2 += 64;  // 16 B read + 16 B written
   }
   __syncthreads();
-  // every workgroup has read its counters: reset them (and the mode word) for the next trace
-  if (tid < BIN_SHARDS) cur[b * BIN_SHARDS + tid] = 0;
-  if (b == 0 && tid == 0) a.bin_cur[0] = 0;
+  // every workgroup has read the mode word: reset it for the next trace
+  if (b == 0 && tid == 0) a.bin_mode_w[0] = 0;
   const uint32_t ws = wave_sum(nb2);
   if (lane_id() == 0 && ws) atomicAdd((unsigned long long *)&g.xbytes[b], (unsigned long long)(ws / 2));
 }
@@ -1316,12 +1285,18 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
   hipExtLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, e[2], e[3], 0, g, a);
   // 8 WGs of 4 waves per CU
   if (roots && a.nbins) {
-    // the pseudo-root level, binned when it is wide: both kernels timed as its expand
-    const size_t lds = (size_t)(3 * BIN_MAX + a.nbins * BIN_SB) * 4;
-    // as many workgroups as are resident at once (LDS-bound: ~4 KiB static besides)
-    const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, (uint32_t)((160u << 10) / (lds + 4608))));
-    const uint32_t bgrid = std::min<uint32_t>(STAT_WG, 256 * per_cu);
-    hipExtLaunchKernelGGL(k_expand_bin, dim3(bgrid), dim3(256), lds, s, e[4], nullptr, 0, g, a);
+    // the pseudo-root level, binned when it is wide: count, scan, place and
+    // apply, timed together as its expand
+    hipExtLaunchKernelGGL(k_bin_walk<0>, dim3(a.bin_grid), dim3(256), 0, s, e[4], nullptr, 0, g, a);
+    ScanSet q{};
+    q.k = 1;
+    q.n = (uint64_t)a.nbins * a.bin_grid;
+    q.in[0] = a.bin_cnt;
+    q.out[0] = a.bin_off;
+    q.total[0] = a.bin_tot;
+    q.bsum = a.bin_bsum;
+    if (hipError_t r = run_scan(q, s)) return r;
+    hipLaunchKernelGGL(k_bin_walk<1>, dim3(a.bin_grid), dim3(256), 0, s, g, a);
     hipExtLaunchKernelGGL(k_bin_apply, dim3(a.nbins), dim3(1024), (size_t)(1u << a.bin_shift) / 8, s, nullptr,
                           e[5], 0, g, a);
     return hipGetLastError();
