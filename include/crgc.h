@@ -378,6 +378,12 @@ int crgc_host_unregister(crgc_graph *g, void *ptr);
 /* Human-readable text for a status code. */
 const char *crgc_strerror(int code);
 
+/* Where the calling thread's last failed call went wrong ("file:line: what",
+   e.g. the HIP status a runtime call returned, or the device error flags);
+   empty when its last call through a graph handle succeeded.  Diagnostics
+   only: the status code is the contract. */
+const char *crgc_last_error_detail(void);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -220,6 +220,7 @@ EXPORTED_SYMBOLS = (
     "crgc_undo_acc_export",
     "crgc_merge_undo_acc",
     "crgc_strerror",
+    "crgc_last_error_detail",
     "crgc_transport_rccl_id",
     "crgc_transport_rccl",
     "crgc_transport_local",
@@ -279,6 +280,9 @@ def load_library(path: str | None = None) -> C.CDLL:
     lib.crgc_last_trace.argtypes = [_P, C.POINTER(CrgcTraceOut)]
     lib.crgc_strerror.restype = C.c_char_p
     lib.crgc_strerror.argtypes = [C.c_int]
+    if hasattr(lib, "crgc_last_error_detail"):  # an A/B build may predate it
+        lib.crgc_last_error_detail.restype = C.c_char_p
+        lib.crgc_last_error_detail.argtypes = []
     lib.crgc_transport_rccl_id.restype = C.c_int
     lib.crgc_transport_rccl_id.argtypes = [C.c_char_p]
     lib.crgc_transport_rccl.restype = C.c_int
@@ -316,9 +320,18 @@ def load_library(path: str | None = None) -> C.CDLL:
 
 
 class CrgcError(RuntimeError):
-    def __init__(self, code: int, where: str):
+    def __init__(self, code: int, where: str, detail: str = ""):
         self.code = code
-        super().__init__(f"{where}: {code} ({ERROR_NAMES.get(code, '?')})")
+        self.detail = detail
+        super().__init__(f"{where}: {code} ({ERROR_NAMES.get(code, '?')})"
+                         + (f" at {detail}" if detail else ""))
+
+
+def last_error_detail() -> str:
+    """crgc_last_error_detail(): where this thread's last failed call went wrong."""
+    if _lib is None or not hasattr(_lib, "crgc_last_error_detail"):
+        return ""
+    return (_lib.crgc_last_error_detail() or b"").decode(errors="replace")
 
 
 ERROR_NAMES = {

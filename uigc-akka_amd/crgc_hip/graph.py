@@ -104,7 +104,7 @@ class ShadowGraph:
     @staticmethod
     def _chk(rc: int, where: str):
         if rc != abi.OK:
-            raise abi.CrgcError(rc, where)
+            raise abi.CrgcError(rc, where, abi.last_error_detail())
 
     # -- merges ---------------------------------------------------------------
     def mergeEntry(self, entry: Entry):

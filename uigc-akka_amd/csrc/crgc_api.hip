@@ -363,13 +363,27 @@ struct crgc_graph {
 };
 
 namespace {
+thread_local int api_depth = 0;
+thread_local char err_detail[256];
+}  // namespace
 
-int map_hip(hipError_t e) {
+void crgc::note_error(const char *file, int line, const char *what) {
+  if (err_detail[0]) return;  // the first failure of the call is the cause
+  const char *base = strrchr(file, '/');
+  snprintf(err_detail, sizeof err_detail, "%s:%d: %s", base ? base + 1 : file, line,
+           what && *what ? what : "failed");
+}
+
+namespace {
+
+int map_hip_at(hipError_t e, int line) {
   if (e == hipSuccess) return CRGC_OK;
+  note_error(__FILE__, line, hipGetErrorName(e));
   if (e == hipErrorOutOfMemory) return CRGC_E_NOMEM;
   if (e == hipErrorLaunchTimeOut) return CRGC_E_TIMEOUT;
   return CRGC_E_DEVICE;
 }
+#define map_hip(e) map_hip_at((e), __LINE__)
 
 #define HIP_TRY(x)                                  \
   do {                                              \
@@ -383,11 +397,13 @@ int map_hip(hipError_t e) {
 struct DeviceGuard {
   int prev = -1;
   explicit DeviceGuard(int dev) {
+    if (api_depth++ == 0) err_detail[0] = 0;  // a new call: forget the last one's failure
     (void)hipGetLastError();
     hipGetDevice(&prev);
     if (prev != dev) hipSetDevice(dev);
   }
   ~DeviceGuard() {
+    --api_depth;
     int cur;
     hipGetDevice(&cur);
     if (prev >= 0 && cur != prev) hipSetDevice(prev);
@@ -432,9 +448,12 @@ int device_error(crgc_graph *h) {
   const uint64_t err = h->hctr->err;
   if (!err) return CRGC_OK;
   h->poisoned = true;
+  char what[48];
+  snprintf(what, sizeof what, "device error flags 0x%llx", (unsigned long long)err);
+  note_error(__FILE__, __LINE__, what);
   if (err & (ERR_RESERVED_ID | ERR_TOO_MANY | ERR_BAD_OFFSETS)) return CRGC_E_INVAL;
   if (err & ERR_SPIN) return CRGC_E_TIMEOUT;
-  if (err & ERR_QUEUE_FULL) return CRGC_E_DEVICE;
+  if (err & ERR_QUEUE_FULL) return DEV_FAIL("");
   return CRGC_E_NOMEM;
 }
 
@@ -645,6 +664,8 @@ const char *crgc_strerror(int code) {
   }
 }
 
+const char *crgc_last_error_detail(void) { return err_detail; }
+
 int crgc_create(const crgc_config *cfg, crgc_graph **out) {
   if (!out) return CRGC_E_INVAL;
   *out = nullptr;
@@ -676,21 +697,21 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
       h->stream = (hipStream_t)cfg->stream;
     } else {
       if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
-        rc = CRGC_E_DEVICE;
+        rc = DEV_FAIL("");
         break;
       }
       h->own_stream = true;
     }
     for (auto &e : h->ev)
-      if (hipEventCreate(&e) != hipSuccess) rc = CRGC_E_DEVICE;
+      if (hipEventCreate(&e) != hipSuccess) rc = DEV_FAIL("");
     h->use_side = h->knobs.side_stream;  // A/B switch
     h->chunk_host = h->knobs.chunk_host;
     h->chunk_max = h->knobs.chunk_max;
     if (hipStreamCreateWithFlags(&h->cpy, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_cstart, hipEventDisableTiming) != hipSuccess)
-      rc = CRGC_E_DEVICE;
+      rc = DEV_FAIL("");
     for (auto &e : h->ev_chunk)
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = CRGC_E_DEVICE;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = DEV_FAIL("");
     // CRGC_SIDE_PRIO=1: the side stream (the merge's critical path) at the
     // device's highest priority, so its workgroups dispatch first
     int prio_lo = 0, prio_hi = 0;
@@ -699,7 +720,7 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     if (hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, side_prio) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess)
-      rc = CRGC_E_DEVICE;
+      rc = DEV_FAIL("");
     if (rc) break;
     if (hipMalloc(&h->ctr, sizeof(Counters)) != hipSuccess ||
         hipHostMalloc(&h->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess ||
@@ -712,7 +733,7 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     hipMemsetAsync(h->ctr, 0, sizeof(Counters), h->stream);
     memset(h->hctr, 0, sizeof(Counters));
     if (hipHostGetDevicePointer((void **)&h->hctr_dev, h->hctr, 0) != hipSuccess || !h->hctr_dev) {
-      rc = CRGC_E_DEVICE;
+      rc = DEV_FAIL("");
       break;
     }
     const uint64_t v0 = cfg && cfg->vertex_capacity ? cfg->vertex_capacity : (1u << 16);
@@ -722,7 +743,7 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
       rc = map_hip(e);
       break;
     }
-    if (hipStreamSynchronize(h->stream) != hipSuccess) rc = CRGC_E_DEVICE;
+    if (hipStreamSynchronize(h->stream) != hipSuccess) rc = DEV_FAIL("");
   } while (0);
   if (rc) {
     crgc_destroy(h);
@@ -2204,7 +2225,7 @@ static int xclosure(crgc_graph *h, bool investigate, const XRecv &xr, uint64_t *
     if (int rc = ag_u64(h, {{x.xl_n, 1}}, cnt.data())) return rc;  // synchronises
     if (fl[0]) {
       h->poisoned = true;
-      return CRGC_E_DEVICE;  // a proxy without a resolved home slot: the resolution step failed
+      return DEV_FAIL("");  // a proxy without a resolved home slot: the resolution step failed
     }
     ++*rounds;
     bool jumped = false;
@@ -3156,7 +3177,7 @@ int crgc_host_register(crgc_graph *h, void *ptr, uint64_t bytes) {
   if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess || !dev) {
     (void)hipGetLastError();
     hipHostUnregister(ptr);
-    return CRGC_E_DEVICE;
+    return DEV_FAIL("");
   }
   h->pinned.push_back({b, bytes, (char *)dev});
   return CRGC_OK;

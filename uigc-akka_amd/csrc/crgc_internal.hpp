@@ -30,6 +30,12 @@ namespace crgc {
 // call left behind and reports only its own launches.
 inline void launch_begin() { (void)hipGetLastError(); }
 
+// Where this thread's last failing API call went wrong: file:line and what
+// failed (the HIP status name, device error flags, a transport step).  The
+// first failure of a call wins; crgc_last_error_detail() returns it.
+void note_error(const char *file, int line, const char *what);
+#define DEV_FAIL(what) (note_error(__FILE__, __LINE__, (what)), CRGC_E_DEVICE)
+
 constexpr uint64_t KEY_EMPTY = 0xFFFFFFFFFFFFFFFFull;
 constexpr uint32_t PHS_NONE = 0xFFFFFFFFu;    // proxy's home slot not resolved yet
 constexpr uint32_t PHS_ABSENT = 0xFFFFFFFEu;  // the home shard has no live shadow of the id

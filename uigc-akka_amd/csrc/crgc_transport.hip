@@ -36,21 +36,21 @@ int LocalTransport::barrier() {
 
 int LocalTransport::allgather(uint32_t shard, const void *send, void *recv, size_t bytes,
                               hipStream_t s) {
-  if (hipStreamSynchronize(s) != hipSuccess) return CRGC_E_DEVICE;  // send is complete
+  if (hipStreamSynchronize(s) != hipSuccess) return DEV_FAIL("transport");  // send is complete
   post[shard].ptr = send;
   if (int rc = barrier()) return rc;
   for (uint32_t r = 0; r < n_shards; ++r)
     if (bytes && hipMemcpyAsync((char *)recv + (size_t)r * bytes, post[r].ptr, bytes, hipMemcpyDefault,
                                 s) != hipSuccess)
-      return CRGC_E_DEVICE;
-  if (hipStreamSynchronize(s) != hipSuccess) return CRGC_E_DEVICE;
+      return DEV_FAIL("transport");
+  if (hipStreamSynchronize(s) != hipSuccess) return DEV_FAIL("transport");
   return barrier();  // nobody reuses its send buffer before every peer has copied it
 }
 
 int LocalTransport::alltoallv(uint32_t shard, const void *send, const size_t *soff, const size_t *sbytes,
                               void *recv, const size_t *roff, const size_t *rbytes, hipStream_t s) {
   (void)sbytes;
-  if (hipStreamSynchronize(s) != hipSuccess) return CRGC_E_DEVICE;
+  if (hipStreamSynchronize(s) != hipSuccess) return DEV_FAIL("transport");
   post[shard].ptr = send;
   post[shard].soff = soff;
   if (int rc = barrier()) return rc;
@@ -58,9 +58,9 @@ int LocalTransport::alltoallv(uint32_t shard, const void *send, const size_t *so
     if (!rbytes[r]) continue;
     const char *src = (const char *)post[r].ptr + post[r].soff[shard];
     if (hipMemcpyAsync((char *)recv + roff[r], src, rbytes[r], hipMemcpyDefault, s) != hipSuccess)
-      return CRGC_E_DEVICE;
+      return DEV_FAIL("transport");
   }
-  if (hipStreamSynchronize(s) != hipSuccess) return CRGC_E_DEVICE;
+  if (hipStreamSynchronize(s) != hipSuccess) return DEV_FAIL("transport");
   return barrier();
 }
 
@@ -85,21 +85,21 @@ struct RcclTransport final : crgc_transport {
   }
   bool accepts(uint32_t shard, int dev) const override { return shard == rank && dev == device; }
   int allgather(uint32_t, const void *send, void *recv, size_t bytes, hipStream_t s) override {
-    if (!comm) return CRGC_E_DEVICE;
+    if (!comm) return DEV_FAIL("transport");
     if (!bytes) return CRGC_OK;
     if (ncclAllGather(send, recv, bytes, ncclUint8, comm, s) == ncclSuccess) return CRGC_OK;
     abort();
-    return CRGC_E_DEVICE;
+    return DEV_FAIL("transport");
   }
   int alltoallv(uint32_t, const void *send, const size_t *soff, const size_t *sbytes, void *recv,
                 const size_t *roff, const size_t *rbytes, hipStream_t s) override {
-    if (!comm) return CRGC_E_DEVICE;
+    if (!comm) return DEV_FAIL("transport");
     // own block: a device copy; peers: one grouped send/recv per direction
     if (rbytes[rank] &&
         hipMemcpyAsync((char *)recv + roff[rank], (const char *)send + soff[rank], rbytes[rank],
                        hipMemcpyDeviceToDevice, s) != hipSuccess) {
       abort();  // the peers' exchange with this rank is never posted: fail it for them
-      return CRGC_E_DEVICE;
+      return DEV_FAIL("transport");
     }
     struct Ops {
       RcclTransport *t;
@@ -144,7 +144,7 @@ struct RcclTransport final : crgc_transport {
 int rccl_unique_id(uint8_t id[128]) {
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
   ncclUniqueId u;
-  if (ncclGetUniqueId(&u) != ncclSuccess) return CRGC_E_DEVICE;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return DEV_FAIL("transport");
   memcpy(id, &u, 128);
   return CRGC_OK;
 }
@@ -170,7 +170,7 @@ crgc_transport *make_rccl_transport(const uint8_t id[128], uint32_t n_shards, ui
   if (r != ncclSuccess) {
     t->comm = nullptr;
     delete t;
-    *rc = CRGC_E_DEVICE;
+    *rc = DEV_FAIL("transport");
     return nullptr;
   }
   *rc = CRGC_OK;
