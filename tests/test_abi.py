@@ -43,6 +43,11 @@ def test_library_loads_and_exports_every_declared_symbol():
     for name in _declared_functions():
         assert hasattr(lib, name), name
     assert lib.crgc_strerror(abi.E_NULL_SUPERVISOR).startswith(b"local garbage")
+    # no call has failed on this thread: the failure detail is empty, and a
+    # CrgcError carries it when there is one
+    assert lib.crgc_last_error_detail() == b"" and abi.last_error_detail() == ""
+    e = abi.CrgcError(abi.E_DEVICE, "crgc_merge_entries", "crgc_api.hip:1234: hipErrorLaunchFailure")
+    assert "CRGC_E_DEVICE" in str(e) and e.detail.endswith("hipErrorLaunchFailure")
 
 
 def test_library_is_gfx950_only(tmp_path):

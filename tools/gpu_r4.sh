@@ -8,6 +8,7 @@
 #   pmc              FETCH_SIZE and WRITE_SIZE passes of the same command, one run each
 #   probe            tools/hip_probe.hip: HIP last-error / event / pointer-range semantics
 #   c4               C4 unsharded on one GPU (1e8 actors / 1e9 edges, the scaling anchor)
+#   kt4              kernel trace of the C4 N = 1 line (load and wakeups)
 #   c4l8 c2l8        C4 / C2 over 8 logical shards on the one GPU (the sharded protocol at full size)
 #   c2rs c4rs        the N>1 bench path itself on one rank (nccl group, RCCL transport, one shard)
 set -euo pipefail
@@ -42,6 +43,9 @@ for step in "$@"; do
     probe) (cd "$ROOT" && timeout -k 10 60 ./tools/_build/hip_probe > "$O/hip_probe.txt" 2>&1) ;;
     c4) (cd /tmp && CRGC_LEVEL_LOG=1 timeout -k 10 1000 python3 -u "$ROOT/bench.py" --workload c4 --steps 5 \
           --warmup 2 --no-pcie > "$O/bench_c4.json" 2> "$O/bench_c4.err") ;;
+    kt4) (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt4" -o kt -- \
+          python3 "$ROOT/bench.py" --workload c4 --steps 3 --warmup 1 --no-cpu-baseline --no-pcie \
+          > "$O/bench_kt4.json" 2> "$O/bench_kt4.err") ;;
     c4l8) (cd /tmp && CRGC_LEVEL_LOG=1 timeout -k 10 1000 python3 -u "$ROOT/bench.py" --workload c4 --logical-shards 8 \
           --steps 3 --warmup 1 > "$O/bench_c4l8.json" 2> "$O/bench_c4l8.err") ;;
     c2rs) (cd /tmp && timeout -k 10 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node=1 \
