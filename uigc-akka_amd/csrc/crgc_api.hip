@@ -1888,7 +1888,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   // up to 256 bins of >= 65536 slots (an LDS bitmap of <= 128 KiB each), a region
   // for half the graph's edge keys (targets past it are stored at once), the
   // per-(bin, workgroup) counts and their scan; the mode word is zeroed with a
-  // fresh allocation and reset by k_bin_apply.
+  // fresh allocation and cleared by each trace's count pass.
   if (roots && kn.bin && !kn.alpha && top > 0 && top >= kn.bin_min) {
     uint32_t lg = 0;
     while (lg < 63 && (1ull << lg) < top) ++lg;

@@ -671,7 +671,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 //                  atomics
 //   k_bin_apply    one workgroup per bin: its region into an LDS bitmap of the
 //                  bin's slot range (16-B loads), then the range's candidate
-//                  bytes OR-ed with it in 16-B groups; the mode word reset.
+//                  bytes OR-ed with it in 16-B groups.
 // Used only when the level-0 frontier is >= 1/32 of the slots (every kernel
 // derives the same answer; the mode word tells k_bin_apply).  Not binned, the
 // place pass stores the bytes at once.
@@ -688,6 +688,9 @@ __global__ __launch_bounds__(256) void k_bin_walk(DevGraph g, LevelArgs a) {
   __shared__ uint32_t s_ulist[256], s_utag[256], s_wcnt[4], s_nact;
   __shared__ uint32_t lc[BIN_MAX];  // count: targets per bin; place: the next position of each bin's slice
   Counters *c = g.ctr;
+  // the count pass clears the mode word of the previous trace (its k_bin_apply
+  // has finished: stream order); the place pass sets it when this level is binned
+  if (PASS == 0 && blockIdx.x == 0 && threadIdx.x == 0) a.bin_mode_w[0] = 0;
   if (c->tail_state) return;
   const bool binned = bin_mode(c, a);
   if (PASS == 0 && !binned) return;  // not binned: the place pass stores the bytes
@@ -862,9 +865,8 @@ __global__ __launch_bounds__(1024) void k_bin_apply(DevGraph g, LevelArgs a) {
     *(uint4 *)(Fn + q) = make_uint4(w[0], w[1], w[2], w[3]);
     nb2 += 64;  // 16 B read + 16 B written
   }
-  __syncthreads();
-  // every workgroup has read the mode word: reset it for the next trace
-  if (b == 0 && tid == 0) a.bin_mode_w[0] = 0;
+  // (the mode word is not reset here: a workgroup scheduled after this one
+  // ended must still read it — the next trace's count pass clears it)
   const uint32_t ws = wave_sum(nb2);
   if (lane_id() == 0 && ws) atomicAdd((unsigned long long *)&g.xbytes[b], (unsigned long long)(ws / 2));
 }
