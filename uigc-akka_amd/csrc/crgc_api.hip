@@ -485,14 +485,12 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   uint32_t *map = cv.take<uint32_t>(src_top + 1);
   uint64_t *offs = cv.take<uint64_t>(c.scap);
   void *scan_tmp = cv.take<uint64_t>(rebuild_scan_tmp_bytes(c.scap) / 8);
-  hipMemsetAsync(offs, 0, c.scap * 8, h->stream);
+  hipError_t e = hipMemsetAsync(offs, 0, c.scap * 8, h->stream);
   // new generation counters: slot_top, pool_top, etab_used restart
-  hipMemsetAsync((char *)h->ctr + CTR_OFF(slot_top), 0, 8, h->stream);
-  hipMemsetAsync((char *)h->ctr + CTR_OFF(pool_top), 0, 8, h->stream);
-  hipMemsetAsync((char *)h->ctr + CTR_OFF(rpool_top), 0, 8, h->stream);
-  hipMemsetAsync((char *)h->ctr + CTR_OFF(etab_used), 0, 8, h->stream);
+  for (size_t off : {CTR_OFF(slot_top), CTR_OFF(pool_top), CTR_OFF(rpool_top), CTR_OFF(etab_used)})
+    if (e == hipSuccess) e = hipMemsetAsync((char *)h->ctr + off, 0, 8, h->stream);
   // src keeps a view of the old counters' bound via src_top (passed by value)
-  hipError_t e = launch_rebuild(h->g.d, src_top, dst.d, map, nullptr, offs, scan_tmp, h->stream);
+  if (e == hipSuccess) e = launch_rebuild(h->g.d, src_top, dst.d, map, nullptr, offs, scan_tmp, h->stream);
   // The last trace's garbage / kill lists outlive the generation: crgc_last_trace
   // may still copy them (two-phase trace, or a trace whose buffers were short).
   // They can hold more ids than the compacted generation has slots.
