@@ -341,7 +341,6 @@ struct crgc_graph {
   Scratch x_chain;           // chain mode (crgc_chain.hip)
   Scratch x_chunk;           // rebased offsets of a large device batch's sub-merges
   Scratch x_bin;             // the pseudo-root level's binned push: counters, then bin regions
-  uint64_t x_bin_zeroed = 0;  // x_bin allocation (Scratch::gen) whose counters were zeroed
   Scratch x_gc, x_gc_list;   // replicated chain closure of sharded marks (crgc_xchain.hip)
   uint64_t *h_small = nullptr;       // pinned host staging for small all-gathers
   uint64_t *h_bounce = nullptr;      // pinned bounce for id lists into partly pinned caller buffers
@@ -1882,39 +1881,30 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   la.xslices = kn.xslices;
   la.tail_start = std::min<uint32_t>(kn.tail_start, TAIL_QCAP);
   la.tail_max = std::min<uint32_t>(std::max(kn.tail_max, 1u), TAIL_QCAP);
-  // The pseudo-root level's binned push (crgc_trace.hip k_bin_walk / k_bin_apply):
-  // up to 256 bins of >= 65536 slots (an LDS bitmap of <= 128 KiB each), a region
-  // for half the graph's edge keys (targets past it are stored at once), the
-  // per-(bin, workgroup) counts and their scan; the mode word is zeroed with a
-  // fresh allocation and cleared by each trace's count pass.
+  // The pseudo-root level's binned push (crgc_trace.hip k_bin_place / k_bin_apply):
+  // up to 256 bins of >= 65536 slots (an LDS bitmap of <= 128 KiB each), BIN_WG
+  // place workgroups with a fixed-capacity slice of every bin each; the slices
+  // together hold half the graph's edge keys (targets past a slice are stored
+  // at once).  The place pass writes the mode word k_bin_apply reads.
   if (roots && kn.bin && !kn.alpha && top > 0 && top >= kn.bin_min) {
     uint32_t lg = 0;
     while (lg < 63 && (1ull << lg) < top) ++lg;
     const uint32_t shift = std::max<uint32_t>(16, lg > 8 ? lg - 8 : 0);
     const uint64_t nb = (top + (1ull << shift) - 1) >> shift;
     if (shift <= 20 && nb <= BIN_MAX) {
-      const uint32_t G = STAT_WG;  // both walk passes (8 workgroups per CU: ~6 KiB of LDS each)
-      const uint64_t nc = nb * G;
-      const uint64_t cap = round_up(std::max<uint64_t>(1u << 16, (h->etab_used + h->atoms_since) / 2), 64);
-      const size_t need = Carver::need({16, 16, nc * 4, nc * 8, ((nc + 1023) / 1024) * 4 * 8 + 64, cap * 4});
+      const uint64_t nc = nb * BIN_WG;
+      const uint64_t want = std::max<uint64_t>(1u << 16, (h->etab_used + h->atoms_since) / 2);
+      const uint64_t sc = std::min<uint64_t>(std::max<uint64_t>(round_up(want / nc, 4), 16), 1u << 24);
+      const size_t need = Carver::need({16, nc * 4, nc * sc * 4});
       HIP_TRY(h->x_bin.ensure(need));
       Carver cv(h->x_bin.ptr);
       la.bin_mode_w = cv.take<uint32_t>(4);
-      la.bin_tot = cv.take<unsigned long long>(2);
       la.bin_cnt = cv.take<uint32_t>(nc);
-      la.bin_off = cv.take<uint64_t>(nc);
-      la.bin_bsum = cv.take<uint64_t>(((nc + 1023) / 1024) * 4 + 8);
-      la.bins = cv.take<uint32_t>(cap);
-      // a fresh allocation (compared by generation: a reallocation may return
-      // the same base address) starts with the mode word clear
-      if (h->x_bin_zeroed != h->x_bin.gen) {
-        HIP_TRY(hipMemsetAsync(la.bin_mode_w, 0, 16, h->stream));
-        h->x_bin_zeroed = h->x_bin.gen;
-      }
+      la.bins = cv.take<uint32_t>(nc * sc);
+      la.bin_slice = (uint32_t)sc;
       la.bin_shift = shift;
       la.nbins = (uint32_t)nb;
-      la.bin_cap = cap;
-      la.bin_grid = G;
+      la.bin_grid = BIN_WG;
     }
   }
   // Device times, from timing-only events (no system-scope fence):

@@ -185,18 +185,16 @@ struct LevelArgs {
   uint32_t chain_after;    // k_tail hands a deep mark to chain mode after this many rounds (0: never)
   uint32_t xslices;        // push levels: 1, 2, 4 or 8 target slices (k_expand: XCD-local candidate stores)
   uint16_t location;
-  // the pseudo-root level's binned push (k_bin_walk count / place, k_bin_apply), nbins == 0: off
-  uint32_t *bins;          // the targets, bin-major: bin b, workgroup w at bin_off[b * bin_grid + w]
-  uint32_t *bin_cnt;       // [nbins x bin_grid] targets per (bin, workgroup), bin-major (count pass)
-  uint64_t *bin_off;       // [nbins x bin_grid] their exclusive scan
-  unsigned long long *bin_tot;  // [1] the scan's total
-  uint64_t *bin_bsum;      // scan scratch
-  uint32_t *bin_mode_w;    // [1] the binned-mode word (set by the place pass, reset by k_bin_apply)
-  uint64_t bin_cap;        // entries of `bins` (targets past it are stored as bytes at once)
+  // the pseudo-root level's binned push (k_bin_place, k_bin_apply), nbins == 0: off
+  uint32_t *bins;          // the targets: slice (bin b, workgroup w) at [(b * bin_grid + w) * bin_slice, + bin_slice)
+  uint32_t *bin_cnt;       // [nbins x bin_grid] targets in each slice, bin-major (place pass)
+  uint32_t *bin_mode_w;    // [1] the binned-mode word (written by the place pass, read by k_bin_apply)
+  uint32_t bin_slice;      // entries of a slice (a multiple of 4; targets past it are stored as bytes at once)
   uint32_t bin_shift;      // a bin covers slots [b << bin_shift, (b + 1) << bin_shift)
   uint32_t nbins;
-  uint32_t bin_grid;       // workgroups of both walk passes (the same units per workgroup)
+  uint32_t bin_grid;       // workgroups of the place pass
 };
+constexpr uint32_t BIN_WG = 512;     // k_bin_place workgroups (16 waves each)
 constexpr uint32_t BIN_MAX = 256;    // bins at most (one LDS counter each)
 
 // Chain mode (crgc_chain.hip).

@@ -654,47 +654,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 // The pseudo-root level's push, binned.  Level 0 of a wide trace pushes ~1e7
 // candidate bytes to random slots of a ~10 MB byte map that no XCD's 4 MB L2
 // holds: the edge stream takes ~22 us, the random byte stores ~215 us (C2,
-// profiles/r3g/lv1).  Binned, the stores become sequential.  Round 4 does it
-// as count-then-place (round 3 staged targets in LDS bins flushed in lock-step
-// rounds — four barriers per four units and a returning global atomic per bin
-// and flush: 166 us against the 22-us stream):
-//   k_bin_walk<0>  count: each workgroup walks its units (light chunks, hub
-//                  pieces; the same units in both passes) and counts its
-//                  targets per bin (nbins <= 256 ranges of 2^bin_shift slots)
-//                  in LDS; the counts go out bin-major: no barrier per unit
-//   run_scan       exclusive scan of the (bin, workgroup) counts: every
-//                  workgroup's slice of every bin's region
-//   k_bin_walk<1>  place: the same walk; each target takes the next position of
-//                  its (bin, workgroup) slice from an LDS cursor and is stored
-//                  there (each slice fills front to back, so its lines fill in
-//                  the XCD's L2 before they leave it); no staging, no global
-//                  atomics
-//   k_bin_apply    one workgroup per bin: its region into an LDS bitmap of the
-//                  bin's slot range (16-B loads), then the range's candidate
-//                  bytes OR-ed with it in 16-B groups.
-// Used only when the level-0 frontier is >= 1/32 of the slots (every kernel
-// derives the same answer; the mode word tells k_bin_apply).  Not binned, the
-// place pass stores the bytes at once.
+// profiles/r3g/lv1).  Binned, the stores become sequential.
+//   k_bin_place  one walk over the level's units (light chunks, hub pieces) by
+//                BIN_WG workgroups of 16 waves; each target goes to the next
+//                position of its (bin, workgroup) slice — a fixed-capacity
+//                piece of the region, bin-major — from an LDS cursor (nbins <=
+//                256 ranges of 2^bin_shift slots); a target past its slice's
+//                capacity is stored as a byte at once.  The slice counts go out
+//                at the end.  No staging, no barrier per unit, no global atomic.
+//   k_bin_apply  one workgroup per bin: its slices (16-B loads, the slice
+//                counts in LDS) into an LDS bitmap of the bin's slot range,
+//                then the range's candidate bytes OR-ed with it in 16-B groups.
+// The line footprint of the open slices is what the place pass pays for: with
+// 2048 workgroups of 4 waves (round 4's first count-then-place form) the
+// ~344k slices' partly written lines did not fit the L2s and left them partly
+// written, and a count pass + scan sized the slices exactly (level 0: 60 + 15
+// + 131 + 28 us, profiles/r4d); 512 workgroups of 16 waves keep the same waves
+// with a quarter of the slices, and fixed-capacity slices need no count pass.
+// Used only when the level-0 frontier is >= 1/32 of the slots (the place pass
+// derives it and sets the mode word for k_bin_apply; not binned, it stores the
+// bytes at once).
 // ---------------------------------------------------------------------------
 __device__ inline bool bin_mode(const Counters *c, const LevelArgs &a) {
   return a.nbins > 0 && a.nbins <= BIN_MAX && c->ring[0] * 32 >= c->slot_top;
 }
 
-template <int PASS>  // 0: count, 1: place
-__global__ __launch_bounds__(256) void k_bin_walk(DevGraph g, LevelArgs a) {
+constexpr int BIN_T = 1024;  // threads of a k_bin_place / k_bin_apply workgroup
+constexpr int BIN_NW = BIN_T / 64;
+
+__global__ __launch_bounds__(BIN_T) void k_bin_place(DevGraph g, LevelArgs a) {
   constexpr int U = EXPAND_U;
-  __shared__ uint32_t s_start[4][65];
-  __shared__ uint32_t s_off[4][64];
-  __shared__ uint32_t s_ulist[256], s_utag[256], s_wcnt[4], s_nact;
-  __shared__ uint32_t lc[BIN_MAX];  // count: targets per bin; place: the next position of each bin's slice
+  __shared__ uint32_t s_start[BIN_NW][65];
+  __shared__ uint32_t s_off[BIN_NW][64];
+  __shared__ uint32_t s_ulist[BIN_T], s_utag[BIN_T], s_wcnt[BIN_NW], s_nact;
+  __shared__ uint32_t lc[BIN_MAX];  // the next position of each bin's slice of this workgroup
   Counters *c = g.ctr;
-  // the count pass clears the mode word of the previous trace (its k_bin_apply
-  // has finished: stream order); the place pass sets it when this level is binned
-  if (PASS == 0 && blockIdx.x == 0 && threadIdx.x == 0) a.bin_mode_w[0] = 0;
+  const bool binned = !c->tail_state && bin_mode(c, a);
+  // k_bin_apply runs after this kernel (stream order) and reads the word
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.bin_mode_w[0] = binned ? 1u : 0u;
   if (c->tail_state) return;
-  const bool binned = bin_mode(c, a);
-  if (PASS == 0 && !binned) return;  // not binned: the place pass stores the bytes
   const uint32_t NB = a.nbins;
+  const uint32_t SC = a.bin_slice;
   uint8_t *Fn = g.front[1];
   const int wv = threadIdx.x >> 6, lane = lane_id(), tid = threadIdx.x;
   const uint64_t G = gridDim.x, wg = blockIdx.x;
@@ -704,8 +704,7 @@ __global__ __launch_bounds__(256) void k_bin_walk(DevGraph g, LevelArgs a) {
   const uint64_t nunits = ncid + nh;
   uint32_t nb2 = 0;
   if (binned)
-    for (uint32_t k = tid; k < NB; k += 256) lc[k] = PASS == 0 ? 0u : (uint32_t)a.bin_off[(uint64_t)k * G + wg];
-  if (PASS == 1 && binned && wg == 0 && tid == 0) a.bin_mode_w[0] = 1;
+    for (uint32_t k = tid; k < NB; k += BIN_T) lc[k] = 0;
   __syncthreads();
 
   auto put = [&](uint32_t t) {
@@ -714,13 +713,12 @@ __global__ __launch_bounds__(256) void k_bin_walk(DevGraph g, LevelArgs a) {
       return;
     }
     const uint32_t b = t >> a.bin_shift;
-    if (PASS == 0) {
-      atomicAdd(&lc[b], 1u);
-    } else {
-      const uint32_t pos = atomicAdd(&lc[b], 1u);
-      if (pos < a.bin_cap) a.bins[pos] = t;
-      else Fn[t] = 1;  // past the region: the byte at once
+    const uint32_t pos = b < NB ? atomicAdd(&lc[b], 1u) : SC;  // (a slot past the bins: never, slot_top is synced)
+    if (pos < SC) {
+      a.bins[((uint64_t)b * G + wg) * SC + pos] = t;
       nb2 += 8;
+    } else {
+      Fn[t] = 1;  // past the slice: the byte at once
     }
   };
   auto edges = [&](const uint64_t (&ed)[U]) {
@@ -778,11 +776,11 @@ __global__ __launch_bounds__(256) void k_bin_walk(DevGraph g, LevelArgs a) {
   };
 
   // Unit ids are dealt round-robin over the workgroups (workgroup w, window i,
-  // thread t: id (256 i + t) G + w): light chunks with work cluster at the
+  // thread t: id (BIN_T i + t) G + w): light chunks with work cluster at the
   // low ids (k = 0 .. 3 of every block at level 0), so consecutive windows
   // would leave most workgroups idle.  Within a window every wave takes every
-  // fourth unit with work, at its own pace: nothing waits on another wave.
-  for (uint64_t ub = 0; ub * G < nunits; ub += 256) {
+  // BIN_NW-th unit with work, at its own pace: nothing waits on another wave.
+  for (uint64_t ub = 0; ub * G < nunits; ub += BIN_T) {
     const uint64_t u = (ub + tid) * G + wg;
     uint32_t tag = 0;
     bool act = false;
@@ -803,49 +801,60 @@ __global__ __launch_bounds__(256) void k_bin_walk(DevGraph g, LevelArgs a) {
       s_ulist[i] = (uint32_t)tid;
       s_utag[i] = tag;
     }
-    if (tid == 0) s_nact = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
+    if (tid == 0) {
+      uint32_t n = 0;
+      for (int w = 0; w < BIN_NW; ++w) n += s_wcnt[w];
+      s_nact = n;
+    }
     __syncthreads();
     const uint32_t nact = s_nact;
-    for (uint32_t r = wv; r < nact; r += 4) unit((ub + s_ulist[r]) * G + wg, s_utag[r]);
+    for (uint32_t r = wv; r < nact; r += BIN_NW) unit((ub + s_ulist[r]) * G + wg, s_utag[r]);
     __syncthreads();  // s_ulist is rewritten by the next window
   }
-  if (PASS == 0)
-    for (uint32_t k = tid; k < NB; k += 256) a.bin_cnt[(uint64_t)k * G + wg] = lc[k];
+  if (binned)
+    for (uint32_t k = tid; k < NB; k += BIN_T) a.bin_cnt[(uint64_t)k * G + wg] = min(lc[k], SC);
   expand_bytes_out(g, nb2);
 }
 
-__global__ __launch_bounds__(1024) void k_bin_apply(DevGraph g, LevelArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t bm[];  // 2^bin_shift bits
+__global__ __launch_bounds__(BIN_T) void k_bin_apply(DevGraph g, LevelArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t bm[];  // 2^bin_shift bits, then the slice counts
   if (!a.bins || a.bin_mode_w[0] == 0) return;  // level 0 was not binned
   const uint32_t b = blockIdx.x, tid = threadIdx.x;
   const uint32_t span = 1u << a.bin_shift, words = span / 32;
-  for (uint32_t k = tid; k < words; k += 1024) bm[k] = 0;
+  const uint32_t G = a.bin_grid, SC = a.bin_slice, S4 = SC / 4;
+  uint32_t *cnt = bm + words;
+  for (uint32_t k = tid; k < words; k += BIN_T) bm[k] = 0;
+  for (uint32_t k = tid; k < G; k += BIN_T) cnt[k] = a.bin_cnt[(uint64_t)b * G + k];
   __syncthreads();
   uint32_t nb2 = 0;
-  // the bin's region [r0, r1) of `bins`, read in aligned 16-B groups, 4 in flight per thread
-  const uint64_t G = a.bin_grid;
-  const uint64_t r0 = min(a.bin_off[(uint64_t)b * G], a.bin_cap);
-  const uint64_t r1 = min(b + 1 < a.nbins ? a.bin_off[(uint64_t)(b + 1) * G] : (uint64_t)*a.bin_tot, a.bin_cap);
+  // the bin's G slices, four at a time per wave (their counts from LDS: the
+  // loop bounds are wave-uniform), each slice's filled part in 16-B groups
+  const uint4 *src = (const uint4 *)(a.bins + (uint64_t)b * G * SC);
   const uint32_t base = b << a.bin_shift;
-  const uint64_t q0 = r0 & ~3ull;
-  for (uint64_t i = q0 + (uint64_t)tid * 4; i < r1; i += 1024 * 4 * 4) {
-    uint4 q[4];
+  for (uint32_t w0 = (uint32_t)(tid >> 6); w0 < G; w0 += BIN_NW * 4) {
+    uint32_t n[4], mx = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint64_t at = i + (uint64_t)j * 1024 * 4;
-      q[j] = at < r1 ? *(const uint4 *)(a.bins + at) : make_uint4(0, 0, 0, 0);
+      const uint32_t w = w0 + j * BIN_NW;
+      n[j] = w < G ? cnt[w] : 0u;
+      mx = max(mx, n[j]);
     }
+    for (uint32_t i = (uint32_t)lane_id() * 4; i - (uint32_t)lane_id() * 4 < mx; i += 256) {
+      uint4 v4[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint64_t at = i + (uint64_t)j * 1024 * 4;
-      const uint32_t v[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+      for (int j = 0; j < 4; ++j)
+        v4[j] = i < n[j] ? src[(uint64_t)(w0 + j * BIN_NW) * S4 + i / 4] : make_uint4(0, 0, 0, 0);
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (at + k >= r0 && at + k < r1) {
-          const uint32_t t = v[k] - base;
-          atomicOr(&bm[t >> 5], 1u << (t & 31));
-          nb2 += 8;
-        }
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t v[4] = {v4[j].x, v4[j].y, v4[j].z, v4[j].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (i + k < n[j]) {
+            const uint32_t t = v[k] - base;
+            atomicOr(&bm[t >> 5], 1u << (t & 31));
+            nb2 += 8;
+          }
+      }
     }
   }
   __syncthreads();
@@ -853,7 +862,7 @@ __global__ __launch_bounds__(1024) void k_bin_apply(DevGraph g, LevelArgs a) {
   const uint64_t lo = (uint64_t)b << a.bin_shift;
   const uint64_t top = g.ctr->slot_top;
   const uint64_t hi = min(lo + span, (top + 15) & ~15ull);  // Fn holds scap >= this (a multiple of 2048)
-  for (uint64_t q = lo + (uint64_t)tid * 16; q < hi; q += 1024 * 16) {
+  for (uint64_t q = lo + (uint64_t)tid * 16; q < hi; q += BIN_T * 16) {
     const uint32_t rel = (uint32_t)(q - lo);
     const uint32_t bits = (bm[rel >> 5] >> (rel & 31)) & 0xFFFFu;
     if (!bits) continue;
@@ -865,8 +874,6 @@ __global__ __launch_bounds__(1024) void k_bin_apply(DevGraph g, LevelArgs a) {
     *(uint4 *)(Fn + q) = make_uint4(w[0], w[1], w[2], w[3]);
     nb2 += 64;  // 16 B read + 16 B written
   }
-  // (the mode word is not reset here: a workgroup scheduled after this one
-  // ended must still read it — the next trace's count pass clears it)
   const uint32_t ws = wave_sum(nb2);
   if (lane_id() == 0 && ws) atomicAdd((unsigned long long *)&g.xbytes[b], (unsigned long long)(ws / 2));
 }
@@ -1287,20 +1294,11 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
   hipExtLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, e[2], e[3], 0, g, a);
   // 8 WGs of 4 waves per CU
   if (roots && a.nbins) {
-    // the pseudo-root level, binned when it is wide: count, scan, place and
-    // apply, timed together as its expand
-    hipExtLaunchKernelGGL(k_bin_walk<0>, dim3(a.bin_grid), dim3(256), 0, s, e[4], nullptr, 0, g, a);
-    ScanSet q{};
-    q.k = 1;
-    q.n = (uint64_t)a.nbins * a.bin_grid;
-    q.in[0] = a.bin_cnt;
-    q.out[0] = a.bin_off;
-    q.total[0] = a.bin_tot;
-    q.bsum = a.bin_bsum;
-    if (hipError_t r = run_scan(q, s)) return r;
-    hipLaunchKernelGGL(k_bin_walk<1>, dim3(a.bin_grid), dim3(256), 0, s, g, a);
-    hipExtLaunchKernelGGL(k_bin_apply, dim3(a.nbins), dim3(1024), (size_t)(1u << a.bin_shift) / 8, s, nullptr,
-                          e[5], 0, g, a);
+    // the pseudo-root level, binned when it is wide: place and apply, timed
+    // together as its expand
+    hipExtLaunchKernelGGL(k_bin_place, dim3(a.bin_grid), dim3(BIN_T), 0, s, e[4], nullptr, 0, g, a);
+    hipExtLaunchKernelGGL(k_bin_apply, dim3(a.nbins), dim3(BIN_T),
+                          (size_t)(1u << a.bin_shift) / 8 + (size_t)a.bin_grid * 4, s, nullptr, e[5], 0, g, a);
     return hipGetLastError();
   }
   auto expand = [&](auto kern) {
