@@ -7,6 +7,7 @@
 #   kt               rocprofv3 --kernel-trace --stats of the timed C2 wakeups only (--no-pcie)
 #   pmc              FETCH_SIZE and WRITE_SIZE passes of the same command, one run each
 #   probe            tools/hip_probe.hip: HIP last-error / event / pointer-range semantics
+#   rand             tools/rand_probe.hip: random-access ceilings (loads, atomics, CAS, stores)
 #   c4               C4 unsharded on one GPU (1e8 actors / 1e9 edges, the scaling anchor)
 #   kt4              kernel trace of the C4 N = 1 line (load and wakeups)
 #   c4l8 c2l8        C4 / C2 over 8 logical shards on the one GPU (the sharded protocol at full size)
@@ -41,6 +42,7 @@ for step in "$@"; do
           timeout -k 10 420 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o pmc -- $B \
             > "$O/bench_write.json" 2> "$O/bench_write.err") ;;
     probe) (cd "$ROOT" && timeout -k 10 60 ./tools/_build/hip_probe > "$O/hip_probe.txt" 2>&1) ;;
+    rand) (cd "$ROOT" && timeout -k 10 120 ./tools/_build/rand_probe > "$O/rand_probe.txt" 2>&1) ;;
     c4) (cd /tmp && CRGC_LEVEL_LOG=1 timeout -k 10 1000 python3 -u "$ROOT/bench.py" --workload c4 --steps 5 \
           --warmup 2 --no-pcie > "$O/bench_c4.json" 2> "$O/bench_c4.err") ;;
     kt4) (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt4" -o kt -- \
