@@ -704,15 +704,19 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     h->use_side = h->knobs.side_stream;  // A/B switch
     h->chunk_host = h->knobs.chunk_host;
     h->chunk_max = h->knobs.chunk_max;
-    if (hipStreamCreateWithFlags(&h->cpy, hipStreamNonBlocking) != hipSuccess ||
+    // The copy stream at the device's highest priority: a registered batch's
+    // next chunk is read over PCIe by a small kernel on it (k_copy_ranges)
+    // while the merge kernels of the chunk before fill the CUs, and its
+    // workgroups should take the first free slots.
+    int prio_lo = 0, prio_hi = 0;
+    hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    if (hipStreamCreateWithPriority(&h->cpy, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_cstart, hipEventDisableTiming) != hipSuccess)
       rc = DEV_FAIL("");
     for (auto &e : h->ev_chunk)
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = DEV_FAIL("");
     // CRGC_SIDE_PRIO=1: the side stream (the merge's critical path) at the
     // device's highest priority, so its workgroups dispatch first
-    int prio_lo = 0, prio_hi = 0;
-    hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     const int side_prio = h->knobs.side_prio ? prio_hi : 0;
     if (hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, side_prio) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
