@@ -158,7 +158,8 @@ def test_large_host_batches_chunked_and_registered(hip_mod, oracle_mod, monkeypa
     """Host batches of >= 2^19 entries take the merge's host paths (crgc_api.hip
     crgc_merge_entries): a pageable batch is copied and merged in chunks, one
     merge per chunk with its own epoch (merge_entries_chunked); a batch in a
-    buffer registered with crgc_host_register is copied whole.  Both graphs must
+    buffer registered with crgc_host_register too, in up to CRGC_CHUNK_REG
+    chunks read over PCIe by k_copy_ranges (4 here).  Both graphs must
     equal the oracle's after every merge, and their traces too
     (ShadowGraph.java:64-156, 205-289)."""
     from crgc_hip import HostArena
@@ -177,7 +178,7 @@ def test_large_host_batches_chunked_and_registered(hip_mod, oracle_mod, monkeypa
     hr.register_host(arena.buf)
     for b in big:
         hp.merge_entries(b)                # pageable: chunked
-        hr.merge_entries(arena.pack(b))    # registered: whole
+        hr.merge_entries(arena.pack(b))    # registered: chunked, kernel copies
         o.merge_entries(b)
         want = o.export()
         assert hp.export() == want

@@ -242,7 +242,8 @@ struct Knobs {
   bool side_stream = false;      // CRGC_SIDE_STREAM=1: edge pipeline beside the vertex updates
   bool side_prio = false;        // CRGC_SIDE_PRIO=1: that side stream at the highest priority
   bool chunk_host = true;        // CRGC_CHUNK_HOST=0: large pageable host batches in one piece
-  uint32_t chunk_max = 4;        // CRGC_CHUNK_MAX: at most this many chunks (2 .. 4)
+  uint32_t chunk_max = 4;        // CRGC_CHUNK_MAX: at most this many chunks (2 .. 8)
+  uint32_t chunk_reg = 6;        // CRGC_CHUNK_REG: at most this many chunks of a registered batch (2 .. 8)
   uint64_t dev_chunk = 0;        // CRGC_DEV_CHUNK: sub-merge size of large device batches (test hook; 0 = 2^20)
   bool repack_each = false;      // CRGC_REPACK_EACH_MERGE=1: repack the pools before every merge (test hook)
   void read() {
@@ -283,7 +284,8 @@ struct Knobs {
     if (const char *m = env("CRGC_SIDE_STREAM")) side_stream = atoi(m) != 0;
     if (const char *m = env("CRGC_SIDE_PRIO")) side_prio = atoi(m) != 0;
     if (const char *m = env("CRGC_CHUNK_HOST")) chunk_host = atoi(m) != 0;
-    if (const char *m = env("CRGC_CHUNK_MAX")) chunk_max = std::min<uint32_t>(4, std::max(2, atoi(m)));
+    if (const char *m = env("CRGC_CHUNK_MAX")) chunk_max = std::min<uint32_t>(8, std::max(2, atoi(m)));
+    if (const char *m = env("CRGC_CHUNK_REG")) chunk_reg = std::min<uint32_t>(8, std::max(2, atoi(m)));
     if (const char *m = env("CRGC_DEV_CHUNK")) dev_chunk = std::max<uint64_t>(64, strtoull(m, nullptr, 10));
     if (const char *m = env("CRGC_REPACK_EACH_MERGE")) repack_each = atoi(m) != 0;
   }
@@ -321,7 +323,8 @@ struct crgc_graph {
   // it on C2, profiles/r3f/ab_merge.txt)
   bool use_side = false;
   bool chunk_host = true;  // CRGC_CHUNK_HOST=0: large host batches in one piece
-  uint32_t chunk_max = 4;  // CRGC_CHUNK_MAX: at most this many chunks (2 .. 4)
+  uint32_t chunk_max = 4;  // CRGC_CHUNK_MAX: at most this many chunks (2 .. 8)
+  uint32_t chunk_reg = 6;  // CRGC_CHUNK_REG: the same for registered batches (kernel copies: no per-copy cost)
   // last trace
   uint64_t last_garbage = 0, last_kill = 0, last_live = 0;
   crgc_trace_stats last_stats{};
@@ -704,6 +707,7 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     h->use_side = h->knobs.side_stream;  // A/B switch
     h->chunk_host = h->knobs.chunk_host;
     h->chunk_max = h->knobs.chunk_max;
+    h->chunk_reg = h->knobs.chunk_reg;
     // The copy stream at the device's highest priority: a registered batch's
     // next chunk is read over PCIe by a small kernel on it (k_copy_ranges)
     // while the merge kernels of the chunk before fill the CUs, and its
@@ -1315,8 +1319,9 @@ static const char *registered_view(const crgc_graph *h, const void *p) {
   return nullptr;
 }
 
-constexpr uint64_t CHUNK_MIN = 1u << 18;  // entries per chunk at least
-constexpr uint32_t CHUNK_MAX = 4;
+constexpr uint64_t CHUNK_MIN = 1u << 18;      // entries per chunk at least (runtime copies)
+constexpr uint64_t CHUNK_MIN_REG = 1u << 17;  // (kernel copies of a registered batch)
+constexpr uint32_t CHUNK_MAX = 8;
 
 static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint32_t K, bool registered) {
   const uint64_t n = b->n_entries;
@@ -1522,9 +1527,12 @@ int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
         b->created_owner && b->created_target &&
         b->spawned && b->updated_ref && b->updated_info)
       return merge_entries_dev_chunked(h, b);
-    if (b->memory == CRGC_MEM_HOST && b->n_entries >= 2 * CHUNK_MIN && h->chunk_host)
-      return merge_entries_chunked(h, b, (uint32_t)std::min<uint64_t>(h->chunk_max, b->n_entries / CHUNK_MIN),
-                                   host_registered(h, b, C, S, U));
+    if (b->memory == CRGC_MEM_HOST && h->chunk_host) {
+      const bool reg = host_registered(h, b, C, S, U);
+      const uint64_t k = reg ? std::min<uint64_t>(h->chunk_reg, b->n_entries / CHUNK_MIN_REG)
+                             : std::min<uint64_t>(h->chunk_max, b->n_entries / CHUNK_MIN);
+      if (k >= 2) return merge_entries_chunked(h, b, (uint32_t)k, reg);
+    }
     return merge_entries_one(h, b, C, S, U);
   }
   if (h->route && h->G <= ROUTE_MAX_SHARDS && h->F <= ROUTE_MAX_F)
