@@ -382,3 +382,32 @@ def test_c4_shape_eight_shards_closure(sharded, oracle_mod, monkeypatch):
         o.merge_entries(b)
         _same(h.trace(True), o.trace(True))
     assert h.export() == o.export()
+
+
+def test_rebuild_keeps_every_proxy_before_any_trace(sharded, oracle_mod, capfd, monkeypatch):
+    """A sharded load that outgrows its capacity before the first trace: every
+    shard's alive slots are mostly proxies (the far ends of its edges), far more
+    than twice the home shadows it created.  The rebuild must size the new
+    arrays from the alive slots (crgc_api.hip rebuild: counted on the device),
+    not from the homes created since the last trace — round 4's C4 over 8
+    logical shards put 68 M alive slots into 27 M and its passes wrote past the
+    new arrays.  Sets and counts must equal the oracle's."""
+    monkeypatch.setenv("CRGC_LEVEL_LOG", "1")
+    w = world.World(seed=0x5EED + 44)
+    w.bulk_graph(200_000, 2_000_000, alpha=2.1, n_roots=200)
+    h, o = sharded(8, vertex_capacity=4096, edge_capacity=32768), oracle_mod.OracleGraph()
+    for b in w.batches(1 << 13):
+        h.merge_entries(b, split=True)
+        o.merge_entries(b)
+    rh, ro = h.trace(True), o.trace(True)
+    _same(rh, ro)
+    err = capfd.readouterr().err
+    alive = [int(line.split("(alive ")[1].split(")")[0]) for line in err.splitlines()
+             if line.startswith("[crgc] rebuild:")]
+    assert alive, "the load was meant to outgrow the first capacity"
+    assert max(alive) > 100_000  # homes ~25 k per shard: the proxies dominate
+    b = w.wakeup(20_000, busy=18_000, pending=2_000)
+    h.merge_entries(b, split=True)
+    o.merge_entries(b)
+    _same(h.trace(True), o.trace(True))
+    assert h.export() == o.export()

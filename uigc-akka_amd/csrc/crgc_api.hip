@@ -464,12 +464,19 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   HIP_TRY(sync_counters(h));
   if (int rc = device_error(h)) return rc;
   const uint64_t src_top = h->slot_top;
-  // live upper bound: live at the last trace + vertices created since
-  const uint64_t live_ub =
-      std::min<uint64_t>(src_top, h->live + (h->hctr->inserted - h->inserted_at_trace));
+  // The slots the rebuild keeps, counted exactly: every alive slot, proxies of
+  // a sharded graph included.  (Round 4 sized the new arrays from the live
+  // count at the last trace plus the *home* shadows created since —
+  // Counters::inserted is totalActorsSeen — which left out the proxies a
+  // sharded load creates: 68 M alive slots went into 27 M at C4 over 8 logical
+  // shards, and the rebuild's passes wrote past the new arrays.)
+  HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(n_out), 0, 8, h->stream));
+  HIP_TRY(launch_count_alive(h->g.d, src_top, &h->ctr->n_out, h->stream));
+  HIP_TRY(sync_counters(h));
+  const uint64_t live_ub = std::min<uint64_t>(src_top, h->hctr->n_out);
   Caps c = caps_for(std::max<uint64_t>(live_ub, 1), h->etab_used, ids, atoms);
   if (h->knobs.level_log)
-    fprintf(stderr, "[crgc] rebuild: slots %llu (live <= %llu) pool %llu / %llu rpool %llu edge keys %llu / %llu "
+    fprintf(stderr, "[crgc] rebuild: slots %llu (alive %llu) pool %llu / %llu rpool %llu edge keys %llu / %llu "
                     "-> slots %llu pool %llu edge table %llu\n",
             (unsigned long long)src_top, (unsigned long long)live_ub, (unsigned long long)h->pool_top,
             (unsigned long long)h->g.caps.pcap, (unsigned long long)h->rpool_top,

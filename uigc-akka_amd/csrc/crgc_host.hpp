@@ -299,6 +299,7 @@ hipError_t launch_local_roots(const DevGraph &g, uint64_t slot_top, hipStream_t 
 // rebuild: compact `src` (live vertices only, purged edges) into `dst`,
 // whose arrays are freshly allocated and initialised by init_graph_arrays.
 hipError_t launch_init_arrays(const DevGraph &g, hipStream_t s);
+hipError_t launch_count_alive(const DevGraph &src, uint64_t src_top, unsigned long long *out, hipStream_t s);
 hipError_t launch_rebuild(const DevGraph &src, uint64_t src_slot_top, const DevGraph &dst,
                           uint32_t *map, uint32_t *newdeg, uint64_t *offs, void *scan_tmp,
                           hipStream_t s);

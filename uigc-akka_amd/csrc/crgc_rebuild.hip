@@ -29,9 +29,12 @@ __global__ __launch_bounds__(256) void k_rb_vertices(DevGraph src, uint64_t src_
     const uint64_t v = base + lane_id();
     const bool alive = v < src_top && (src.flags[v] & FL_ALIVE);
     const unsigned long long ns = wave_append(&dst.ctr->slot_top, alive);
-    if (v < src_top) map[v] = alive ? (uint32_t)ns : SLOT_NONE;
+    // past the new arrays (the host sized them too small): dropped, so no later
+    // pass indexes a new array with it; the error poisons the handle
+    const bool fits = alive && ns < dst.scap;
+    if (v < src_top) map[v] = fits ? (uint32_t)ns : SLOT_NONE;
     if (!alive) continue;
-    if (ns >= dst.scap) {
+    if (!fits) {
       set_err(dst.ctr, ERR_SLOTS_FULL);
       continue;
     }
@@ -87,6 +90,7 @@ __global__ __launch_bounds__(256) void k_rb_edges(DevGraph src, uint64_t src_top
           const uint32_t t = edge_target(ed);
           if (edge_count(ed) == 0 || !(src.flags[t] & FL_ALIVE)) continue;
           const uint32_t nt = map[t];
+          if (nt == SLOT_NONE) continue;  // a target dropped by an overflow (ERR_SLOTS_FULL is set)
           dst.pool[off + kept] = pack_edge(nt, edge_count(ed));
           atomicAdd(&dst.rnew[nt], 1u);  // in-degree, for the candidate lists
           const uint64_t key = edge_key(ns, nt);
@@ -111,7 +115,7 @@ __global__ __launch_bounds__(256) void k_rb_edges(DevGraph src, uint64_t src_top
         const uint32_t s = src.sup[v];
         uint32_t nsup = SLOT_NONE;
         if (s == SLOT_DEAD) nsup = SLOT_DEAD;
-        else if (s != SLOT_NONE) nsup = (src.flags[s] & FL_ALIVE) ? map[s] : SLOT_DEAD;
+        else if (s != SLOT_NONE) nsup = (src.flags[s] & FL_ALIVE) ? map[s] : SLOT_DEAD;  // (NONE: overflow)
         dst.sup[ns] = nsup;
       }
     }
@@ -299,6 +303,33 @@ hipError_t launch_repack(const DevGraph &g, uint64_t top, uint64_t *pp, uint64_t
   hipLaunchKernelGGL(k_rb_pool_top, dim3(1), dim3(1), 0, s, g.ctr, tp + nb);
   hipLaunchKernelGGL(k_rb_rpool_top, dim3(1), dim3(1), 0, s, g.ctr, tr + nb);
   hipLaunchKernelGGL(k_rp_move, dim3(grid_for(top, 256, 8192)), dim3(256), 0, s, g, top, pp, rp, pool2, rpool2);
+  return hipGetLastError();
+}
+
+// 0. the alive slots a rebuild keeps (homes and proxies), counted exactly: the
+//    host sizes the new arrays from it.
+__global__ __launch_bounds__(256) void k_rb_count_alive(DevGraph src, uint64_t src_top, unsigned long long *out) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256 * 16;
+  uint32_t k = 0;
+  for (uint64_t v = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16; v < src_top; v += stride) {
+    if (v + 16 <= src_top) {
+      const uint4 f = *(const uint4 *)(src.flags + v);
+      const uint32_t w[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) k += __popc(w[j] & 0x01010101u * FL_ALIVE);
+    } else {
+      for (uint64_t u = v; u < src_top; ++u) k += (src.flags[u] & FL_ALIVE) ? 1u : 0u;
+    }
+  }
+  const uint32_t ws = wave_sum(k);
+  if (lane_id() == 0 && ws) atomicAdd(out, (unsigned long long)ws);
+}
+
+hipError_t launch_count_alive(const DevGraph &src, uint64_t src_top, unsigned long long *out, hipStream_t s) {
+  launch_begin();
+  if (src_top == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rb_count_alive, dim3(grid_for((src_top + 15) / 16, 256, 4096)), dim3(256), 0, s, src,
+                     src_top, out);
   return hipGetLastError();
 }
 
