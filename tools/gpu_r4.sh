@@ -10,7 +10,8 @@
 #   rand             tools/rand_probe.hip: random-access ceilings (loads, atomics, CAS, stores)
 #   c4               C4 unsharded on one GPU (1e8 actors / 1e9 edges, the scaling anchor)
 #   kt4              kernel trace of the C4 N = 1 line (load and wakeups)
-#   c4l8 c2l8        C4 / C2 over 8 logical shards on the one GPU (the sharded protocol at full size)
+#   c4l8 c2l8        C4 (at half size: 8 proxy-heavy shards of the full graph need > 288 GB) / C2 over
+#                    8 logical shards on the one GPU (the sharded protocol at scale)
 #   c2rs c4rs        the N>1 bench path itself on one rank (nccl group, RCCL transport, one shard)
 set -euo pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -49,6 +50,7 @@ for step in "$@"; do
           python3 "$ROOT/bench.py" --workload c4 --steps 3 --warmup 1 --no-cpu-baseline --no-pcie \
           > "$O/bench_kt4.json" 2> "$O/bench_kt4.err") ;;
     c4l8) (cd /tmp && CRGC_LEVEL_LOG=1 timeout -k 10 1000 python3 -u "$ROOT/bench.py" --workload c4 --logical-shards 8 \
+          --actors 50000000 --edges 500000000 --batch 5000000 \
           --steps 3 --warmup 1 > "$O/bench_c4l8.json" 2> "$O/bench_c4l8.err") ;;
     c2rs) (cd /tmp && timeout -k 10 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node=1 \
           --master-addr=127.0.0.1 --master-port=29517 "$ROOT/bench.py" --gpus 1 --workload c2 --rehearse-sharded \
