@@ -662,9 +662,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 //                256 ranges of 2^bin_shift slots); a target past its slice's
 //                capacity is stored as a byte at once.  The slice counts go out
 //                at the end.  No staging, no barrier per unit, no global atomic.
-//   k_bin_apply  one workgroup per bin: its slices (16-B loads, the slice
-//                counts in LDS) into an LDS bitmap of the bin's slot range,
-//                then the range's candidate bytes OR-ed with it in 16-B groups.
+//   k_bin_apply  two workgroups per bin, each over half its slices (16-B
+//                loads, the slice counts in LDS) into an LDS bitmap of the
+//                bin's slot range, whose bits become candidate bytes.
 // The line footprint of the open slices is what the place pass pays for: with
 // 2048 workgroups of 4 waves (round 4's first count-then-place form) the
 // ~344k slices' partly written lines did not fit the L2s and left them partly
@@ -881,34 +881,42 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
   expand_bytes_out(g, nb2);
 }
 
+// BIN_SPLIT workgroups per bin, each over every BIN_SPLIT-th slice into a
+// bitmap of its own; the bits become candidate bytes by byte stores (a wave
+// covers 64 consecutive slots: one masked 64-B write), which the bin's other
+// workgroups' stores to the same lines cannot undo.  (One workgroup per bin
+// read-modify-wrote 16-B groups: 168 workgroups on a 256-CU chip, 34 us.)
+constexpr uint32_t BIN_SPLIT = 2;
+
 __global__ __launch_bounds__(BIN_T) void k_bin_apply(DevGraph g, LevelArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t bm[];  // 2^bin_shift bits, then the slice counts
   if (!a.bins || a.bin_mode_w[0] == 0) return;  // level 0 was not binned
-  const uint32_t b = blockIdx.x, tid = threadIdx.x;
+  const uint32_t b = blockIdx.x / BIN_SPLIT, h = blockIdx.x % BIN_SPLIT, tid = threadIdx.x;
   const uint32_t span = 1u << a.bin_shift, words = span / 32;
   const uint32_t G = a.bin_grid, SC = a.bin_slice, S4 = SC / 4;
+  const uint32_t NS = (G - h + BIN_SPLIT - 1) / BIN_SPLIT;  // this workgroup's slices: w = h + BIN_SPLIT k
   uint32_t *cnt = bm + words;
   for (uint32_t k = tid; k < words; k += BIN_T) bm[k] = 0;
-  for (uint32_t k = tid; k < G; k += BIN_T) cnt[k] = a.bin_cnt[(uint64_t)b * G + k];
+  for (uint32_t k = tid; k < NS; k += BIN_T) cnt[k] = a.bin_cnt[(uint64_t)b * G + h + BIN_SPLIT * k];
   __syncthreads();
   uint32_t nb2 = 0;
-  // the bin's G slices, four at a time per wave (their counts from LDS: the
-  // loop bounds are wave-uniform), each slice's filled part in 16-B groups
+  // its slices, four at a time per wave (their counts from LDS: the loop
+  // bounds are wave-uniform), each slice's filled part in 16-B groups
   const uint4 *src = (const uint4 *)(a.bins + (uint64_t)b * G * SC);
   const uint32_t base = b << a.bin_shift;
-  for (uint32_t w0 = (uint32_t)(tid >> 6); w0 < G; w0 += BIN_NW * 4) {
+  for (uint32_t k0 = (uint32_t)(tid >> 6); k0 < NS; k0 += BIN_NW * 4) {
     uint32_t n[4], mx = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint32_t w = w0 + j * BIN_NW;
-      n[j] = w < G ? cnt[w] : 0u;
+      const uint32_t k = k0 + j * BIN_NW;
+      n[j] = k < NS ? cnt[k] : 0u;
       mx = max(mx, n[j]);
     }
     for (uint32_t i = (uint32_t)lane_id() * 4; i - (uint32_t)lane_id() * 4 < mx; i += 256) {
       uint4 v4[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        v4[j] = i < n[j] ? src[(uint64_t)(w0 + j * BIN_NW) * S4 + i / 4] : make_uint4(0, 0, 0, 0);
+        v4[j] = i < n[j] ? src[(uint64_t)(h + BIN_SPLIT * (k0 + j * BIN_NW)) * S4 + i / 4] : make_uint4(0, 0, 0, 0);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t v[4] = {v4[j].x, v4[j].y, v4[j].z, v4[j].w};
@@ -926,21 +934,16 @@ __global__ __launch_bounds__(BIN_T) void k_bin_apply(DevGraph g, LevelArgs a) {
   uint8_t *Fn = g.front[1];
   const uint64_t lo = (uint64_t)b << a.bin_shift;
   const uint64_t top = g.ctr->slot_top;
-  const uint64_t hi = min(lo + span, (top + 15) & ~15ull);  // Fn holds scap >= this (a multiple of 2048)
-  for (uint64_t q = lo + (uint64_t)tid * 16; q < hi; q += BIN_T * 16) {
+  const uint64_t hi = min(lo + span, top);
+  for (uint64_t q = lo + tid; q < hi; q += BIN_T) {
     const uint32_t rel = (uint32_t)(q - lo);
-    const uint32_t bits = (bm[rel >> 5] >> (rel & 31)) & 0xFFFFu;
-    if (!bits) continue;
-    uint4 v = *(const uint4 *)(Fn + q);
-    uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if ((bits >> j) & 1u) w[j >> 2] |= 1u << (8 * (j & 3));
-    *(uint4 *)(Fn + q) = make_uint4(w[0], w[1], w[2], w[3]);
-    nb2 += 64;  // 16 B read + 16 B written
+    if ((bm[rel >> 5] >> (rel & 31)) & 1u) {
+      Fn[q] = 1;
+      nb2 += 2;
+    }
   }
   const uint32_t ws = wave_sum(nb2);
-  if (lane_id() == 0 && ws) atomicAdd((unsigned long long *)&g.xbytes[b], (unsigned long long)(ws / 2));
+  if (lane_id() == 0 && ws) atomicAdd((unsigned long long *)&g.xbytes[blockIdx.x], (unsigned long long)(ws / 2));
 }
 
 // ---------------------------------------------------------------------------
@@ -1363,7 +1366,7 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
     // together as its expand
     hipExtLaunchKernelGGL(k_bin_place, dim3(a.bin_grid), dim3(BIN_T), (size_t)a.nbins * BIN_R * 8, s, e[4],
                           nullptr, 0, g, a);
-    hipExtLaunchKernelGGL(k_bin_apply, dim3(a.nbins), dim3(BIN_T),
+    hipExtLaunchKernelGGL(k_bin_apply, dim3(a.nbins * BIN_SPLIT), dim3(BIN_T),
                           (size_t)(1u << a.bin_shift) / 8 + (size_t)a.bin_grid * 4, s, nullptr, e[5], 0, g, a);
     return hipGetLastError();
   }
