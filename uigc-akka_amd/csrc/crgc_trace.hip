@@ -693,26 +693,41 @@ constexpr uint32_t BIN_GRP = 16;  // a group: 64 B of a slice, flushed by one la
 // eviction racing), always with the same value at the same position; nobody
 // waits on another wave.
 __device__ inline void bin_try_flush(unsigned long long *ring, uint32_t *slice, uint32_t g0) {
+  // (entries are read as whole 8-B words, the unit a writer exchanges)
   const uint32_t s0 = g0 % BIN_R;
-  const uint4 *w4 = (const uint4 *)(ring + s0);  // two entries per 16 B: {target, position + 1} x 2
   for (int attempt = 0; attempt < 4; ++attempt) {
     bool all = true;
 #pragma unroll 1
-    for (uint32_t q = 0; q < BIN_GRP / 2 && all; q += 2) {
-      const uint4 x = w4[q], y = w4[q + 1];
-      all = x.y == g0 + 2 * q + 1 && x.w == g0 + 2 * q + 2 && y.y == g0 + 2 * q + 3 && y.w == g0 + 2 * q + 4;
+    for (uint32_t q = 0; q < BIN_GRP && all; q += 4) {
+      const unsigned long long e0 = ring[s0 + q], e1 = ring[s0 + q + 1], e2 = ring[s0 + q + 2],
+                               e3 = ring[s0 + q + 3];
+      const uint32_t p = g0 + q + 1;
+      all = (uint32_t)(e0 >> 32) == p && (uint32_t)(e1 >> 32) == p + 1 && (uint32_t)(e2 >> 32) == p + 2 &&
+            (uint32_t)(e3 >> 32) == p + 3;
     }
     if (all) {
       uint4 *dst = (uint4 *)(slice + g0);  // g0 % 16 == 0 and slices start 16-B aligned
 #pragma unroll 1
-      for (uint32_t q = 0; q < BIN_GRP / 4; ++q) {
-        const uint4 x = w4[2 * q], y = w4[2 * q + 1];
-        dst[q] = make_uint4(x.x, x.z, y.x, y.z);
-        const uint32_t p0 = g0 + 4 * q + 1;  // cleared unless a later lap took the slot
-        atomicCAS(&ring[s0 + 4 * q], ((unsigned long long)p0 << 32) | x.x, 0ull);
-        atomicCAS(&ring[s0 + 4 * q + 1], ((unsigned long long)(p0 + 1) << 32) | x.z, 0ull);
-        atomicCAS(&ring[s0 + 4 * q + 2], ((unsigned long long)(p0 + 2) << 32) | y.x, 0ull);
-        atomicCAS(&ring[s0 + 4 * q + 3], ((unsigned long long)(p0 + 3) << 32) | y.z, 0ull);
+      for (uint32_t q = 0; q < BIN_GRP; q += 4) {
+        // Read again: a writer one lap later may have exchanged a slot out
+        // since the check (it then stored that entry itself).  Only entries
+        // still tagged with their position are ours to store; a quad with all
+        // four goes out as one 16-B store.
+        const unsigned long long e[4] = {ring[s0 + q], ring[s0 + q + 1], ring[s0 + q + 2], ring[s0 + q + 3]};
+        const uint32_t p = g0 + q + 1;
+        bool m[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) m[k] = (uint32_t)(e[k] >> 32) == p + k;
+        if (m[0] && m[1] && m[2] && m[3]) {
+          dst[q / 4] = make_uint4((uint32_t)e[0], (uint32_t)e[1], (uint32_t)e[2], (uint32_t)e[3]);
+        } else {
+#pragma unroll
+          for (uint32_t k = 0; k < 4; ++k)
+            if (m[k]) slice[g0 + q + k] = (uint32_t)e[k];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)  // cleared unless a later lap took the slot
+          if (m[k]) atomicCAS(&ring[s0 + q + k], e[k], 0ull);
       }
       return;
     }
@@ -727,7 +742,7 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
   __shared__ uint32_t s_off[BIN_NW][64];
   __shared__ uint32_t s_ulist[BIN_T], s_utag[BIN_T], s_wcnt[BIN_NW], s_nact;
   __shared__ uint32_t lc[BIN_MAX];  // the next position of each bin's slice of this workgroup
-  extern __shared__ unsigned long long st[];  // [nbins x BIN_R] staging rings (binned only)
+  extern __shared__ __attribute__((aligned(16))) unsigned long long st[];  // [nbins x BIN_R] staging rings (binned only)
   Counters *c = g.ctr;
   const bool binned = !c->tail_state && bin_mode(c, a);
   // k_bin_apply runs after this kernel (stream order) and reads the word
