@@ -671,6 +671,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 // written, and a count pass + scan sized the slices exactly (level 0: 60 + 15
 // + 131 + 28 us, profiles/r4d); 512 workgroups of 16 waves keep the same waves
 // with a quarter of the slices, and fixed-capacity slices need no count pass.
+// Staging the targets in per-bin LDS rings and storing whole 64-B groups
+// (a lock-free ring: exchange, group flush by the last position's lane,
+// eviction, final flush) was correct but slower, 150 -> 220 us: the 8-B LDS
+// exchanges and flush checks cost more than the stores they combined
+// (profiles/r4i).
 // Used only when the level-0 frontier is >= 1/32 of the slots (the place pass
 // derives it and sets the mode word for k_bin_apply; not binned, it stores the
 // bytes at once).
@@ -681,68 +686,13 @@ __device__ inline bool bin_mode(const Counters *c, const LevelArgs &a) {
 
 constexpr int BIN_T = 1024;  // threads of a k_bin_place / k_bin_apply workgroup
 constexpr int BIN_NW = BIN_T / 64;
-constexpr uint32_t BIN_R = 32;    // LDS staging slots per bin (two groups of BIN_GRP)
-constexpr uint32_t BIN_GRP = 16;  // a group: 64 B of a slice, flushed by one lane in 4 16-B stores
 
-// A staged target is (position + 1) << 32 | target in its bin's ring of BIN_R
-// slots (position mod BIN_R).  Every staged entry reaches its slice exactly
-// as stored, by one of: the group flush (the lane that took a group's last
-// position finds all BIN_GRP entries there, bounded retries), an eviction (a
-// writer one lap later exchanges it out and stores it alone), or the final
-// flush after the walk.  An entry can be stored twice (a flush and an
-// eviction racing), always with the same value at the same position; nobody
-// waits on another wave.
-__device__ inline void bin_try_flush(unsigned long long *ring, uint32_t *slice, uint32_t g0) {
-  // (entries are read as whole 8-B words, the unit a writer exchanges)
-  const uint32_t s0 = g0 % BIN_R;
-  for (int attempt = 0; attempt < 4; ++attempt) {
-    bool all = true;
-#pragma unroll 1
-    for (uint32_t q = 0; q < BIN_GRP && all; q += 4) {
-      const unsigned long long e0 = ring[s0 + q], e1 = ring[s0 + q + 1], e2 = ring[s0 + q + 2],
-                               e3 = ring[s0 + q + 3];
-      const uint32_t p = g0 + q + 1;
-      all = (uint32_t)(e0 >> 32) == p && (uint32_t)(e1 >> 32) == p + 1 && (uint32_t)(e2 >> 32) == p + 2 &&
-            (uint32_t)(e3 >> 32) == p + 3;
-    }
-    if (all) {
-      uint4 *dst = (uint4 *)(slice + g0);  // g0 % 16 == 0 and slices start 16-B aligned
-#pragma unroll 1
-      for (uint32_t q = 0; q < BIN_GRP; q += 4) {
-        // Read again: a writer one lap later may have exchanged a slot out
-        // since the check (it then stored that entry itself).  Only entries
-        // still tagged with their position are ours to store; a quad with all
-        // four goes out as one 16-B store.
-        const unsigned long long e[4] = {ring[s0 + q], ring[s0 + q + 1], ring[s0 + q + 2], ring[s0 + q + 3]};
-        const uint32_t p = g0 + q + 1;
-        bool m[4];
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) m[k] = (uint32_t)(e[k] >> 32) == p + k;
-        if (m[0] && m[1] && m[2] && m[3]) {
-          dst[q / 4] = make_uint4((uint32_t)e[0], (uint32_t)e[1], (uint32_t)e[2], (uint32_t)e[3]);
-        } else {
-#pragma unroll
-          for (uint32_t k = 0; k < 4; ++k)
-            if (m[k]) slice[g0 + q + k] = (uint32_t)e[k];
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k)  // cleared unless a later lap took the slot
-          if (m[k]) atomicCAS(&ring[s0 + q + k], e[k], 0ull);
-      }
-      return;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  // left in LDS: evicted one by one by the next lap, or stored by the final flush
-}
-
-__global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_bin_place(DevGraph g, LevelArgs a) {
+__global__ __launch_bounds__(BIN_T) void k_bin_place(DevGraph g, LevelArgs a) {
   constexpr int U = EXPAND_U;
   __shared__ uint32_t s_start[BIN_NW][65];
   __shared__ uint32_t s_off[BIN_NW][64];
   __shared__ uint32_t s_ulist[BIN_T], s_utag[BIN_T], s_wcnt[BIN_NW], s_nact;
   __shared__ uint32_t lc[BIN_MAX];  // the next position of each bin's slice of this workgroup
-  extern __shared__ __attribute__((aligned(16))) unsigned long long st[];  // [nbins x BIN_R] staging rings (binned only)
   Counters *c = g.ctr;
   const bool binned = !c->tail_state && bin_mode(c, a);
   // k_bin_apply runs after this kernel (stream order) and reads the word
@@ -758,46 +708,28 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
   const uint64_t nh = min(c->qh[0], (unsigned long long)g.qh_cap);
   const uint64_t nunits = ncid + nh;
   uint32_t nb2 = 0;
-  if (binned) {
+  if (binned)
     for (uint32_t k = tid; k < NB; k += BIN_T) lc[k] = 0;
-    for (uint32_t k = tid; k < NB * BIN_R; k += BIN_T) st[k] = 0;
-  }
   __syncthreads();
 
-  // A target into its bin's staging ring; returns a group-flush request
-  // (1 + (bin << 20 | first position / 16)) when it took a group's last position.
-  auto put = [&](uint32_t t) -> uint32_t {
+  auto put = [&](uint32_t t) {
     if (!binned) {
       Fn[t] = 1;
-      return 0;
+      return;
     }
     const uint32_t b = t >> a.bin_shift;
     const uint32_t pos = b < NB ? atomicAdd(&lc[b], 1u) : SC;  // (a slot past the bins: never, slot_top is synced)
-    if (pos >= SC) {
+    if (pos < SC) {
+      a.bins[((uint64_t)b * G + wg) * SC + pos] = t;
+      nb2 += 8;
+    } else {
       Fn[t] = 1;  // past the slice: the byte at once
-      return 0;
     }
-    nb2 += 8;
-    const unsigned long long old = atomicExch(&st[b * BIN_R + pos % BIN_R], ((unsigned long long)(pos + 1) << 32) | t);
-    if (old)  // an older lap's entry, unflushed: stored alone
-      a.bins[((uint64_t)b * G + wg) * SC + (uint32_t)(old >> 32) - 1] = (uint32_t)old;
-    return pos % BIN_GRP == BIN_GRP - 1 ? 1 + ((b << 20) | (pos / BIN_GRP)) : 0;
   };
-  static_assert(EXPAND_U == 4, "the loop below names four edges");
   auto edges = [&](const uint64_t (&ed)[U]) {
-    // one put / flush site, the edges in turn (unrolled, the four inlined
-    // copies held 88 VGPRs: 5 waves per SIMD instead of 8)
-#pragma unroll 1
-    for (int u = 0; u < U; ++u) {
-      const uint64_t e = u == 0 ? ed[0] : u == 1 ? ed[1] : u == 2 ? ed[2] : ed[3];
-      if (edge_count(e) > 0) {
-        const uint32_t r = put(edge_target(e));
-        if (r) {
-          const uint32_t b = (r - 1) >> 20, g0 = ((r - 1) & 0xFFFFFu) * BIN_GRP;
-          bin_try_flush(st + b * BIN_R, a.bins + ((uint64_t)b * G + wg) * SC, g0);
-        }
-      }
-    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (edge_count(ed[u]) > 0) put(edge_target(ed[u]));
   };
   auto unit = [&](uint64_t un, uint32_t tag) {
     if (un < ncid) {  // light ranges: chunk (block b, k-th 64)
@@ -884,15 +816,8 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     for (uint32_t r = wv; r < nact; r += BIN_NW) unit((ub + s_ulist[r]) * G + wg, s_utag[r]);
     __syncthreads();  // s_ulist is rewritten by the next window
   }
-  if (binned) {
-    // the final flush: what no group flush or eviction took (consecutive slots
-    // of a ring are consecutive positions of one slice: coalesced stores)
-    for (uint32_t k = tid; k < NB * BIN_R; k += BIN_T) {
-      const unsigned long long e = st[k];
-      if (e) a.bins[((uint64_t)(k / BIN_R) * G + wg) * SC + (uint32_t)(e >> 32) - 1] = (uint32_t)e;
-    }
+  if (binned)
     for (uint32_t k = tid; k < NB; k += BIN_T) a.bin_cnt[(uint64_t)k * G + wg] = min(lc[k], SC);
-  }
   expand_bytes_out(g, nb2);
 }
 
@@ -1379,8 +1304,7 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
   if (roots && a.nbins) {
     // the pseudo-root level, binned when it is wide: place and apply, timed
     // together as its expand
-    hipExtLaunchKernelGGL(k_bin_place, dim3(a.bin_grid), dim3(BIN_T), (size_t)a.nbins * BIN_R * 8, s, e[4],
-                          nullptr, 0, g, a);
+    hipExtLaunchKernelGGL(k_bin_place, dim3(a.bin_grid), dim3(BIN_T), 0, s, e[4], nullptr, 0, g, a);
     hipExtLaunchKernelGGL(k_bin_apply, dim3(a.nbins * BIN_SPLIT), dim3(BIN_T),
                           (size_t)(1u << a.bin_shift) / 8 + (size_t)a.bin_grid * 4, s, nullptr, e[5], 0, g, a);
     return hipGetLastError();
