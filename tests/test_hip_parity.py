@@ -378,3 +378,18 @@ def test_device_sub_merges_and_pool_repacks(hip_mod, oracle_mod, monkeypatch, se
         _same_trace(rh, ro)
         fz.sync(o.export())
     assert h.total_actors_seen() == o.total_actors_seen()
+
+
+def test_failure_detail_names_the_call(hip_mod):
+    """A status code says what failed, crgc_last_error_detail() where: a graph
+    whose slot capacity cannot be allocated fails with CRGC_E_NOMEM, and the
+    exception carries the call site and the HIP status (crgc_api.hip map_hip_at);
+    the next successful call clears it."""
+    from crgc_hip import abi
+    with pytest.raises(abi.CrgcError) as ei:
+        hip_mod.ShadowGraph(vertex_capacity=1 << 40, edge_capacity=1 << 20)
+    assert ei.value.code == abi.E_NOMEM
+    assert "crgc_api.hip:" in ei.value.detail and "hipErrorOutOfMemory" in ei.value.detail
+    g = hip_mod.ShadowGraph(vertex_capacity=1024, edge_capacity=4096)
+    g.trace(True)
+    assert abi.last_error_detail() == ""
