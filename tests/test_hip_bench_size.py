@@ -159,7 +159,7 @@ def test_large_host_batches_chunked_and_registered(hip_mod, oracle_mod, monkeypa
     crgc_merge_entries): a pageable batch is copied and merged in chunks, one
     merge per chunk with its own epoch (merge_entries_chunked); a batch in a
     buffer registered with crgc_host_register too, in up to CRGC_CHUNK_REG
-    chunks read over PCIe by k_copy_ranges (4 here).  Both graphs must
+    chunks read over PCIe by k_copy_ranges (2 here).  Both graphs must
     equal the oracle's after every merge, and their traces too
     (ShadowGraph.java:64-156, 205-289)."""
     from crgc_hip import HostArena

@@ -243,7 +243,7 @@ struct Knobs {
   bool side_prio = false;        // CRGC_SIDE_PRIO=1: that side stream at the highest priority
   bool chunk_host = true;        // CRGC_CHUNK_HOST=0: large pageable host batches in one piece
   uint32_t chunk_max = 4;        // CRGC_CHUNK_MAX: at most this many chunks (2 .. 8)
-  uint32_t chunk_reg = 6;        // CRGC_CHUNK_REG: at most this many chunks of a registered batch (2 .. 8)
+  uint32_t chunk_reg = 4;        // CRGC_CHUNK_REG: at most this many chunks of a registered batch (2 .. 8)
   uint64_t dev_chunk = 0;        // CRGC_DEV_CHUNK: sub-merge size of large device batches (test hook; 0 = 2^20)
   bool repack_each = false;      // CRGC_REPACK_EACH_MERGE=1: repack the pools before every merge (test hook)
   void read() {
@@ -324,7 +324,7 @@ struct crgc_graph {
   bool use_side = false;
   bool chunk_host = true;  // CRGC_CHUNK_HOST=0: large host batches in one piece
   uint32_t chunk_max = 4;  // CRGC_CHUNK_MAX: at most this many chunks (2 .. 8)
-  uint32_t chunk_reg = 6;  // CRGC_CHUNK_REG: the same for registered batches (kernel copies: no per-copy cost)
+  uint32_t chunk_reg = 4;  // CRGC_CHUNK_REG: the same for registered batches (kernel copies: no per-copy cost)
   // last trace
   uint64_t last_garbage = 0, last_kill = 0, last_live = 0;
   crgc_trace_stats last_stats{};
@@ -715,13 +715,12 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     h->chunk_host = h->knobs.chunk_host;
     h->chunk_max = h->knobs.chunk_max;
     h->chunk_reg = h->knobs.chunk_reg;
-    // The copy stream at the device's highest priority: a registered batch's
-    // next chunk is read over PCIe by a small kernel on it (k_copy_ranges)
-    // while the merge kernels of the chunk before fill the CUs, and its
-    // workgroups should take the first free slots.
+    // (The copy stream at the highest priority, with registered batches in up
+    // to 6 chunks, made the registered merge call slower, 1.19 -> 1.47 ms:
+    // profiles/r4j.  Each chunk is a whole merge with its fixed costs.)
     int prio_lo = 0, prio_hi = 0;
     hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    if (hipStreamCreateWithPriority(&h->cpy, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+    if (hipStreamCreateWithFlags(&h->cpy, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_cstart, hipEventDisableTiming) != hipSuccess)
       rc = DEV_FAIL("");
     for (auto &e : h->ev_chunk)
@@ -1327,7 +1326,7 @@ static const char *registered_view(const crgc_graph *h, const void *p) {
 }
 
 constexpr uint64_t CHUNK_MIN = 1u << 18;      // entries per chunk at least (runtime copies)
-constexpr uint64_t CHUNK_MIN_REG = 1u << 17;  // (kernel copies of a registered batch)
+constexpr uint64_t CHUNK_MIN_REG = 1u << 18;  // (kernel copies of a registered batch)
 constexpr uint32_t CHUNK_MAX = 8;
 
 static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint32_t K, bool registered) {
