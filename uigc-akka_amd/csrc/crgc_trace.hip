@@ -688,7 +688,7 @@ constexpr int BIN_T = 1024;  // threads of a k_bin_place / k_bin_apply workgroup
 constexpr int BIN_NW = BIN_T / 64;
 
 __global__ __launch_bounds__(BIN_T) void k_bin_place(DevGraph g, LevelArgs a) {
-  constexpr int U = EXPAND_U;
+  constexpr int U = 2 * EXPAND_U;  // 8 edge loads in flight per lane (vs 4: level 0 -4 %, profiles/r4k)
   __shared__ uint32_t s_start[BIN_NW][65];
   __shared__ uint32_t s_off[BIN_NW][64];
   __shared__ uint32_t s_ulist[BIN_T], s_utag[BIN_T], s_wcnt[BIN_NW], s_nact;
