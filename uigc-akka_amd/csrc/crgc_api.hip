@@ -1480,18 +1480,16 @@ static int merge_entries_dev_chunked(crgc_graph *h, const crgc_entry_batch *b) {
   const uint64_t CH = h->knobs.dev_chunk ? h->knobs.dev_chunk : DEV_CHUNK;
   const uint64_t K = (n + CH - 1) / CH;
   std::vector<uint32_t> bo(3 * (K + 1));
-  for (uint64_t j = 0; j <= K; ++j) {
-    const uint64_t at = std::min(n, j * CH);
-    HIP_TRY(hipMemcpyAsync(&bo[3 * j], b->created_off + at, 4, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipMemcpyAsync(&bo[3 * j + 1], b->spawned_off + at, 4, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipMemcpyAsync(&bo[3 * j + 2], b->updated_off + at, 4, hipMemcpyDeviceToHost, h->stream));
-  }
-  HIP_TRY(hsync(h));
-  if (bo[0] || bo[1] || bo[2]) return CRGC_E_INVAL;
-  if (h->x_chunk.ensure(Carver::need({(CH + 1) * 4, (CH + 1) * 4, (CH + 1) * 4})) != hipSuccess)
+  if (h->x_chunk.ensure(Carver::need({(CH + 1) * 4, (CH + 1) * 4, (CH + 1) * 4, 3 * (K + 1) * 4})) != hipSuccess)
     return CRGC_E_NOMEM;
   Carver cv(h->x_chunk.ptr);
   uint32_t *co = cv.take<uint32_t>(CH + 1), *so = cv.take<uint32_t>(CH + 1), *uo = cv.take<uint32_t>(CH + 1);
+  uint32_t *dbo = cv.take<uint32_t>(3 * (K + 1));
+  // the boundaries' offsets in one gather and one copy
+  HIP_TRY(launch_bounds(b->created_off, b->spawned_off, b->updated_off, n, CH, K, dbo, h->stream));
+  HIP_TRY(hipMemcpyAsync(bo.data(), dbo, bo.size() * 4, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hsync(h));
+  if (bo[0] || bo[1] || bo[2]) return CRGC_E_INVAL;
   for (uint64_t j = 0; j < K; ++j) {
     const uint64_t lo = j * CH, hi = std::min(n, lo + CH), m = hi - lo;
     const uint32_t c0 = bo[3 * j], s0 = bo[3 * j + 1], u0 = bo[3 * j + 2];
@@ -1499,10 +1497,8 @@ static int merge_entries_dev_chunked(crgc_graph *h, const crgc_entry_batch *b) {
     if (c1 < c0 || s1 < s0 || u1 < u0 || c1 - c0 > m * h->F || s1 - s0 > m * h->F || u1 - u0 > m * h->F)
       return CRGC_E_INVAL;  // offsets run backwards or past F per entry: refused (chunks before it merged)
     // (stream order: the previous chunk's kernels have read these buffers)
-    HIP_TRY(hipMemcpyAsync(co, b->created_off + lo, (m + 1) * 4, hipMemcpyDeviceToDevice, h->stream));
-    HIP_TRY(hipMemcpyAsync(so, b->spawned_off + lo, (m + 1) * 4, hipMemcpyDeviceToDevice, h->stream));
-    HIP_TRY(hipMemcpyAsync(uo, b->updated_off + lo, (m + 1) * 4, hipMemcpyDeviceToDevice, h->stream));
-    HIP_TRY(launch_rebase(co, so, uo, m + 1, c0, s0, u0, h->stream));
+    HIP_TRY(launch_rebase_copy(b->created_off + lo, b->spawned_off + lo, b->updated_off + lo, co, so, uo, m + 1, c0,
+                               s0, u0, h->stream));
     crgc_entry_batch v{};
     v.n_entries = m;
     v.self = b->self + lo;

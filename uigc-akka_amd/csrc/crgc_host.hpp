@@ -224,6 +224,11 @@ struct HostCopy {
   int n;
 };
 hipError_t launch_copy_ranges(const HostCopy &c, hipStream_t s);
+hipError_t launch_bounds(const uint32_t *c_off, const uint32_t *s_off, const uint32_t *u_off, uint64_t n,
+                         uint64_t ch, uint64_t k, uint32_t *out, hipStream_t s);
+hipError_t launch_rebase_copy(const uint32_t *c_src, const uint32_t *s_src, const uint32_t *u_src, uint32_t *c_off,
+                              uint32_t *s_off, uint32_t *u_off, uint64_t n, uint32_t c0, uint32_t s0, uint32_t u0,
+                              hipStream_t s);
 hipError_t launch_rebase(uint32_t *c_off, uint32_t *s_off, uint32_t *u_off, uint64_t n, uint32_t c0, uint32_t s0,
                          uint32_t u0, hipStream_t s);
 hipError_t launch_undo_check(const DevGraph &g, const UndoArgs &a, hipStream_t s);

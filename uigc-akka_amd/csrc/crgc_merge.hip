@@ -534,6 +534,48 @@ __global__ __launch_bounds__(256) void k_rebase(uint32_t *c_off, uint32_t *s_off
   u_off[i] -= u0;
 }
 
+// A large device batch's sub-merge boundaries: the three record offsets at
+// every multiple of `ch` (and at n), gathered for one device-to-host copy.
+__global__ __launch_bounds__(256) void k_bounds(const uint32_t *c_off, const uint32_t *s_off,
+                                                const uint32_t *u_off, uint64_t n, uint64_t ch, uint64_t k,
+                                                uint32_t *out) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j > k) return;
+  const uint64_t at = min(n, j * ch);
+  out[3 * j] = c_off[at];
+  out[3 * j + 1] = s_off[at];
+  out[3 * j + 2] = u_off[at];
+}
+
+hipError_t launch_bounds(const uint32_t *c_off, const uint32_t *s_off, const uint32_t *u_off, uint64_t n,
+                         uint64_t ch, uint64_t k, uint32_t *out, hipStream_t s) {
+  launch_begin();
+  hipLaunchKernelGGL(k_bounds, dim3((k + 1 + 255) / 256), dim3(256), 0, s, c_off, s_off, u_off, n, ch, k, out);
+  return hipGetLastError();
+}
+
+// A sub-merge's offset arrays, copied and rebased in one pass.
+__global__ __launch_bounds__(256) void k_rebase_copy(const uint32_t *c_src, const uint32_t *s_src,
+                                                     const uint32_t *u_src, uint32_t *c_off, uint32_t *s_off,
+                                                     uint32_t *u_off, uint64_t n, uint32_t c0, uint32_t s0,
+                                                     uint32_t u0) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  c_off[i] = c_src[i] - c0;
+  s_off[i] = s_src[i] - s0;
+  u_off[i] = u_src[i] - u0;
+}
+
+hipError_t launch_rebase_copy(const uint32_t *c_src, const uint32_t *s_src, const uint32_t *u_src, uint32_t *c_off,
+                              uint32_t *s_off, uint32_t *u_off, uint64_t n, uint32_t c0, uint32_t s0, uint32_t u0,
+                              hipStream_t s) {
+  launch_begin();
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rebase_copy, dim3((n + 255) / 256), dim3(256), 0, s, c_src, s_src, u_src, c_off, s_off, u_off,
+                     n, c0, s0, u0);
+  return hipGetLastError();
+}
+
 hipError_t launch_rebase(uint32_t *c_off, uint32_t *s_off, uint32_t *u_off, uint64_t n, uint32_t c0, uint32_t s0,
                          uint32_t u0, hipStream_t s) {
   launch_begin();
