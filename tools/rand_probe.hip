@@ -6,7 +6,7 @@
 // HBM bytes.  This probe measures that rate on the box for the access forms
 // the kernels use (loads, no-return and returning atomics, CAS, stores, a
 // dependent pair), over tables of 128 MB (inside the Infinity Cache), 1 GB
-// (the C2 id table) and 4 GB.  Built here (tools/_build/rand_probe), run on
+// (the C2 id table), 4 GB and 32 GB (the C4 edge table).  Built here (tools/_build/rand_probe), run on
 // the GPU box by tools/gpu_r4.sh step `rand`; one line per (form, table).
 // Nothing here is product code.
 #include <hip/hip_runtime.h>
@@ -95,7 +95,9 @@ static float run(uint64_t *tab, uint64_t entries, uint32_t rounds, uint64_t *sin
 }
 
 int main() {
-  const uint64_t sizes_mb[3] = {128, 1024, 4096};
+  // 128 MB: inside the Infinity Cache; 1 GB: the C2 id table; 4 GB: the C2
+  // edge table; 32 GB: the C4 edge table and pool (TLB reach)
+  const uint64_t sizes_mb[4] = {128, 1024, 4096, 32768};
   const uint32_t rounds = 16;
   const double ops = 4096.0 * 256 * rounds * IN_FLIGHT;
   uint64_t *sink = nullptr;
