@@ -3,4 +3,4 @@
 # and the N > 1 code path rehearsed on one rank (nccl group, RCCL transport) at C2.
 set -euo pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
-bash "$ROOT/tools/gpu_r4.sh" "$1" c2 c4 c2rs
+bash "$ROOT/tools/gpu_r4.sh" "$1" rand c2 c4 c2rs
