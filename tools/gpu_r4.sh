@@ -9,6 +9,7 @@
 #   probe            tools/hip_probe.hip: HIP last-error / event / pointer-range semantics
 #   rand             tools/rand_probe.hip: random-access ceilings (loads, atomics, CAS, stores)
 #   c4               C4 unsharded on one GPU (1e8 actors / 1e9 edges, the scaling anchor)
+#   c4q              the C4 line without the OpenMP leg (no set comparison)
 #   kt4              kernel trace of the C4 N = 1 line (load and wakeups)
 #   c4l8 c2l8        C4 (at half size: 8 proxy-heavy shards of the full graph need > 288 GB) / C2 over
 #                    8 logical shards on the one GPU (the sharded protocol at scale)
@@ -46,6 +47,8 @@ for step in "$@"; do
     rand) (cd "$ROOT" && timeout -k 10 120 ./tools/_build/rand_probe > "$O/rand_probe.txt" 2>&1) ;;
     c4) (cd /tmp && CRGC_LEVEL_LOG=1 timeout -k 10 1000 python3 -u "$ROOT/bench.py" --workload c4 --steps 5 \
           --warmup 2 --no-pcie > "$O/bench_c4.json" 2> "$O/bench_c4.err") ;;
+    c4q) (cd /tmp && timeout -k 10 900 python3 -u "$ROOT/bench.py" --workload c4 --steps 5 --warmup 2 --no-pcie \
+          --no-cpu-baseline > "$O/bench_c4q.json" 2> "$O/bench_c4q.err") ;;
     kt4) (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt4" -o kt -- \
           python3 "$ROOT/bench.py" --workload c4 --steps 3 --warmup 1 --no-cpu-baseline --no-pcie \
           > "$O/bench_kt4.json" 2> "$O/bench_kt4.err") ;;

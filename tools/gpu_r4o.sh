@@ -10,3 +10,4 @@ mkdir -p "$O"
 tail -1 "$O/wsort_tests.log"
 bash "$ROOT/tools/gpu_ab2.sh" "$1/ab" - uigc-akka_amd/lib/ab/wsort.so uigc-akka_amd/lib/ab/wg256.so \
   uigc-akka_amd/lib/ab/wg1024.so
+bash "$ROOT/tools/gpu_r4.sh" "$1" c4q
