@@ -245,6 +245,7 @@ struct Knobs {
   uint32_t chunk_max = 4;        // CRGC_CHUNK_MAX: at most this many chunks (2 .. 8)
   uint32_t chunk_reg = 4;        // CRGC_CHUNK_REG: at most this many chunks of a registered batch (2 .. 8)
   uint64_t dev_chunk = 0;        // CRGC_DEV_CHUNK: sub-merge size of large device batches (test hook; 0 = 2^20)
+  uint32_t spin_us = SPIN_US_DEFAULT;  // CRGC_SPIN_US: host waits poll this long before blocking (0: block at once)
   bool repack_each = false;      // CRGC_REPACK_EACH_MERGE=1: repack the pools before every merge (test hook)
   void read() {
     auto env = [](const char *k) { return getenv(k); };
@@ -287,6 +288,7 @@ struct Knobs {
     if (const char *m = env("CRGC_CHUNK_MAX")) chunk_max = std::min<uint32_t>(8, std::max(2, atoi(m)));
     if (const char *m = env("CRGC_CHUNK_REG")) chunk_reg = std::min<uint32_t>(8, std::max(2, atoi(m)));
     if (const char *m = env("CRGC_DEV_CHUNK")) dev_chunk = std::max<uint64_t>(64, strtoull(m, nullptr, 10));
+    if (const char *m = env("CRGC_SPIN_US")) spin_us = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_REPACK_EACH_MERGE")) repack_each = atoi(m) != 0;
   }
 };
@@ -417,7 +419,7 @@ struct DeviceGuard {
 // communicator reports an asynchronous error (a failed peer), and the handle
 // is poisoned, instead of blocking forever in a collective.
 hipError_t hsync(crgc_graph *h) {
-  if (!h->tp) return hipStreamSynchronize(h->stream);
+  if (!h->tp) return stream_wait(h->stream, h->knobs.spin_us);
   const int rc = h->tp->wait(h->stream);
   if (rc == CRGC_OK) return hipSuccess;
   h->poisoned = true;
@@ -639,7 +641,7 @@ struct Staged {
   hipError_t wait() {
     if (!armed) return hipSuccess;
     armed = false;
-    return recorded ? hipEventSynchronize(h->ev[3]) : hipStreamSynchronize(h->stream);
+    return recorded ? event_wait(h->ev[3], h->knobs.spin_us) : stream_wait(h->stream, h->knobs.spin_us);
   }
   ~Staged() { wait(); }
   Staged(const Staged &) = delete;
@@ -1434,7 +1436,7 @@ static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint3
     rc = merge_entries_one(h, &v, q.c1 - q.c0, q.s1 - q.s0, q.u1 - q.u0);
   }
   // the caller's buffers are read only during the call
-  const hipError_t e = hipStreamSynchronize(h->cpy);
+  const hipError_t e = stream_wait(h->cpy, h->knobs.spin_us);
   if (rc == CRGC_OK && e != hipSuccess) rc = map_hip(e);
   return rc;
 }

@@ -656,12 +656,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 // holds: the edge stream takes ~22 us, the random byte stores ~215 us (C2,
 // profiles/r3g/lv1).  Binned, the stores become sequential.
 //   k_bin_place  one walk over the level's units (light chunks, hub pieces) by
-//                BIN_WG workgroups of 16 waves; each target goes to the next
-//                position of its (bin, workgroup) slice — a fixed-capacity
-//                piece of the region, bin-major — from an LDS cursor (nbins <=
-//                256 ranges of 2^bin_shift slots); a target past its slice's
+//                BIN_WG workgroups of 16 waves; each wave sorts a window of its
+//                targets by bin in LDS, reserves each bin's run in its
+//                (bin, workgroup) slice — a fixed-capacity piece of the region,
+//                bin-major — from an LDS cursor (nbins <= 256 ranges of
+//                2^bin_shift slots), and stores the runs from consecutive lanes
+//                (r4o: level 0 138 -> 133 us); a target past its slice's
 //                capacity is stored as a byte at once.  The slice counts go out
-//                at the end.  No staging, no barrier per unit, no global atomic.
+//                at the end.  No barrier per unit, no global atomic.
 //   k_bin_apply  two workgroups per bin, each over half its slices (16-B
 //                loads, the slice counts in LDS) into an LDS bitmap of the
 //                bin's slot range, whose bits become candidate bytes.
@@ -687,12 +689,16 @@ __device__ inline bool bin_mode(const Counters *c, const LevelArgs &a) {
 constexpr int BIN_T = 1024;  // threads of a k_bin_place / k_bin_apply workgroup
 constexpr int BIN_NW = BIN_T / 64;
 
-__global__ __launch_bounds__(BIN_T) void k_bin_place(DevGraph g, LevelArgs a) {
-  constexpr int U = 2 * EXPAND_U;  // 8 edge loads in flight per lane (vs 4: level 0 -4 %, profiles/r4k)
+__global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_bin_place(DevGraph g, LevelArgs a) {
+  constexpr int U = EXPAND_U;  // (8 edge loads per lane did not pay with the sorted stores' registers)
   __shared__ uint32_t s_start[BIN_NW][65];
   __shared__ uint32_t s_off[BIN_NW][64];
   __shared__ uint32_t s_ulist[BIN_T], s_utag[BIN_T], s_wcnt[BIN_NW], s_nact;
   __shared__ uint32_t lc[BIN_MAX];  // the next position of each bin's slice of this workgroup
+  // per wave: a bin table (counts, then prefixes, then slice-position offsets)
+  // and the window's targets sorted by bin
+  __shared__ uint32_t s_wa[BIN_NW][BIN_MAX], s_wb[BIN_NW][BIN_MAX];
+  __shared__ uint32_t s_ws[BIN_NW][64 * U];
   Counters *c = g.ctr;
   const bool binned = !c->tail_state && bin_mode(c, a);
   // k_bin_apply runs after this kernel (stream order) and reads the word
@@ -726,10 +732,61 @@ __global__ __launch_bounds__(BIN_T) void k_bin_place(DevGraph g, LevelArgs a) {
       Fn[t] = 1;  // past the slice: the byte at once
     }
   };
+  // A window of the wave's targets (64 U), binned: counted per bin in the
+  // wave's table, a slice range reserved per (wave, bin) at once, the targets
+  // sorted by bin in LDS, then stored by consecutive lanes in sorted order, so
+  // a bin's run of targets goes out as consecutive addresses of its slice
+  // (one memory request per run instead of one per target).
   auto edges = [&](const uint64_t (&ed)[U]) {
+    if (!binned) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (edge_count(ed[u]) > 0) put(edge_target(ed[u]));
+      return;
+    }
+    uint32_t *A = s_wa[wv], *S = s_ws[wv];
+    for (uint32_t k = lane; k < NB; k += 64) A[k] = 0;
+    wave_lds_fence();
+    uint32_t t[U], r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      t[u] = edge_target(ed[u]);
+      const uint32_t b = t[u] >> a.bin_shift;
+      r[u] = 0xFFFFFFFFu;
+      if (edge_count(ed[u]) > 0) {
+        if (b < NB) r[u] = atomicAdd(&A[b], 1u);
+        else Fn[t[u]] = 1;  // (a slot past the bins: never, slot_top is synced)
+      }
+    }
+    wave_lds_fence();
+    uint32_t *B = s_wb[wv], run = 0;
+    for (uint32_t k0 = 0; k0 < NB; k0 += 64) {  // A: counts -> prefixes; B: slice position - prefix
+      const uint32_t k = k0 + lane;
+      const uint32_t cnt = k < NB ? A[k] : 0u;
+      const uint32_t incl = wave_incl_scan(cnt);
+      const uint32_t pre = run + incl - cnt;
+      if (k < NB) {
+        B[k] = (cnt ? atomicAdd(&lc[k], cnt) : 0u) - pre;
+        A[k] = pre;
+      }
+      run += __shfl(incl, 63);
+    }
+    wave_lds_fence();
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (edge_count(ed[u]) > 0) put(edge_target(ed[u]));
+      if (r[u] != 0xFFFFFFFFu) S[A[t[u] >> a.bin_shift] + r[u]] = t[u];
+    wave_lds_fence();
+    for (uint32_t i = lane; i < run; i += 64) {
+      const uint32_t tt = S[i], b = tt >> a.bin_shift;
+      const uint32_t pos = B[b] + i;  // slice position = reservation + rank = B + sorted index
+      if (pos < SC) {
+        a.bins[((uint64_t)b * G + wg) * SC + pos] = tt;
+        nb2 += 8;
+      } else {
+        Fn[tt] = 1;  // past the slice: the byte at once
+      }
+    }
+    wave_lds_fence();  // the table and the sorted window are reused by the next window
   };
   auto unit = [&](uint64_t un, uint32_t tag) {
     if (un < ncid) {  // light ranges: chunk (block b, k-th 64)

@@ -36,21 +36,21 @@ int LocalTransport::barrier() {
 
 int LocalTransport::allgather(uint32_t shard, const void *send, void *recv, size_t bytes,
                               hipStream_t s) {
-  if (hipStreamSynchronize(s) != hipSuccess) return DEV_FAIL("transport");  // send is complete
+  if (stream_wait(s) != hipSuccess) return DEV_FAIL("transport");  // send is complete
   post[shard].ptr = send;
   if (int rc = barrier()) return rc;
   for (uint32_t r = 0; r < n_shards; ++r)
     if (bytes && hipMemcpyAsync((char *)recv + (size_t)r * bytes, post[r].ptr, bytes, hipMemcpyDefault,
                                 s) != hipSuccess)
       return DEV_FAIL("transport");
-  if (hipStreamSynchronize(s) != hipSuccess) return DEV_FAIL("transport");
+  if (stream_wait(s) != hipSuccess) return DEV_FAIL("transport");
   return barrier();  // nobody reuses its send buffer before every peer has copied it
 }
 
 int LocalTransport::alltoallv(uint32_t shard, const void *send, const size_t *soff, const size_t *sbytes,
                               void *recv, const size_t *roff, const size_t *rbytes, hipStream_t s) {
   (void)sbytes;
-  if (hipStreamSynchronize(s) != hipSuccess) return DEV_FAIL("transport");
+  if (stream_wait(s) != hipSuccess) return DEV_FAIL("transport");
   post[shard].ptr = send;
   post[shard].soff = soff;
   if (int rc = barrier()) return rc;
@@ -60,7 +60,7 @@ int LocalTransport::alltoallv(uint32_t shard, const void *send, const size_t *so
     if (hipMemcpyAsync((char *)recv + roff[r], src, rbytes[r], hipMemcpyDefault, s) != hipSuccess)
       return DEV_FAIL("transport");
   }
-  if (hipStreamSynchronize(s) != hipSuccess) return DEV_FAIL("transport");
+  if (stream_wait(s) != hipSuccess) return DEV_FAIL("transport");
   return barrier();
 }
 

@@ -23,6 +23,8 @@
 #include <cstdint>
 #include <mutex>
 
+#include "crgc_internal.hpp"
+
 struct crgc_transport {
   uint32_t n_shards = 1;
   virtual ~crgc_transport() = default;
@@ -37,7 +39,7 @@ struct crgc_transport {
   // Host wait for the graph's stream.  RCCL: bounded, and ended early by the
   // communicator's asynchronous error, so a failed or hung peer cannot block
   // this rank forever (crgc_xpost.hpp).
-  virtual int wait(hipStream_t s) { return hipStreamSynchronize(s) == hipSuccess ? 0 : -3; }
+  virtual int wait(hipStream_t s) { return crgc::stream_wait(s) == hipSuccess ? 0 : -3; }
 };
 
 namespace crgc {
