@@ -287,7 +287,10 @@ struct Knobs {
     if (const char *m = env("CRGC_CHUNK_HOST")) chunk_host = atoi(m) != 0;
     if (const char *m = env("CRGC_CHUNK_MAX")) chunk_max = std::min<uint32_t>(8, std::max(2, atoi(m)));
     if (const char *m = env("CRGC_CHUNK_REG")) chunk_reg = std::min<uint32_t>(8, std::max(2, atoi(m)));
-    if (const char *m = env("CRGC_DEV_CHUNK")) dev_chunk = std::max<uint64_t>(64, strtoull(m, nullptr, 10));
+    if (const char *m = env("CRGC_DEV_CHUNK")) {  // 0: the default
+      dev_chunk = strtoull(m, nullptr, 10);
+      if (dev_chunk) dev_chunk = std::max<uint64_t>(64, dev_chunk);
+    }
     if (const char *m = env("CRGC_SPIN_US")) spin_us = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_REPACK_EACH_MERGE")) repack_each = atoi(m) != 0;
   }
