@@ -1492,8 +1492,14 @@ static int merge_entries_dev_chunked(crgc_graph *h, const crgc_entry_batch *b) {
   uint32_t *dbo = cv.take<uint32_t>(3 * (K + 1));
   // the boundaries' offsets in one gather and one copy
   HIP_TRY(launch_bounds(b->created_off, b->spawned_off, b->updated_off, n, CH, K, dbo, h->stream));
-  HIP_TRY(hipMemcpyAsync(bo.data(), dbo, bo.size() * 4, hipMemcpyDeviceToHost, h->stream));
+  // into the pinned staging words when they fit (a copy into pageable memory is
+  // staged and waited for inside the runtime, where our polling cannot reach)
+  const size_t small = 8 * (size_t)MAX_SHARDS * (MAX_SHARDS + 8);
+  const bool pinned = bo.size() * 4 <= small;
+  void *dst = pinned ? (void *)h->h_small : (void *)bo.data();
+  HIP_TRY(hipMemcpyAsync(dst, dbo, bo.size() * 4, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hsync(h));
+  if (pinned) memcpy(bo.data(), h->h_small, bo.size() * 4);
   if (bo[0] || bo[1] || bo[2]) return CRGC_E_INVAL;
   for (uint64_t j = 0; j < K; ++j) {
     const uint64_t lo = j * CH, hi = std::min(n, lo + CH), m = hi - lo;
