@@ -911,9 +911,13 @@ static int ag_u64(crgc_graph *h, std::initializer_list<std::pair<const void *, u
     h->poisoned = true;
     return rc;
   }
-  HIP_TRY(hipMemcpyAsync(h->h_small, rcv, bytes * h->G, hipMemcpyDeviceToHost, h->stream));
+  // the pinned staging words hold 8 * MAX_SHARDS * (MAX_SHARDS + 8) bytes; a
+  // larger gather (K = 2 + 4G at G > 47) lands in `out` directly
+  const bool staged = bytes * h->G <= 8 * (size_t)MAX_SHARDS * (MAX_SHARDS + 8);
+  HIP_TRY(hipMemcpyAsync(staged ? (void *)h->h_small : (void *)out, rcv, bytes * h->G, hipMemcpyDeviceToHost,
+                         h->stream));
   HIP_TRY(hsync(h));
-  memcpy(out, h->h_small, bytes * h->G);
+  if (staged) memcpy(out, h->h_small, bytes * h->G);
   return CRGC_OK;
 }
 
@@ -1035,6 +1039,20 @@ extern "C" {
 
 // Validates an entry batch and learns its record counts (exact for host
 // batches; for device batches too when `exact`, by reading the last offsets).
+// Small device-to-host reads go through the handle's pinned staging words when
+// they fit: a copy into pageable memory is staged and waited for inside the
+// runtime, on its blocking wait (not our polling one, crgc_internal.hpp).
+// `off` keeps a read clear of the words an all-gather in flight uses.
+constexpr size_t SMALL_BYTES = 8 * (size_t)MAX_SHARDS * (MAX_SHARDS + 8);
+constexpr size_t SMALL_XFLAG_OFF = SMALL_BYTES / 2;
+static hipError_t d2h_small(crgc_graph *h, void *dst, const void *src, size_t bytes, size_t off = 0) {
+  void *to = off + bytes <= SMALL_BYTES ? (void *)((char *)h->h_small + off) : dst;
+  return hipMemcpyAsync(to, src, bytes, hipMemcpyDeviceToHost, h->stream);
+}
+static void d2h_small_done(crgc_graph *h, void *dst, size_t bytes, size_t off = 0) {
+  if (off + bytes <= SMALL_BYTES) memcpy(dst, (char *)h->h_small + off, bytes);
+}
+
 static int entry_counts(crgc_graph *h, const crgc_entry_batch *b, bool exact, uint64_t *C, uint64_t *S,
                         uint64_t *U) {
   if (!b || b->memory > CRGC_MEM_DEVICE) return CRGC_E_INVAL;
@@ -1494,12 +1512,9 @@ static int merge_entries_dev_chunked(crgc_graph *h, const crgc_entry_batch *b) {
   HIP_TRY(launch_bounds(b->created_off, b->spawned_off, b->updated_off, n, CH, K, dbo, h->stream));
   // into the pinned staging words when they fit (a copy into pageable memory is
   // staged and waited for inside the runtime, where our polling cannot reach)
-  const size_t small = 8 * (size_t)MAX_SHARDS * (MAX_SHARDS + 8);
-  const bool pinned = bo.size() * 4 <= small;
-  void *dst = pinned ? (void *)h->h_small : (void *)bo.data();
-  HIP_TRY(hipMemcpyAsync(dst, dbo, bo.size() * 4, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(d2h_small(h, bo.data(), dbo, bo.size() * 4));
   HIP_TRY(hsync(h));
-  if (pinned) memcpy(bo.data(), h->h_small, bo.size() * 4);
+  d2h_small_done(h, bo.data(), bo.size() * 4);
   if (bo[0] || bo[1] || bo[2]) return CRGC_E_INVAL;
   for (uint64_t j = 0; j < K; ++j) {
     const uint64_t lo = j * CH, hi = std::min(n, lo + CH), m = hi - lo;
@@ -1830,8 +1845,9 @@ static int run_chains(crgc_graph *h, bool investigate, uint64_t top) {
       }
     }
     HIP_TRY(launch_chain(g, ca, 2, nullptr, nullptr, top, 2 * R, 0, 0, h->stream));
-    HIP_TRY(hipMemcpyAsync(fl.data(), ca.flag, fl.size() * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(d2h_small(h, fl.data(), ca.flag, fl.size() * 4));
     HIP_TRY(hsync(h));
+    d2h_small_done(h, fl.data(), fl.size() * 4);
     bool any = false;
     for (uint32_t f : fl)
       if (f) {
@@ -2234,8 +2250,9 @@ static int xclosure(crgc_graph *h, bool investigate, const XRecv &xr, uint64_t *
       }
     }
     HIP_TRY(launch_xclosure(g, x, 3, nullptr, nullptr, 0, 0, 0, h->stream));
-    HIP_TRY(hipMemcpyAsync(fl.data(), x.flag, (size_t)nflag * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(d2h_small(h, fl.data(), x.flag, (size_t)nflag * 4, SMALL_XFLAG_OFF));
     if (int rc = ag_u64(h, {{x.xl_n, 1}}, cnt.data())) return rc;  // synchronises
+    d2h_small_done(h, fl.data(), (size_t)nflag * 4, SMALL_XFLAG_OFF);
     if (fl[0]) {
       h->poisoned = true;
       return DEV_FAIL("");  // a proxy without a resolved home slot: the resolution step failed
