@@ -5,6 +5,7 @@
 #   tests[:-k expr]  pytest -m gpu (optionally -k)        smoke   __graft_entry__.smoke()
 #   c2 c1 c3 c5      bench.py lines                        levels  C2 level log (CRGC_LEVEL_LOG)
 #   kt               rocprofv3 --kernel-trace --stats of the timed C2 wakeups only (--no-pcie)
+#   ktp              the same with the PCIe-inclusive wakeups (pageable, then registered host batches) at the end
 #   pmc              FETCH_SIZE and WRITE_SIZE passes of the same command, one run each
 #   probe            tools/hip_probe.hip: HIP last-error / event / pointer-range semantics
 #   rand             tools/rand_probe.hip: random-access ceilings (loads, atomics, CAS, stores)
@@ -39,6 +40,8 @@ for step in "$@"; do
     levels) (cd /tmp && CRGC_LEVEL_LOG=1 CRGC_KERNEL_TIMING=2 timeout -k 10 420 $B > "$O/levels.json" 2> "$O/levels.err") ;;
     kt) (cd /tmp && timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o kt -- $B \
           > "$O/bench_kt.json" 2> "$O/bench_kt.err") ;;
+    ktp) (cd /tmp && timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ktp" -o kt -- \
+          python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$O/bench_ktp.json" 2> "$O/bench_ktp.err") ;;
     pmc) (cd /tmp && timeout -k 10 420 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o pmc -- $B \
             > "$O/bench_fetch.json" 2> "$O/bench_fetch.err" &&
           timeout -k 10 420 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o pmc -- $B \
