@@ -154,16 +154,18 @@ def test_c3_chains_eight_shards(hip_mod, oracle_mod):
         g.close()
 
 
-def test_large_host_batches_chunked_and_registered(hip_mod, oracle_mod, monkeypatch):
+@pytest.mark.parametrize("reg_chunks", ["1", "2"])
+def test_large_host_batches_chunked_and_registered(hip_mod, oracle_mod, monkeypatch, reg_chunks):
     """Host batches of >= 2^19 entries take the merge's host paths (crgc_api.hip
     crgc_merge_entries): a pageable batch is copied and merged in chunks, one
     merge per chunk with its own epoch (merge_entries_chunked); a batch in a
-    buffer registered with crgc_host_register too, in up to CRGC_CHUNK_REG
-    chunks read over PCIe by k_copy_ranges (2 here).  Both graphs must
+    buffer registered with crgc_host_register is read over PCIe by
+    k_copy_ranges, in one piece (the default) or in CRGC_CHUNK_REG = 2 chunks.  Both graphs must
     equal the oracle's after every merge, and their traces too
     (ShadowGraph.java:64-156, 205-289)."""
     from crgc_hip import HostArena
     monkeypatch.setenv("CRGC_BIN_MIN_SLOTS", "0")  # and the pseudo-root level binned at this size
+    monkeypatch.setenv("CRGC_CHUNK_REG", reg_chunks)
     w = world.World(seed=0x5EED + 7)
     w.bulk_graph(200_000, 2_000_000)
     hp, hr, o = hip_mod.ShadowGraph(), hip_mod.ShadowGraph(), oracle_mod.OracleGraph()
@@ -178,7 +180,7 @@ def test_large_host_batches_chunked_and_registered(hip_mod, oracle_mod, monkeypa
     hr.register_host(arena.buf)
     for b in big:
         hp.merge_entries(b)                # pageable: chunked
-        hr.merge_entries(arena.pack(b))    # registered: chunked, kernel copies
+        hr.merge_entries(arena.pack(b))    # registered: kernel copies
         o.merge_entries(b)
         want = o.export()
         assert hp.export() == want

@@ -243,7 +243,7 @@ struct Knobs {
   bool side_prio = false;        // CRGC_SIDE_PRIO=1: that side stream at the highest priority
   bool chunk_host = true;        // CRGC_CHUNK_HOST=0: large pageable host batches in one piece
   uint32_t chunk_max = 4;        // CRGC_CHUNK_MAX: at most this many chunks (2 .. 8)
-  uint32_t chunk_reg = 4;        // CRGC_CHUNK_REG: at most this many chunks of a registered batch (2 .. 8)
+  uint32_t chunk_reg = 1;        // CRGC_CHUNK_REG: at most this many chunks of a registered batch (1 .. 8)
   uint64_t dev_chunk = 0;        // CRGC_DEV_CHUNK: sub-merge size of large device batches (test hook; 0 = 2^20)
   uint32_t spin_us = SPIN_US_DEFAULT;  // CRGC_SPIN_US: host waits poll this long before blocking (0: block at once)
   bool repack_each = false;      // CRGC_REPACK_EACH_MERGE=1: repack the pools before every merge (test hook)
@@ -286,7 +286,7 @@ struct Knobs {
     if (const char *m = env("CRGC_SIDE_PRIO")) side_prio = atoi(m) != 0;
     if (const char *m = env("CRGC_CHUNK_HOST")) chunk_host = atoi(m) != 0;
     if (const char *m = env("CRGC_CHUNK_MAX")) chunk_max = std::min<uint32_t>(8, std::max(2, atoi(m)));
-    if (const char *m = env("CRGC_CHUNK_REG")) chunk_reg = std::min<uint32_t>(8, std::max(2, atoi(m)));
+    if (const char *m = env("CRGC_CHUNK_REG")) chunk_reg = std::min<uint32_t>(8, std::max(1, atoi(m)));
     if (const char *m = env("CRGC_DEV_CHUNK")) {  // 0: the default
       dev_chunk = strtoull(m, nullptr, 10);
       if (dev_chunk) dev_chunk = std::max<uint64_t>(64, dev_chunk);
@@ -329,7 +329,7 @@ struct crgc_graph {
   bool use_side = false;
   bool chunk_host = true;  // CRGC_CHUNK_HOST=0: large host batches in one piece
   uint32_t chunk_max = 4;  // CRGC_CHUNK_MAX: at most this many chunks (2 .. 8)
-  uint32_t chunk_reg = 4;  // CRGC_CHUNK_REG: the same for registered batches (kernel copies: no per-copy cost)
+  uint32_t chunk_reg = 1;  // CRGC_CHUNK_REG: the same for registered batches (kernel copies; 1: one piece)
   // last trace
   uint64_t last_garbage = 0, last_kill = 0, last_live = 0;
   crgc_trace_stats last_stats{};
@@ -1559,6 +1559,12 @@ int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
       const bool reg = host_registered(h, b, C, S, U);
       const uint64_t k = reg ? std::min<uint64_t>(h->chunk_reg, b->n_entries / CHUNK_MIN_REG)
                              : std::min<uint64_t>(h->chunk_max, b->n_entries / CHUNK_MIN);
+      // A registered batch of >= CHUNK_MIN_REG entries is read over PCIe by
+      // k_copy_ranges in one piece and merged once: merge kernels running beside
+      // a PCIe-reading copy slow down 5-25x (profiles/r4ab), so overlapping
+      // chunks bought nothing (C2 registered wakeup 2.20 ms in one piece, 2.30
+      // in 3 chunks, interleaved on one box, profiles/r4ae)
+      if (reg && b->n_entries >= CHUNK_MIN_REG) return merge_entries_chunked(h, b, (uint32_t)std::max<uint64_t>(k, 1), true);
       if (k >= 2) return merge_entries_chunked(h, b, (uint32_t)k, reg);
     }
     return merge_entries_one(h, b, C, S, U);

@@ -591,6 +591,9 @@ hipError_t launch_rebase(uint32_t *c_off, uint32_t *s_off, uint32_t *u_off, uint
 // (profiles/r3g/pcie_probe.txt), so the chunks are copied by this kernel
 // instead.  Source and destination share their alignment mod 16 (the caller
 // places the destination so): the body moves in 16-B groups, the ends by byte.
+constexpr int COPY_IN_FLIGHT = 8;
+constexpr int COPY_WG = 32;
+
 __global__ __launch_bounds__(256) void k_copy_ranges(HostCopy c) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   const uint64_t tid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -603,7 +606,19 @@ __global__ __launch_bounds__(256) void k_copy_ranges(HostCopy c) {
     if (tid < head) d[tid] = s[tid];
     const uint4 *s4 = (const uint4 *)(s + head);
     uint4 *d4 = (uint4 *)(d + head);
-    for (uint64_t i = tid; i < body / 16; i += stride) d4[i] = s4[i];
+    // COPY_IN_FLIGHT 16-B reads per lane issued before any store: a few
+    // workgroups keep the link full (the latency is ~2 us), so the merge
+    // kernels running beside the copy keep their CUs (see launch_copy_ranges)
+    const uint64_t n4 = body / 16;
+    uint64_t i = tid;
+    for (; i + (COPY_IN_FLIGHT - 1) * stride < n4; i += COPY_IN_FLIGHT * stride) {
+      uint4 v[COPY_IN_FLIGHT];
+#pragma unroll
+      for (int k = 0; k < COPY_IN_FLIGHT; ++k) v[k] = s4[i + k * stride];
+#pragma unroll
+      for (int k = 0; k < COPY_IN_FLIGHT; ++k) d4[i + k * stride] = v[k];
+    }
+    for (; i < n4; i += stride) d4[i] = s4[i];
     const uint64_t tail = len - head - body;
     if (tid < tail) d[head + body + tid] = s[head + body + tid];
   }
@@ -614,8 +629,12 @@ hipError_t launch_copy_ranges(const HostCopy &c, hipStream_t s) {
   uint64_t tot = 0;
   for (int r = 0; r < c.n; ++r) tot += c.bytes[r];
   if (!tot) return hipSuccess;
-  // enough 16-B requests in flight to fill the link, few CUs taken from the merge
-  hipLaunchKernelGGL(k_copy_ranges, dim3(grid_for(tot / 16, 256, 128)), dim3(256), 0, s, c);
+  // enough 16-B requests in flight to fill the link (32 x 256 lanes x 8 x 16 B =
+  // 1 MiB), few CUs taken from the merge: with 128 workgroups of one read per
+  // lane, the merge kernels beside the copy ran 5-25x slower (k_rebase 134 us
+  // against 5, profiles/r4ab) — their waves queued behind PCIe reads on the
+  // copy's CUs
+  hipLaunchKernelGGL(k_copy_ranges, dim3(grid_for(tot / 16, 256, COPY_WG)), dim3(256), 0, s, c);
   return hipGetLastError();
 }
 
