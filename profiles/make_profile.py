@@ -1,4 +1,4 @@
-"""Collect one GPU measurement directory (tools/gpu_r3.sh output) into profiles/<tag>/.
+"""Collect one GPU measurement directory (tools/gpu_run.sh output) into profiles/<tag>/.
 
 usage: python profiles/make_profile.py gpurun_out/<run> profiles/<tag> [--pmc-latest]
 
@@ -57,7 +57,7 @@ def main():
             kernels = json.loads(out.strip().splitlines()[-1])
             doc = {"source": f"{dst}/c2_pmc_steady.txt (rocprofv3 --pmc FETCH_SIZE, then WRITE_SIZE, separate "
                              "runs of bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-pcie; dispatches of "
-                             "the 4 timed wakeups; tools/gpu_r4.sh pmc)",
+                             "the 4 timed wakeups; tools/gpu_run.sh pmc)",
                    "calibration": "profiles/r2d/calib_summary.txt (tools/calib_pmc.hip): FETCH_SIZE = 0.50 x "
                                   "bytes for 16-B and 8-B/lane streaming reads, 48-64 B per random 1-B read "
                                   "(line granularity), ~0 for L2-resident random 4-B probes",

@@ -35,12 +35,30 @@ def test_bench_refuses_a_world_size_other_than_gpus():
     assert p.returncode == 2 and "world size 1 != --gpus 2" in p.stderr
 
 
-def test_eight_gpu_default_is_c4_strong_scaling():
-    """--gpus N > 1 quotes BASELINE's C4: one 1e8-actor / 1e9-edge graph sharded
-    over the N ranks (strong scaling), every producer on exactly one rank."""
-    p = _run(["--gpus", "8", "--dry-run", "--steps", "1", "--warmup", "0"])
+def _dry(args):
+    p = _run(args + ["--dry-run", "--steps", "1", "--warmup", "0"])
     assert p.returncode == 0, p.stderr[-2000:]
-    out = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")][0]
-    assert out["config"]["edges"] == 1_000_000_000 and out["config"]["actors"] == 100_000_000
-    assert out["config"]["workload"].startswith("C4") and out["scaling"] == "strong"
-    assert sorted(k for ks in out["producers"] for k in ks) == list(range(8))
+    return [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")][0]
+
+
+def test_default_curve_is_one_workload():
+    """The driver's --gpus 1/2/4/8 lines quote one workload: C2 per rank (at
+    N > 1 the ranks' nodes as one hash-sharded graph), weak scaling, and the
+    config block differs only in `parallelism` (VERDICT r4 weak #7)."""
+    one, eight = _dry(["--gpus", "1"]), _dry(["--gpus", "8"])
+    assert one["scaling"] == eight["scaling"] == "weak"
+    assert one["config"]["workload"].startswith("C2")
+    assert {k: v for k, v in one["config"].items() if k != "parallelism"} == \
+        {k: v for k, v in eight["config"].items() if k != "parallelism"}
+    assert eight["config"]["parallelism"].startswith("hash-sharded x8")
+
+
+def test_c4_curve_config_is_the_same_at_every_n():
+    """--workload c4: one 1e8-actor / 1e9-edge graph at every N (strong
+    scaling), every producer on exactly one rank, one config block."""
+    one, eight = _dry(["--gpus", "1", "--workload", "c4"]), _dry(["--gpus", "8", "--workload", "c4"])
+    for out in (one, eight):
+        assert out["config"]["edges"] == 1_000_000_000 and out["config"]["actors"] == 100_000_000
+        assert out["config"]["workload"].startswith("C4") and out["scaling"] == "strong"
+    assert one["config"]["workload"] == eight["config"]["workload"]
+    assert sorted(k for ks in eight["producers"] for k in ks) == list(range(8))

@@ -380,6 +380,38 @@ def test_device_sub_merges_and_pool_repacks(hip_mod, oracle_mod, monkeypatch, se
     assert h.total_actors_seen() == o.total_actors_seen()
 
 
+def test_device_sub_merge_bad_later_boundary_refused_whole(hip_mod, oracle_mod, monkeypatch):
+    """a large device batch whose created offsets run backwards at a
+    later sub-merge boundary is refused whole (CRGC_E_INVAL) before any
+    sub-merge runs — the graph is unchanged and stays usable, as for a host
+    batch — instead of being refused after the earlier chunks merged."""
+    from crgc_hip.batch import EntryBatch
+    monkeypatch.setenv("CRGC_DEV_CHUNK", "300")
+    h, o = _pair(hip_mod, oracle_mod)
+    fz = fuzz.Fuzz(41)
+    eb = fz.entries(2000)
+    h.merge_entries(eb.to_device())
+    o.merge_entries(eb)
+    fz.sync(o.export())
+    before = h.export()
+    assert before == o.export()
+    bad = fz.entries(700)
+    co = bad.created_off.copy()
+    co[600] = co[700] + 1        # chunk [600, 700) runs backwards; chunk [300, 600) stays legal
+    assert co[600] - co[300] <= 300 * 4
+    nb = EntryBatch(bad.self, bad.recv_count, bad.flags, co, bad.created_owner, bad.created_target,
+                    bad.spawned_off, bad.spawned, bad.updated_off, bad.updated_ref, bad.updated_info)
+    with pytest.raises(abi.CrgcError) as ei:
+        h.merge_entries(nb.to_device())
+    assert ei.value.code == abi.E_INVAL
+    assert h.export() == before   # nothing merged, not poisoned
+    good = fz.entries(700)
+    h.merge_entries(good.to_device())
+    o.merge_entries(good)
+    assert h.export() == o.export()
+    _same_trace(h.trace(True), o.trace(True))
+
+
 def test_failure_detail_names_the_call(hip_mod):
     """A status code says what failed, crgc_last_error_detail() where: a graph
     whose slot capacity cannot be allocated fails with CRGC_E_NOMEM, and the

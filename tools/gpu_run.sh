@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-4 GPU driver (run through gpurun from the repo root):
-#   bash tools/gpu_r4.sh <tag> <steps...>
+# GPU driver (run through gpurun from the repo root):
+#   bash tools/gpu_run.sh <tag> <steps...>
 # steps (each under its own time limit, chained: the first failure ends the call):
 #   tests[:-k expr]  pytest -m gpu (optionally -k)        smoke   __graft_entry__.smoke()
 #   c2 c1 c3 c5      bench.py lines                        levels  C2 level log (CRGC_LEVEL_LOG)
@@ -15,6 +15,8 @@
 #   c4l8 c2l8        C4 (at half size: 8 proxy-heavy shards of the full graph need > 288 GB) / C2 over
 #                    8 logical shards on the one GPU (the sharded protocol at scale)
 #   c2rs c4rs        the N>1 bench path itself on one rank (nccl group, RCCL transport, one shard)
+#   ktl8             kernel trace of c4l8 (every shard's kernels, one process)
+#   long             C2 over 200 wakeups: the steady state, rebuilds / repacks amortized in
 set -euo pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1; shift
@@ -66,6 +68,12 @@ for step in "$@"; do
           --steps 3 --warmup 1 --no-pcie --no-cpu-baseline > "$O/bench_c4rs.json" 2> "$O/bench_c4rs.err") ;;
     c2l8) (cd /tmp && timeout -k 10 600 python3 -u "$ROOT/bench.py" --workload c2 --logical-shards 8 \
           --steps 5 --warmup 2 > "$O/bench_c2l8.json" 2> "$O/bench_c2l8.err") ;;
+    ktl8) (cd /tmp && timeout -k 10 1000 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ktl8" -o kt -- \
+          python3 -u "$ROOT/bench.py" --workload c4 --logical-shards 8 \
+          --actors 50000000 --edges 500000000 --batch 5000000 --no-cpu-baseline \
+          --steps 2 --warmup 1 > "$O/bench_ktl8.json" 2> "$O/bench_ktl8.err") ;;
+    long) (cd /tmp && timeout -k 10 900 python3 -u "$ROOT/bench.py" --steps 200 --warmup 2 --no-pcie \
+          --no-cpu-baseline > "$O/bench_long.json" 2> "$O/bench_long.err") ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

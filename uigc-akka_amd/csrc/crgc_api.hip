@@ -207,6 +207,8 @@ Caps caps_create(uint64_t v0, uint64_t e0) {
 //   CRGC_KERNEL_TIMING    0: chunk events only, 1 (default): k_expand's dispatch
 //                         events too (the roofline's live timing), 2: every level kernel
 //   CRGC_LEVEL_LOG        per-level device times on stderr (diagnostics)
+//   CRGC_SPIN_US          host waits poll the stream this long before blocking
+//                         (default 20000; 0 blocks at once; crgc_internal.hpp)
 // (and, in the transports, CRGC_RCCL_TIMEOUT_S / CRGC_LOCAL_BARRIER_S).
 // Everything else — the A/B variants of DESIGN.md §4 and the test hooks of
 // tests/ — is read only when CRGC_TEST_HOOKS=1, so a JVM host that inherits a
@@ -245,7 +247,7 @@ struct Knobs {
   uint32_t chunk_max = 4;        // CRGC_CHUNK_MAX: at most this many chunks (2 .. 8)
   uint32_t chunk_reg = 1;        // CRGC_CHUNK_REG: at most this many chunks of a registered batch (1 .. 8)
   uint64_t dev_chunk = 0;        // CRGC_DEV_CHUNK: sub-merge size of large device batches (test hook; 0 = 2^20)
-  uint32_t spin_us = SPIN_US_DEFAULT;  // CRGC_SPIN_US: host waits poll this long before blocking (0: block at once)
+  uint32_t spin_us = spin_us_default();  // CRGC_SPIN_US (production): host waits poll this long before blocking (0: block at once)
   bool repack_each = false;      // CRGC_REPACK_EACH_MERGE=1: repack the pools before every merge (test hook)
   void read() {
     auto env = [](const char *k) { return getenv(k); };
@@ -291,7 +293,6 @@ struct Knobs {
       dev_chunk = strtoull(m, nullptr, 10);
       if (dev_chunk) dev_chunk = std::max<uint64_t>(64, dev_chunk);
     }
-    if (const char *m = env("CRGC_SPIN_US")) spin_us = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_REPACK_EACH_MERGE")) repack_each = atoi(m) != 0;
   }
 };
@@ -1516,12 +1517,22 @@ static int merge_entries_dev_chunked(crgc_graph *h, const crgc_entry_batch *b) {
   HIP_TRY(hsync(h));
   d2h_small_done(h, bo.data(), bo.size() * 4);
   if (bo[0] || bo[1] || bo[2]) return CRGC_E_INVAL;
+  // Every chunk's boundaries are checked before the first sub-merge, so a batch
+  // refused for them is refused whole (a later chunk's bad boundary
+  // used to surface after the chunks before it had merged).  Offsets that run
+  // backwards inside a chunk are the device's ERR_BAD_OFFSETS, which poisons
+  // the handle (device_error), as a single merge does.
   for (uint64_t j = 0; j < K; ++j) {
     const uint64_t lo = j * CH, hi = std::min(n, lo + CH), m = hi - lo;
     const uint32_t c0 = bo[3 * j], s0 = bo[3 * j + 1], u0 = bo[3 * j + 2];
     const uint32_t c1 = bo[3 * j + 3], s1 = bo[3 * j + 4], u1 = bo[3 * j + 5];
     if (c1 < c0 || s1 < s0 || u1 < u0 || c1 - c0 > m * h->F || s1 - s0 > m * h->F || u1 - u0 > m * h->F)
-      return CRGC_E_INVAL;  // offsets run backwards or past F per entry: refused (chunks before it merged)
+      return CRGC_E_INVAL;  // offsets run backwards or past F per entry: refused, nothing merged
+  }
+  for (uint64_t j = 0; j < K; ++j) {
+    const uint64_t lo = j * CH, hi = std::min(n, lo + CH), m = hi - lo;
+    const uint32_t c0 = bo[3 * j], s0 = bo[3 * j + 1], u0 = bo[3 * j + 2];
+    const uint32_t c1 = bo[3 * j + 3], s1 = bo[3 * j + 4], u1 = bo[3 * j + 5];
     // (stream order: the previous chunk's kernels have read these buffers)
     HIP_TRY(launch_rebase_copy(b->created_off + lo, b->spawned_off + lo, b->updated_off + lo, co, so, uo, m + 1, c0,
                                s0, u0, h->stream));

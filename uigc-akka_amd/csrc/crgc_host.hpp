@@ -16,7 +16,6 @@ namespace crgc {
 struct Scratch {
   void *ptr = nullptr;
   size_t bytes = 0;
-  uint64_t gen = 0;  // bumped by every allocation (the allocator may return the same base)
   hipError_t ensure(size_t need) {
     if (need <= bytes) return hipSuccess;
     if (ptr) hipFree(ptr);
@@ -24,10 +23,7 @@ struct Scratch {
     bytes = 0;
     size_t sz = need + need / 4 + 4096;
     hipError_t e = hipMalloc(&ptr, sz);
-    if (e == hipSuccess) {
-      bytes = sz;
-      ++gen;
-    }
+    if (e == hipSuccess) bytes = sz;
     return e;
   }
   void release() {

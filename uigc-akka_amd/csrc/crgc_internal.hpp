@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include <chrono>
+#include <cstdlib>
 
 namespace crgc {
 
@@ -30,8 +31,18 @@ namespace crgc {
 // 1e7-entry merge waits once per 2^20-entry sub-merge (profiles/r4o: the merge
 // 15.8 ms against 5.8 ms of kernels).  A not-ready query leaves no sticky
 // error (tools/hip_probe.hip).
+// CRGC_SPIN_US (a production switch; read once per process)
+// sets the bound: 0 blocks at once, which frees the waiting core (a JVM host with
+// one thread per shard may prefer that over the ~1 ms later wake-up).
 constexpr uint32_t SPIN_US_DEFAULT = 20000;
-inline hipError_t stream_wait(hipStream_t s, uint32_t spin_us = SPIN_US_DEFAULT) {
+inline uint32_t spin_us_default() {
+  static const uint32_t v = [] {
+    const char *m = getenv("CRGC_SPIN_US");
+    return m ? (uint32_t)strtoul(m, nullptr, 10) : SPIN_US_DEFAULT;
+  }();
+  return v;
+}
+inline hipError_t stream_wait(hipStream_t s, uint32_t spin_us = spin_us_default()) {
   if (spin_us) {
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
@@ -42,7 +53,7 @@ inline hipError_t stream_wait(hipStream_t s, uint32_t spin_us = SPIN_US_DEFAULT)
   }
   return hipStreamSynchronize(s);
 }
-inline hipError_t event_wait(hipEvent_t ev, uint32_t spin_us = SPIN_US_DEFAULT) {
+inline hipError_t event_wait(hipEvent_t ev, uint32_t spin_us = spin_us_default()) {
   if (spin_us) {
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {

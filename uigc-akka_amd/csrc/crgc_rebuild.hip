@@ -210,8 +210,10 @@ __global__ __launch_bounds__(256) void k_rb_rcaps(DevGraph dst, uint64_t *caps) 
     caps[v] = v < n ? rb_cap(dst.rnew[v]) : 0;
 }
 
+// (slot_top clamped to the new arrays: k_rb_vertices maps slots past dst.scap to
+// SLOT_NONE, but slot_top still counts them — ADVICE r4)
 __global__ __launch_bounds__(256) void k_rb_rsetup(DevGraph dst, const uint64_t *offs) {
-  const uint64_t n = dst.ctr->slot_top;
+  const uint64_t n = min((uint64_t)dst.ctr->slot_top, dst.scap);
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < n; v += stride) {
     dst.radj[v] = make_uint2((uint32_t)offs[v], rseg_pack(0, rb_cap(dst.rnew[v])));
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(256) void k_rb_rsetup(DevGraph dst, const uint64_t 
 }
 
 __global__ __launch_bounds__(256) void k_rb_rfill(DevGraph dst) {
-  const uint64_t n = dst.ctr->slot_top;
+  const uint64_t n = min((uint64_t)dst.ctr->slot_top, dst.scap);
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t o = (uint64_t)blockIdx.x * 256 + threadIdx.x; o < n; o += stride) {
     const uint2 ad = dst.adj[o];
