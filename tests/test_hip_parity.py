@@ -405,9 +405,8 @@ def test_device_sub_merge_bad_later_boundary_refused_whole(hip_mod, oracle_mod, 
         h.merge_entries(nb.to_device())
     assert ei.value.code == abi.E_INVAL
     assert h.export() == before   # nothing merged, not poisoned
-    good = fz.entries(700)
-    h.merge_entries(good.to_device())
-    o.merge_entries(good)
+    h.merge_entries(bad.to_device())   # the same entries with their offsets intact
+    o.merge_entries(bad)
     assert h.export() == o.export()
     _same_trace(h.trace(True), o.trace(True))
 
