@@ -39,8 +39,8 @@
 extern "C" {
 #endif
 
-#define CRGC_ABI_VERSION 4u  /* 2: crgc_trace_stats.expand_launches / expand_bytes; 3: exchange_bytes;
-                                 4: time_query_failures, direct_lists */
+#define CRGC_ABI_VERSION 5u  /* 2: crgc_trace_stats.expand_launches / expand_bytes; 3: exchange_bytes;
+                                 4: time_query_failures, direct_lists; 5: crgc_config.proxy_capacity */
 
 /* ---- status codes ------------------------------------------------------- */
 #define CRGC_OK 0
@@ -118,6 +118,9 @@ typedef struct crgc_config {
   uint32_t n_shards;           /* 0 or 1: unsharded                         */
   uint32_t shard;              /* this handle's shard, < n_shards           */
   crgc_transport *transport;   /* required when n_shards > 1                */
+  uint64_t proxy_capacity;     /* n_shards > 1, hint: expected proxy slots   */
+                               /* (far ends homed elsewhere); 0: like        */
+                               /* vertex_capacity                            */
 } crgc_config;
 
 /*

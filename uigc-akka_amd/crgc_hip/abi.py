@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 OK = 0
 E_INVAL = -1
@@ -55,6 +55,7 @@ class CrgcConfig(C.Structure):
         ("n_shards", C.c_uint32),
         ("shard", C.c_uint32),
         ("transport", _P),
+        ("proxy_capacity", _U64),
     ]
 
 

@@ -53,7 +53,7 @@ class ShadowGraph:
     def __init__(self, entry_field_size: int = 4, delta_graph_size: int = 64,
                  device: int = 0, vertex_capacity: int = 0, edge_capacity: int = 0,
                  stream: Optional[int] = None, n_shards: int = 1, shard: int = 0,
-                 transport=None):
+                 transport=None, proxy_capacity: int = 0):
         """One shadow graph, or (n_shards > 1) shard `shard` of a hash-partitioned
         one whose shards exchange through `transport` (a Transport).  Merges,
         traces and investigateRemotelyHeldActors are then collective."""
@@ -69,6 +69,7 @@ class ShadowGraph:
         cfg.n_shards = n_shards
         cfg.shard = shard
         cfg.transport = transport.t if transport is not None else None
+        cfg.proxy_capacity = proxy_capacity
         self.n_shards, self.shard = n_shards, shard
         self._transport = transport  # keeps it alive at least as long as this handle
         h = C.c_void_p()
@@ -451,14 +452,15 @@ class ShardedShadowGraph:
     """
 
     def __init__(self, n_shards: int, devices=None, entry_field_size: int = 4,
-                 vertex_capacity: int = 0, edge_capacity: int = 0):
+                 vertex_capacity: int = 0, edge_capacity: int = 0, proxy_capacity: int = 0):
         import concurrent.futures as cf
         self.G = n_shards
         devices = list(devices) if devices is not None else [0] * n_shards
         self.transport = Transport.local(n_shards)
         self.shards = [ShadowGraph(entry_field_size=entry_field_size, device=devices[r],
                                    vertex_capacity=vertex_capacity, edge_capacity=edge_capacity,
-                                   n_shards=n_shards, shard=r, transport=self.transport)
+                                   n_shards=n_shards, shard=r, transport=self.transport,
+                                   proxy_capacity=proxy_capacity)
                        for r in range(n_shards)]
         self._pool = cf.ThreadPoolExecutor(max_workers=n_shards)
 

@@ -26,6 +26,7 @@ uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
 
 struct Caps {
   uint64_t scap, hcap, pcap, ecap;
+  uint64_t pbase;  // first proxy slot; == scap without a proxy region (unsharded graphs)
 };
 
 // Device arrays of one graph generation.
@@ -67,6 +68,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   d.hcap = c.hcap;
   d.hmask = c.hcap - 1;
   d.scap = c.scap;
+  d.pbase = c.pbase;
   d.pcap = c.pcap;
   d.ecap_tab = c.ecap;
   d.emask = c.ecap - 1;
@@ -169,10 +171,18 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   return ms;
 }
 
-Caps caps_for(uint64_t live, uint64_t edges, uint64_t ids_pending, uint64_t atoms_pending) {
+// Slots of one region for `live` kept shadows and `ids` that a pending merge may add.
+uint64_t region_cap(uint64_t live, uint64_t ids) {
+  return round_up(std::max<uint64_t>(2 * live + ids, live + 2 * ids) + 8192, BLK_SLOTS);
+}
+
+// Sharded graphs (G > 1) keep their proxies in a region of their own above
+// pbase (DevGraph::pbase), sized like the shadows' region from the live
+// proxies; the id table and the pools serve both.
+Caps caps_regions(uint64_t H, uint64_t P, uint64_t edges, uint64_t atoms_pending) {
   Caps c;
-  c.scap = round_up(std::max<uint64_t>(2 * live + ids_pending, live + 2 * ids_pending) + 8192,
-                    BLK_SLOTS);
+  c.pbase = H;
+  c.scap = H + P;
   c.hcap = pow2ceil(c.scap * 3 / 2 + 1024);
   uint64_t pc = 4 * edges + 8 * atoms_pending + 4 * c.scap + 65536;
   c.pcap = std::min<uint64_t>(pc, 0xFFFFFFF0ull);
@@ -180,17 +190,23 @@ Caps caps_for(uint64_t live, uint64_t edges, uint64_t ids_pending, uint64_t atom
   return c;
 }
 
-// A new graph's capacities from the caller's hints (expected live shadows v0
-// and live (owner, target) pairs e0): slots for twice the live shadows (a trace
-// compacts once dead slots outnumber live ones), the id table at load <= 1/3,
-// the edge table at load <= 2/3 of e0, the pools for power-of-two segments with
-// room to move.  (caps_for sizes a rebuild, which also reserves for the
-// pending merge.)  At C4 on one GPU (1.1e8 / 1.1e9 hints) this is ~130 GB of
-// the 288 GB: caps_for(v0, e0, v0, e0) asked for ~250 GB there.
-Caps caps_create(uint64_t v0, uint64_t e0) {
-  Caps c;
-  c.scap = round_up(2 * v0 + v0 / 4 + 8192, BLK_SLOTS);
-  c.hcap = pow2ceil(c.scap * 3 / 2 + 1024);
+Caps caps_for(uint64_t live, uint64_t live_proxies, bool proxies, uint64_t edges, uint64_t ids_pending,
+              uint64_t atoms_pending) {
+  return caps_regions(region_cap(live, ids_pending), proxies ? region_cap(live_proxies, ids_pending) : 0, edges,
+                      atoms_pending);
+}
+
+// A new graph's capacities from the caller's hints (expected live shadows v0,
+// proxies p0 of a sharded graph, and live (owner, target) pairs e0): slots for
+// twice the live shadows (a trace compacts once dead slots outnumber live
+// ones), the id table at load <= 1/3, the edge table at load <= 2/3 of e0, the
+// pools for power-of-two segments with room to move.  (caps_for sizes a
+// rebuild, which also reserves for the pending merge.)  At C4 on one GPU
+// (1.1e8 / 1.1e9 hints) this is ~130 GB of the 288 GB: caps_for(v0, e0, v0, e0)
+// asked for ~250 GB there.
+Caps caps_create(uint64_t v0, uint64_t p0, bool proxies, uint64_t e0) {
+  auto reg = [](uint64_t v) { return round_up(2 * v + v / 4 + 8192, BLK_SLOTS); };
+  Caps c = caps_regions(reg(v0), proxies ? reg(p0) : 0, 0, 0);
   c.pcap = std::min<uint64_t>(4 * e0 + 4 * c.scap + 65536, 0xFFFFFFF0ull);
   c.ecap = pow2ceil(e0 * 3 / 2 + 65536);
   return c;
@@ -237,6 +253,10 @@ struct Knobs {
   uint32_t xclosure_after = 8;   // CRGC_XCLOSURE_AFTER
   uint32_t xclosure_narrow = 1024;  // CRGC_XCLOSURE_NARROW
   uint32_t xslices = 1;          // CRGC_XSLICES: push-level target slices (1, 2, 4, 8)
+  // Sharded marks: a round runs at most this many level launches before its
+  // exchange (0: to the shard's local fixpoint).  Pending candidates carry
+  // over into the next round.
+  uint32_t xlevels = 0;          // CRGC_XLEVELS
   bool bin = true;               // CRGC_BIN=0: the pseudo-root level pushes candidate bytes directly
   uint64_t bin_min = 1ull << 22; // CRGC_BIN_MIN_SLOTS: binned only above this many slots (a smaller
                                  // candidate byte map stays in the L2: C1 mark +10 us binned)
@@ -279,6 +299,7 @@ struct Knobs {
     if (const char *m = env("CRGC_XCLOSURE_NARROW")) xclosure_narrow = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_BIN")) bin = atoi(m) != 0;
     if (const char *m = env("CRGC_BIN_MIN_SLOTS")) bin_min = strtoull(m, nullptr, 10);
+    if (const char *m = env("CRGC_XLEVELS")) xlevels = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_XSLICES")) {
       const uint32_t v = (uint32_t)strtoul(m, nullptr, 10);
       xslices = v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
@@ -311,6 +332,7 @@ struct crgc_graph {
   bool poisoned = false;
   // exact values as of the last synchronisation + upper-bound increments since
   uint64_t slot_top = 0, pool_top = 0, rpool_top = 0, etab_used = 0, live = 0;
+  uint64_t proxy_top = 0;  // proxy region slots in use (sharded graphs), as of the last synchronisation
   uint64_t ids_since = 0, atoms_since = 0;
   uint64_t inserted_at_trace = 0;  // Counters::inserted when `live` was exact
   Scratch stage, work;
@@ -343,7 +365,7 @@ struct crgc_graph {
   // sharded graphs (G > 1): transport and exchange buffers
   crgc_transport *tp = nullptr;
   uint32_t G = 1, shard = 0;
-  uint64_t n_proxy = 0;              // alive proxy slots at the last sweep
+  uint64_t n_proxy = 0;              // alive proxy slots after the last trace
   Scratch x_send, x_slot, x_recv, x_ans, x_ans_back, x_small, x_pack, x_pack_recv;
   Scratch x_route, x_route_send, x_cat;  // routed entry merges
   Scratch x_dg, x_dg_out;    // DeltaGraph production
@@ -446,6 +468,7 @@ hipError_t sync_counters(crgc_graph *h) {
 // Bookkeeping from a fresh host copy of the counters.
 void absorb_counters(crgc_graph *h) {
   h->slot_top = h->hctr->slot_top;
+  h->proxy_top = h->hctr->proxy_top;
   h->pool_top = h->hctr->pool_top;
   h->rpool_top = h->hctr->rpool_top;
   h->etab_used = h->hctr->etab_used;
@@ -469,18 +492,19 @@ int device_error(crgc_graph *h) {
 int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   HIP_TRY(sync_counters(h));
   if (int rc = device_error(h)) return rc;
-  const uint64_t src_top = h->slot_top;
-  // The slots the rebuild keeps, counted exactly: every alive slot, proxies of
-  // a sharded graph included.  (Round 4 sized the new arrays from the live
-  // count at the last trace plus the *home* shadows created since —
-  // Counters::inserted is totalActorsSeen — which left out the proxies a
-  // sharded load creates: 68 M alive slots went into 27 M at C4 over 8 logical
-  // shards, and the rebuild's passes wrote past the new arrays.)
-  HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(n_out), 0, 8, h->stream));
-  HIP_TRY(launch_count_alive(h->g.d, src_top, &h->ctr->n_out, h->stream));
+  const uint64_t src_top = h->slot_top, src_ptop = h->proxy_top;
+  // The slots the rebuild keeps, counted exactly: every alive slot, the
+  // shadows' and (sharded graphs) the proxies'.  (Round 4 sized the new arrays
+  // from the live count at the last trace plus the *home* shadows created
+  // since — Counters::inserted is totalActorsSeen — which left out the proxies
+  // a sharded load creates: 68 M alive slots went into 27 M at C4 over 8
+  // logical shards, and the rebuild's passes wrote past the new arrays.)
+  HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(alive_cnt), 0, 16, h->stream));
+  HIP_TRY(launch_count_alive(h->g.d, src_top, src_ptop, h->ctr->alive_cnt, h->stream));
   HIP_TRY(sync_counters(h));
-  const uint64_t live_ub = std::min<uint64_t>(src_top, h->hctr->n_out);
-  Caps c = caps_for(std::max<uint64_t>(live_ub, 1), h->etab_used, ids, atoms);
+  const uint64_t live_ub = std::min<uint64_t>(src_top, h->hctr->alive_cnt[0]);
+  const uint64_t live_p = std::min<uint64_t>(src_ptop, h->hctr->alive_cnt[1]);
+  Caps c = caps_for(std::max<uint64_t>(live_ub, 1), live_p, h->G > 1, h->etab_used, ids, atoms);
   if (h->knobs.level_log)
     fprintf(stderr, "[crgc] rebuild: slots %llu (alive %llu) pool %llu / %llu rpool %llu edge keys %llu / %llu "
                     "-> slots %llu pool %llu edge table %llu\n",
@@ -491,21 +515,22 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   Arrays dst;
   HIP_TRY(alloc_arrays(dst, c, h->ctr, h->stream, h->G, h->shard, h->tp != nullptr));
   Scratch tmp;
-  const size_t need = Carver::need({src_top * 4 + 4, c.scap * 8, rebuild_scan_tmp_bytes(c.scap)});
+  const size_t need = Carver::need({h->g.caps.scap * 4 + 4, c.scap * 8, rebuild_scan_tmp_bytes(c.scap)});
   if (tmp.ensure(need) != hipSuccess) {
     free_arrays(dst);
     return CRGC_E_NOMEM;
   }
   Carver cv(tmp.ptr);
-  uint32_t *map = cv.take<uint32_t>(src_top + 1);
+  uint32_t *map = cv.take<uint32_t>(h->g.caps.scap + 1);  // by source slot (both regions)
   uint64_t *offs = cv.take<uint64_t>(c.scap);
   void *scan_tmp = cv.take<uint64_t>(rebuild_scan_tmp_bytes(c.scap) / 8);
   hipError_t e = hipMemsetAsync(offs, 0, c.scap * 8, h->stream);
-  // new generation counters: slot_top, pool_top, etab_used restart
-  for (size_t off : {CTR_OFF(slot_top), CTR_OFF(pool_top), CTR_OFF(rpool_top), CTR_OFF(etab_used)})
+  // new generation counters: slot_top, pool_top, etab_used, the proxy region's restart
+  for (size_t off : {CTR_OFF(slot_top), CTR_OFF(pool_top), CTR_OFF(rpool_top), CTR_OFF(etab_used),
+                     CTR_OFF(proxy_top), CTR_OFF(proxy_dead), CTR_OFF(res_top)})
     if (e == hipSuccess) e = hipMemsetAsync((char *)h->ctr + off, 0, 8, h->stream);
-  // src keeps a view of the old counters' bound via src_top (passed by value)
-  if (e == hipSuccess) e = launch_rebuild(h->g.d, src_top, dst.d, map, nullptr, offs, scan_tmp, h->stream);
+  // src keeps a view of the old counters' bounds via src_top / src_ptop (passed by value)
+  if (e == hipSuccess) e = launch_rebuild(h->g.d, src_top, src_ptop, dst.d, map, offs, scan_tmp, h->stream);
   // The last trace's garbage / kill lists outlive the generation: crgc_last_trace
   // may still copy them (two-phase trace, or a trace whose buffers were short).
   // They can hold more ids than the compacted generation has slots.
@@ -559,7 +584,7 @@ int repack(crgc_graph *h) {
   uint64_t *pp = cv.take<uint64_t>(c.scap), *rp = cv.take<uint64_t>(c.scap);
   void *st = cv.take<uint64_t>(2 * scan / 8);
   const uint64_t old_p = h->pool_top, old_r = h->rpool_top;
-  hipError_t e = launch_repack(h->g.d, h->slot_top, pp, rp, st, pool2, rpool2, h->stream);
+  hipError_t e = launch_repack(h->g.d, h->slot_top, h->proxy_top, pp, rp, st, pool2, rpool2, h->stream);
   if (e == hipSuccess) e = sync_counters(h);
   tmp.release();
   if (e != hipSuccess) {  // the device may have moved part of adj / radj: unusable
@@ -587,20 +612,23 @@ int ensure_capacity(crgc_graph *h, uint64_t ids, uint64_t atoms) {
     const Caps &c = h->g.caps;
     return pt + 2 * eu + 6 * atoms <= c.pcap && rt + 2 * eu + 6 * atoms + 4 * ids <= c.pcap;
   };
-  auto rest_fits = [&](uint64_t st, uint64_t eu) {
+  // (new shadows fill the shadows' region, new proxies the proxy region; `ids`
+  // bounds either)
+  auto rest_fits = [&](uint64_t st, uint64_t pt, uint64_t eu) {
     const Caps &c = h->g.caps;
-    return st + ids <= c.scap && (st + ids) * 10 <= c.hcap * 7 && (eu + atoms) * 10 <= c.ecap * 7;
+    return st + ids <= c.pbase && (h->G <= 1 || pt + ids <= c.scap - c.pbase) &&
+           (st + pt + ids) * 10 <= c.hcap * 7 && (eu + atoms) * 10 <= c.ecap * 7;
   };
   // upper bounds since the last sync
-  const uint64_t st = h->slot_top + h->ids_since;
+  const uint64_t st = h->slot_top + h->ids_since, pt = h->proxy_top + h->ids_since;
   const uint64_t eu = h->etab_used + h->atoms_since;
   const uint64_t grow = 2 * (h->etab_used + h->atoms_since) + 6 * h->atoms_since;
   // (+ 4 reverse-candidate entries per new shadow: k_ids' first segments)
-  if (rest_fits(st, eu) && pools_fit(h->pool_top + grow, h->rpool_top + grow + 4 * h->ids_since, eu))
+  if (rest_fits(st, pt, eu) && pools_fit(h->pool_top + grow, h->rpool_top + grow + 4 * h->ids_since, eu))
     return CRGC_OK;
   HIP_TRY(sync_counters(h));
   if (int rc = device_error(h)) return rc;
-  const bool rest = rest_fits(h->slot_top, h->etab_used);
+  const bool rest = rest_fits(h->slot_top, h->proxy_top, h->etab_used);
   if (rest && pools_fit(h->pool_top, h->rpool_top, h->etab_used)) return CRGC_OK;
   // only the pools are short: reclaim their dead space before rebuilding the
   // whole graph (a rebuild allocates a second graph; a repack, two pools)
@@ -611,6 +639,16 @@ int ensure_capacity(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   }
   return rebuild(h, ids, atoms);
 }
+
+// Upper bounds, without a synchronisation, of the slots in use: the shadows'
+// (slot_top) and the proxy region's (sharded graphs), and their blocks.
+uint64_t home_top_ub(const crgc_graph *h) {
+  return std::min<uint64_t>(h->slot_top + h->ids_since, h->g.caps.pbase);
+}
+uint64_t proxy_top_ub(const crgc_graph *h) {
+  return h->G > 1 ? std::min<uint64_t>(h->proxy_top + h->ids_since, h->g.caps.scap - h->g.caps.pbase) : 0;
+}
+uint64_t blocks_of(uint64_t slots) { return (slots + BLK_SLOTS - 1) / BLK_SLOTS; }
 
 void note_merge(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   h->ids_since += ids;
@@ -755,7 +793,10 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     }
     const uint64_t v0 = cfg && cfg->vertex_capacity ? cfg->vertex_capacity : (1u << 16);
     const uint64_t e0 = cfg && cfg->edge_capacity ? cfg->edge_capacity : 8 * v0;
-    Caps c = caps_create(v0, e0);
+    // a shard's proxy region from its own hint (ABI 5); without one it is sized
+    // like the shadows' region
+    const uint64_t p0 = cfg && cfg->proxy_capacity ? cfg->proxy_capacity : v0;
+    Caps c = caps_create(v0, p0, h->G > 1, e0);
     if (hipError_t e = alloc_arrays(h->g, c, h->ctr, h->stream, h->G, h->shard, h->tp != nullptr)) {
       rc = map_hip(e);
       break;
@@ -1046,6 +1087,7 @@ extern "C" {
 // `off` keeps a read clear of the words an all-gather in flight uses.
 constexpr size_t SMALL_BYTES = 8 * (size_t)MAX_SHARDS * (MAX_SHARDS + 8);
 constexpr size_t SMALL_XFLAG_OFF = SMALL_BYTES / 2;
+constexpr size_t SMALL_PEND_OFF = SMALL_BYTES - 64;  // a mark round's pending word (mark_all)
 static hipError_t d2h_small(crgc_graph *h, void *dst, const void *src, size_t bytes, size_t off = 0) {
   void *to = off + bytes <= SMALL_BYTES ? (void *)((char *)h->h_small + off) : dst;
   return hipMemcpyAsync(to, src, bytes, hipMemcpyDeviceToHost, h->stream);
@@ -1900,9 +1942,14 @@ static void collect_times(crgc_graph *h, LevelRun &lr, size_t nl, size_t nc, int
 // first empty one), so a steady-state wakeup needs one host synchronisation
 // and launches no idle levels.  *end = the first empty
 // level (levels start .. *end-1 were non-empty).
+// max_levels > 0 (sharded rounds): at most that many level launches after
+// level 0; a round that reaches it with work left returns *capped = true and
+// *end = the next level, whose candidates are pending.
 static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64_t top, bool roots,
                       int start, LevelRun &lr, int *end,
-                      const std::function<hipError_t()> &after_chunk = nullptr) {
+                      const std::function<hipError_t()> &after_chunk = nullptr, int max_levels = 0,
+                      bool *capped = nullptr) {
+  if (capped) *capped = false;
   LevelArgs la{};
   la.location = location;
   // Losing A/B variants of round 1 (atomicOr candidate bitmap, 8 edges per lane,
@@ -1910,6 +1957,11 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   // always-on marked-word filter) were removed; their records stay in
   // profiles/r1h, r1n, r1r.
   const Knobs &kn = h->knobs;
+  // sharded graphs: the level kernels visit the proxy region too (grids from
+  // vtop), and level 0's bins cover it (imax: one past the largest slot)
+  const uint64_t ptop = proxy_top_ub(h);
+  const uint64_t vtop = top + ptop;
+  const uint64_t imax = ptop ? h->g.caps.pbase + ptop : top;
   la.flags = 0;
   la.sparse_thresh = (uint32_t)std::max<uint64_t>(64, (top / BLK_SLOTS) / 4);
   // Direction optimisation: dense levels after a frontier of >= top/div shadows pull.
@@ -1946,9 +1998,9 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   // at once).  The place pass writes the mode word k_bin_apply reads.
   if (roots && kn.bin && !kn.alpha && top > 0 && top >= kn.bin_min) {
     uint32_t lg = 0;
-    while (lg < 63 && (1ull << lg) < top) ++lg;
+    while (lg < 63 && (1ull << lg) < imax) ++lg;
     const uint32_t shift = std::max<uint32_t>(16, lg > 8 ? lg - 8 : 0);
-    const uint64_t nb = (top + (1ull << shift) - 1) >> shift;
+    const uint64_t nb = (imax + (1ull << shift) - 1) >> shift;
     if (shift <= 20 && nb <= BIN_MAX) {
       const uint64_t nc = nb * BIN_WG;
       const uint64_t want = std::max<uint64_t>(1u << 16, (h->etab_used + h->atoms_since) / 2);
@@ -1988,7 +2040,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
       for (int k = timing >= 2 ? 0 : 4; k < 6; ++k) ev[k] = h->lvl_ev[6 * nl + k];
     }
     la.level = level;
-    hipError_t r = launch_level(h->g.d, la, rootk, investigate, top, h->stream, ev);
+    hipError_t r = launch_level(h->g.d, la, rootk, investigate, vtop, h->stream, ev);
     ++nl;
     return r;
   };
@@ -2012,11 +2064,13 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   // the (level + 1) << 12 tag width, passes by a count and a wall clock.
   const auto loop_t0 = std::chrono::steady_clock::now();
   int last_bail = -1;
+  int launched = 0;  // level launches of this call after level 0
   for (uint64_t pass = 0;; ++pass) {
     if (pass > 4096 || std::chrono::steady_clock::now() - loop_t0 > std::chrono::seconds(kn.level_timeout_s)) {
       h->poisoned = true;
       return CRGC_E_TIMEOUT;
     }
+    if (max_levels) chunk = std::max(1, std::min(chunk, max_levels - launched));
     if (nc % 2 == 0) HIP_TRY(chunk_event());
     for (int k = 0; k < chunk; ++k) HIP_TRY(launch(L + k, false));
     HIP_TRY(chunk_event());
@@ -2078,6 +2132,21 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
       }
     }
     L += chunk;
+    launched += chunk;
+    if (max_levels && launched >= max_levels) {  // the round's exchange comes first; level L is pending
+      *end = L;
+      if (capped) *capped = true;
+      lr.levels += (uint64_t)launched;
+      lr.launches += nl;
+      lr.pending = [h, nl, nc, timing, log, roots, start, last, ring, &lr]() {
+        collect_times(h, lr, nl, nc, timing, log, roots ? 0 : (size_t)start, (size_t)last, ring);
+      };
+      if (!lr.defer) {
+        lr.pending();
+        lr.pending = nullptr;
+      }
+      return CRGC_OK;
+    }
     chunk = std::min(chunk * 2, 512);
     if ((uint64_t)L > (1ull << 19)) return CRGC_E_TIMEOUT;  // (level + 1) << 12 tags are 32-bit
   }
@@ -2121,9 +2190,8 @@ static void collect_times(crgc_graph *h, LevelRun &lr, size_t nl, size_t nc, int
 static void reset_trace_counters(crgc_graph *h) {
   // marked .. the level ring, and the per-block state of the blocks this trace can touch
   const size_t a = CTR_OFF(marked), b = sizeof(Counters);
-  const uint64_t top = h->slot_top + h->ids_since;
-  const uint64_t nblk = round_up(std::min<uint64_t>(top, h->g.caps.scap), BLK_SLOTS) / BLK_SLOTS;
-  launch_trace_reset(h->g.d, nblk, (uint32_t)(a / 8), (uint32_t)((b - a) / 8), h->stream);
+  launch_trace_reset(h->g.d, blocks_of(home_top_ub(h)), blocks_of(proxy_top_ub(h)), (uint32_t)(a / 8),
+                     (uint32_t)((b - a) / 8), h->stream);
 }
 
 // Mark to the global fixpoint: local levels, then (sharded graphs) rounds of
@@ -2150,27 +2218,32 @@ static int resolve_home_slots(crgc_graph *h, uint64_t top, int xmode, uint64_t *
     h->peer_top[d] = T[2 * d + 1];
   }
   if (xmode == 0) return CRGC_OK;  // ids only: nothing to resolve
-  if (mask) HIP_TRY(launch_resolve(h->g.d, 0, mask, nullptr, nullptr, nullptr, 0, nullptr, top, h->stream));
+  const uint64_t ptop = proxy_top_ub(h);  // (grids over the proxy region)
+  if (mask) HIP_TRY(launch_resolve(h->g.d, 0, mask, nullptr, nullptr, nullptr, 0, nullptr, ptop, h->stream));
   HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(xcnt), 0, 2 * MAX_SHARDS * 8, h->stream));
-  HIP_TRY(launch_resolve(h->g.d, 1, 0, nullptr, nullptr, nullptr, 0, nullptr, top, h->stream));
+  HIP_TRY(launch_resolve(h->g.d, 1, 0, nullptr, nullptr, nullptr, 0, nullptr, ptop, h->stream));
   std::vector<uint64_t> M((size_t)G * G);
   if (int rc = ag_u64(h, {{(char *)h->ctr + CTR_OFF(xcnt), G}}, M.data())) return rc;
   uint64_t total = 0, nsend = 0;
   for (uint64_t v : M) total += v;
   for (uint32_t d = 0; d < G; ++d) nsend += M[(size_t)me * G + d];
-  if (total == 0) return CRGC_OK;
+  if (total == 0) {
+    HIP_TRY(launch_resolve(h->g.d, 5, 0, nullptr, nullptr, nullptr, 0, nullptr, 0, h->stream));
+    return CRGC_OK;
+  }
   if (h->x_send.ensure(nsend * 8 + 8) != hipSuccess || h->x_slot.ensure(nsend * 4 + 8) != hipSuccess)
     return CRGC_E_NOMEM;
   HIP_TRY(launch_resolve(h->g.d, 2, 0, (uint64_t *)h->x_send.ptr, (uint32_t *)h->x_slot.ptr, nullptr, 0,
-                         nullptr, top, h->stream));
+                         nullptr, ptop, h->stream));
+  HIP_TRY(launch_resolve(h->g.d, 5, 0, nullptr, nullptr, nullptr, 0, nullptr, 0, h->stream));
   uint64_t nin = 0, nback = 0;
   if (int rc = a2a(h, h->x_send.ptr, M.data(), 8, h->x_recv, false, &nin)) return rc;
   if (h->x_ans.ensure(nin * 4 + 8) != hipSuccess) return CRGC_E_NOMEM;
   HIP_TRY(launch_resolve(h->g.d, 3, 0, nullptr, nullptr, (const uint64_t *)h->x_recv.ptr, nin,
-                         (uint32_t *)h->x_ans.ptr, top, h->stream));
+                         (uint32_t *)h->x_ans.ptr, ptop, h->stream));
   if (int rc = a2a(h, h->x_ans.ptr, M.data(), 4, h->x_ans_back, true, &nback)) return rc;
   HIP_TRY(launch_resolve(h->g.d, 4, 0, nullptr, (uint32_t *)h->x_slot.ptr, nullptr, nsend,
-                         (uint32_t *)h->x_ans_back.ptr, top, h->stream));
+                         (uint32_t *)h->x_ans_back.ptr, ptop, h->stream));
   *bytes += nsend * 8 + nin * 4;
   return CRGC_OK;
 }
@@ -2313,10 +2386,17 @@ static int xclosure(crgc_graph *h, bool investigate, const XRecv &xr, uint64_t *
 // as a bitmap over the home's slots once the list would be longer (a dense
 // round) — and as its id otherwise.  CRGC_XBITS: 0 ids only, 1 (default) the
 // cheaper form per destination, 2 bitmaps whenever slots are sent.
+//
+// CRGC_XLEVELS = k > 0 caps a round at k level launches (after level 0): the
+// exchange then follows the BFS level by level rather than each shard's local
+// fixpoint, and a capped shard's pending candidates carry into its next round.
+// The mark ends when no shard sends anything and none has pending work.
 static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t top, LevelRun &lr,
                     uint64_t *rounds, uint64_t *ids_sent, double *ms_x, uint64_t *x_bytes) {
   int end = 0;
-  if (int rc = run_levels(h, investigate, location, top, true, 0, lr, &end)) return rc;
+  bool capped = false;
+  const int cap = h->tp ? (int)h->knobs.xlevels : 0;
+  if (int rc = run_levels(h, investigate, location, top, true, 0, lr, &end, nullptr, cap, &capped)) return rc;
   *rounds = 1;
   if (!h->tp) return CRGC_OK;
   const uint32_t G = h->G, me = h->shard;
@@ -2326,10 +2406,11 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
     if (int rc = resolve_home_slots(h, top, xmode, x_bytes)) return rc;
     *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
-  const uint64_t nblk = round_up(std::min<uint64_t>(top, h->g.caps.scap), BLK_SLOTS) / BLK_SLOTS;
-  std::vector<uint64_t> M((size_t)G * 2 * G);
-  auto n_id = [&](uint32_t r, uint32_t d) { return M[(size_t)r * 2 * G + d]; };
-  auto n_sl = [&](uint32_t r, uint32_t d) { return M[(size_t)r * 2 * G + G + d]; };
+  // marked proxies are listed in the proxy region's blocks
+  const uint64_t npb = blocks_of(proxy_top_ub(h)), p0 = h->g.caps.pbase / BLK_SLOTS;
+  std::vector<uint64_t> M((size_t)G * (2 * G + 1));  // per shard: ids, slots per destination; pending
+  auto n_id = [&](uint32_t r, uint32_t d) { return M[(size_t)r * (2 * G + 1) + d]; };
+  auto n_sl = [&](uint32_t r, uint32_t d) { return M[(size_t)r * (2 * G + 1) + G + d]; };
   auto words = [&](uint32_t d) { return (h->peer_top[d] + 31) / 32; };
   auto bitmap = [&](uint32_t r, uint32_t d) {
     return n_sl(r, d) > 0 && (xmode == 2 || n_sl(r, d) > words(d));
@@ -2343,12 +2424,18 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
     HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(xcnt), 0, 4 * MAX_SHARDS * 8, h->stream));
     XSend xs{};
     xs.use_slots = xmode != 0;
-    HIP_TRY(launch_xlist(h->g.d, false, nblk, nullptr, xs, h->stream));
-    if (int rc = ag_u64(h, {{(char *)h->ctr + CTR_OFF(xcnt), G}, {(char *)h->ctr + CTR_OFF(xcnt2), G}}, M.data()))
+    HIP_TRY(launch_xlist(h->g.d, false, npb, nullptr, xs, h->stream));
+    // (with the counts, whether each shard's round was capped with work pending)
+    h->h_small[SMALL_PEND_OFF / 8] = capped ? 1 : 0;
+    if (int rc = ag_u64(h, {{(char *)h->ctr + CTR_OFF(xcnt), G}, {(char *)h->ctr + CTR_OFF(xcnt2), G},
+                            {h->h_small + SMALL_PEND_OFF / 8, 1}}, M.data()))
       return rc;
-    uint64_t total = 0, nsend = 0;
-    for (uint64_t v : M) total += v;
-    if (total == 0) {
+    uint64_t total = 0, nsend = 0, pending = 0;
+    for (uint32_t r = 0; r < G; ++r) {
+      for (uint32_t k = 0; k < 2 * G; ++k) total += M[(size_t)r * (2 * G + 1) + k];
+      pending += M[(size_t)r * (2 * G + 1) + 2 * G];
+    }
+    if (total == 0 && pending == 0) {
       *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       return CRGC_OK;
     }
@@ -2367,8 +2454,8 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
     if (h->x_send.ensure(so + 8) != hipSuccess) return CRGC_E_NOMEM;
     for (uint32_t d = 0; d < G; ++d)
       if (xs.bitmap[d]) HIP_TRY(hipMemsetAsync((char *)h->x_send.ptr + xs.sl_off[d], 0, 4 * words(d), h->stream));
-    HIP_TRY(launch_xlist(h->g.d, true, nblk, (char *)h->x_send.ptr, xs, h->stream));
-    HIP_TRY(hipMemsetAsync(h->g.d.xp_cnt, 0, nblk * 4, h->stream));
+    HIP_TRY(launch_xlist(h->g.d, true, npb, (char *)h->x_send.ptr, xs, h->stream));
+    if (npb) HIP_TRY(hipMemsetAsync(h->g.d.xp_cnt + p0, 0, npb * 4, h->stream));
     uint64_t nrecv = 0;
     if (int rc = a2a(h, h->x_send.ptr, B.data(), 1, h->x_recv, false, &nrecv)) return rc;
     *ids_sent += nsend;
@@ -2390,10 +2477,10 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
     // same all-gathered counts.
     {
       const Knobs &kn = h->knobs;
-      uint64_t n_all = 0, marks = 0;
+      uint64_t n_all = 0, marks = total;
       for (uint32_t d = 0; d < G; ++d) n_all += h->peer_top[d];
-      for (uint64_t v : M) marks += v;
-      if (xmode != 0 && kn.xclosure_after && *rounds >= kn.xclosure_after &&
+      // (never with candidates pending: the closure starts from marks only)
+      if (xmode != 0 && pending == 0 && kn.xclosure_after && *rounds >= kn.xclosure_after &&
           (kn.xclosure_narrow == 0 || marks * kn.xclosure_narrow <= n_all) && n_all < 0xF0000000ull) {
         *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         const auto t1 = std::chrono::steady_clock::now();
@@ -2402,15 +2489,19 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
         return rc;
       }
     }
-    // received marks are candidates of level L (a sparse level after an empty one)
-    const int L = end + 2;
-    HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(ring) + ((L - 2) % LEVEL_RING) * 8, 0, 8, h->stream));
-    HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(ring) + ((L - 1) % LEVEL_RING) * 8, 0, 8, h->stream));
+    // received marks are candidates of level L: a sparse level after an empty
+    // one, or — the round was capped — the pending level itself, whose
+    // candidates (and the counts of the levels before it) are already there
+    const int L = capped ? end : end + 2;
+    if (!capped) {
+      HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(ring) + ((L - 2) % LEVEL_RING) * 8, 0, 8, h->stream));
+      HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(ring) + ((L - 1) % LEVEL_RING) * 8, 0, 8, h->stream));
+      HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(qh) + (L & 1) * 8, 0, 8, h->stream));
+    }
     HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(tail_state), 0, 8, h->stream));
-    HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(qh) + (L & 1) * 8, 0, 8, h->stream));
     HIP_TRY(launch_ximport(h->g.d, (const char *)h->x_recv.ptr, xr, L, h->stream));
     *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    if (int rc = run_levels(h, investigate, location, top, false, L, lr, &end)) return rc;
+    if (int rc = run_levels(h, investigate, location, top, false, L, lr, &end, nullptr, cap, &capped)) return rc;
     ++*rounds;
   }
 }
@@ -2669,7 +2760,7 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   st.direct_lists = direct ? 1 : 0;
   st.pseudo_roots = lr.roots;
   h->live = c.n_live;
-  h->n_proxy = c.n_proxy;
+  h->n_proxy = c.proxy_top - std::min(c.proxy_top, c.proxy_dead);
   h->inserted_at_trace = c.inserted;
   h->have_last = true;
   h->last_levels = lr.first_chunk;
@@ -2677,8 +2768,11 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   h->last_stats = st;
   out->stats = st;
-  // Keep the slot space dense: rebuild once dead slots outnumber live ones.
-  if (rc == CRGC_OK && h->slot_top > 65536 && h->slot_top > 2 * (h->live + h->n_proxy)) {
+  // Keep the slot space dense: rebuild once dead slots outnumber live ones in
+  // the shadows' region, or (sharded graphs) in the proxy region.
+  const uint64_t ptop = c.proxy_top;
+  if (rc == CRGC_OK && ((h->slot_top > 65536 && h->slot_top > 2 * h->live) ||
+                        (ptop > 65536 && ptop > 2 * h->n_proxy))) {
     if (int r2 = rebuild(h, 0, 0)) return r2;
   }
   return rc;
@@ -3286,6 +3380,26 @@ int crgc_export(crgc_graph *h, crgc_graph_export *out) {
   }
   if (h->pool_top)
     HIP_TRY(hipMemcpy(pool.data(), h->g.d.pool, h->pool_top * 8, hipMemcpyDeviceToHost));
+  // far ends in the proxy region (sharded graphs)
+  const uint64_t pb = h->g.caps.pbase, ptop = h->proxy_top;
+  std::vector<uint64_t> pvid(ptop);
+  std::vector<uint8_t> pfl(ptop);
+  if (ptop) {
+    HIP_TRY(hipMemcpy(pvid.data(), h->g.d.vid + pb, ptop * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(pfl.data(), h->g.d.flags + pb, ptop, hipMemcpyDeviceToHost));
+  }
+  // the actor id of an alive slot (a shadow or a proxy), or false
+  auto alive_id = [&](uint32_t t, uint64_t *id) {
+    if (t < top && (fl[t] & FL_ALIVE)) {
+      *id = vid[t];
+      return true;
+    }
+    if (t >= pb && t - pb < ptop && (pfl[t - pb] & FL_ALIVE)) {
+      *id = pvid[t - pb];
+      return true;
+    }
+    return false;
+  };
   uint64_t nv = 0, ne = 0;
   bool big = false;
   for (uint64_t v = 0; v < top; ++v) {
@@ -3296,9 +3410,10 @@ int crgc_export(crgc_graph *h, crgc_graph_export *out) {
         out->recv_count[nv] = recv[v];
         out->flags[nv] = fl[v] & (uint8_t)~FL_ALIVE;
         const uint32_t s = sup[v];
-        out->supervisor[nv] = s == SLOT_NONE                         ? CRGC_NO_ACTOR
-                              : (s < top && (fl[s] & FL_ALIVE)) ? vid[s]
-                                                                    : CRGC_DEAD_ACTOR;
+        uint64_t sid = CRGC_DEAD_ACTOR;
+        if (s == SLOT_NONE) sid = CRGC_NO_ACTOR;
+        else if (!alive_id(s, &sid)) sid = CRGC_DEAD_ACTOR;
+        out->supervisor[nv] = sid;
       } else {
         big = true;
       }
@@ -3308,11 +3423,12 @@ int crgc_export(crgc_graph *h, crgc_graph_export *out) {
       const uint64_t ed = pool[(uint64_t)adj[v].x + e];
       const uint32_t t = (uint32_t)ed;
       const int32_t cnt = (int32_t)(uint32_t)(ed >> 32);
-      if (cnt == 0 || t >= top || !(fl[t] & FL_ALIVE)) continue;
+      uint64_t tid;
+      if (cnt == 0 || !alive_id(t, &tid)) continue;
       if (out->edge_owner) {
         if (ne < out->edge_cap) {
           out->edge_owner[ne] = vid[v];
-          out->edge_target[ne] = vid[t];
+          out->edge_target[ne] = tid;
           out->edge_count[ne] = cnt;
         } else {
           big = true;

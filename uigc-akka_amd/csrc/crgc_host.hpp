@@ -235,7 +235,8 @@ hipError_t launch_edges(const DevGraph &g, const EdgeArgs &a, hipStream_t s);
 // ev: null, or 6 events: start / stop of k_frontier, k_tail, k_expand
 hipError_t launch_level(const DevGraph &g, const LevelArgs &a, bool roots, bool investigate,
                         uint64_t slot_top, hipStream_t s, hipEvent_t *ev = nullptr);
-hipError_t launch_trace_reset(const DevGraph &g, uint64_t nblk, uint32_t ctr_from, uint32_t ctr_words,
+// nh blocks of the shadows' own slots and np of the proxy region
+hipError_t launch_trace_reset(const DevGraph &g, uint64_t nh, uint64_t np, uint32_t ctr_from, uint32_t ctr_words,
                               hipStream_t s);
 // sweep + id compaction + removal of the garbage (skipped on a reference NPE)
 // phase 1: classify + counts (k_sweep, k_sweep_scan); phase 2: ids + commit
@@ -264,6 +265,7 @@ struct XRecv {
   uint64_t start[MAX_SHARDS + 1];  // work items before each source (ids + slots / words)
   uint8_t bitmap[MAX_SHARDS];
 };
+// (nblk: a bound of the proxy region's blocks, for the grid)
 hipError_t launch_xlist(const DevGraph &g, bool scatter, uint64_t nblk, char *send, const XSend &x,
                         hipStream_t s);
 // The replicated chain closure of deep sharded marks (crgc_xchain.hip).
@@ -288,9 +290,10 @@ hipError_t launch_xclosure(const DevGraph &g, const XcArgs &x, int step, const v
                            uint32_t fi, int first, hipStream_t s);
 hipError_t launch_ximport(const DevGraph &g, const char *recv, const XRecv &x, int level, hipStream_t s);
 // home-slot resolution: 0 reset(mask), 1 count unresolved, 2 list them (ids, slots),
-// 3 answer asked ids (at the home), 4 store the answers
+// 3 answer asked ids (at the home), 4 store the answers, 5 every proxy so far has asked
+// (n_proxy: a bound of the proxy slots, for the grids)
 hipError_t launch_resolve(const DevGraph &g, int step, uint64_t mask, uint64_t *send, uint32_t *slots,
-                          const uint64_t *ids, uint64_t n, uint32_t *ans, uint64_t slot_top, hipStream_t s);
+                          const uint64_t *ids, uint64_t n, uint32_t *ans, uint64_t n_proxy, hipStream_t s);
 hipError_t launch_requests(const DevGraph &g, int phase, const uint64_t *ids, uint64_t n, uint8_t *ans,
                            const uint32_t *slots, hipStream_t s);
 hipError_t launch_invalidate(const DevGraph &g, const uint64_t *ids, uint64_t n, hipStream_t s);
@@ -300,15 +303,17 @@ hipError_t launch_local_roots(const DevGraph &g, uint64_t slot_top, hipStream_t 
 // rebuild: compact `src` (live vertices only, purged edges) into `dst`,
 // whose arrays are freshly allocated and initialised by init_graph_arrays.
 hipError_t launch_init_arrays(const DevGraph &g, hipStream_t s);
-hipError_t launch_count_alive(const DevGraph &src, uint64_t src_top, unsigned long long *out, hipStream_t s);
-hipError_t launch_rebuild(const DevGraph &src, uint64_t src_slot_top, const DevGraph &dst,
-                          uint32_t *map, uint32_t *newdeg, uint64_t *offs, void *scan_tmp,
-                          hipStream_t s);
+// (src_top / src_ptop: the source's shadow and proxy slot counts; out[0] / out[1]
+// the alive ones of each; map: src.scap + 1 entries, by source slot)
+hipError_t launch_count_alive(const DevGraph &src, uint64_t src_top, uint64_t src_ptop, unsigned long long *out,
+                              hipStream_t s);
+hipError_t launch_rebuild(const DevGraph &src, uint64_t src_top, uint64_t src_ptop, const DevGraph &dst, uint32_t *map,
+                          uint64_t *offs, void *scan_tmp, hipStream_t s);
 size_t rebuild_scan_tmp_bytes(uint64_t n);
 // the pools alone, packed into pool2 / rpool2 (pp / rp: scap u64 each; scan_tmp:
 // 2 x rebuild_scan_tmp_bytes(scap)); slots and tables unchanged
-hipError_t launch_repack(const DevGraph &g, uint64_t top, uint64_t *pp, uint64_t *rp, void *scan_tmp, uint64_t *pool2,
-                         uint32_t *rpool2, hipStream_t s);
+hipError_t launch_repack(const DevGraph &g, uint64_t top, uint64_t ptop, uint64_t *pp, uint64_t *rp, void *scan_tmp,
+                         uint64_t *pool2, uint32_t *rpool2, hipStream_t s);
 
 // routed sharded entry merges (crgc_route.hip)
 constexpr int RT_THREADS = 256;

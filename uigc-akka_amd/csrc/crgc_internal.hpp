@@ -122,6 +122,13 @@ struct Counters {
   unsigned long long pool_top;       // next free edge in pool
   unsigned long long rpool_top;      // next free reverse-candidate entry
   unsigned long long etab_used;      // edge-table keys ever inserted
+  // Sharded graphs: proxy slots live in their own region, [pbase, pbase + proxy_top)
+  // (DevGraph::pbase), so the per-slot passes over the shard's own shadows
+  // (pseudo-roots, sweep, dense frontier scans) never read them.
+  unsigned long long proxy_top;      // proxy slots allocated in this generation
+  unsigned long long proxy_dead;     // ... of which invalidated (their home collected the actor)
+  unsigned long long res_top;        // proxies below pbase + res_top have asked their homes (resolution)
+  unsigned long long alive_cnt[2];   // a rebuild's kept shadows / proxies (k_rb_count_alive)
   // per-merge lists (reset together before every edge pipeline)
   unsigned long long err;
   unsigned long long spin_max;
@@ -146,7 +153,6 @@ struct Counters {
   unsigned long long tail_from;      // level at which k_tail took over
   unsigned long long qn[2], qh[2];   // per-level edge-range queue lengths
   // sharded graphs
-  unsigned long long n_proxy;        // alive proxy slots seen by the last sweep
   unsigned long long n_req;          // kill requests (garbage with a remote supervisor)
   unsigned long long xcnt[MAX_SHARDS];  // ids to send per destination shard
   unsigned long long xpos[MAX_SHARDS];  // scatter cursors
@@ -178,7 +184,9 @@ struct DevGraph {
   uint64_t hcap, hmask;
   IdBucket *htab;
   // vertex SoA
-  uint64_t scap;  // slot capacity (multiple of BLK_SLOTS)
+  uint64_t scap;   // slot capacity (multiple of BLK_SLOTS)
+  uint64_t pbase;  // first proxy slot (multiple of BLK_SLOTS): homes in [0, pbase), proxies in
+                   // [pbase, scap); == scap for an unsharded graph (no proxy region)
   uint64_t *vid;
   int32_t *recv;
   uint8_t *flags;
@@ -280,6 +288,33 @@ __host__ __device__ inline uint32_t shard_of(uint64_t id, uint32_t n_shards) {
 
 __device__ inline bool is_home(const DevGraph &g, uint64_t id) {
   return g.n_shards <= 1 || shard_of(id, g.n_shards) == g.shard;
+}
+
+// Blocks of the slot space a per-block pass visits: the shadows' own blocks
+// [0, nh) and, when `proxies`, the proxy region's [p0, p0 + np), as one run of
+// virtual block numbers vb < n (at(vb) is the real block).
+struct VBlocks {
+  uint32_t nh, n, p0;
+  __device__ uint32_t at(uint32_t vb) const { return vb < nh ? vb : p0 + (vb - nh); }
+  __device__ bool proxy(uint32_t vb) const { return vb >= nh; }
+};
+__device__ inline VBlocks vblocks(const DevGraph &g, bool proxies) {
+  const Counters *c = g.ctr;
+  VBlocks b;
+  b.nh = (uint32_t)((c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS);
+  const uint32_t np = proxies ? (uint32_t)((c->proxy_top + BLK_SLOTS - 1) / BLK_SLOTS) : 0u;
+  b.n = b.nh + np;
+  b.p0 = (uint32_t)(g.pbase / BLK_SLOTS);
+  return b;
+}
+// One past the largest slot in use (homes, and the proxy region when it has any).
+__device__ inline uint64_t slot_end(const DevGraph &g) {
+  const Counters *c = g.ctr;
+  return c->proxy_top ? g.pbase + c->proxy_top : c->slot_top;
+}
+// Virtual slot u of [0, slot_top + proxy_top) -> real slot.
+__device__ inline uint64_t vslot(const DevGraph &g, uint64_t u, uint64_t nh) {
+  return u < nh ? u : g.pbase + (u - nh);
 }
 
 __host__ __device__ inline bool reserved_id(uint64_t id) {
@@ -415,15 +450,24 @@ __device__ inline int id_probe(const DevGraph &g, uint64_t id, uint64_t &bucket,
   return RS_FOUND;
 }
 
+// A new shadow's slot: homes from slot_top (below pbase), proxies from
+// proxy_top (at pbase and above).  SLOT_INVALID (and ERR_SLOTS_FULL) past a region.
+__device__ inline uint64_t region_slot(const DevGraph &g, bool home, unsigned long long k) {
+  const uint64_t s = home ? k : g.pbase + k;
+  return (home ? s < g.pbase : s < g.scap) ? s : ~0ull;
+}
+
 __device__ inline uint32_t id_settle(const DevGraph &g, uint64_t id, uint64_t bucket,
                                      uint32_t slot, int state) {
   const bool ins = state == RS_INSERTED;
   const bool home = ins && is_home(g, id);
-  const unsigned long long s = wave_append(&g.ctr->slot_top, ins);
+  const unsigned long long kh = wave_append(&g.ctr->slot_top, home);
+  const unsigned long long kp = wave_append(&g.ctr->proxy_top, ins && !home);
+  const uint64_t s = ins ? region_slot(g, home, home ? kh : kp) : ~0ull;
   const uint64_t ball = __ballot(home);
   if (lane_id() == 0 && ball) atomicAdd(&g.ctr->inserted, (unsigned long long)__popcll(ball));
   if (ins) {
-    if (s >= g.scap) {
+    if (s == ~0ull) {
       set_err(g.ctr, ERR_SLOTS_FULL);
       slot = SLOT_INVALID;
     } else {
@@ -455,13 +499,13 @@ __device__ inline uint32_t id_settle_block(const DevGraph &g, uint64_t id, uint6
                                            uint32_t slot, int state) {
   const bool ins = state == RS_INSERTED;
   const bool home = ins && is_home(g, id);
-  unsigned long long *const ctrs[2] = {&g.ctr->slot_top, &g.ctr->inserted};
-  const uint32_t v[2] = {ins ? 1u : 0u, home ? 1u : 0u};
-  unsigned long long base[2];
-  block_append<2>(ctrs, v, base);
+  unsigned long long *const ctrs[3] = {&g.ctr->slot_top, &g.ctr->proxy_top, &g.ctr->inserted};
+  const uint32_t v[3] = {home ? 1u : 0u, ins && !home ? 1u : 0u, home ? 1u : 0u};
+  unsigned long long base[3];
+  block_append<3>(ctrs, v, base);
   if (ins) {
-    const unsigned long long s = base[0];
-    if (s >= g.scap) {
+    const uint64_t s = region_slot(g, home, home ? base[0] : base[1]);
+    if (s == ~0ull) {
       set_err(g.ctr, ERR_SLOTS_FULL);
       slot = SLOT_INVALID;
     } else {

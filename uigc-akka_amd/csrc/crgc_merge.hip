@@ -114,17 +114,21 @@ __global__ __launch_bounds__(IDS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 
       // A new shadow starts with a reverse-candidate segment of IDS_RCAP
       // entries: most take their first in-edges in this same merge, which would
       // otherwise all go through k_rv_grow's overflow path (crgc_edges.hip §3).
-      unsigned long long *const ctrs[3] = {&g.ctr->slot_top, &g.ctr->inserted, &g.ctr->rpool_top};
-      const uint32_t v[3] = {nins, nhome, nins * IDS_RCAP};
-      unsigned long long base[3];
-      block_append<3>(ctrs, v, base);
-      unsigned long long s = base[0], ro = base[2];
+      // Homes take slots from slot_top, proxies (sharded graphs) from proxy_top
+      // in their own region above pbase.
+      unsigned long long *const ctrs[4] = {&g.ctr->slot_top, &g.ctr->inserted, &g.ctr->rpool_top,
+                                           &g.ctr->proxy_top};
+      const uint32_t v[4] = {nhome, nhome, nins * IDS_RCAP, nins - nhome};
+      unsigned long long base[4];
+      block_append<4>(ctrs, v, base);
+      unsigned long long kh = base[0], kp = base[3], ro = base[2];
       const bool rfit = ro + (uint64_t)nins * IDS_RCAP <= g.rpcap;
 #pragma unroll
       for (int j = 0; j < IDS_K; ++j) {
         if (st[j] != RS_INSERTED) continue;
         const bool home = is_home(g, id[j]);
-        if (s >= g.scap) {
+        const uint64_t s = region_slot(g, home, home ? kh++ : kp++);
+        if (s == ~0ull) {
           set_err(g.ctr, ERR_SLOTS_FULL);
           slot[j] = SLOT_INVALID;
         } else {
@@ -135,7 +139,6 @@ __global__ __launch_bounds__(IDS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 
             g.radj[s] = make_uint2((uint32_t)ro, rseg_pack(0, IDS_RCAP));
           }
         }
-        ++s;
         ro += IDS_RCAP;
         atomicExch(&g.htab[bucket[j]].val, slot[j]);
       }

@@ -20,19 +20,26 @@ __device__ inline uint32_t rb_cap(uint32_t k) {
   return c;
 }
 
-// 1. live vertices -> dense new slots, id table rebuilt.
-__global__ __launch_bounds__(256) void k_rb_vertices(DevGraph src, uint64_t src_top, DevGraph dst,
+// 1. live vertices -> dense new slots, id table rebuilt.  The source's slots
+//    are visited as one virtual run: its shadows [0, src_top), then its proxy
+//    region [src.pbase, + src_ptop); homes go to the new graph's low slots,
+//    proxies to its proxy region.  `map` is indexed by source slot.
+__global__ __launch_bounds__(256) void k_rb_vertices(DevGraph src, uint64_t src_top, uint64_t src_ptop, DevGraph dst,
                                                      uint32_t *map) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t base = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); base < src_top;
-       base += stride) {
-    const uint64_t v = base + lane_id();
-    const bool alive = v < src_top && (src.flags[v] & FL_ALIVE);
-    const unsigned long long ns = wave_append(&dst.ctr->slot_top, alive);
+  const uint64_t vtop = src_top + src_ptop;
+  for (uint64_t base = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); base < vtop; base += stride) {
+    const uint64_t u = base + lane_id();
+    const uint64_t v = vslot(src, u, src_top);
+    const uint8_t f = u < vtop ? src.flags[v] : 0;
+    const bool alive = f & FL_ALIVE, home = alive && !(f & FL_PROXY);
+    const unsigned long long kh = wave_append(&dst.ctr->slot_top, home);
+    const unsigned long long kp = wave_append(&dst.ctr->proxy_top, alive && !home);
     // past the new arrays (the host sized them too small): dropped, so no later
     // pass indexes a new array with it; the error poisons the handle
-    const bool fits = alive && ns < dst.scap;
-    if (v < src_top) map[v] = fits ? (uint32_t)ns : SLOT_NONE;
+    const uint64_t ns = alive ? region_slot(dst, home, home ? kh : kp) : ~0ull;
+    const bool fits = ns != ~0ull;
+    if (u < vtop) map[v] = fits ? (uint32_t)ns : SLOT_NONE;
     if (!alive) continue;
     if (!fits) {
       set_err(dst.ctr, ERR_SLOTS_FULL);
@@ -41,7 +48,7 @@ __global__ __launch_bounds__(256) void k_rb_vertices(DevGraph src, uint64_t src_
     const uint64_t id = src.vid[v];
     dst.vid[ns] = id;
     dst.recv[ns] = src.recv[v];
-    dst.flags[ns] = src.flags[v];
+    dst.flags[ns] = f;
     uint64_t h = mix64(id) & dst.hmask;
     for (uint64_t p = 0; p < dst.hcap; ++p) {
       if (atomicCAS((unsigned long long *)&dst.htab[h].key, (unsigned long long)KEY_EMPTY,
@@ -203,26 +210,33 @@ __global__ void k_rb_rpool_top(Counters *c, const uint64_t *grand) { c->rpool_to
 
 // 5. reverse candidate lists from the kept edges: capacities from the
 //    in-degrees counted in k_rb_edges, offsets by scan, then a fill pass.
-__global__ __launch_bounds__(256) void k_rb_rcaps(DevGraph dst, uint64_t *caps) {
-  const uint64_t n = dst.ctr->slot_top;
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < dst.scap; v += stride)
-    caps[v] = v < n ? rb_cap(dst.rnew[v]) : 0;
+// Whether slot v of a (new) graph is in use: its shadows [0, slot_top), its
+// proxies [pbase, pbase + proxy_top) — both clamped to the arrays (k_rb_vertices
+// maps slots past a region to SLOT_NONE, but the counters still count them —
+// ADVICE r4).
+__device__ inline bool rb_used(const DevGraph &d, uint64_t v) {
+  const Counters *c = d.ctr;
+  return v < min((uint64_t)c->slot_top, d.pbase) || (v >= d.pbase && v < min(d.pbase + c->proxy_top, d.scap));
 }
 
-// (slot_top clamped to the new arrays: k_rb_vertices maps slots past dst.scap to
-// SLOT_NONE, but slot_top still counts them — ADVICE r4)
-__global__ __launch_bounds__(256) void k_rb_rsetup(DevGraph dst, const uint64_t *offs) {
-  const uint64_t n = min((uint64_t)dst.ctr->slot_top, dst.scap);
+__global__ __launch_bounds__(256) void k_rb_rcaps(DevGraph dst, uint64_t *caps) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < n; v += stride) {
+  for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < dst.scap; v += stride)
+    caps[v] = rb_used(dst, v) ? rb_cap(dst.rnew[v]) : 0;
+}
+
+__global__ __launch_bounds__(256) void k_rb_rsetup(DevGraph dst, const uint64_t *offs) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < dst.scap; v += stride) {
+    if (!rb_used(dst, v)) continue;
     dst.radj[v] = make_uint2((uint32_t)offs[v], rseg_pack(0, rb_cap(dst.rnew[v])));
     dst.rnew[v] = 0;
   }
 }
 
+// (owners: the shadows' own slots; proxies have no out-edges)
 __global__ __launch_bounds__(256) void k_rb_rfill(DevGraph dst) {
-  const uint64_t n = min((uint64_t)dst.ctr->slot_top, dst.scap);
+  const uint64_t n = min((uint64_t)dst.ctr->slot_top, dst.pbase);
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t o = (uint64_t)blockIdx.x * 256 + threadIdx.x; o < n; o += stride) {
     const uint2 ad = dst.adj[o];
@@ -249,11 +263,14 @@ __global__ __launch_bounds__(256) void k_rb_rfill(DevGraph dst) {
 // change.  So a merge whose pools would overflow repacks instead of rebuilding
 // the graph — no slot renumbering, and about a third of a rebuild's memory
 // (the C4 graph on one GPU: 51 GB of new pools against a second 130-GB graph).
-__global__ __launch_bounds__(256) void k_rp_sizes(DevGraph g, uint64_t top, uint64_t *pp, uint64_t *rp) {
+// (top / ptop: the graph's shadow and proxy slot counts)
+__global__ __launch_bounds__(256) void k_rp_sizes(DevGraph g, uint64_t top, uint64_t ptop, uint64_t *pp,
+                                                  uint64_t *rp) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < g.scap; v += stride) {
-    pp[v] = v < top ? seg_cap(g.adj[v].y) : 0;
-    rp[v] = v < top ? rseg_cap(g.radj[v].y) : 0;
+    const bool used = v < top || (v >= g.pbase && v < g.pbase + ptop);
+    pp[v] = used ? seg_cap(g.adj[v].y) : 0;
+    rp[v] = used ? rseg_cap(g.radj[v].y) : 0;
   }
 }
 
@@ -275,12 +292,14 @@ __device__ inline void rp_copy(const T *from, T *to, uint32_t len) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_rp_move(DevGraph g, uint64_t top, const uint64_t *pp, const uint64_t *rp,
-                                                 uint64_t *pool2, uint32_t *rpool2) {
+__global__ __launch_bounds__(256) void k_rp_move(DevGraph g, uint64_t top, uint64_t ptop, const uint64_t *pp,
+                                                 const uint64_t *rp, uint64_t *pool2, uint32_t *rpool2) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t base = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); base < top; base += stride) {
-    const uint64_t v = base + lane_id();
-    const bool in = v < top;
+  const uint64_t vtop = top + ptop;
+  for (uint64_t base = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); base < vtop; base += stride) {
+    const uint64_t u = base + lane_id();
+    const bool in = u < vtop;
+    const uint64_t v = vslot(g, u, top);
     const uint2 ad = in ? g.adj[v] : make_uint2(0, 0);
     const uint2 rd = in ? g.radj[v] : make_uint2(0, 0);
     const uint64_t po = in ? pp[v] : 0, ro = in ? rp[v] : 0;
@@ -293,54 +312,63 @@ __global__ __launch_bounds__(256) void k_rp_move(DevGraph g, uint64_t top, const
   }
 }
 
-hipError_t launch_repack(const DevGraph &g, uint64_t top, uint64_t *pp, uint64_t *rp, void *scan_tmp, uint64_t *pool2,
-                         uint32_t *rpool2, hipStream_t s) {
+hipError_t launch_repack(const DevGraph &g, uint64_t top, uint64_t ptop, uint64_t *pp, uint64_t *rp, void *scan_tmp,
+                         uint64_t *pool2, uint32_t *rpool2, hipStream_t s) {
   launch_begin();
   const int grid = grid_for(g.scap, 256, 8192);
   const uint64_t nb = (g.scap + SCAN_TILE - 1) / SCAN_TILE;
   uint64_t *tp = (uint64_t *)scan_tmp, *tr = tp + nb + 2;
-  hipLaunchKernelGGL(k_rp_sizes, dim3(grid), dim3(256), 0, s, g, top, pp, rp);
+  hipLaunchKernelGGL(k_rp_sizes, dim3(grid), dim3(256), 0, s, g, top, ptop, pp, rp);
   exclusive_scan(pp, g.scap, tp, s);
   exclusive_scan(rp, g.scap, tr, s);
   hipLaunchKernelGGL(k_rb_pool_top, dim3(1), dim3(1), 0, s, g.ctr, tp + nb);
   hipLaunchKernelGGL(k_rb_rpool_top, dim3(1), dim3(1), 0, s, g.ctr, tr + nb);
-  hipLaunchKernelGGL(k_rp_move, dim3(grid_for(top, 256, 8192)), dim3(256), 0, s, g, top, pp, rp, pool2, rpool2);
+  hipLaunchKernelGGL(k_rp_move, dim3(grid_for(top + ptop, 256, 8192)), dim3(256), 0, s, g, top, ptop, pp, rp, pool2,
+                     rpool2);
   return hipGetLastError();
 }
 
-// 0. the alive slots a rebuild keeps (homes and proxies), counted exactly: the
-//    host sizes the new arrays from it.
-__global__ __launch_bounds__(256) void k_rb_count_alive(DevGraph src, uint64_t src_top, unsigned long long *out) {
+// 0. the alive slots a rebuild keeps, counted exactly (out[0] shadows, out[1]
+//    proxies): the host sizes the new arrays from them.
+__global__ __launch_bounds__(256) void k_rb_count_alive(DevGraph src, uint64_t src_top, uint64_t src_ptop,
+                                                        unsigned long long *out) {
   const uint64_t stride = (uint64_t)gridDim.x * 256 * 16;
-  uint32_t k = 0;
-  for (uint64_t v = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16; v < src_top; v += stride) {
-    if (v + 16 <= src_top) {
-      const uint4 f = *(const uint4 *)(src.flags + v);
-      const uint32_t w[4] = {f.x, f.y, f.z, f.w};
+  uint32_t k[2] = {0, 0};
+  for (int r = 0; r < 2; ++r) {
+    const uint64_t lo = r ? src.pbase : 0, n = r ? src_ptop : src_top;
+    for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16; i < n; i += stride) {
+      const uint64_t v = lo + i;
+      if (i + 16 <= n) {
+        const uint4 f = *(const uint4 *)(src.flags + v);
+        const uint32_t w[4] = {f.x, f.y, f.z, f.w};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) k += __popc(w[j] & 0x01010101u * FL_ALIVE);
-    } else {
-      for (uint64_t u = v; u < src_top; ++u) k += (src.flags[u] & FL_ALIVE) ? 1u : 0u;
+        for (int j = 0; j < 4; ++j) k[r] += __popc(w[j] & 0x01010101u * FL_ALIVE);
+      } else {
+        for (uint64_t u = v; u < lo + n; ++u) k[r] += (src.flags[u] & FL_ALIVE) ? 1u : 0u;
+      }
     }
   }
-  const uint32_t ws = wave_sum(k);
-  if (lane_id() == 0 && ws) atomicAdd(out, (unsigned long long)ws);
+  for (int r = 0; r < 2; ++r) {
+    const uint32_t ws = wave_sum(k[r]);
+    if (lane_id() == 0 && ws) atomicAdd(&out[r], (unsigned long long)ws);
+  }
 }
 
-hipError_t launch_count_alive(const DevGraph &src, uint64_t src_top, unsigned long long *out, hipStream_t s) {
+hipError_t launch_count_alive(const DevGraph &src, uint64_t src_top, uint64_t src_ptop, unsigned long long *out,
+                              hipStream_t s) {
   launch_begin();
-  if (src_top == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rb_count_alive, dim3(grid_for((src_top + 15) / 16, 256, 4096)), dim3(256), 0, s, src,
-                     src_top, out);
+  if (src_top + src_ptop == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rb_count_alive, dim3(grid_for((std::max(src_top, src_ptop) + 15) / 16, 256, 4096)), dim3(256),
+                     0, s, src, src_top, src_ptop, out);
   return hipGetLastError();
 }
 
-hipError_t launch_rebuild(const DevGraph &src, uint64_t src_top, const DevGraph &dst, uint32_t *map,
-                          uint32_t *newdeg, uint64_t *offs, void *scan_tmp, hipStream_t s) {
+hipError_t launch_rebuild(const DevGraph &src, uint64_t src_top, uint64_t src_ptop, const DevGraph &dst, uint32_t *map,
+                          uint64_t *offs, void *scan_tmp, hipStream_t s) {
   launch_begin();
-  (void)newdeg;
   const int grid = grid_for(src_top, 256, 8192);
-  hipLaunchKernelGGL(k_rb_vertices, dim3(grid), dim3(256), 0, s, src, src_top, dst, map);
+  hipLaunchKernelGGL(k_rb_vertices, dim3(grid_for(src_top + src_ptop, 256, 8192)), dim3(256), 0, s, src, src_top,
+                     src_ptop, dst, map);
   hipLaunchKernelGGL(k_rb_count, dim3(grid), dim3(256), 0, s, src, src_top, map, offs);
   exclusive_scan(offs, dst.scap, (uint64_t *)scan_tmp, s);
   const uint64_t nb = (dst.scap + SCAN_TILE - 1) / SCAN_TILE;

@@ -132,8 +132,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   }
   const bool sp_cur = !ROOTS && sparse_level(c, L, a.sparse_thresh);
   const bool sp_next = sparse_level(c, L + 1, a.sparse_thresh);
-  const uint64_t slot_top = c->slot_top;
-  const uint32_t nblk = (uint32_t)((slot_top + BLK_SLOTS - 1) / BLK_SLOTS);
+  // Level 0 scans the shadows' own blocks; later levels the proxy region too
+  // (sharded graphs: a proxy block only marks and lists its proxies).
+  const VBlocks vbs = vblocks(g, !ROOTS);
   const int wv = threadIdx.x >> 6;
   const int lane = lane_id();
   const uint32_t gw = blockIdx.x * 4 + wv;
@@ -152,7 +153,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   const bool lane_pull = pull && !listing && !sharded && !a.alpha;
   uint32_t n_front = 0, n_sup = 0, n_edges = 0;
 
-  for (uint32_t blk = gw; blk < nblk; blk += nw) {
+  for (uint32_t vb = gw; vb < vbs.n; vb += nw) {
+    const uint32_t blk = vbs.at(vb);
     if (sp_cur && Dc[blk] == 0) continue;
     const uint64_t base = (uint64_t)blk * BLK_SLOTS + (uint64_t)lane * 32;
     const uint32_t word = g.vis[(uint64_t)blk * 64 + lane];
@@ -205,6 +207,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     }
     if (m) g.vis[(uint64_t)blk * 64 + lane] = word | m;
     if (sp_cur && lane == 0) Dc[blk] = 0;
+    if (!ROOTS && vbs.proxy(vb)) {
+      // A proxy block: its newly marked proxies join the block's export list
+      // (sent home after the round); proxies have no edges, so nothing else —
+      // and they do not count in the level's frontier (a level that only
+      // reaches proxies ends the round).
+      const uint32_t cnt = __popc(m);
+      if (__ballot(cnt != 0)) {
+        const uint32_t incl = wave_incl_scan(cnt);
+        const uint32_t n0 = g.xp_cnt[blk];
+        uint32_t pos = n0 + incl - cnt;
+        for (uint32_t mm = m; mm; mm &= mm - 1) g.xp_buf[(uint64_t)blk * BLK_SLOTS + pos++] = (uint32_t)(base + __ffs(mm) - 1);
+        if (lane == 63) g.xp_cnt[blk] = n0 + incl;
+      }
+      continue;
+    }
 
     // Compact this block's frontier slots into LDS (ballot/popc scan).
     const uint32_t cnt = __popc(m);
@@ -453,13 +470,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     // positive count (RC_POS), and stops at the first.  A thread owns 4
     // consecutive slots (their candidate bytes are one u32), so loads of
     // flags / bytes / radj are coalesced across the wave.
-    const uint64_t nq = (c->slot_top + 3) / 4;
+    // (sharded graphs: the proxy region's quads after the shadows' own — a
+    // proxy reached from the expandable frontier is marked like any target)
+    const uint64_t nqh = (c->slot_top + 3) / 4;
+    const uint64_t nq = nqh + (c->proxy_top + 3) / 4;
     const uint64_t gs = (uint64_t)gridDim.x * 256;
     // (Loading the hints and in-candidate ranges with the flags while a
     // quarter of the slots are unmarked, and the hints' frontier bits with
     // the lists' first chunks, made level 1 slower: 146 -> 181 us, r3g/ab4.)
     for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += gs) {
-      const uint64_t v0 = q * 4;
+      const uint64_t v0 = q < nqh ? q * 4 : g.pbase + (q - nqh) * 4;
       const uint32_t fl = *(const uint32_t *)(g.flags + v0);
       const uint32_t cand = *(const uint32_t *)(Fn + v0);
       const uint32_t vb = (g.vis[v0 >> 5] >> (v0 & 31)) & 0xFu;
@@ -930,7 +950,7 @@ __global__ __launch_bounds__(BIN_T) void k_bin_apply(DevGraph g, LevelArgs a) {
   __syncthreads();
   uint8_t *Fn = g.front[1];
   const uint64_t lo = (uint64_t)b << a.bin_shift;
-  const uint64_t top = g.ctr->slot_top;
+  const uint64_t top = slot_end(g);  // (sharded graphs: bins over the proxy region too)
   const uint64_t hi = min(lo + span, top);
   for (uint64_t q = lo + tid; q < hi; q += BIN_T) {
     const uint32_t rel = (uint32_t)(q - lo);
@@ -1288,8 +1308,10 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
       base += tot;
     }
   }
-  const bool lv = top <= (uint64_t)TAIL_LVIS_WORDS * 32;
-  const uint32_t nw = (uint32_t)((top + 31) / 32);
+  // (the LDS copy must cover every slot a walk can claim: proxies too)
+  const uint64_t vend = slot_end(g);
+  const bool lv = vend <= (uint64_t)TAIL_LVIS_WORDS * 32;
+  const uint32_t nw = (uint32_t)((vend + 31) / 32);
   if (lv)
     for (uint32_t k = threadIdx.x; k < nw; k += TAIL_THREADS) s_vis[k] = g.vis[k];
   __syncthreads();
@@ -1376,13 +1398,17 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
 // Per-trace reset in one launch: the marked bitmap, the per-block level tags
 // and proxy listings of the blocks this trace can touch, the per-workgroup
 // statistics, and the trace counters (marked .. the end of the level ring).
-__global__ __launch_bounds__(256) void k_trace_reset(DevGraph g, uint64_t nblk, uint32_t ctr_from,
+// nh blocks from slot 0 and np blocks from the proxy region (pbase).
+__global__ __launch_bounds__(256) void k_trace_reset(DevGraph g, uint64_t nh, uint64_t np, uint32_t ctr_from,
                                                      uint32_t ctr_words) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   const uint64_t t0 = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t nblk = nh + np, p0 = g.pbase / BLK_SLOTS;
+  auto at = [&](uint64_t vb) { return vb < nh ? vb : p0 + (vb - nh); };
   uint4 *vis4 = reinterpret_cast<uint4 *>(g.vis);  // 2048 slots = 64 words = 16 uint4 per block
-  for (uint64_t i = t0; i < nblk * 16; i += stride) vis4[i] = make_uint4(0, 0, 0, 0);
-  for (uint64_t i = t0; i < nblk; i += stride) {
+  for (uint64_t i = t0; i < nblk * 16; i += stride) vis4[at(i / 16) * 16 + i % 16] = make_uint4(0, 0, 0, 0);
+  for (uint64_t vb = t0; vb < nblk; vb += stride) {
+    const uint64_t i = at(vb);
     g.qn_tag[i] = 0;
     g.tl_tag[i] = 0;
     if (g.xp_cnt) g.xp_cnt[i] = 0;
@@ -1393,11 +1419,11 @@ __global__ __launch_bounds__(256) void k_trace_reset(DevGraph g, uint64_t nblk, 
   for (uint64_t i = t0; i < ctr_words; i += stride) cw[i] = 0;
 }
 
-hipError_t launch_trace_reset(const DevGraph &g, uint64_t nblk, uint32_t ctr_from, uint32_t ctr_words,
+hipError_t launch_trace_reset(const DevGraph &g, uint64_t nh, uint64_t np, uint32_t ctr_from, uint32_t ctr_words,
                               hipStream_t s) {
   launch_begin();
-  hipLaunchKernelGGL(k_trace_reset, dim3(grid_for(std::max<uint64_t>(nblk * 16, ctr_words), 256, 2048)),
-                     dim3(256), 0, s, g, nblk, ctr_from, ctr_words);
+  hipLaunchKernelGGL(k_trace_reset, dim3(grid_for(std::max<uint64_t>((nh + np) * 16, ctr_words), 256, 2048)),
+                     dim3(256), 0, s, g, nh, np, ctr_from, ctr_words);
   return hipGetLastError();
 }
 
@@ -1420,14 +1446,14 @@ __global__ __launch_bounds__(256) void k_sweep(DevGraph g, int should_kill) {
   const int lane = lane_id();
   const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const uint32_t nw = gridDim.x * 4;
-  uint32_t n_live = 0, n_npe = 0, n_prox = 0, n_req = 0;
+  uint32_t n_live = 0, n_npe = 0, n_req = 0;
   uint64_t n_edges = 0;
   for (uint32_t blk = gw; blk < nblk; blk += nw) {
     const uint64_t base = (uint64_t)blk * BLK_SLOTS + (uint64_t)lane * 32;
     const uint32_t word = g.vis[(uint64_t)blk * 64 + lane];
     const uint4 f4[2] = {*(const uint4 *)(g.flags + base), *(const uint4 *)(g.flags + base + 16)};
     const uint32_t fa = flag_bits(f4, FL_ALIVE), fp = flag_bits(f4, FL_PROXY);
-    const uint32_t alive = fa & ~fp, prox = fa & fp;
+    const uint32_t alive = fa & ~fp;  // (proxies live in their own region: none here)
     const uint32_t halted = flag_bits(f4, FL_HALTED), local = flag_bits(f4, FL_LOCAL);
     uint32_t kill = 0, req = 0;
     // traced edges (:231): the nonzero out-counts of the marked, unhalted shadows
@@ -1451,7 +1477,6 @@ __global__ __launch_bounds__(256) void k_sweep(DevGraph g, int should_kill) {
     }
     const uint32_t garbage = alive & ~word;
     n_live += __popc(alive & word);
-    n_prox += __popc(prox);
     uint32_t gm = garbage;
     while (gm) {
       const int j = __ffs(gm) - 1;
@@ -1508,14 +1533,12 @@ __global__ __launch_bounds__(256) void k_sweep(DevGraph g, int should_kill) {
   }
   const uint64_t tl = block_sum4(n_live);
   const uint64_t tn = block_sum4(n_npe);
-  const uint64_t tp = block_sum4(n_prox);
   const uint64_t tr = block_sum4(n_req);
   const uint64_t te = block_sum64(n_edges);
   if (threadIdx.x == 0) {
     g.blkstat[(uint64_t)blockIdx.x * 4 + STAT_LIVE] = tl;
     g.blkstat[(uint64_t)blockIdx.x * 4 + STAT_EDGES] = te;  // the only writer of this partial
     if (tn) atomicAdd(&c->npe, (unsigned long long)tn);
-    if (tp) atomicAdd(&c->n_proxy, (unsigned long long)tp);
     if (tr) atomicAdd(&c->n_req, (unsigned long long)tr);
   }
 }
@@ -1777,12 +1800,18 @@ hipError_t launch_list(const DevGraph &g, int mode, bool scatter, uint32_t *buf,
 // slots, or — when that is longer — a bitmap over the home's slots; one
 // without travels as its id.
 
-// Proxies homed at the shards in `mask` forget their home slots.
+// Proxies homed at the shards in `mask` forget their home slots, and every
+// proxy is looked at again by the next listing (res_top).
 __global__ __launch_bounds__(256) void k_phs_reset(DevGraph g, uint64_t mask) {
-  const uint64_t top = g.ctr->slot_top, stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < top; v += stride)
+  const uint64_t top = g.pbase + g.ctr->proxy_top, stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t v = g.pbase + (uint64_t)blockIdx.x * 256 + threadIdx.x; v < top; v += stride)
     if ((g.flags[v] & FL_PROXY) && ((mask >> shard_of(g.vid[v], g.n_shards)) & 1ull)) g.phs[v] = PHS_NONE;
+  if (blockIdx.x == 0 && threadIdx.x == 0) g.ctr->res_top = 0;
 }
+
+// Proxies below res_top have asked already (or were reset and res_top is 0):
+// after a resolution every proxy so far has.
+__global__ void k_res_done(Counters *c) { c->res_top = c->proxy_top; }
 
 __device__ inline bool unresolved_proxy(const DevGraph &g, uint64_t v) {
   return (g.flags[v] & (FL_ALIVE | FL_PROXY)) == (FL_ALIVE | FL_PROXY) && g.phs[v] == PHS_NONE;
@@ -1796,8 +1825,10 @@ __global__ __launch_bounds__(256) void k_res_list(DevGraph g, uint64_t *send, ui
   __shared__ unsigned long long base[MAX_SHARDS];
   for (uint32_t d = threadIdx.x; d < MAX_SHARDS; d += 256) hist[d] = 0;
   __syncthreads();
-  const uint64_t top = g.ctr->slot_top, stride = (uint64_t)gridDim.x * 256;
-  const uint64_t v0 = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  // the proxies created since the last resolution (all of them after a reset):
+  // steady-state traces list only the new ones
+  const uint64_t top = g.pbase + g.ctr->proxy_top, stride = (uint64_t)gridDim.x * 256;
+  const uint64_t v0 = g.pbase + g.ctr->res_top + (uint64_t)blockIdx.x * 256 + threadIdx.x;
   for (uint64_t v = v0; v < top; v += stride)
     if (unresolved_proxy(g, v)) atomicAdd(&hist[shard_of(g.vid[v], g.n_shards)], 1u);
   __syncthreads();
@@ -1840,10 +1871,11 @@ __global__ __launch_bounds__(256) void k_phs_set(DevGraph g, const uint32_t *slo
 }
 
 hipError_t launch_resolve(const DevGraph &g, int step, uint64_t mask, uint64_t *send, uint32_t *slots,
-                          const uint64_t *ids, uint64_t n, uint32_t *ans, uint64_t slot_top, hipStream_t s) {
+                          const uint64_t *ids, uint64_t n, uint32_t *ans, uint64_t n_proxy, hipStream_t s) {
   launch_begin();
-  const int vgrid = grid_for(slot_top, 256, 4096);
+  const int vgrid = grid_for(std::max<uint64_t>(n_proxy, 1), 256, 4096);
   switch (step) {
+    case 5: hipLaunchKernelGGL(k_res_done, dim3(1), dim3(1), 0, s, g.ctr); break;
     case 0: hipLaunchKernelGGL(k_phs_reset, dim3(vgrid), dim3(256), 0, s, g, mask); break;
     case 1: hipLaunchKernelGGL(k_res_list<false>, dim3(vgrid), dim3(256), 0, s, g, send, slots); break;
     case 2: hipLaunchKernelGGL(k_res_list<true>, dim3(vgrid), dim3(256), 0, s, g, send, slots); break;
@@ -1859,15 +1891,18 @@ hipError_t launch_resolve(const DevGraph &g, int step, uint64_t mask, uint64_t *
 // Marked proxies listed by k_frontier / k_tail, by destination: ids of the
 // unresolved (xcnt), home slots of the resolved (xcnt2); then the scatter
 // into the byte layout the host derived from the all-gathered counts.
+// Marked proxies are listed in the proxy region's blocks (k_frontier, k_tail).
 template <bool SCATTER>
-__global__ __launch_bounds__(256) void k_xlist(DevGraph g, const uint32_t *buf, const uint32_t *cnt,
-                                               uint64_t nblk, char *send, XSend x) {
+__global__ __launch_bounds__(256) void k_xlist(DevGraph g, const uint32_t *buf, const uint32_t *cnt, char *send,
+                                               XSend x) {
   __shared__ uint32_t hist[2][MAX_SHARDS];
   __shared__ unsigned long long base[2][MAX_SHARDS];
   for (uint32_t d = threadIdx.x; d < 2 * MAX_SHARDS; d += 256) hist[d / MAX_SHARDS][d % MAX_SHARDS] = 0;
   __syncthreads();
   const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
-  for (uint64_t blk = gw; blk < nblk; blk += nw) {
+  const uint64_t p0 = g.pbase / BLK_SLOTS;
+  const uint64_t nblk = p0 + (g.ctr->proxy_top + BLK_SLOTS - 1) / BLK_SLOTS;
+  for (uint64_t blk = p0 + gw; blk < nblk; blk += nw) {
     const uint32_t n = cnt[blk];
     for (uint32_t i = lane_id(); i < n; i += 64) {
       const uint32_t v = buf[blk * BLK_SLOTS + i];
@@ -1891,7 +1926,7 @@ __global__ __launch_bounds__(256) void k_xlist(DevGraph g, const uint32_t *buf, 
     hist[0][d] = hist[1][d] = 0;
   }
   __syncthreads();
-  for (uint64_t blk = gw; blk < nblk; blk += nw) {
+  for (uint64_t blk = p0 + gw; blk < nblk; blk += nw) {
     const uint32_t n = cnt[blk];
     for (uint32_t i = lane_id(); i < n; i += 64) {
       const uint32_t v = buf[blk * BLK_SLOTS + i];
@@ -1915,11 +1950,11 @@ hipError_t launch_xlist(const DevGraph &g, bool scatter, uint64_t nblk, char *se
                         hipStream_t s) {
   launch_begin();
   if (nblk == 0) return hipSuccess;
-  const int grid = (int)((nblk + 3) / 4);
+  const int grid = (int)std::min<uint64_t>((nblk + 3) / 4, 8192);
   if (scatter)
-    hipLaunchKernelGGL(k_xlist<true>, dim3(grid), dim3(256), 0, s, g, g.xp_buf, g.xp_cnt, nblk, send, x);
+    hipLaunchKernelGGL(k_xlist<true>, dim3(grid), dim3(256), 0, s, g, g.xp_buf, g.xp_cnt, send, x);
   else
-    hipLaunchKernelGGL(k_xlist<false>, dim3(grid), dim3(256), 0, s, g, g.xp_buf, g.xp_cnt, nblk, send, x);
+    hipLaunchKernelGGL(k_xlist<false>, dim3(grid), dim3(256), 0, s, g, g.xp_buf, g.xp_cnt, send, x);
   return hipGetLastError();
 }
 
@@ -2008,6 +2043,7 @@ hipError_t launch_requests(const DevGraph &g, int phase, const uint64_t *ids, ui
 // will name a new incarnation if they ever reappear — SURVEY E9).
 __global__ __launch_bounds__(256) void k_invalidate(DevGraph g, const uint64_t *ids, uint64_t n) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
+  uint32_t dead = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
     uint64_t bucket = KEY_EMPTY;
     const uint32_t v = id_find(g, ids[i], &bucket);
@@ -2015,7 +2051,10 @@ __global__ __launch_bounds__(256) void k_invalidate(DevGraph g, const uint64_t *
     if ((g.flags[v] & (FL_ALIVE | FL_PROXY)) != (FL_ALIVE | FL_PROXY)) continue;
     g.htab[bucket].key = KEY_TOMB;
     g.flags[v] = 0;
+    ++dead;
   }
+  const uint64_t t = block_sum4(dead);  // the proxy region's dead slots (the rebuild trigger)
+  if (threadIdx.x == 0 && t) atomicAdd(&g.ctr->proxy_dead, (unsigned long long)t);
 }
 
 hipError_t launch_invalidate(const DevGraph &g, const uint64_t *ids, uint64_t n, hipStream_t s) {
