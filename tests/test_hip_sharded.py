@@ -74,12 +74,15 @@ def test_random_spec_sharded_matches_oracle_every_wakeup(sharded, oracle_mod, G,
     assert h.live_count() == 1
 
 
-@pytest.mark.parametrize("xbits", ["1", "2"])
+@pytest.mark.parametrize("xbits,xlevels", [("1", "0"), ("2", "0"), ("1", "1"), ("2", "2")])
 @pytest.mark.parametrize("G,seed,cap", [(2, 11, 0), (3, 12, 0), (4, 13, 64)])
-def test_fuzz_sharded(sharded, oracle_mod, G, seed, cap, xbits, monkeypatch):
+def test_fuzz_sharded(sharded, oracle_mod, G, seed, cap, xbits, xlevels, monkeypatch):
     # CRGC_XBITS=2: every resolved mark travels in a home-slot bitmap; cap 64
-    # rebuilds the shards often, so cached home slots go stale and re-resolve
+    # rebuilds the shards often (both slot regions), so cached home slots go
+    # stale and re-resolve; CRGC_XLEVELS=k: every mark round runs at most k
+    # levels, its pending candidates carried into the next round
     monkeypatch.setenv("CRGC_XBITS", xbits)
+    monkeypatch.setenv("CRGC_XLEVELS", xlevels)
     h, o = sharded(G, vertex_capacity=cap, edge_capacity=cap), oracle_mod.OracleGraph()
     fz = fuzz.Fuzz(seed)
     for step in range(14):
@@ -281,13 +284,16 @@ def test_rccl_transport_single_rank(hip_mod, oracle_mod):
         t.close()
 
 
-@pytest.mark.parametrize("xbits", ["0", "1", "2"])
-def test_c4_shape_eight_shards(sharded, oracle_mod, xbits, monkeypatch):
+@pytest.mark.parametrize("xbits,xlevels", [("0", "0"), ("1", "0"), ("2", "0"), ("1", "1"), ("1", "3")])
+def test_c4_shape_eight_shards(sharded, oracle_mod, xbits, xlevels, monkeypatch):
     """G = 8 logical shards (the 8-GPU layout of C4) on a scaled C2/C4-shaped
     power-law graph with §8d wakeups (9 % busy, 1 % in flight), split batches:
     bit-exact against the unsharded oracle at every wakeup, with marks sent as
-    ids only (0), in the cheaper of home slots / bitmaps (1), or as bitmaps (2)."""
+    ids only (0), in the cheaper of home slots / bitmaps (1), or as bitmaps (2),
+    and rounds run to each shard's local fixpoint (XLEVELS 0) or capped at 1 / 3
+    levels."""
     monkeypatch.setenv("CRGC_XBITS", xbits)
+    monkeypatch.setenv("CRGC_XLEVELS", xlevels)
     V = 200_000
     w = world.World(seed=0x5EED + 4)
     w.bulk_graph(V, 10 * V, alpha=2.1, n_roots=V // 1000, cap=100000)
