@@ -488,8 +488,81 @@ int device_error(crgc_graph *h) {
   return CRGC_E_NOMEM;
 }
 
+// The last trace's garbage / kill lists outlive a generation: crgc_last_trace
+// may still copy them (two-phase trace, or a trace whose buffers were short).
+// They can hold more ids than the new generation has slots.
+hipError_t carry_lists(crgc_graph *h, Arrays &dst) {
+  if (!h->have_last) return hipSuccess;
+  auto carry = [&](uint64_t *&dptr, const uint64_t *src, uint64_t n) -> hipError_t {
+    if (n > dst.caps.scap) {
+      hipFree(dptr);
+      dptr = nullptr;
+      if (hipError_t r = dmalloc(&dptr, n)) return r;
+    }
+    return n ? hipMemcpyAsync(dptr, src, n * 8, hipMemcpyDeviceToDevice, h->stream) : hipSuccess;
+  };
+  hipError_t e = carry(dst.d.out_ids, h->g.d.out_ids, h->last_garbage);
+  if (e == hipSuccess) e = carry(dst.d.out_kill, h->g.d.out_kill, h->last_kill);
+  return e;
+}
+
+// Larger arrays for the same slots (crgc_rebuild.hip, grow): an unsharded graph
+// that outgrew its capacities with few dead slots keeps its numbering — the
+// per-slot arrays and the pools are copied as they are, the hash tables are
+// re-hashed — instead of a rebuild (the C2 long run: 129 ms per rebuild,
+// profiles/r5a; nothing of the trace's pull hints or candidate order is lost).
+int grow(crgc_graph *h, uint64_t ids, uint64_t atoms) {
+  const uint64_t top = h->slot_top;
+  Caps c = caps_for(std::max<uint64_t>(top, 1), 0, false, h->etab_used, ids, atoms);
+  // never smaller than before (a grow may be for the tables, not the slots)
+  const Caps &oc = h->g.caps;
+  c.scap = c.pbase = std::max(c.scap, oc.scap);
+  c.hcap = std::max(c.hcap, oc.hcap);
+  c.ecap = std::max(c.ecap, oc.ecap);
+  c.pcap = std::min<uint64_t>(std::max(c.pcap, oc.pcap + oc.pcap / 2), 0xFFFFFFF0ull);
+  if (h->knobs.level_log)
+    fprintf(stderr, "[crgc] grow: slots %llu -> %llu, id table %llu -> %llu, edge table %llu -> %llu, pools %llu -> %llu\n",
+            (unsigned long long)h->g.caps.scap, (unsigned long long)c.scap, (unsigned long long)h->g.caps.hcap,
+            (unsigned long long)c.hcap, (unsigned long long)h->g.caps.ecap, (unsigned long long)c.ecap,
+            (unsigned long long)h->g.caps.pcap, (unsigned long long)c.pcap);
+  Arrays dst;
+  HIP_TRY(alloc_arrays(dst, c, h->ctr, h->stream, h->G, h->shard, h->tp != nullptr));
+  const DevGraph &o = h->g.d;
+  DevGraph &d = dst.d;
+  hipError_t e = hipSuccess;
+  auto cp = [&](void *to, const void *from, size_t bytes) {
+    if (e == hipSuccess && bytes) e = hipMemcpyAsync(to, from, bytes, hipMemcpyDeviceToDevice, h->stream);
+  };
+  cp(d.vid, o.vid, top * 8);
+  cp(d.recv, o.recv, top * 4);
+  cp(d.flags, o.flags, top);
+  cp(d.sup, o.sup, top * 4);
+  cp(d.adj, o.adj, top * 8);
+  cp(d.vseq, o.vseq, top * 8);
+  cp(d.sseq, o.sseq, top * 8);
+  cp(d.nzdeg, o.nzdeg, top * 4);
+  cp(d.radj, o.radj, top * 8);
+  cp(d.par, o.par, top * 4);
+  cp(d.pool, o.pool, h->pool_top * 8);
+  cp(d.rpool, o.rpool, h->rpool_top * 4);
+  if (e == hipSuccess) e = launch_grow_tables(o, d, h->stream);
+  if (e == hipSuccess) e = carry_lists(h, dst);
+  if (e == hipSuccess) e = sync_counters(h);
+  if (e != hipSuccess) {
+    free_arrays(dst);
+    h->poisoned = true;
+    return map_hip(e);
+  }
+  free_arrays(h->g);
+  h->g = dst;
+  if (int rc = device_error(h)) return rc;
+  return CRGC_OK;
+}
+
 // Rebuild into fresh arrays with room for `ids`/`atoms` more, then swap.
-int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms) {
+// may_grow: an unsharded graph with few dead slots (at most a quarter) grows
+// instead (same slots, larger arrays).
+int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms, bool may_grow = false) {
   HIP_TRY(sync_counters(h));
   if (int rc = device_error(h)) return rc;
   const uint64_t src_top = h->slot_top, src_ptop = h->proxy_top;
@@ -504,6 +577,7 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   HIP_TRY(sync_counters(h));
   const uint64_t live_ub = std::min<uint64_t>(src_top, h->hctr->alive_cnt[0]);
   const uint64_t live_p = std::min<uint64_t>(src_ptop, h->hctr->alive_cnt[1]);
+  if (may_grow && h->G <= 1 && live_ub * 4 >= src_top * 3) return grow(h, ids, atoms);
   Caps c = caps_for(std::max<uint64_t>(live_ub, 1), live_p, h->G > 1, h->etab_used, ids, atoms);
   if (h->knobs.level_log)
     fprintf(stderr, "[crgc] rebuild: slots %llu (alive %llu) pool %llu / %llu rpool %llu edge keys %llu / %llu "
@@ -531,21 +605,7 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms) {
     if (e == hipSuccess) e = hipMemsetAsync((char *)h->ctr + off, 0, 8, h->stream);
   // src keeps a view of the old counters' bounds via src_top / src_ptop (passed by value)
   if (e == hipSuccess) e = launch_rebuild(h->g.d, src_top, src_ptop, dst.d, map, offs, scan_tmp, h->stream);
-  // The last trace's garbage / kill lists outlive the generation: crgc_last_trace
-  // may still copy them (two-phase trace, or a trace whose buffers were short).
-  // They can hold more ids than the compacted generation has slots.
-  if (e == hipSuccess && h->have_last) {
-    auto carry = [&](uint64_t *&dptr, const uint64_t *src, uint64_t n) -> hipError_t {
-      if (n > dst.caps.scap) {
-        hipFree(dptr);
-        dptr = nullptr;
-        if (hipError_t r = dmalloc(&dptr, n)) return r;
-      }
-      return n ? hipMemcpyAsync(dptr, src, n * 8, hipMemcpyDeviceToDevice, h->stream) : hipSuccess;
-    };
-    e = carry(dst.d.out_ids, h->g.d.out_ids, h->last_garbage);
-    if (e == hipSuccess) e = carry(dst.d.out_kill, h->g.d.out_kill, h->last_kill);
-  }
+  if (e == hipSuccess) e = carry_lists(h, dst);
   if (e == hipSuccess) e = sync_counters(h);
   tmp.release();
   if (e != hipSuccess) {
@@ -633,6 +693,17 @@ int ensure_capacity(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   // only the pools are short: reclaim their dead space before rebuilding the
   // whole graph (a rebuild allocates a second graph; a repack, two pools)
   if (rest) {
+    const int rc = repack(h);
+    if (rc == CRGC_OK && pools_fit(h->pool_top, h->rpool_top, h->etab_used)) return CRGC_OK;
+    if (rc != CRGC_OK && rc != CRGC_E_NOMEM) return rc;
+    return rebuild(h, ids, atoms);
+  }
+  // slots or tables are short: a graph with few dead slots grows (same slots),
+  // whose pools may then want a repack; else a rebuild
+  if (int rc = rebuild(h, ids, atoms, /*may_grow=*/true)) return rc;
+  if (rest_fits(h->slot_top, h->proxy_top, h->etab_used) && pools_fit(h->pool_top, h->rpool_top, h->etab_used))
+    return CRGC_OK;
+  if (rest_fits(h->slot_top, h->proxy_top, h->etab_used)) {
     const int rc = repack(h);
     if (rc == CRGC_OK && pools_fit(h->pool_top, h->rpool_top, h->etab_used)) return CRGC_OK;
     if (rc != CRGC_OK && rc != CRGC_E_NOMEM) return rc;

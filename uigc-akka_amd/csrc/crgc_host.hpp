@@ -310,6 +310,9 @@ hipError_t launch_count_alive(const DevGraph &src, uint64_t src_top, uint64_t sr
 hipError_t launch_rebuild(const DevGraph &src, uint64_t src_top, uint64_t src_ptop, const DevGraph &dst, uint32_t *map,
                           uint64_t *offs, void *scan_tmp, hipStream_t s);
 size_t rebuild_scan_tmp_bytes(uint64_t n);
+// grow: both hash tables of `src` re-hashed into `dst`'s (larger) ones; the
+// caller copies the per-slot arrays and the pools (same slots, same offsets)
+hipError_t launch_grow_tables(const DevGraph &src, const DevGraph &dst, hipStream_t s);
 // the pools alone, packed into pool2 / rpool2 (pp / rp: scap u64 each; scan_tmp:
 // 2 x rebuild_scan_tmp_bytes(scap)); slots and tables unchanged
 hipError_t launch_repack(const DevGraph &g, uint64_t top, uint64_t ptop, uint64_t *pp, uint64_t *rp, void *scan_tmp,

@@ -363,6 +363,56 @@ hipError_t launch_count_alive(const DevGraph &src, uint64_t src_top, uint64_t sr
   return hipGetLastError();
 }
 
+// ---- grow: larger arrays, the same slots -------------------------------------
+// A graph that outgrows its capacities with few dead slots keeps its slot
+// numbering: the per-slot arrays and the pools are copied as they are and the
+// two hash tables are re-hashed into larger ones (collected ids' tombstones
+// dropped).  About a tenth of a rebuild's work: no renumbering, no CSR or
+// candidate-list rebuild.
+__global__ __launch_bounds__(256) void k_gr_ids(DevGraph src, DevGraph dst) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x; b < src.hcap; b += stride) {
+    const uint4 k4 = load_bucket(&src.htab[b]);
+    const uint64_t key = bucket_key(k4);
+    if (key == KEY_EMPTY || key == KEY_TOMB) continue;
+    uint64_t h = mix64(key) & dst.hmask;
+    for (uint64_t p = 0; p < dst.hcap; ++p) {
+      if (atomicCAS((unsigned long long *)&dst.htab[h].key, (unsigned long long)KEY_EMPTY,
+                    (unsigned long long)key) == KEY_EMPTY) {
+        dst.htab[h].val = k4.z;
+        break;
+      }
+      h = (h + 1) & dst.hmask;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gr_edges(DevGraph src, DevGraph dst) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x; b < src.ecap_tab; b += stride) {
+    const uint4 k4 = load_bucket(&src.etab[b]);
+    const uint64_t key = bucket_key(k4);
+    if (key == KEY_EMPTY) continue;
+    uint64_t h = mix64(key) & dst.emask;
+    for (uint64_t p = 0; p < dst.ecap_tab; ++p) {
+      if (atomicCAS((unsigned long long *)&dst.etab[h].key, (unsigned long long)KEY_EMPTY,
+                    (unsigned long long)key) == KEY_EMPTY) {
+        dst.etab[h].val = k4.z;
+        dst.etab[h].rev = k4.w;
+        break;
+      }
+      h = (h + 1) & dst.emask;
+    }
+  }
+}
+
+hipError_t launch_grow_tables(const DevGraph &src, const DevGraph &dst, hipStream_t s) {
+  launch_begin();
+  hipLaunchKernelGGL(k_gr_ids, dim3(grid_for(src.hcap, 256, 8192)), dim3(256), 0, s, src, dst);
+  hipLaunchKernelGGL(k_gr_edges, dim3(grid_for(src.ecap_tab, 256, 8192)), dim3(256), 0, s, src, dst);
+  return hipGetLastError();
+}
+
 hipError_t launch_rebuild(const DevGraph &src, uint64_t src_top, uint64_t src_ptop, const DevGraph &dst, uint32_t *map,
                           uint64_t *offs, void *scan_tmp, hipStream_t s) {
   launch_begin();
