@@ -392,12 +392,13 @@ def test_c4_shape_eight_shards_closure(sharded, oracle_mod, monkeypatch):
 
 def test_rebuild_keeps_every_proxy_before_any_trace(sharded, oracle_mod, capfd, monkeypatch):
     """A sharded load that outgrows its capacity before the first trace: every
-    shard's alive slots are mostly proxies (the far ends of its edges), far more
-    than twice the home shadows it created.  The rebuild must size the new
-    arrays from the alive slots (crgc_api.hip rebuild: counted on the device),
-    not from the homes created since the last trace — round 4's C4 over 8
-    logical shards put 68 M alive slots into 27 M and its passes wrote past the
-    new arrays.  Sets and counts must equal the oracle's."""
+    shard's alive slots are mostly proxies (the far ends of its edges, in the
+    proxy region since round 5), far more than the home shadows it created.  The
+    rebuild must size both new regions from the alive slots (crgc_api.hip
+    rebuild: counted on the device), not from the homes created since the last
+    trace — round 4's C4 over 8 logical shards put 68 M alive slots into 27 M
+    and its passes wrote past the new arrays.  Sets and counts must equal the
+    oracle's."""
     monkeypatch.setenv("CRGC_LEVEL_LOG", "1")
     w = world.World(seed=0x5EED + 44)
     w.bulk_graph(200_000, 2_000_000, alpha=2.1, n_roots=200)
@@ -408,10 +409,12 @@ def test_rebuild_keeps_every_proxy_before_any_trace(sharded, oracle_mod, capfd, 
     rh, ro = h.trace(True), o.trace(True)
     _same(rh, ro)
     err = capfd.readouterr().err
-    alive = [int(line.split("(alive ")[1].split(")")[0]) for line in err.splitlines()
-             if line.startswith("[crgc] rebuild:")]
-    assert alive, "the load was meant to outgrow the first capacity"
-    assert max(alive) > 100_000  # homes ~25 k per shard: the proxies dominate
+    lines = [line for line in err.splitlines() if line.startswith("[crgc] rebuild:")]
+    assert lines, "the load was meant to outgrow the first capacity"
+    homes = [int(line.split("(alive ")[1].split(")")[0]) for line in lines]
+    proxies = [int(line.split("(alive ")[2].split(")")[0]) for line in lines]
+    assert max(homes) <= 30_000          # homes ~25 k per shard
+    assert max(proxies) > 100_000        # the proxies dominate
     b = w.wakeup(20_000, busy=18_000, pending=2_000)
     h.merge_entries(b, split=True)
     o.merge_entries(b)

@@ -580,9 +580,10 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms, bool may_grow = false) 
   if (may_grow && h->G <= 1 && live_ub * 4 >= src_top * 3) return grow(h, ids, atoms);
   Caps c = caps_for(std::max<uint64_t>(live_ub, 1), live_p, h->G > 1, h->etab_used, ids, atoms);
   if (h->knobs.level_log)
-    fprintf(stderr, "[crgc] rebuild: slots %llu (alive %llu) pool %llu / %llu rpool %llu edge keys %llu / %llu "
-                    "-> slots %llu pool %llu edge table %llu\n",
-            (unsigned long long)src_top, (unsigned long long)live_ub, (unsigned long long)h->pool_top,
+    fprintf(stderr, "[crgc] rebuild: slots %llu (alive %llu) proxies %llu (alive %llu) pool %llu / %llu rpool %llu "
+                    "edge keys %llu / %llu -> slots %llu pool %llu edge table %llu\n",
+            (unsigned long long)src_top, (unsigned long long)live_ub, (unsigned long long)src_ptop,
+            (unsigned long long)live_p, (unsigned long long)h->pool_top,
             (unsigned long long)h->g.caps.pcap, (unsigned long long)h->rpool_top,
             (unsigned long long)h->etab_used, (unsigned long long)h->g.caps.ecap, (unsigned long long)c.scap,
             (unsigned long long)c.pcap, (unsigned long long)c.ecap);
