@@ -2075,7 +2075,8 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
     if (shift <= 20 && nb <= BIN_MAX) {
       const uint64_t nc = nb * BIN_WG;
       const uint64_t want = std::max<uint64_t>(1u << 16, (h->etab_used + h->atoms_since) / 2);
-      const uint64_t sc = std::min<uint64_t>(std::max<uint64_t>(round_up(want / nc, 4), 16), 1u << 24);
+      // (a multiple of 8: the apply pass reads a slice of u16 offsets in 16-B groups)
+      const uint64_t sc = std::min<uint64_t>(std::max<uint64_t>(round_up(want / nc, 8), 16), 1u << 24);
       const size_t need = Carver::need({16, nc * 4, nc * sc * 4});
       HIP_TRY(h->x_bin.ensure(need));
       Carver cv(h->x_bin.ptr);
