@@ -49,7 +49,7 @@ void free_arrays(Arrays &a) {
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat, d.xbytes,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill,
                 d.nzdeg, d.radj, d.rnew, d.rpool, d.par, d.fx, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
-                d.xp_buf, d.xp_cnt, d.rq_buf, d.rq_cnt, d.phs};
+                d.xp_buf, d.xp_cnt, d.rq_buf, d.rq_cnt, d.phs, d.psh};
   for (void *p : ps)
     if (p) hipFree(p);
   a.allocated = false;
@@ -129,6 +129,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
     A(dmalloc(&d.rq_buf, c.scap));
     A(dmalloc(&d.rq_cnt, c.scap / BLK_SLOTS));
     A(dmalloc(&d.phs, c.scap));
+    A(dmalloc(&d.psh, c.scap));
   }
 #undef A
   a.allocated = true;

@@ -1811,7 +1811,7 @@ hipError_t launch_list(const DevGraph &g, int mode, bool scatter, uint32_t *buf,
 __global__ __launch_bounds__(256) void k_phs_reset(DevGraph g, uint64_t mask) {
   const uint64_t top = g.pbase + g.ctr->proxy_top, stride = (uint64_t)gridDim.x * 256;
   for (uint64_t v = g.pbase + (uint64_t)blockIdx.x * 256 + threadIdx.x; v < top; v += stride)
-    if ((g.flags[v] & FL_PROXY) && ((mask >> shard_of(g.vid[v], g.n_shards)) & 1ull)) g.phs[v] = PHS_NONE;
+    if ((g.flags[v] & FL_PROXY) && ((mask >> g.psh[v]) & 1ull)) g.phs[v] = PHS_NONE;
   if (blockIdx.x == 0 && threadIdx.x == 0) g.ctr->res_top = 0;
 }
 
@@ -1836,7 +1836,7 @@ __global__ __launch_bounds__(256) void k_res_list(DevGraph g, uint64_t *send, ui
   const uint64_t top = g.pbase + g.ctr->proxy_top, stride = (uint64_t)gridDim.x * 256;
   const uint64_t v0 = g.pbase + g.ctr->res_top + (uint64_t)blockIdx.x * 256 + threadIdx.x;
   for (uint64_t v = v0; v < top; v += stride)
-    if (unresolved_proxy(g, v)) atomicAdd(&hist[shard_of(g.vid[v], g.n_shards)], 1u);
+    if (unresolved_proxy(g, v)) atomicAdd(&hist[g.psh[v]], 1u);
   __syncthreads();
   if (!SCATTER) {
     for (uint32_t d = threadIdx.x; d < g.n_shards; d += 256)
@@ -1854,7 +1854,7 @@ __global__ __launch_bounds__(256) void k_res_list(DevGraph g, uint64_t *send, ui
   for (uint64_t v = v0; v < top; v += stride) {
     if (!unresolved_proxy(g, v)) continue;
     const uint64_t id = g.vid[v];
-    const uint32_t d = shard_of(id, g.n_shards);
+    const uint32_t d = g.psh[v];
     const uint64_t at = base[d] + atomicAdd(&hist[d], 1u);
     send[at] = id;
     send_slot[at] = (uint32_t)v;
@@ -1912,7 +1912,7 @@ __global__ __launch_bounds__(256) void k_xlist(DevGraph g, const uint32_t *buf, 
     const uint32_t n = cnt[blk];
     for (uint32_t i = lane_id(); i < n; i += 64) {
       const uint32_t v = buf[blk * BLK_SLOTS + i];
-      const uint32_t d = shard_of(g.vid[v], g.n_shards);
+      const uint32_t d = g.psh[v];
       const bool res = x.use_slots && g.phs[v] < PHS_ABSENT;
       atomicAdd(&hist[res ? 1 : 0][d], 1u);
     }
@@ -1936,12 +1936,11 @@ __global__ __launch_bounds__(256) void k_xlist(DevGraph g, const uint32_t *buf, 
     const uint32_t n = cnt[blk];
     for (uint32_t i = lane_id(); i < n; i += 64) {
       const uint32_t v = buf[blk * BLK_SLOTS + i];
-      const uint64_t id = g.vid[v];
-      const uint32_t d = shard_of(id, g.n_shards);
+      const uint32_t d = g.psh[v];
       const uint32_t hs = x.use_slots ? g.phs[v] : PHS_NONE;
-      if (hs >= PHS_ABSENT) {
+      if (hs >= PHS_ABSENT) {  // (the id only for the unresolved)
         const uint64_t at = base[0][d] + atomicAdd(&hist[0][d], 1u);
-        ((uint64_t *)(send + x.id_off[d]))[at] = id;
+        ((uint64_t *)(send + x.id_off[d]))[at] = g.vid[v];
       } else if (x.bitmap[d]) {
         atomicOr((uint32_t *)(send + x.sl_off[d]) + (hs >> 5), 1u << (hs & 31));
       } else {
