@@ -1467,7 +1467,10 @@ constexpr uint64_t CHUNK_MIN = 1u << 18;      // entries per chunk at least (run
 constexpr uint64_t CHUNK_MIN_REG = 1u << 18;  // (kernel copies of a registered batch)
 constexpr uint32_t CHUNK_MAX = 8;
 
-static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint32_t K, bool registered) {
+// async (crgc_merge_entries_async, registered batches): return without waiting
+// for the copies; the caller keeps the buffers until a trace or sync.
+static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint32_t K, bool registered,
+                                 bool async = false) {
   const uint64_t n = b->n_entries;
   struct Part {
     uint64_t lo, hi, c0, c1, s0, s1, u0, u1;
@@ -1571,7 +1574,10 @@ static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint3
     v.memory = CRGC_MEM_DEVICE;
     rc = merge_entries_one(h, &v, q.c1 - q.c0, q.s1 - q.s0, q.u1 - q.u0);
   }
-  // the caller's buffers are read only during the call
+  // the caller's buffers are read only during the call (async: until the
+  // next trace or sync, which wait for the graph's stream and so for these
+  // copies, its merges' dependencies)
+  if (async && registered && rc == CRGC_OK) return CRGC_OK;
   const hipError_t e = stream_wait(h->cpy, h->knobs.spin_us);
   if (rc == CRGC_OK && e != hipSuccess) rc = map_hip(e);
   return rc;
@@ -1669,7 +1675,12 @@ static int merge_entries_dev_chunked(crgc_graph *h, const crgc_entry_batch *b) {
   return CRGC_OK;
 }
 
-int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
+static int merge_entries(crgc_graph *h, const crgc_entry_batch *b, bool async);
+
+int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) { return merge_entries(h, b, false); }
+int crgc_merge_entries_async(crgc_graph *h, const crgc_entry_batch *b) { return merge_entries(h, b, true); }
+
+static int merge_entries(crgc_graph *h, const crgc_entry_batch *b, bool async) {
   if (int rc = check_graph(h)) return rc;
   DeviceGuard dg(h->device);
   uint64_t C = 0, S = 0, U = 0;
@@ -1689,7 +1700,8 @@ int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
       // a PCIe-reading copy slow down 5-25x (profiles/r4ab), so overlapping
       // chunks bought nothing (C2 registered wakeup 2.20 ms in one piece, 2.30
       // in 3 chunks, interleaved on one box, profiles/r4ae)
-      if (reg && b->n_entries >= CHUNK_MIN_REG) return merge_entries_chunked(h, b, (uint32_t)std::max<uint64_t>(k, 1), true);
+      if (reg && (b->n_entries >= CHUNK_MIN_REG || async))
+        return merge_entries_chunked(h, b, (uint32_t)std::max<uint64_t>(k, 1), true, async);
       if (k >= 2) return merge_entries_chunked(h, b, (uint32_t)k, reg);
     }
     return merge_entries_one(h, b, C, S, U);
