@@ -2537,8 +2537,9 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
       nsend += n_id(me, d) + n_sl(me, d);
     }
     if (h->x_send.ensure(so + 8) != hipSuccess) return CRGC_E_NOMEM;
-    for (uint32_t d = 0; d < G; ++d)
-      if (xs.bitmap[d]) HIP_TRY(hipMemsetAsync((char *)h->x_send.ptr + xs.sl_off[d], 0, 4 * words(d), h->stream));
+    bool any_bitmap = false;  // (the bitmap segments zeroed by one memset of the send buffer)
+    for (uint32_t d = 0; d < G; ++d) any_bitmap |= xs.bitmap[d] != 0;
+    if (any_bitmap) HIP_TRY(hipMemsetAsync(h->x_send.ptr, 0, so, h->stream));
     HIP_TRY(launch_xlist(h->g.d, true, npb, (char *)h->x_send.ptr, xs, h->stream));
     if (npb) HIP_TRY(hipMemsetAsync(h->g.d.xp_cnt + p0, 0, npb * 4, h->stream));
     uint64_t nrecv = 0;
@@ -2578,12 +2579,7 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
     // one, or — the round was capped — the pending level itself, whose
     // candidates (and the counts of the levels before it) are already there
     const int L = capped ? end : end + 2;
-    if (!capped) {
-      HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(ring) + ((L - 2) % LEVEL_RING) * 8, 0, 8, h->stream));
-      HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(ring) + ((L - 1) % LEVEL_RING) * 8, 0, 8, h->stream));
-      HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(qh) + (L & 1) * 8, 0, 8, h->stream));
-    }
-    HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(tail_state), 0, 8, h->stream));
+    HIP_TRY(launch_round_start(h->ctr, L, !capped, h->stream));
     HIP_TRY(launch_ximport(h->g.d, (const char *)h->x_recv.ptr, xr, L, h->stream));
     *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (int rc = run_levels(h, investigate, location, top, false, L, lr, &end, nullptr, cap, &capped)) return rc;

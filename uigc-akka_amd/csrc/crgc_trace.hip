@@ -2004,6 +2004,25 @@ __global__ __launch_bounds__(256) void k_ximport(DevGraph g, const char *recv, X
   if (threadIdx.x == 0 && t) atomicAdd(&g.ctr->ring[(L - 1) % LEVEL_RING], (unsigned long long)t);
 }
 
+// A mark round's start (one launch instead of four memsets): the trace state a
+// fresh sparse level L needs — the two level counts before it and its hub queue
+// zeroed (not when the round continues a capped one: level L's candidates and
+// counts are the previous round's) — and no narrow-frontier state.
+__global__ void k_round_start(Counters *c, int L, int fresh) {
+  if (fresh) {
+    c->ring[(L - 2) % LEVEL_RING] = 0;
+    c->ring[(L - 1) % LEVEL_RING] = 0;
+    c->qh[L & 1] = 0;
+  }
+  c->tail_state = 0;
+}
+
+hipError_t launch_round_start(Counters *c, int level, bool fresh, hipStream_t s) {
+  launch_begin();
+  hipLaunchKernelGGL(k_round_start, dim3(1), dim3(1), 0, s, c, level, fresh ? 1 : 0);
+  return hipGetLastError();
+}
+
 hipError_t launch_ximport(const DevGraph &g, const char *recv, const XRecv &x, int level, hipStream_t s) {
   launch_begin();
   const uint64_t n = x.start[x.G];
