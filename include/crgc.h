@@ -326,6 +326,15 @@ void crgc_destroy(crgc_graph *g);
  * called from LocalGC Wakeup (LocalGC.scala:152-172). */
 int crgc_merge_entries(crgc_graph *g, const crgc_entry_batch *batch);
 
+/* The same merge for a drain loop that hands a wakeup's entries over in
+ * chunks as it packs them (LocalGC.scala:152-172): a host batch wholly inside
+ * memory registered with crgc_host_register is only enqueued — its PCIe read
+ * and merge run while the caller packs the next chunk — and must stay
+ * unchanged until the next crgc_trace or crgc_sync returns.  Any other batch
+ * is merged exactly as by crgc_merge_entries.  Chunks merge in call order,
+ * each its own merge (last write wins across chunks in that order). */
+int crgc_merge_entries_async(crgc_graph *g, const crgc_entry_batch *batch);
+
 /* N x ShadowGraph.mergeDelta(DeltaGraph) — ShadowGraph.java:127-156,
  * called on DeltaMsg (LocalGC.scala:124-136). */
 int crgc_merge_deltas(crgc_graph *g, const crgc_delta_batch *batch);

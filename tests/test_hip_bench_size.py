@@ -189,3 +189,36 @@ def test_large_host_batches_chunked_and_registered(hip_mod, oracle_mod, monkeypa
         _same(hp.trace(True), ro)
         _same(hr.trace(True), ro)
     hr.unregister_host(arena.buf)
+
+
+def test_drain_loop_chunks_merged_async_from_registered_arena(hip_mod, oracle_mod):
+    """crgc_merge_entries_async: the drain loop packs a wakeup's entries into a
+    registered arena chunk by chunk (LocalGC.scala:152-172) and hands each chunk
+    over as soon as it is packed; the merges run while the next chunk is packed,
+    and the arena is reused only after the trace.  Chunks merge in call order,
+    so the graph equals the oracle's after the whole batch, and the traces too."""
+    from crgc_hip import HostArena
+    w = world.World(seed=0x5EED + 9)
+    w.bulk_graph(100_000, 1_000_000)
+    h, o = hip_mod.ShadowGraph(), oracle_mod.OracleGraph()
+    for b in w.batches(1 << 20):
+        h.merge_entries(b.to_device())
+        o.merge_entries(b)
+    _same(h.trace(True), o.trace(True))
+    wake = [w.wakeup(100_000, busy=9_000, pending=1_000) for _ in range(3)]
+    arena = HostArena(max(b.nbytes() for b in wake) * 1.2 + (1 << 22))
+    h.register_host(arena.buf)
+    try:
+        for b in wake:
+            at = 0
+            n = len(b.self)
+            for lo in range(0, n, 30_000):          # 4 chunks, the last short
+                hb = arena.pack(b.slice(lo, min(n, lo + 30_000)), at)
+                at = (arena.end + 255) & ~255
+                h.merge_entries_async(hb)
+            o.merge_entries(b)
+            ro = o.trace(True)
+            _same(h.trace(True), ro)
+            assert h.export() == o.export()
+    finally:
+        h.unregister_host(arena.buf)

@@ -202,6 +202,7 @@ EXPORTED_SYMBOLS = (
     "crgc_create",
     "crgc_destroy",
     "crgc_merge_entries",
+    "crgc_merge_entries_async",
     "crgc_merge_deltas",
     "crgc_merge_undo",
     "crgc_trace",
@@ -238,6 +239,7 @@ def _declare(lib: C.CDLL, prefix: str) -> None:
     g = _P
     sig = {
         "merge_entries": (C.c_int, [g, P(CrgcEntryBatch)]),
+        "merge_entries_async": (C.c_int, [g, P(CrgcEntryBatch)]),
         "merge_deltas": (C.c_int, [g, P(CrgcDeltaBatch)]),
         "merge_undo": (C.c_int, [g, P(CrgcUndoLog)]),
         "trace": (C.c_int, [g, C.c_int, P(CrgcTraceOut)]),

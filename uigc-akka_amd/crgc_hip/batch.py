@@ -438,9 +438,11 @@ class HostArena:
     def __init__(self, nbytes: int):
         self.buf = np.empty(int(nbytes) + 4096, dtype=np.uint8)
 
-    def pack(self, b: "EntryBatch") -> "EntryBatch":
+    def pack(self, b: "EntryBatch", at: int = 0) -> "EntryBatch":
+        """Pack `b` into the arena from byte `at` on (the drain loop packs a
+        wakeup's chunks one after the other: pack_end() tells where one ended)."""
         assert b.memory == abi.MEM_HOST
-        views, off = [], 0
+        views, off = [], int(at)
         for k in EntryBatch.__slots__[:11]:
             a = np.ascontiguousarray(getattr(b, k))
             off = (off + 255) & ~255
@@ -450,4 +452,5 @@ class HostArena:
             v[...] = a
             views.append(v)
             off += a.nbytes
+        self.end = off
         return EntryBatch(*views)

@@ -131,6 +131,16 @@ class ShadowGraph:
                   "crgc_merge_entries")
         self._hold(batch)
 
+    def merge_entries_async(self, batch: EntryBatch):
+        """crgc_merge_entries_async: a batch packed into registered host memory
+        is only enqueued (its buffers must stay unchanged until the next trace or
+        sync); any other batch merges as merge_entries does."""
+        self._chk(self.lib.crgc_merge_entries_async(self.h, C.byref(batch.struct())),
+                  "crgc_merge_entries_async")
+        self._hold(batch)
+        if batch.memory == abi.MEM_HOST:
+            self._inflight.append(batch)  # (its arrays stay referenced until the stream drains)
+
     def merge_deltas(self, batch: DeltaBatch):
         self.flush()
         self._chk(self.lib.crgc_merge_deltas(self.h, C.byref(batch.struct())),

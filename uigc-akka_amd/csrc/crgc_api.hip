@@ -49,7 +49,7 @@ void free_arrays(Arrays &a) {
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat, d.xbytes,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill,
                 d.nzdeg, d.radj, d.rnew, d.rpool, d.par, d.fx, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
-                d.xp_buf, d.xp_cnt, d.rq_buf, d.rq_cnt, d.phs};
+                d.xp_buf, d.xp_cnt, d.rq_buf, d.rq_cnt, d.phs, d.psh};
   for (void *p : ps)
     if (p) hipFree(p);
   a.allocated = false;
@@ -129,6 +129,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
     A(dmalloc(&d.rq_buf, c.scap));
     A(dmalloc(&d.rq_cnt, c.scap / BLK_SLOTS));
     A(dmalloc(&d.phs, c.scap));
+    A(dmalloc(&d.psh, c.scap));
   }
 #undef A
   a.allocated = true;
@@ -1467,7 +1468,10 @@ constexpr uint64_t CHUNK_MIN = 1u << 18;      // entries per chunk at least (run
 constexpr uint64_t CHUNK_MIN_REG = 1u << 18;  // (kernel copies of a registered batch)
 constexpr uint32_t CHUNK_MAX = 8;
 
-static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint32_t K, bool registered) {
+// async (crgc_merge_entries_async, registered batches): return without waiting
+// for the copies; the caller keeps the buffers until a trace or sync.
+static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint32_t K, bool registered,
+                                 bool async = false) {
   const uint64_t n = b->n_entries;
   struct Part {
     uint64_t lo, hi, c0, c1, s0, s1, u0, u1;
@@ -1571,7 +1575,10 @@ static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint3
     v.memory = CRGC_MEM_DEVICE;
     rc = merge_entries_one(h, &v, q.c1 - q.c0, q.s1 - q.s0, q.u1 - q.u0);
   }
-  // the caller's buffers are read only during the call
+  // the caller's buffers are read only during the call (async: until the
+  // next trace or sync, which wait for the graph's stream and so for these
+  // copies, its merges' dependencies)
+  if (async && registered && rc == CRGC_OK) return CRGC_OK;
   const hipError_t e = stream_wait(h->cpy, h->knobs.spin_us);
   if (rc == CRGC_OK && e != hipSuccess) rc = map_hip(e);
   return rc;
@@ -1669,7 +1676,12 @@ static int merge_entries_dev_chunked(crgc_graph *h, const crgc_entry_batch *b) {
   return CRGC_OK;
 }
 
-int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
+static int merge_entries(crgc_graph *h, const crgc_entry_batch *b, bool async);
+
+int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) { return merge_entries(h, b, false); }
+int crgc_merge_entries_async(crgc_graph *h, const crgc_entry_batch *b) { return merge_entries(h, b, true); }
+
+static int merge_entries(crgc_graph *h, const crgc_entry_batch *b, bool async) {
   if (int rc = check_graph(h)) return rc;
   DeviceGuard dg(h->device);
   uint64_t C = 0, S = 0, U = 0;
@@ -1689,7 +1701,8 @@ int crgc_merge_entries(crgc_graph *h, const crgc_entry_batch *b) {
       // a PCIe-reading copy slow down 5-25x (profiles/r4ab), so overlapping
       // chunks bought nothing (C2 registered wakeup 2.20 ms in one piece, 2.30
       // in 3 chunks, interleaved on one box, profiles/r4ae)
-      if (reg && b->n_entries >= CHUNK_MIN_REG) return merge_entries_chunked(h, b, (uint32_t)std::max<uint64_t>(k, 1), true);
+      if (reg && (b->n_entries >= CHUNK_MIN_REG || async))
+        return merge_entries_chunked(h, b, (uint32_t)std::max<uint64_t>(k, 1), true, async);
       if (k >= 2) return merge_entries_chunked(h, b, (uint32_t)k, reg);
     }
     return merge_entries_one(h, b, C, S, U);
@@ -2076,7 +2089,8 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
     if (shift <= 20 && nb <= BIN_MAX) {
       const uint64_t nc = nb * BIN_WG;
       const uint64_t want = std::max<uint64_t>(1u << 16, (h->etab_used + h->atoms_since) / 2);
-      const uint64_t sc = std::min<uint64_t>(std::max<uint64_t>(round_up(want / nc, 4), 16), 1u << 24);
+      // (a multiple of 8: the apply pass reads a slice of u16 offsets in 16-B groups)
+      const uint64_t sc = std::min<uint64_t>(std::max<uint64_t>(round_up(want / nc, 8), 16), 1u << 24);
       const size_t need = Carver::need({16, nc * 4, nc * sc * 4});
       HIP_TRY(h->x_bin.ensure(need));
       Carver cv(h->x_bin.ptr);
@@ -2524,8 +2538,9 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
       nsend += n_id(me, d) + n_sl(me, d);
     }
     if (h->x_send.ensure(so + 8) != hipSuccess) return CRGC_E_NOMEM;
-    for (uint32_t d = 0; d < G; ++d)
-      if (xs.bitmap[d]) HIP_TRY(hipMemsetAsync((char *)h->x_send.ptr + xs.sl_off[d], 0, 4 * words(d), h->stream));
+    bool any_bitmap = false;  // (the bitmap segments zeroed by one memset of the send buffer)
+    for (uint32_t d = 0; d < G; ++d) any_bitmap |= xs.bitmap[d] != 0;
+    if (any_bitmap) HIP_TRY(hipMemsetAsync(h->x_send.ptr, 0, so, h->stream));
     HIP_TRY(launch_xlist(h->g.d, true, npb, (char *)h->x_send.ptr, xs, h->stream));
     if (npb) HIP_TRY(hipMemsetAsync(h->g.d.xp_cnt + p0, 0, npb * 4, h->stream));
     uint64_t nrecv = 0;
@@ -2565,12 +2580,7 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
     // one, or — the round was capped — the pending level itself, whose
     // candidates (and the counts of the levels before it) are already there
     const int L = capped ? end : end + 2;
-    if (!capped) {
-      HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(ring) + ((L - 2) % LEVEL_RING) * 8, 0, 8, h->stream));
-      HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(ring) + ((L - 1) % LEVEL_RING) * 8, 0, 8, h->stream));
-      HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(qh) + (L & 1) * 8, 0, 8, h->stream));
-    }
-    HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(tail_state), 0, 8, h->stream));
+    HIP_TRY(launch_round_start(h->ctr, L, !capped, h->stream));
     HIP_TRY(launch_ximport(h->g.d, (const char *)h->x_recv.ptr, xr, L, h->stream));
     *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (int rc = run_levels(h, investigate, location, top, false, L, lr, &end, nullptr, cap, &capped)) return rc;

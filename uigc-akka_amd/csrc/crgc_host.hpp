@@ -289,6 +289,7 @@ struct XcArgs {
 hipError_t launch_xclosure(const DevGraph &g, const XcArgs &x, int step, const void *p0, uint32_t *p1, uint64_t n,
                            uint32_t fi, int first, hipStream_t s);
 hipError_t launch_ximport(const DevGraph &g, const char *recv, const XRecv &x, int level, hipStream_t s);
+hipError_t launch_round_start(Counters *c, int level, bool fresh, hipStream_t s);
 // home-slot resolution: 0 reset(mask), 1 count unresolved, 2 list them (ids, slots),
 // 3 answer asked ids (at the home), 4 store the answers, 5 every proxy so far has asked
 // (n_proxy: a bound of the proxy slots, for the grids)

@@ -239,6 +239,7 @@ struct DevGraph {
   uint32_t *rq_buf;   // per-block regions: garbage slots whose kill waits on a remote mark
   uint32_t *rq_cnt;   // per block: listed requests
   uint32_t *phs;      // per proxy slot: its slot at the home shard (PHS_NONE / PHS_ABSENT)
+  uint8_t *psh;       // per proxy slot: its home shard (the exchange lists read it, not the id)
   Counters *ctr;
 };
 
@@ -474,6 +475,7 @@ __device__ inline uint32_t id_settle(const DevGraph &g, uint64_t id, uint64_t bu
       slot = (uint32_t)s;
       g.vid[s] = id;
       g.flags[s] = home ? FL_ALIVE : (FL_ALIVE | FL_PROXY);
+      if (!home) g.psh[s] = (uint8_t)shard_of(id, g.n_shards);
     }
     atomicExch(&g.htab[bucket].val, slot);
   }
@@ -512,6 +514,7 @@ __device__ inline uint32_t id_settle_block(const DevGraph &g, uint64_t id, uint6
       slot = (uint32_t)s;
       g.vid[s] = id;
       g.flags[s] = home ? FL_ALIVE : (FL_ALIVE | FL_PROXY);
+      if (!home) g.psh[s] = (uint8_t)shard_of(id, g.n_shards);
     }
     atomicExch(&g.htab[bucket].val, slot);
   }

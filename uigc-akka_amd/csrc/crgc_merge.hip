@@ -135,6 +135,7 @@ __global__ __launch_bounds__(IDS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 
           slot[j] = (uint32_t)s;
           g.vid[s] = id[j];
           g.flags[s] = home ? FL_ALIVE : (FL_ALIVE | FL_PROXY);
+          if (!home) g.psh[s] = (uint8_t)shard_of(id[j], g.n_shards);
           if (rfit) {
             g.radj[s] = make_uint2((uint32_t)ro, rseg_pack(0, IDS_RCAP));
           }

@@ -49,6 +49,7 @@ __global__ __launch_bounds__(256) void k_rb_vertices(DevGraph src, uint64_t src_
     dst.vid[ns] = id;
     dst.recv[ns] = src.recv[v];
     dst.flags[ns] = f;
+    if (!home) dst.psh[ns] = src.psh[v];
     uint64_t h = mix64(id) & dst.hmask;
     for (uint64_t p = 0; p < dst.hcap; ++p) {
       if (atomicCAS((unsigned long long *)&dst.htab[h].key, (unsigned long long)KEY_EMPTY,

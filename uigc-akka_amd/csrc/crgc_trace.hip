@@ -709,6 +709,10 @@ __device__ inline bool bin_mode(const Counters *c, const LevelArgs &a) {
 constexpr int BIN_T = 1024;  // threads of a k_bin_place / k_bin_apply workgroup
 constexpr int BIN_NW = BIN_T / 64;
 
+// B16 (bins of 2^16 slots, C2 scale): a target is stored as its 16-bit offset
+// in the bin, halving the place pass's writes and the apply pass's reads
+// (57 MB of 4-B slots per launch for a 13 MB byte map).
+template <bool B16>
 __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_bin_place(DevGraph g, LevelArgs a) {
   constexpr int U = EXPAND_U;  // (8 edge loads per lane did not pay with the sorted stores' registers)
   __shared__ uint32_t s_start[BIN_NW][65];
@@ -738,20 +742,8 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     for (uint32_t k = tid; k < NB; k += BIN_T) lc[k] = 0;
   __syncthreads();
 
-  auto put = [&](uint32_t t) {
-    if (!binned) {
-      Fn[t] = 1;
-      return;
-    }
-    const uint32_t b = t >> a.bin_shift;
-    const uint32_t pos = b < NB ? atomicAdd(&lc[b], 1u) : SC;  // (a slot past the bins: never, slot_top is synced)
-    if (pos < SC) {
-      a.bins[((uint64_t)b * G + wg) * SC + pos] = t;
-      nb2 += 8;
-    } else {
-      Fn[t] = 1;  // past the slice: the byte at once
-    }
-  };
+  // (not binned: the candidate byte at once; a binned level goes through `edges`)
+  auto put = [&](uint32_t t) { Fn[t] = 1; };
   // A window of the wave's targets (64 U), binned: counted per bin in the
   // wave's table, a slice range reserved per (wave, bin) at once, the targets
   // sorted by bin in LDS, then stored by consecutive lanes in sorted order, so
@@ -800,8 +792,14 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
       const uint32_t tt = S[i], b = tt >> a.bin_shift;
       const uint32_t pos = B[b] + i;  // slice position = reservation + rank = B + sorted index
       if (pos < SC) {
-        a.bins[((uint64_t)b * G + wg) * SC + pos] = tt;
-        nb2 += 8;
+        const uint64_t at = ((uint64_t)b * G + wg) * SC + pos;
+        if (B16) {
+          reinterpret_cast<uint16_t *>(a.bins)[at] = (uint16_t)(tt - (b << 16));
+          nb2 += 4;
+        } else {
+          a.bins[at] = tt;
+          nb2 += 8;
+        }
       } else {
         Fn[tt] = 1;  // past the slice: the byte at once
       }
@@ -905,12 +903,15 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 // read-modify-wrote 16-B groups: 168 workgroups on a 256-CU chip, 34 us.)
 constexpr uint32_t BIN_SPLIT = 2;
 
+template <bool B16>
 __global__ __launch_bounds__(BIN_T) void k_bin_apply(DevGraph g, LevelArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t bm[];  // 2^bin_shift bits, then the slice counts
   if (!a.bins || a.bin_mode_w[0] == 0) return;  // level 0 was not binned
   const uint32_t b = blockIdx.x / BIN_SPLIT, h = blockIdx.x % BIN_SPLIT, tid = threadIdx.x;
   const uint32_t span = 1u << a.bin_shift, words = span / 32;
-  const uint32_t G = a.bin_grid, SC = a.bin_slice, S4 = SC / 4;
+  // a slice is SC entries: SC / 4 16-B groups of u32 targets, or SC / 8 of u16 offsets
+  const uint32_t G = a.bin_grid, SC = a.bin_slice, S4 = B16 ? SC / 8 : SC / 4;
+  constexpr uint32_t PER = B16 ? 8 : 4;  // entries per 16-B group
   const uint32_t NS = (G - h + BIN_SPLIT - 1) / BIN_SPLIT;  // this workgroup's slices: w = h + BIN_SPLIT k
   uint32_t *cnt = bm + words;
   for (uint32_t k = tid; k < words; k += BIN_T) bm[k] = 0;
@@ -929,20 +930,20 @@ __global__ __launch_bounds__(BIN_T) void k_bin_apply(DevGraph g, LevelArgs a) {
       n[j] = k < NS ? cnt[k] : 0u;
       mx = max(mx, n[j]);
     }
-    for (uint32_t i = (uint32_t)lane_id() * 4; i - (uint32_t)lane_id() * 4 < mx; i += 256) {
+    for (uint32_t i = (uint32_t)lane_id() * PER; i - (uint32_t)lane_id() * PER < mx; i += 64 * PER) {
       uint4 v4[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        v4[j] = i < n[j] ? src[(uint64_t)(h + BIN_SPLIT * (k0 + j * BIN_NW)) * S4 + i / 4] : make_uint4(0, 0, 0, 0);
+        v4[j] = i < n[j] ? src[(uint64_t)(h + BIN_SPLIT * (k0 + j * BIN_NW)) * S4 + i / PER] : make_uint4(0, 0, 0, 0);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t v[4] = {v4[j].x, v4[j].y, v4[j].z, v4[j].w};
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+        for (int k = 0; k < (int)PER; ++k)
           if (i + k < n[j]) {
-            const uint32_t t = v[k] - base;
+            const uint32_t t = B16 ? (v[k / 2] >> (16 * (k & 1))) & 0xFFFFu : v[k] - base;
             atomicOr(&bm[t >> 5], 1u << (t & 31));
-            nb2 += 8;
+            nb2 += B16 ? 4 : 8;
           }
       }
     }
@@ -1383,9 +1384,14 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
   if (roots && a.nbins) {
     // the pseudo-root level, binned when it is wide: place and apply, timed
     // together as its expand
-    hipExtLaunchKernelGGL(k_bin_place, dim3(a.bin_grid), dim3(BIN_T), 0, s, e[4], nullptr, 0, g, a);
-    hipExtLaunchKernelGGL(k_bin_apply, dim3(a.nbins * BIN_SPLIT), dim3(BIN_T),
-                          (size_t)(1u << a.bin_shift) / 8 + (size_t)a.bin_grid * 4, s, nullptr, e[5], 0, g, a);
+    const size_t lds = (size_t)(1u << a.bin_shift) / 8 + (size_t)a.bin_grid * 4;
+    if (a.bin_shift == 16) {
+      hipExtLaunchKernelGGL(k_bin_place<true>, dim3(a.bin_grid), dim3(BIN_T), 0, s, e[4], nullptr, 0, g, a);
+      hipExtLaunchKernelGGL(k_bin_apply<true>, dim3(a.nbins * BIN_SPLIT), dim3(BIN_T), lds, s, nullptr, e[5], 0, g, a);
+    } else {
+      hipExtLaunchKernelGGL(k_bin_place<false>, dim3(a.bin_grid), dim3(BIN_T), 0, s, e[4], nullptr, 0, g, a);
+      hipExtLaunchKernelGGL(k_bin_apply<false>, dim3(a.nbins * BIN_SPLIT), dim3(BIN_T), lds, s, nullptr, e[5], 0, g, a);
+    }
     return hipGetLastError();
   }
   auto expand = [&](auto kern) {
@@ -1805,7 +1811,7 @@ hipError_t launch_list(const DevGraph &g, int mode, bool scatter, uint32_t *buf,
 __global__ __launch_bounds__(256) void k_phs_reset(DevGraph g, uint64_t mask) {
   const uint64_t top = g.pbase + g.ctr->proxy_top, stride = (uint64_t)gridDim.x * 256;
   for (uint64_t v = g.pbase + (uint64_t)blockIdx.x * 256 + threadIdx.x; v < top; v += stride)
-    if ((g.flags[v] & FL_PROXY) && ((mask >> shard_of(g.vid[v], g.n_shards)) & 1ull)) g.phs[v] = PHS_NONE;
+    if ((g.flags[v] & FL_PROXY) && ((mask >> g.psh[v]) & 1ull)) g.phs[v] = PHS_NONE;
   if (blockIdx.x == 0 && threadIdx.x == 0) g.ctr->res_top = 0;
 }
 
@@ -1830,7 +1836,7 @@ __global__ __launch_bounds__(256) void k_res_list(DevGraph g, uint64_t *send, ui
   const uint64_t top = g.pbase + g.ctr->proxy_top, stride = (uint64_t)gridDim.x * 256;
   const uint64_t v0 = g.pbase + g.ctr->res_top + (uint64_t)blockIdx.x * 256 + threadIdx.x;
   for (uint64_t v = v0; v < top; v += stride)
-    if (unresolved_proxy(g, v)) atomicAdd(&hist[shard_of(g.vid[v], g.n_shards)], 1u);
+    if (unresolved_proxy(g, v)) atomicAdd(&hist[g.psh[v]], 1u);
   __syncthreads();
   if (!SCATTER) {
     for (uint32_t d = threadIdx.x; d < g.n_shards; d += 256)
@@ -1848,7 +1854,7 @@ __global__ __launch_bounds__(256) void k_res_list(DevGraph g, uint64_t *send, ui
   for (uint64_t v = v0; v < top; v += stride) {
     if (!unresolved_proxy(g, v)) continue;
     const uint64_t id = g.vid[v];
-    const uint32_t d = shard_of(id, g.n_shards);
+    const uint32_t d = g.psh[v];
     const uint64_t at = base[d] + atomicAdd(&hist[d], 1u);
     send[at] = id;
     send_slot[at] = (uint32_t)v;
@@ -1906,7 +1912,7 @@ __global__ __launch_bounds__(256) void k_xlist(DevGraph g, const uint32_t *buf, 
     const uint32_t n = cnt[blk];
     for (uint32_t i = lane_id(); i < n; i += 64) {
       const uint32_t v = buf[blk * BLK_SLOTS + i];
-      const uint32_t d = shard_of(g.vid[v], g.n_shards);
+      const uint32_t d = g.psh[v];
       const bool res = x.use_slots && g.phs[v] < PHS_ABSENT;
       atomicAdd(&hist[res ? 1 : 0][d], 1u);
     }
@@ -1930,12 +1936,11 @@ __global__ __launch_bounds__(256) void k_xlist(DevGraph g, const uint32_t *buf, 
     const uint32_t n = cnt[blk];
     for (uint32_t i = lane_id(); i < n; i += 64) {
       const uint32_t v = buf[blk * BLK_SLOTS + i];
-      const uint64_t id = g.vid[v];
-      const uint32_t d = shard_of(id, g.n_shards);
+      const uint32_t d = g.psh[v];
       const uint32_t hs = x.use_slots ? g.phs[v] : PHS_NONE;
-      if (hs >= PHS_ABSENT) {
+      if (hs >= PHS_ABSENT) {  // (the id only for the unresolved)
         const uint64_t at = base[0][d] + atomicAdd(&hist[0][d], 1u);
-        ((uint64_t *)(send + x.id_off[d]))[at] = id;
+        ((uint64_t *)(send + x.id_off[d]))[at] = g.vid[v];
       } else if (x.bitmap[d]) {
         atomicOr((uint32_t *)(send + x.sl_off[d]) + (hs >> 5), 1u << (hs & 31));
       } else {
@@ -1997,6 +2002,25 @@ __global__ __launch_bounds__(256) void k_ximport(DevGraph g, const char *recv, X
   }
   const uint64_t t = block_sum4(found);
   if (threadIdx.x == 0 && t) atomicAdd(&g.ctr->ring[(L - 1) % LEVEL_RING], (unsigned long long)t);
+}
+
+// A mark round's start (one launch instead of four memsets): the trace state a
+// fresh sparse level L needs — the two level counts before it and its hub queue
+// zeroed (not when the round continues a capped one: level L's candidates and
+// counts are the previous round's) — and no narrow-frontier state.
+__global__ void k_round_start(Counters *c, int L, int fresh) {
+  if (fresh) {
+    c->ring[(L - 2) % LEVEL_RING] = 0;
+    c->ring[(L - 1) % LEVEL_RING] = 0;
+    c->qh[L & 1] = 0;
+  }
+  c->tail_state = 0;
+}
+
+hipError_t launch_round_start(Counters *c, int level, bool fresh, hipStream_t s) {
+  launch_begin();
+  hipLaunchKernelGGL(k_round_start, dim3(1), dim3(1), 0, s, c, level, fresh ? 1 : 0);
+  return hipGetLastError();
 }
 
 hipError_t launch_ximport(const DevGraph &g, const char *recv, const XRecv &x, int level, hipStream_t s) {

@@ -48,7 +48,7 @@ __device__ inline uint32_t gc_global(const DevGraph &g, const XcArgs &x, uint32_
     return GC_NONE;
   }
   if (p == PHS_ABSENT) return GC_NONE;
-  const uint32_t home = shard_of(g.vid[t], g.n_shards);
+  const uint32_t home = g.psh[t];
   return (uint32_t)(x.off[home] + p);
 }
 
