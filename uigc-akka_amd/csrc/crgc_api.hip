@@ -2695,14 +2695,19 @@ static int sweep_sharded(crgc_graph *h, int should_kill, uint64_t top, double *m
   HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(xcnt), 0, 2 * MAX_SHARDS * 8, h->stream));
   HIP_TRY(launch_list(h->g.d, 1, false, h->g.d.rq_buf, h->g.d.rq_cnt, nblk, nullptr, nullptr, h->stream));
   const auto t0 = std::chrono::steady_clock::now();
-  std::vector<uint64_t> V((size_t)G * (G + 1));
-  if (int rc = ag_u64(h, {{(char *)h->ctr + CTR_OFF(npe), 1}, {(char *)h->ctr + CTR_OFF(xcnt), G}}, V.data()))
+  // one all-gather: every shard's NPE count, garbage count (k_sweep_scan has it)
+  // and kill requests per destination
+  const uint32_t K = G + 2;
+  std::vector<uint64_t> V((size_t)G * K);
+  if (int rc = ag_u64(h, {{(char *)h->ctr + CTR_OFF(npe), 1}, {(char *)h->ctr + CTR_OFF(n_garbage), 1},
+                          {(char *)h->ctr + CTR_OFF(xcnt), G}}, V.data()))
     return rc;
   uint64_t npe = 0;
-  std::vector<uint64_t> R((size_t)G * G);
+  std::vector<uint64_t> R((size_t)G * G), NG(G);
   for (uint32_t r = 0; r < G; ++r) {
-    npe += V[(size_t)r * (G + 1)];
-    for (uint32_t d = 0; d < G; ++d) R[(size_t)r * G + d] = V[(size_t)r * (G + 1) + 1 + d];
+    npe += V[(size_t)r * K];
+    NG[r] = V[(size_t)r * K + 1];
+    for (uint32_t d = 0; d < G; ++d) R[(size_t)r * G + d] = V[(size_t)r * K + 2 + d];
   }
   if (npe) {  // the reference's NullPointerException on some shard: nobody commits
     HIP_TRY(hipMemcpyAsync((char *)h->ctr + CTR_OFF(npe), &npe, 8, hipMemcpyHostToDevice, h->stream));
@@ -2732,8 +2737,6 @@ static int sweep_sharded(crgc_graph *h, int should_kill, uint64_t top, double *m
     HIP_TRY(launch_requests(h->g.d, 1, nullptr, nreq, (uint8_t *)h->x_ans_back.ptr,
                             (const uint32_t *)h->x_slot.ptr, h->stream));
   // the other shards' proxies of this shard's garbage die with it
-  std::vector<uint64_t> NG(G);
-  if (int rc = ag_u64(h, {{(char *)h->ctr + CTR_OFF(n_garbage), 1}}, NG.data())) return rc;
   uint64_t tg = 0;
   for (uint64_t v : NG) tg += v;
   if (tg) {
