@@ -239,7 +239,6 @@ def _declare(lib: C.CDLL, prefix: str) -> None:
     g = _P
     sig = {
         "merge_entries": (C.c_int, [g, P(CrgcEntryBatch)]),
-        "merge_entries_async": (C.c_int, [g, P(CrgcEntryBatch)]),
         "merge_deltas": (C.c_int, [g, P(CrgcDeltaBatch)]),
         "merge_undo": (C.c_int, [g, P(CrgcUndoLog)]),
         "trace": (C.c_int, [g, C.c_int, P(CrgcTraceOut)]),
@@ -250,9 +249,10 @@ def _declare(lib: C.CDLL, prefix: str) -> None:
         "export": (C.c_int, [g, P(CrgcGraphExport)]),
         "destroy": (None, [g]),
     }
-    if prefix == "crgc_":  # product-only entry point (the JVM compacts by itself)
+    if prefix == "crgc_":  # product-only entry points (the JVM compacts by itself; drain-loop chunks)
         sig["compact"] = (C.c_int, [g])
         sig["sync"] = (C.c_int, [g])
+        sig["merge_entries_async"] = (C.c_int, [g, P(CrgcEntryBatch)])
     for name, (res, args) in sig.items():
         fn = getattr(lib, prefix + name)
         fn.restype = res
