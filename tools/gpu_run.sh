@@ -16,6 +16,7 @@
 #                    8 logical shards on the one GPU (the sharded protocol at scale)
 #   c2rs c4rs        the N>1 bench path itself on one rank (nccl group, RCCL transport, one shard)
 #   ktl8             kernel trace of c4l8 (every shard's kernels, one process)
+#   c2l8x<k> c4l8x<k>  c2l8 / c4l8 with mark rounds capped at k levels (CRGC_XLEVELS, test hook)
 #   long             C2 over 200 wakeups: the steady state, rebuilds / repacks amortized in
 set -euo pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -68,6 +69,13 @@ for step in "$@"; do
           --steps 3 --warmup 1 --no-pcie --no-cpu-baseline > "$O/bench_c4rs.json" 2> "$O/bench_c4rs.err") ;;
     c2l8) (cd /tmp && timeout -k 10 600 python3 -u "$ROOT/bench.py" --workload c2 --logical-shards 8 \
           --steps 5 --warmup 2 > "$O/bench_c2l8.json" 2> "$O/bench_c2l8.err") ;;
+    c2l8x*|c4l8x*)  # the same with CRGC_XLEVELS=<k> (mark rounds capped at k levels; a test hook)
+      k=${step#*x}; wl=${step%%l8x*}
+      extra=()
+      [ "$wl" = c4 ] && extra=(--actors 50000000 --edges 500000000 --batch 5000000 --steps 3 --warmup 1)
+      [ "$wl" = c2 ] && extra=(--steps 5 --warmup 2 --no-cpu-baseline)
+      (cd /tmp && CRGC_TEST_HOOKS=1 CRGC_XLEVELS=$k timeout -k 10 600 python3 -u "$ROOT/bench.py" --workload $wl \
+          --logical-shards 8 "${extra[@]}" > "$O/bench_${step}.json" 2> "$O/bench_${step}.err") ;;
     ktl8) (cd /tmp && timeout -k 10 1000 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ktl8" -o kt -- \
           python3 -u "$ROOT/bench.py" --workload c4 --logical-shards 8 \
           --actors 50000000 --edges 500000000 --batch 5000000 --no-cpu-baseline \
