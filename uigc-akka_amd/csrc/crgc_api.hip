@@ -180,11 +180,14 @@ uint64_t region_cap(uint64_t live, uint64_t ids) {
 // Sharded graphs (G > 1) keep their proxies in a region of their own above
 // pbase (DevGraph::pbase), sized like the shadows' region from the live
 // proxies; the id table and the pools serve both.
-Caps caps_regions(uint64_t H, uint64_t P, uint64_t edges, uint64_t atoms_pending) {
+// idtab_x2: id-table buckets per slot, times 2 (3: load <= 1/3 of the slots'
+// worth at 1.5 buckets per slot; CRGC_IDTAB_X2, an A/B of the table's cache
+// footprint)
+Caps caps_regions(uint64_t H, uint64_t P, uint64_t edges, uint64_t atoms_pending, uint32_t idtab_x2 = 3) {
   Caps c;
   c.pbase = H;
   c.scap = H + P;
-  c.hcap = pow2ceil(c.scap * 3 / 2 + 1024);
+  c.hcap = pow2ceil(c.scap * idtab_x2 / 2 + 1024);
   uint64_t pc = 4 * edges + 8 * atoms_pending + 4 * c.scap + 65536;
   c.pcap = std::min<uint64_t>(pc, 0xFFFFFFF0ull);
   c.ecap = pow2ceil((edges + 2 * atoms_pending) * 3 / 2 + 65536);
@@ -192,9 +195,9 @@ Caps caps_regions(uint64_t H, uint64_t P, uint64_t edges, uint64_t atoms_pending
 }
 
 Caps caps_for(uint64_t live, uint64_t live_proxies, bool proxies, uint64_t edges, uint64_t ids_pending,
-              uint64_t atoms_pending) {
+              uint64_t atoms_pending, uint32_t idtab_x2 = 3) {
   return caps_regions(region_cap(live, ids_pending), proxies ? region_cap(live_proxies, ids_pending) : 0, edges,
-                      atoms_pending);
+                      atoms_pending, idtab_x2);
 }
 
 // A new graph's capacities from the caller's hints (expected live shadows v0,
@@ -205,9 +208,9 @@ Caps caps_for(uint64_t live, uint64_t live_proxies, bool proxies, uint64_t edges
 // rebuild, which also reserves for the pending merge.)  At C4 on one GPU
 // (1.1e8 / 1.1e9 hints) this is ~130 GB of the 288 GB: caps_for(v0, e0, v0, e0)
 // asked for ~250 GB there.
-Caps caps_create(uint64_t v0, uint64_t p0, bool proxies, uint64_t e0) {
+Caps caps_create(uint64_t v0, uint64_t p0, bool proxies, uint64_t e0, uint32_t idtab_x2 = 3) {
   auto reg = [](uint64_t v) { return round_up(2 * v + v / 4 + 8192, BLK_SLOTS); };
-  Caps c = caps_regions(reg(v0), proxies ? reg(p0) : 0, 0, 0);
+  Caps c = caps_regions(reg(v0), proxies ? reg(p0) : 0, 0, 0, idtab_x2);
   c.pcap = std::min<uint64_t>(4 * e0 + 4 * c.scap + 65536, 0xFFFFFFF0ull);
   c.ecap = pow2ceil(e0 * 3 / 2 + 65536);
   return c;
@@ -258,6 +261,7 @@ struct Knobs {
   // exchange (0: to the shard's local fixpoint).  Pending candidates carry
   // over into the next round.
   uint32_t xlevels = 0;          // CRGC_XLEVELS
+  uint32_t idtab_x2 = 3;         // CRGC_IDTAB_X2: id-table buckets per slot x 2 (caps_regions)
   bool bin = true;               // CRGC_BIN=0: the pseudo-root level pushes candidate bytes directly
   uint64_t bin_min = 1ull << 22; // CRGC_BIN_MIN_SLOTS: binned only above this many slots (a smaller
                                  // candidate byte map stays in the L2: C1 mark +10 us binned)
@@ -301,6 +305,7 @@ struct Knobs {
     if (const char *m = env("CRGC_BIN")) bin = atoi(m) != 0;
     if (const char *m = env("CRGC_BIN_MIN_SLOTS")) bin_min = strtoull(m, nullptr, 10);
     if (const char *m = env("CRGC_XLEVELS")) xlevels = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_IDTAB_X2")) idtab_x2 = std::max<uint32_t>(1, (uint32_t)strtoul(m, nullptr, 10));
     if (const char *m = env("CRGC_XSLICES")) {
       const uint32_t v = (uint32_t)strtoul(m, nullptr, 10);
       xslices = v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
@@ -514,7 +519,7 @@ hipError_t carry_lists(crgc_graph *h, Arrays &dst) {
 // profiles/r5a; nothing of the trace's pull hints or candidate order is lost).
 int grow(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   const uint64_t top = h->slot_top;
-  Caps c = caps_for(std::max<uint64_t>(top, 1), 0, false, h->etab_used, ids, atoms);
+  Caps c = caps_for(std::max<uint64_t>(top, 1), 0, false, h->etab_used, ids, atoms, h->knobs.idtab_x2);
   // never smaller than before (a grow may be for the tables, not the slots)
   const Caps &oc = h->g.caps;
   c.scap = c.pbase = std::max(c.scap, oc.scap);
@@ -579,7 +584,7 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms, bool may_grow = false) 
   const uint64_t live_ub = std::min<uint64_t>(src_top, h->hctr->alive_cnt[0]);
   const uint64_t live_p = std::min<uint64_t>(src_ptop, h->hctr->alive_cnt[1]);
   if (may_grow && h->G <= 1 && live_ub * 4 >= src_top * 3) return grow(h, ids, atoms);
-  Caps c = caps_for(std::max<uint64_t>(live_ub, 1), live_p, h->G > 1, h->etab_used, ids, atoms);
+  Caps c = caps_for(std::max<uint64_t>(live_ub, 1), live_p, h->G > 1, h->etab_used, ids, atoms, h->knobs.idtab_x2);
   if (h->knobs.level_log)
     fprintf(stderr, "[crgc] rebuild: slots %llu (alive %llu) proxies %llu (alive %llu) pool %llu / %llu rpool %llu "
                     "edge keys %llu / %llu -> slots %llu pool %llu edge table %llu\n",
@@ -869,7 +874,7 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     // a shard's proxy region from its own hint (ABI 5); without one it is sized
     // like the shadows' region
     const uint64_t p0 = cfg && cfg->proxy_capacity ? cfg->proxy_capacity : v0;
-    Caps c = caps_create(v0, p0, h->G > 1, e0);
+    Caps c = caps_create(v0, p0, h->G > 1, e0, h->knobs.idtab_x2);
     if (hipError_t e = alloc_arrays(h->g, c, h->ctr, h->stream, h->G, h->shard, h->tp != nullptr)) {
       rc = map_hip(e);
       break;
