@@ -262,6 +262,8 @@ struct Knobs {
   // over into the next round.
   uint32_t xlevels = 0;          // CRGC_XLEVELS
   uint32_t idtab_x2 = 3;         // CRGC_IDTAB_X2: id-table buckets per slot x 2 (caps_regions)
+  uint64_t xbitmap_ratio = 8;    // CRGC_XBITMAP_RATIO: a mark round's home slots as a bitmap above
+                                 // this many list bytes per bitmap byte (mark_all)
   bool bin = true;               // CRGC_BIN=0: the pseudo-root level pushes candidate bytes directly
   uint64_t bin_min = 1ull << 22; // CRGC_BIN_MIN_SLOTS: binned only above this many slots (a smaller
                                  // candidate byte map stays in the L2: C1 mark +10 us binned)
@@ -305,6 +307,7 @@ struct Knobs {
     if (const char *m = env("CRGC_BIN")) bin = atoi(m) != 0;
     if (const char *m = env("CRGC_BIN_MIN_SLOTS")) bin_min = strtoull(m, nullptr, 10);
     if (const char *m = env("CRGC_XLEVELS")) xlevels = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_XBITMAP_RATIO")) xbitmap_ratio = std::max<uint64_t>(1, strtoull(m, nullptr, 10));
     if (const char *m = env("CRGC_IDTAB_X2")) idtab_x2 = std::max<uint32_t>(1, (uint32_t)strtoul(m, nullptr, 10));
     if (const char *m = env("CRGC_XSLICES")) {
       const uint32_t v = (uint32_t)strtoul(m, nullptr, 10);
@@ -2503,8 +2506,13 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
   auto n_id = [&](uint32_t r, uint32_t d) { return M[(size_t)r * (2 * G + 1) + d]; };
   auto n_sl = [&](uint32_t r, uint32_t d) { return M[(size_t)r * (2 * G + 1) + G + d]; };
   auto words = [&](uint32_t d) { return (h->peer_top[d] + 31) / 32; };
+  // A destination's home slots travel as a bitmap only once the list would be
+  // xbitmap_ratio times its bytes: a bitmap costs the sender one global atomicOr
+  // per mark (~20 G/s on gfx950), a list an LDS atomic and a coalesced store,
+  // and the receiver imports either mark by mark.
+  const uint64_t ratio = h->knobs.xbitmap_ratio;
   auto bitmap = [&](uint32_t r, uint32_t d) {
-    return n_sl(r, d) > 0 && (xmode == 2 || n_sl(r, d) > words(d));
+    return n_sl(r, d) > 0 && (xmode == 2 || n_sl(r, d) > ratio * words(d));
   };
   auto seg_bytes = [&](uint32_t r, uint32_t d) {
     const uint64_t b = 8 * n_id(r, d) + 4 * (bitmap(r, d) ? words(d) : n_sl(r, d));
