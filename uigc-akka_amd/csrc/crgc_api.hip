@@ -2749,17 +2749,22 @@ static int sweep_sharded(crgc_graph *h, int should_kill, uint64_t top, double *m
   if (nreq)
     HIP_TRY(launch_requests(h->g.d, 1, nullptr, nreq, (uint8_t *)h->x_ans_back.ptr,
                             (const uint32_t *)h->x_slot.ptr, h->stream));
-  // the other shards' proxies of this shard's garbage die with it
-  uint64_t tg = 0;
-  for (uint64_t v : NG) tg += v;
-  if (tg) {
+  // the other shards' proxies of this shard's garbage die with it (a shard
+  // holds no proxy of an actor it homes: nothing goes to itself, so a one-shard
+  // graph exchanges nothing here; the condition is the same on every shard)
+  uint64_t tg = 0, tin = 0;
+  for (uint32_t r = 0; r < G; ++r) {
+    tg += NG[r];
+    if (r != me) tin += NG[r];
+  }
+  if (G > 1 && tg) {
     size_t soff[MAX_SHARDS], sb[MAX_SHARDS], roff[MAX_SHARDS], rb[MAX_SHARDS];
     size_t ro = 0;
     for (uint32_t r = 0; r < G; ++r) {
       soff[r] = 0;
-      sb[r] = NG[me] * 8;
+      sb[r] = r == me ? 0 : NG[me] * 8;
       roff[r] = ro;
-      rb[r] = NG[r] * 8;
+      rb[r] = r == me ? 0 : NG[r] * 8;
       ro += rb[r];
     }
     if (h->x_recv.ensure(ro + 8) != hipSuccess) return CRGC_E_NOMEM;
@@ -2767,7 +2772,7 @@ static int sweep_sharded(crgc_graph *h, int should_kill, uint64_t top, double *m
       h->poisoned = true;
       return rc;
     }
-    HIP_TRY(launch_invalidate(h->g.d, (const uint64_t *)h->x_recv.ptr, tg, h->stream));
+    HIP_TRY(launch_invalidate(h->g.d, (const uint64_t *)h->x_recv.ptr, tin, h->stream));
   }
   *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return CRGC_OK;
