@@ -920,7 +920,7 @@ __global__ __launch_bounds__(BIN_T) void k_bin_apply(DevGraph g, LevelArgs a) {
   uint32_t nb2 = 0;
   // its slices, four at a time per wave (their counts from LDS: the loop
   // bounds are wave-uniform), each slice's filled part in 16-B groups
-  const uint4 *src = (const uint4 *)(a.bins + (uint64_t)b * G * SC);
+  const uint4 *src = (const uint4 *)((const char *)a.bins + (uint64_t)b * G * SC * (B16 ? 2 : 4));
   const uint32_t base = b << a.bin_shift;
   for (uint32_t k0 = (uint32_t)(tid >> 6); k0 < NS; k0 += BIN_NW * 4) {
     uint32_t n[4], mx = 0;
