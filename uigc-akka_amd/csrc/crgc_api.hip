@@ -1509,6 +1509,9 @@ static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint3
       total += sz[i];
     }
   }
+  // (a larger staging area frees the old one: let the work queued on it finish first —
+  // an async merge's copies and merges may still read it)
+  if (total + 256 > h->stage.bytes) HIP_TRY(hsync(h));
   if (h->stage.ensure(total + 256) != hipSuccess) return CRGC_E_NOMEM;
   char *base = (char *)h->stage.ptr;
   // the staging area is free once the work already queued on the graph's stream is done
