@@ -1053,6 +1053,11 @@ __device__ inline void tail_claim_batch(const DevGraph &g, const TailLds &sh, co
 #pragma unroll
   for (int k = 0; k < N; ++k) {
     if ((w[k] >> (t[k] & 31)) & 1u) continue;  // marked already, or not a target
+    if (t[k] >= g.pbase) {  // a proxy (sharded graphs): nothing to walk, listed for the exchange at once
+      const uint32_t pos = atomicAdd(&g.xp_cnt[t[k] >> 11], 1u);
+      g.xp_buf[(uint64_t)(t[k] >> 11) * BLK_SLOTS + pos] = t[k];
+      continue;
+    }
     if (keep && *keep == NO_SLOT) {
       *keep = t[k];
       ++claims;
@@ -1908,44 +1913,67 @@ __global__ __launch_bounds__(256) void k_xlist(DevGraph g, const uint32_t *buf, 
   const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
   const uint64_t p0 = g.pbase / BLK_SLOTS;
   const uint64_t nblk = p0 + (g.ctr->proxy_top + BLK_SLOTS - 1) / BLK_SLOTS;
+  // XU entries per lane in flight: a wave's entries are a chain of dependent
+  // loads (listing -> home shard / home slot), so one at a time left the kernel
+  // latency-bound (round 4: ~600 us per launch at C4 over 8 logical shards)
+  constexpr uint32_t XU = 4;
+  const uint32_t lane = lane_id();
   for (uint64_t blk = p0 + gw; blk < nblk; blk += nw) {
     const uint32_t n = cnt[blk];
-    for (uint32_t i = lane_id(); i < n; i += 64) {
-      const uint32_t v = buf[blk * BLK_SLOTS + i];
-      const uint32_t d = g.psh[v];
-      const bool res = x.use_slots && g.phs[v] < PHS_ABSENT;
-      atomicAdd(&hist[res ? 1 : 0][d], 1u);
+    const uint32_t *lb = buf + blk * BLK_SLOTS;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64 * XU) {
+      uint32_t v[XU], d[XU], hs[XU];
+#pragma unroll
+      for (uint32_t u = 0; u < XU; ++u) v[u] = i0 + u * 64 + lane < n ? lb[i0 + u * 64 + lane] : NO_SLOT;
+#pragma unroll
+      for (uint32_t u = 0; u < XU; ++u) {
+        d[u] = v[u] != NO_SLOT ? g.psh[v[u]] : 0u;
+        hs[u] = v[u] != NO_SLOT && x.use_slots ? g.phs[v[u]] : PHS_NONE;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < XU; ++u)
+        if (v[u] != NO_SLOT) atomicAdd(&hist[hs[u] < PHS_ABSENT ? 1 : 0][d[u]], 1u);
     }
   }
   __syncthreads();
   if (!SCATTER) {
-    for (uint32_t d = threadIdx.x; d < g.n_shards; d += 256) {
-      if (hist[0][d]) atomicAdd(&g.ctr->xcnt[d], (unsigned long long)hist[0][d]);
-      if (hist[1][d]) atomicAdd(&g.ctr->xcnt2[d], (unsigned long long)hist[1][d]);
+    for (uint32_t dd = threadIdx.x; dd < g.n_shards; dd += 256) {
+      if (hist[0][dd]) atomicAdd(&g.ctr->xcnt[dd], (unsigned long long)hist[0][dd]);
+      if (hist[1][dd]) atomicAdd(&g.ctr->xcnt2[dd], (unsigned long long)hist[1][dd]);
     }
     return;
   }
   if (threadIdx.x < g.n_shards) {
-    const uint32_t d = threadIdx.x;
-    base[0][d] = hist[0][d] ? atomicAdd(&g.ctr->xpos[d], (unsigned long long)hist[0][d]) : 0ull;
-    base[1][d] = hist[1][d] && !x.bitmap[d] ? atomicAdd(&g.ctr->xpos2[d], (unsigned long long)hist[1][d]) : 0ull;
-    hist[0][d] = hist[1][d] = 0;
+    const uint32_t dd = threadIdx.x;
+    base[0][dd] = hist[0][dd] ? atomicAdd(&g.ctr->xpos[dd], (unsigned long long)hist[0][dd]) : 0ull;
+    base[1][dd] = hist[1][dd] && !x.bitmap[dd] ? atomicAdd(&g.ctr->xpos2[dd], (unsigned long long)hist[1][dd]) : 0ull;
+    hist[0][dd] = hist[1][dd] = 0;
   }
   __syncthreads();
   for (uint64_t blk = p0 + gw; blk < nblk; blk += nw) {
     const uint32_t n = cnt[blk];
-    for (uint32_t i = lane_id(); i < n; i += 64) {
-      const uint32_t v = buf[blk * BLK_SLOTS + i];
-      const uint32_t d = g.psh[v];
-      const uint32_t hs = x.use_slots ? g.phs[v] : PHS_NONE;
-      if (hs >= PHS_ABSENT) {  // (the id only for the unresolved)
-        const uint64_t at = base[0][d] + atomicAdd(&hist[0][d], 1u);
-        ((uint64_t *)(send + x.id_off[d]))[at] = g.vid[v];
-      } else if (x.bitmap[d]) {
-        atomicOr((uint32_t *)(send + x.sl_off[d]) + (hs >> 5), 1u << (hs & 31));
-      } else {
-        const uint64_t at = base[1][d] + atomicAdd(&hist[1][d], 1u);
-        ((uint32_t *)(send + x.sl_off[d]))[at] = hs;
+    const uint32_t *lb = buf + blk * BLK_SLOTS;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64 * XU) {
+      uint32_t v[XU], d[XU], hs[XU];
+#pragma unroll
+      for (uint32_t u = 0; u < XU; ++u) v[u] = i0 + u * 64 + lane < n ? lb[i0 + u * 64 + lane] : NO_SLOT;
+#pragma unroll
+      for (uint32_t u = 0; u < XU; ++u) {
+        d[u] = v[u] != NO_SLOT ? g.psh[v[u]] : 0u;
+        hs[u] = v[u] != NO_SLOT && x.use_slots ? g.phs[v[u]] : PHS_NONE;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < XU; ++u) {
+        if (v[u] == NO_SLOT) continue;
+        if (hs[u] >= PHS_ABSENT) {  // (the id only for the unresolved)
+          const uint64_t at = base[0][d[u]] + atomicAdd(&hist[0][d[u]], 1u);
+          ((uint64_t *)(send + x.id_off[d[u]]))[at] = g.vid[v[u]];
+        } else if (x.bitmap[d[u]]) {
+          atomicOr((uint32_t *)(send + x.sl_off[d[u]]) + (hs[u] >> 5), 1u << (hs[u] & 31));
+        } else {
+          const uint64_t at = base[1][d[u]] + atomicAdd(&hist[1][d[u]], 1u);
+          ((uint32_t *)(send + x.sl_off[d[u]]))[at] = hs[u];
+        }
       }
     }
   }
