@@ -4,6 +4,7 @@
 # steps (each under its own time limit, chained: the first failure ends the call):
 #   tests[:-k expr]  pytest -m gpu (optionally -k)        smoke   __graft_entry__.smoke()
 #   c2 c1 c3 c5      bench.py lines                        levels  C2 level log (CRGC_LEVEL_LOG)
+#   c2d              the driver's N = 1 command (--gpus 1 --steps 20 --warmup 5)
 #   kt               rocprofv3 --kernel-trace --stats of the timed C2 wakeups only (--no-pcie)
 #   ktp              the same with the PCIe-inclusive wakeups (pageable, then registered host batches) at the end
 #   pmc              FETCH_SIZE and WRITE_SIZE passes of the same command, one run each
@@ -35,6 +36,8 @@ for step in "$@"; do
         --timeout-method thread "${K[@]}" > "$O/gpu_tests.log" 2>&1) ;;
     smoke) (cd "$ROOT" && timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1) ;;
     c2) (cd /tmp && timeout -k 10 480 python3 "$ROOT/bench.py" > "$O/bench_c2.json" 2> "$O/bench_c2.err") ;;
+    c2d) (cd /tmp && timeout -k 10 600 python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 \
+          > "$O/bench_c2d.json" 2> "$O/bench_c2d.err") ;;  # the driver's own N = 1 command
     c2q) (cd /tmp && timeout -k 10 300 python3 "$ROOT/bench.py" --no-cpu-baseline > "$O/bench_c2q.json" 2> "$O/bench_c2q.err") ;;
     c1) (cd /tmp && timeout -k 10 300 python3 "$ROOT/bench.py" --workload c1 > "$O/bench_c1.json" 2> "$O/bench_c1.err") ;;
     c3) (cd /tmp && timeout -k 10 300 python3 "$ROOT/bench.py" --workload c3 > "$O/bench_c3.json" 2> "$O/bench_c3.err") ;;
