@@ -17,8 +17,8 @@
 #                    8 logical shards on the one GPU (the sharded protocol at scale)
 #   c2rs c4rs        the N>1 bench path itself on one rank (nccl group, RCCL transport, one shard)
 #   ktl8             kernel trace of c4l8 (every shard's kernels, one process)
-#   ktl8s            ktl8 with one hardware queue (GPU_MAX_HW_QUEUES=1): the shards' kernels run one at a
-#                    time, so each duration is the kernel's own and their sum is the GPU work per wakeup
+#   ktl8s            ktl8 with every shard on one stream (--shared-stream): the shards' kernels run one at
+#                    a time, so each duration is the kernel's own and their sum is the GPU work per wakeup
 #   kt2l8s           the same for C2 over 8 logical shards
 #   c2l8x<k> c4l8x<k>  c2l8 / c4l8 with mark rounds capped at k levels (CRGC_XLEVELS, test hook)
 #   long             C2 over 200 wakeups: the steady state, rebuilds / repacks amortized in
@@ -86,12 +86,13 @@ for step in "$@"; do
           python3 -u "$ROOT/bench.py" --workload c4 --logical-shards 8 \
           --actors 50000000 --edges 500000000 --batch 5000000 --no-cpu-baseline \
           --steps 2 --warmup 1 > "$O/bench_ktl8.json" 2> "$O/bench_ktl8.err") ;;
-    ktl8s) (cd /tmp && GPU_MAX_HW_QUEUES=1 timeout -k 10 1000 rocprofv3 --kernel-trace --stats --output-format csv \
-          -d "$O/ktl8s" -o kt -- python3 -u "$ROOT/bench.py" --workload c4 --logical-shards 8 \
+    ktl8s) (cd /tmp && timeout -k 10 1000 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$O/ktl8s" -o kt -- python3 -u "$ROOT/bench.py" --workload c4 --logical-shards 8 --shared-stream \
           --actors 50000000 --edges 500000000 --batch 5000000 --no-cpu-baseline \
           --steps 2 --warmup 1 > "$O/bench_ktl8s.json" 2> "$O/bench_ktl8s.err") ;;
-    kt2l8s) (cd /tmp && GPU_MAX_HW_QUEUES=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
-          -d "$O/kt2l8s" -o kt -- python3 -u "$ROOT/bench.py" --workload c2 --logical-shards 8 --no-cpu-baseline \
+    kt2l8s) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$O/kt2l8s" -o kt -- python3 -u "$ROOT/bench.py" --workload c2 --logical-shards 8 --shared-stream \
+          --no-cpu-baseline \
           --steps 4 --warmup 2 > "$O/bench_kt2l8s.json" 2> "$O/bench_kt2l8s.err") ;;
     long) (cd /tmp && timeout -k 10 900 python3 -u "$ROOT/bench.py" --steps 200 --warmup 2 --no-pcie \
           --no-cpu-baseline > "$O/bench_long.json" 2> "$O/bench_long.err") ;;

@@ -462,7 +462,11 @@ class ShardedShadowGraph:
     """
 
     def __init__(self, n_shards: int, devices=None, entry_field_size: int = 4,
-                 vertex_capacity: int = 0, edge_capacity: int = 0, proxy_capacity: int = 0):
+                 vertex_capacity: int = 0, edge_capacity: int = 0, proxy_capacity: int = 0,
+                 stream: Optional[int] = None):
+        """stream: one hipStream_t for every shard (a diagnostic: the shards'
+        kernels then run one at a time, so a kernel trace shows each one's own
+        duration); default, each shard its own stream."""
         import concurrent.futures as cf
         self.G = n_shards
         devices = list(devices) if devices is not None else [0] * n_shards
@@ -470,7 +474,7 @@ class ShardedShadowGraph:
         self.shards = [ShadowGraph(entry_field_size=entry_field_size, device=devices[r],
                                    vertex_capacity=vertex_capacity, edge_capacity=edge_capacity,
                                    n_shards=n_shards, shard=r, transport=self.transport,
-                                   proxy_capacity=proxy_capacity)
+                                   proxy_capacity=proxy_capacity, stream=stream)
                        for r in range(n_shards)]
         self._pool = cf.ThreadPoolExecutor(max_workers=n_shards)
 
