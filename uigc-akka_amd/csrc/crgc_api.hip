@@ -2277,9 +2277,11 @@ static void collect_times(crgc_graph *h, LevelRun &lr, size_t nl, size_t nc, int
     lr.ms_f += t[0];
     lr.ms_t += t[1];
     lr.ms_e += t[2];
+    char who[24] = "";
+    if (log && h->G > 1) snprintf(who, sizeof who, " s%u", h->shard);
     if (log)
-      fprintf(stderr, "[crgc] level %zu frontier %llu  %.1f us (frontier %.1f tail %.1f expand %.1f)\n",
-              first_level + i, first_level + i <= last ? ring[(first_level + i) % LEVEL_RING] : 0ull,
+      fprintf(stderr, "[crgc%s] level %zu frontier %llu  %.1f us (frontier %.1f tail %.1f expand %.1f)\n",
+              who, first_level + i, first_level + i <= last ? ring[(first_level + i) % LEVEL_RING] : 0ull,
               (t[0] + t[1] + t[2]) * 1e3, t[0] * 1e3, t[1] * 1e3, t[2] * 1e3);
   }
 }

@@ -34,6 +34,12 @@ __device__ inline bool sparse_level(const Counters *c, int L, uint32_t thr) {
   return c->ring[(L - 2) % LEVEL_RING] < thr;
 }
 
+// The slots a pull level walks: the shadows' own and, in a sharded graph, the
+// proxy region (a shard of C4 over 8 holds ~6x more proxies than shadows, so a
+// frontier of slot_top / div is far too narrow for a pull to pay there: round
+// 5's C4 logical-shard trace spent 13 of its 18 ms of k_expand in such pulls).
+__device__ inline uint64_t pull_span(const Counters *c) { return c->slot_top + c->proxy_top; }
+
 // Direction choice for level L (same answer in k_frontier and k_expand): pull
 // when the previous frontier was large; the level is then dense, so every
 // block of the slot range is scanned and `fx` is complete.
@@ -41,7 +47,7 @@ __device__ inline bool pull_level(const Counters *c, int L, const LevelArgs &a) 
   if (!(a.flags & LV_PULL) || L < 1) return false;
   if (sparse_level(c, L, a.sparse_thresh) || sparse_level(c, L + 1, a.sparse_thresh)) return false;
   const uint64_t prev = c->ring[(L - 1) % LEVEL_RING];
-  return a.pull_div ? prev * a.pull_div >= c->slot_top : prev >= a.pull_thresh;
+  return a.pull_div ? prev * a.pull_div >= pull_span(c) : prev >= a.pull_thresh;
 }
 
 // Levels whose k_frontier scans every block write `fx`, so k_expand can still
@@ -63,7 +69,7 @@ __device__ inline bool fx_level(const Counters *c, int L, const LevelArgs &a) {
 __device__ inline bool pull_now(const Counters *c, int L, const LevelArgs &a) {
   if (pull_level(c, L, a)) return true;
   if (!fx_level(c, L, a)) return false;
-  if (!a.alpha) return c->ring[L % LEVEL_RING] * a.pull_cur_div >= c->slot_top;
+  if (!a.alpha) return c->ring[L % LEVEL_RING] * a.pull_cur_div >= pull_span(c);
   const uint64_t mu = a.e_total > c->mf_sum ? a.e_total - c->mf_sum : 0;
   return c->mf_level * a.alpha > mu;
 }
