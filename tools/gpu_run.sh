@@ -22,6 +22,7 @@
 #   kt2l8s           the same for C2 over 8 logical shards
 #   c2l8x<k> c4l8x<k>  c2l8 / c4l8 with mark rounds capped at k levels (CRGC_XLEVELS, test hook)
 #   ab2l8:<variants> ab4l8:<variants>  tools/ab_l8.sh A/B of env variants on C2 / C4 logical shards
+#   longkt           kernel trace + level log of the long run
 #   long             C2 over 200 wakeups: the steady state, rebuilds / repacks amortized in
 set -euo pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -96,9 +97,12 @@ for step in "$@"; do
           --no-cpu-baseline \
           --steps 4 --warmup 2 > "$O/bench_kt2l8s.json" 2> "$O/bench_kt2l8s.err") ;;
     ab2l8:*|ab4l8:*)  # tools/ab_l8.sh over the variants after the colon (separated by spaces)
-      wl=${step%%l8:*}; wl=${wl#ab}
+      wl=${step%%l8:*}; wl=c${wl#ab}
       read -ra vs <<< "${step#*:}"
       (cd "$ROOT" && bash tools/ab_l8.sh "$TAG/ab_${wl}l8" "$wl" "${vs[@]}" > /dev/null) ;;
+    longkt) (cd /tmp && CRGC_LEVEL_LOG=1 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$O/longkt" -o kt -- python3 -u "$ROOT/bench.py" --steps 200 --warmup 2 --no-pcie --no-cpu-baseline \
+          > "$O/bench_longkt.json" 2> "$O/bench_longkt.err") ;;
     long) (cd /tmp && timeout -k 10 900 python3 -u "$ROOT/bench.py" --steps 200 --warmup 2 --no-pcie \
           --no-cpu-baseline > "$O/bench_long.json" 2> "$O/bench_long.err") ;;
     *) echo "unknown step $step"; exit 2 ;;
