@@ -20,6 +20,7 @@
 #   ktl8s            ktl8 with every shard on one stream (--shared-stream): the shards' kernels run one at
 #                    a time, so each duration is the kernel's own and their sum is the GPU work per wakeup
 #   kt2l8s           the same for C2 over 8 logical shards
+#   c4l8s c2l8s      logical shards on one shared stream with the per-shard level log (all level kernels timed)
 #   c2l8x<k> c4l8x<k>  c2l8 / c4l8 with mark rounds capped at k levels (CRGC_XLEVELS, test hook)
 #   ab2l8:<variants> ab4l8:<variants>  tools/ab_l8.sh A/B of env variants on C2 / C4 logical shards
 #   longkt           kernel trace + level log of the long run
@@ -69,6 +70,12 @@ for step in "$@"; do
     c4l8) (cd /tmp && CRGC_LEVEL_LOG=1 timeout -k 10 1000 python3 -u "$ROOT/bench.py" --workload c4 --logical-shards 8 \
           --actors 50000000 --edges 500000000 --batch 5000000 \
           --steps 3 --warmup 1 > "$O/bench_c4l8.json" 2> "$O/bench_c4l8.err") ;;
+    c4l8s|c2l8s)  # the logical-shard run on one shared stream with the level log (every level kernel timed)
+      wl=${step%%l8s}; extra=(--steps 3 --warmup 1)
+      [ "$wl" = c4 ] && extra=(--actors 50000000 --edges 500000000 --batch 5000000 --steps 2 --warmup 1)
+      (cd /tmp && CRGC_LEVEL_LOG=1 CRGC_KERNEL_TIMING=2 timeout -k 10 600 python3 -u "$ROOT/bench.py" --workload $wl \
+          --logical-shards 8 --shared-stream --no-cpu-baseline "${extra[@]}" > "$O/bench_${step}.json" \
+          2> "$O/bench_${step}.err") ;;
     c2rs) (cd /tmp && timeout -k 10 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node=1 \
           --master-addr=127.0.0.1 --master-port=29517 "$ROOT/bench.py" --gpus 1 --workload c2 --rehearse-sharded \
           --steps 5 --warmup 2 --no-pcie > "$O/bench_c2rs.json" 2> "$O/bench_c2rs.err") ;;
