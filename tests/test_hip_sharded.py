@@ -284,16 +284,18 @@ def test_rccl_transport_single_rank(hip_mod, oracle_mod):
         t.close()
 
 
-@pytest.mark.parametrize("xbits,xlevels", [("0", "0"), ("1", "0"), ("2", "0"), ("1", "1"), ("1", "3")])
-def test_c4_shape_eight_shards(sharded, oracle_mod, xbits, xlevels, monkeypatch):
+@pytest.mark.parametrize("xbits,xlevels,ratio", [("0", "0", "32"), ("1", "0", "32"), ("1", "0", "1"), ("2", "0", "32"),
+                                                 ("1", "1", "32"), ("1", "3", "32")])
+def test_c4_shape_eight_shards(sharded, oracle_mod, xbits, xlevels, ratio, monkeypatch):
     """G = 8 logical shards (the 8-GPU layout of C4) on a scaled C2/C4-shaped
     power-law graph with §8d wakeups (9 % busy, 1 % in flight), split batches:
     bit-exact against the unsharded oracle at every wakeup, with marks sent as
-    ids only (0), in the cheaper of home slots / bitmaps (1), or as bitmaps (2),
-    and rounds run to each shard's local fixpoint (XLEVELS 0) or capped at 1 / 3
-    levels."""
+    ids only (0), as home-slot lists (1; with CRGC_XBITMAP_RATIO=1 as a bitmap
+    wherever that is smaller), or as bitmaps (2), and rounds run to each shard's
+    local fixpoint (XLEVELS 0) or capped at 1 / 3 levels."""
     monkeypatch.setenv("CRGC_XBITS", xbits)
     monkeypatch.setenv("CRGC_XLEVELS", xlevels)
+    monkeypatch.setenv("CRGC_XBITMAP_RATIO", ratio)
     V = 200_000
     w = world.World(seed=0x5EED + 4)
     w.bulk_graph(V, 10 * V, alpha=2.1, n_roots=V // 1000, cap=100000)

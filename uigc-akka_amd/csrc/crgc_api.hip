@@ -245,6 +245,14 @@ struct Knobs {
   bool tail = true;              // CRGC_TAIL=0: no narrow-frontier takeover
   uint32_t tail_start = 8192;    // CRGC_TAIL_START
   uint32_t tail_max = 32768;     // CRGC_TAIL_MAX
+  // Sharded graphs: one workgroup walks a shard's narrow levels with its marked
+  // bitmap in HBM (no LDS copy past 2^20 slots) and lists most targets as
+  // proxies, ~1 G edges/s: the level kernels are faster from a few thousand
+  // shadows up (C2 over 8 logical shards: 18.4 -> 17.1 ms per wakeup at
+  // 2048 / 4096 against 8192 / 32768, profiles/r5h).  CRGC_TAIL_START /
+  // CRGC_TAIL_MAX set both forms.
+  uint32_t tail_start_sharded = 2048;
+  uint32_t tail_max_sharded = 4096;
   uint32_t chain_after = 64;     // CRGC_CHAIN_AFTER
   int kernel_timing = 1;         // CRGC_KERNEL_TIMING: 0 chunks, 1 k_expand, 2 all level kernels
   bool level_log = false;        // CRGC_LEVEL_LOG
@@ -262,8 +270,8 @@ struct Knobs {
   // over into the next round.
   uint32_t xlevels = 0;          // CRGC_XLEVELS
   uint32_t idtab_x2 = 3;         // CRGC_IDTAB_X2: id-table buckets per slot x 2 (caps_regions)
-  uint64_t xbitmap_ratio = 8;    // CRGC_XBITMAP_RATIO: a mark round's home slots as a bitmap above
-                                 // this many list bytes per bitmap byte (mark_all)
+  uint64_t xbitmap_ratio = 32;   // CRGC_XBITMAP_RATIO: a mark round's home slots as a bitmap above
+                                 // this many list bytes per bitmap byte (mark_all; 32: never)
   bool bin = true;               // CRGC_BIN=0: the pseudo-root level pushes candidate bytes directly
   uint64_t bin_min = 1ull << 22; // CRGC_BIN_MIN_SLOTS: binned only above this many slots (a smaller
                                  // candidate byte map stays in the L2: C1 mark +10 us binned)
@@ -296,8 +304,8 @@ struct Knobs {
       sparse_thresh = (uint32_t)strtoul(m, nullptr, 10);
     }
     if (const char *m = env("CRGC_TAIL")) tail = atoi(m) != 0;
-    if (const char *m = env("CRGC_TAIL_START")) tail_start = (uint32_t)strtoul(m, nullptr, 10);
-    if (const char *m = env("CRGC_TAIL_MAX")) tail_max = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_TAIL_START")) tail_start = tail_start_sharded = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_TAIL_MAX")) tail_max = tail_max_sharded = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_CHAIN_AFTER")) chain_after = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_XBITS")) xbits = atoi(m);
     if (const char *m = env("CRGC_BUCKETS_LOG2"))
@@ -2044,7 +2052,7 @@ static void collect_times(crgc_graph *h, LevelRun &lr, size_t nl, size_t nc, int
 static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64_t top, bool roots,
                       int start, LevelRun &lr, int *end,
                       const std::function<hipError_t()> &after_chunk = nullptr, int max_levels = 0,
-                      bool *capped = nullptr) {
+                      bool *capped = nullptr, int first_chunk = 4) {
   if (capped) *capped = false;
   LevelArgs la{};
   la.location = location;
@@ -2085,8 +2093,8 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   // (pointer jumping, crgc_chain.hip).  Unsharded graphs only.
   la.chain_after = h->tp ? 0 : kn.chain_after;
   la.xslices = kn.xslices;
-  la.tail_start = std::min<uint32_t>(kn.tail_start, TAIL_QCAP);
-  la.tail_max = std::min<uint32_t>(std::max(kn.tail_max, 1u), TAIL_QCAP);
+  la.tail_start = std::min<uint32_t>(h->tp ? kn.tail_start_sharded : kn.tail_start, TAIL_QCAP);
+  la.tail_max = std::min<uint32_t>(std::max(h->tp ? kn.tail_max_sharded : kn.tail_max, 1u), TAIL_QCAP);
   // The pseudo-root level's binned push (crgc_trace.hip k_bin_place / k_bin_apply):
   // up to 256 bins of >= 65536 slots (an LDS bitmap of <= 128 KiB each), BIN_WG
   // place workgroups with a fixed-capacity slice of every bin each; the slices
@@ -2151,7 +2159,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
     HIP_TRY(launch(0, true));
     L = 1;
   }
-  int chunk = roots && h->last_levels ? (int)std::min<uint64_t>(h->last_levels, 512) : 4;
+  int chunk = roots && h->last_levels ? (int)std::min<uint64_t>(h->last_levels, 512) : std::max(first_chunk, 1);
   std::vector<unsigned long long> ring(LEVEL_RING);
   unsigned long long tail[3] = {0, 0, 0};
   const bool log = kn.level_log;
@@ -2601,7 +2609,12 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
     HIP_TRY(launch_round_start(h->ctr, L, !capped, h->stream));
     HIP_TRY(launch_ximport(h->g.d, (const char *)h->x_recv.ptr, xr, L, h->stream));
     *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    if (int rc = run_levels(h, investigate, location, top, false, L, lr, &end, nullptr, cap, &capped)) return rc;
+    // A round from a few received marks is usually finished by k_tail in its
+    // first level: launch one level first, not four (the rest would only check
+    // that the mark is done: ~13 us each)
+    const int first = !capped && items <= h->knobs.tail_start_sharded ? 1 : 4;
+    if (int rc = run_levels(h, investigate, location, top, false, L, lr, &end, nullptr, cap, &capped, first))
+      return rc;
     ++*rounds;
   }
 }

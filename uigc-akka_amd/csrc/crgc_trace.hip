@@ -1912,9 +1912,10 @@ hipError_t launch_resolve(const DevGraph &g, int step, uint64_t mask, uint64_t *
 template <bool SCATTER>
 __global__ __launch_bounds__(256) void k_xlist(DevGraph g, const uint32_t *buf, const uint32_t *cnt, char *send,
                                                XSend x) {
-  __shared__ uint32_t hist[2][MAX_SHARDS];
-  __shared__ unsigned long long base[2][MAX_SHARDS];
-  for (uint32_t d = threadIdx.x; d < 2 * MAX_SHARDS; d += 256) hist[d / MAX_SHARDS][d % MAX_SHARDS] = 0;
+  // per (form, destination): this workgroup's count, then its next position
+  __shared__ uint32_t hist[2 * MAX_SHARDS];
+  __shared__ unsigned long long base[2 * MAX_SHARDS];
+  for (uint32_t d = threadIdx.x; d < 2 * MAX_SHARDS; d += 256) hist[d] = 0;
   __syncthreads();
   const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
   const uint64_t p0 = g.pbase / BLK_SLOTS;
@@ -1924,61 +1925,84 @@ __global__ __launch_bounds__(256) void k_xlist(DevGraph g, const uint32_t *buf, 
   // latency-bound (round 4: ~600 us per launch at C4 over 8 logical shards)
   constexpr uint32_t XU = 4;
   const uint32_t lane = lane_id();
+  // Entry -> key (form << 6 | destination; form 1: a resolved home slot).
+  // Keys are aggregated per wave (one ballot per distinct key, one LDS atomic
+  // per key and wave): 64 lanes' LDS atomics on G counters serialised, and
+  // ranks from them scattered each destination's run over the segment.
+  auto keys = [&](uint64_t blk, uint32_t i0, uint32_t n, uint32_t (&v)[XU], uint32_t (&k)[XU], uint32_t (&hs)[XU]) {
+    const uint32_t *lb = buf + blk * BLK_SLOTS;
+#pragma unroll
+    for (uint32_t u = 0; u < XU; ++u) v[u] = i0 + u * 64 + lane < n ? lb[i0 + u * 64 + lane] : NO_SLOT;
+#pragma unroll
+    for (uint32_t u = 0; u < XU; ++u) {
+      const uint32_t d = v[u] != NO_SLOT ? g.psh[v[u]] : 0u;
+      hs[u] = v[u] != NO_SLOT && x.use_slots ? g.phs[v[u]] : PHS_NONE;
+      k[u] = v[u] == NO_SLOT ? ~0u : ((hs[u] < PHS_ABSENT ? 64u : 0u) | d);
+    }
+  };
   for (uint64_t blk = p0 + gw; blk < nblk; blk += nw) {
     const uint32_t n = cnt[blk];
-    const uint32_t *lb = buf + blk * BLK_SLOTS;
     for (uint32_t i0 = 0; i0 < n; i0 += 64 * XU) {
-      uint32_t v[XU], d[XU], hs[XU];
-#pragma unroll
-      for (uint32_t u = 0; u < XU; ++u) v[u] = i0 + u * 64 + lane < n ? lb[i0 + u * 64 + lane] : NO_SLOT;
+      uint32_t v[XU], k[XU], hs[XU];
+      keys(blk, i0, n, v, k, hs);
 #pragma unroll
       for (uint32_t u = 0; u < XU; ++u) {
-        d[u] = v[u] != NO_SLOT ? g.psh[v[u]] : 0u;
-        hs[u] = v[u] != NO_SLOT && x.use_slots ? g.phs[v[u]] : PHS_NONE;
+        for (uint64_t pend = __ballot(k[u] != ~0u); pend;) {
+          const uint32_t kk = __shfl(k[u], __ffsll((unsigned long long)pend) - 1);
+          const uint64_t m = __ballot(k[u] == kk);
+          if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1))
+            atomicAdd(&hist[(kk >> 6) * MAX_SHARDS + (kk & 63)], (uint32_t)__popcll(m));
+          pend &= ~m;
+        }
       }
-#pragma unroll
-      for (uint32_t u = 0; u < XU; ++u)
-        if (v[u] != NO_SLOT) atomicAdd(&hist[hs[u] < PHS_ABSENT ? 1 : 0][d[u]], 1u);
     }
   }
   __syncthreads();
   if (!SCATTER) {
     for (uint32_t dd = threadIdx.x; dd < g.n_shards; dd += 256) {
-      if (hist[0][dd]) atomicAdd(&g.ctr->xcnt[dd], (unsigned long long)hist[0][dd]);
-      if (hist[1][dd]) atomicAdd(&g.ctr->xcnt2[dd], (unsigned long long)hist[1][dd]);
+      if (hist[dd]) atomicAdd(&g.ctr->xcnt[dd], (unsigned long long)hist[dd]);
+      if (hist[MAX_SHARDS + dd]) atomicAdd(&g.ctr->xcnt2[dd], (unsigned long long)hist[MAX_SHARDS + dd]);
     }
     return;
   }
   if (threadIdx.x < g.n_shards) {
     const uint32_t dd = threadIdx.x;
-    base[0][dd] = hist[0][dd] ? atomicAdd(&g.ctr->xpos[dd], (unsigned long long)hist[0][dd]) : 0ull;
-    base[1][dd] = hist[1][dd] && !x.bitmap[dd] ? atomicAdd(&g.ctr->xpos2[dd], (unsigned long long)hist[1][dd]) : 0ull;
-    hist[0][dd] = hist[1][dd] = 0;
+    base[dd] = hist[dd] ? atomicAdd(&g.ctr->xpos[dd], (unsigned long long)hist[dd]) : 0ull;
+    base[MAX_SHARDS + dd] = hist[MAX_SHARDS + dd] && !x.bitmap[dd]
+                                ? atomicAdd(&g.ctr->xpos2[dd], (unsigned long long)hist[MAX_SHARDS + dd]) : 0ull;
+    hist[dd] = hist[MAX_SHARDS + dd] = 0;
   }
   __syncthreads();
   for (uint64_t blk = p0 + gw; blk < nblk; blk += nw) {
     const uint32_t n = cnt[blk];
-    const uint32_t *lb = buf + blk * BLK_SLOTS;
     for (uint32_t i0 = 0; i0 < n; i0 += 64 * XU) {
-      uint32_t v[XU], d[XU], hs[XU];
-#pragma unroll
-      for (uint32_t u = 0; u < XU; ++u) v[u] = i0 + u * 64 + lane < n ? lb[i0 + u * 64 + lane] : NO_SLOT;
-#pragma unroll
-      for (uint32_t u = 0; u < XU; ++u) {
-        d[u] = v[u] != NO_SLOT ? g.psh[v[u]] : 0u;
-        hs[u] = v[u] != NO_SLOT && x.use_slots ? g.phs[v[u]] : PHS_NONE;
-      }
+      uint32_t v[XU], k[XU], hs[XU];
+      keys(blk, i0, n, v, k, hs);
 #pragma unroll
       for (uint32_t u = 0; u < XU; ++u) {
-        if (v[u] == NO_SLOT) continue;
-        if (hs[u] >= PHS_ABSENT) {  // (the id only for the unresolved)
-          const uint64_t at = base[0][d[u]] + atomicAdd(&hist[0][d[u]], 1u);
-          ((uint64_t *)(send + x.id_off[d[u]]))[at] = g.vid[v[u]];
-        } else if (x.bitmap[d[u]]) {
-          atomicOr((uint32_t *)(send + x.sl_off[d[u]]) + (hs[u] >> 5), 1u << (hs[u] & 31));
+        // this lane's position: its wave's run of the key, at the key's next
+        // position in this workgroup's range (consecutive lanes, consecutive
+        // addresses: one store per run)
+        uint64_t at = 0;
+        for (uint64_t pend = __ballot(k[u] != ~0u); pend;) {
+          const uint32_t kk = __shfl(k[u], __ffsll((unsigned long long)pend) - 1);
+          const uint64_t m = __ballot(k[u] == kk);
+          const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)m) - 1);
+          const bool bm = (kk >> 6) && x.bitmap[kk & 63];
+          uint32_t r0 = 0;
+          if (lane == leader && !bm) r0 = atomicAdd(&hist[(kk >> 6) * MAX_SHARDS + (kk & 63)], (uint32_t)__popcll(m));
+          r0 = __shfl(r0, leader);
+          if (k[u] == kk) at = base[(kk >> 6) * MAX_SHARDS + (kk & 63)] + r0 + __popcll(m & lanemask_lt());
+          pend &= ~m;
+        }
+        if (k[u] == ~0u) continue;
+        const uint32_t d = k[u] & 63;
+        if (!(k[u] >> 6)) {  // (the id only for the unresolved)
+          ((uint64_t *)(send + x.id_off[d]))[at] = g.vid[v[u]];
+        } else if (x.bitmap[d]) {
+          atomicOr((uint32_t *)(send + x.sl_off[d]) + (hs[u] >> 5), 1u << (hs[u] & 31));
         } else {
-          const uint64_t at = base[1][d[u]] + atomicAdd(&hist[1][d[u]], 1u);
-          ((uint32_t *)(send + x.sl_off[d[u]]))[at] = hs[u];
+          ((uint32_t *)(send + x.sl_off[d]))[at] = hs[u];
         }
       }
     }
