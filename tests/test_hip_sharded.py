@@ -313,8 +313,10 @@ def test_c4_shape_eight_shards(sharded, oracle_mod, xbits, xlevels, ratio, monke
         assert rh.rounds >= 2 and rh.ids_sent > 0  # marks crossed shards
         if xbits == "0":
             assert rh.exchange_bytes == 8 * rh.ids_sent  # ids only
-        else:  # proxies resolved by the first trace: marks go as slots / bitmaps
+        elif xlevels == "0":  # proxies resolved by the first trace: marks go as slots / bitmaps
             assert rh.exchange_bytes < 8 * rh.ids_sent
+        # (capped rounds reach the replicated closure, whose all-gathers of the
+        # graph's structure count in exchange_bytes too)
     assert h.export() == o.export()
     assert h.total_actors_seen() == o.total_actors_seen()
 
