@@ -284,18 +284,22 @@ def test_rccl_transport_single_rank(hip_mod, oracle_mod):
         t.close()
 
 
-@pytest.mark.parametrize("xbits,xlevels,ratio", [("0", "0", "32"), ("1", "0", "32"), ("1", "0", "1"), ("2", "0", "32"),
-                                                 ("1", "1", "32"), ("1", "3", "32")])
-def test_c4_shape_eight_shards(sharded, oracle_mod, xbits, xlevels, ratio, monkeypatch):
+@pytest.mark.parametrize("xbits,xlevels,ratio,xfilter", [("0", "0", "32", "1"), ("1", "0", "32", "1"),
+                                                         ("1", "0", "32", "0"), ("1", "0", "1", "1"),
+                                                         ("2", "0", "32", "1"), ("1", "1", "32", "1"),
+                                                         ("1", "3", "32", "1")])
+def test_c4_shape_eight_shards(sharded, oracle_mod, xbits, xlevels, ratio, xfilter, monkeypatch):
     """G = 8 logical shards (the 8-GPU layout of C4) on a scaled C2/C4-shaped
     power-law graph with §8d wakeups (9 % busy, 1 % in flight), split batches:
     bit-exact against the unsharded oracle at every wakeup, with marks sent as
     ids only (0), as home-slot lists (1; with CRGC_XBITMAP_RATIO=1 as a bitmap
     wherever that is smaller), or as bitmaps (2), and rounds run to each shard's
-    local fixpoint (XLEVELS 0) or capped at 1 / 3 levels."""
+    local fixpoint (XLEVELS 0) or capped at 1 / 3 levels; CRGC_XFILTER=0 sends
+    marks whose homes are already marked too (no replicated home bitmaps)."""
     monkeypatch.setenv("CRGC_XBITS", xbits)
     monkeypatch.setenv("CRGC_XLEVELS", xlevels)
     monkeypatch.setenv("CRGC_XBITMAP_RATIO", ratio)
+    monkeypatch.setenv("CRGC_XFILTER", xfilter)
     V = 200_000
     w = world.World(seed=0x5EED + 4)
     w.bulk_graph(V, 10 * V, alpha=2.1, n_roots=V // 1000, cap=100000)
@@ -313,7 +317,7 @@ def test_c4_shape_eight_shards(sharded, oracle_mod, xbits, xlevels, ratio, monke
         assert rh.rounds >= 2 and rh.ids_sent > 0  # marks crossed shards
         if xbits == "0":
             assert rh.exchange_bytes == 8 * rh.ids_sent  # ids only
-        elif xlevels == "0":  # proxies resolved by the first trace: marks go as slots / bitmaps
+        elif xlevels == "0" and xfilter == "0":  # resolved by the first trace: marks go as slots / bitmaps
             assert rh.exchange_bytes < 8 * rh.ids_sent
         # (capped rounds reach the replicated closure, whose all-gathers of the
         # graph's structure count in exchange_bytes too)

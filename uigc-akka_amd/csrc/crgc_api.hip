@@ -270,6 +270,7 @@ struct Knobs {
   // over into the next round.
   uint32_t xlevels = 0;          // CRGC_XLEVELS
   uint32_t idtab_x2 = 3;         // CRGC_IDTAB_X2: id-table buckets per slot x 2 (caps_regions)
+  bool xfilter = true;           // CRGC_XFILTER=0: send every newly marked proxy (mark_all)
   uint64_t xbitmap_ratio = 32;   // CRGC_XBITMAP_RATIO: a mark round's home slots as a bitmap above
                                  // this many list bytes per bitmap byte (mark_all; 32: never)
   bool bin = true;               // CRGC_BIN=0: the pseudo-root level pushes candidate bytes directly
@@ -315,6 +316,7 @@ struct Knobs {
     if (const char *m = env("CRGC_BIN")) bin = atoi(m) != 0;
     if (const char *m = env("CRGC_BIN_MIN_SLOTS")) bin_min = strtoull(m, nullptr, 10);
     if (const char *m = env("CRGC_XLEVELS")) xlevels = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_XFILTER")) xfilter = atoi(m) != 0;
     if (const char *m = env("CRGC_XBITMAP_RATIO")) xbitmap_ratio = std::max<uint64_t>(1, strtoull(m, nullptr, 10));
     if (const char *m = env("CRGC_IDTAB_X2")) idtab_x2 = std::max<uint32_t>(1, (uint32_t)strtoul(m, nullptr, 10));
     if (const char *m = env("CRGC_XSLICES")) {
@@ -390,6 +392,7 @@ struct crgc_graph {
   Scratch x_chunk;           // rebased offsets of a large device batch's sub-merges
   Scratch x_bin;             // the pseudo-root level's binned push: counters, then bin regions
   Scratch x_gc, x_gc_list;   // replicated chain closure of sharded marks (crgc_xchain.hip)
+  Scratch x_gvis;            // every shard's marked bitmap of its shadows (mark_all's send filter)
   uint64_t *h_small = nullptr;       // pinned host staging for small all-gathers
   uint64_t *h_bounce = nullptr;      // pinned bounce for id lists into partly pinned caller buffers
   uint64_t h_bounce_bytes = 0;
@@ -909,7 +912,8 @@ void crgc_destroy(crgc_graph *h) {
   h->work.release();
   for (Scratch *x : {&h->x_send, &h->x_slot, &h->x_recv, &h->x_ans, &h->x_ans_back, &h->x_small,
                      &h->x_pack, &h->x_pack_recv, &h->x_route, &h->x_route_send, &h->x_cat,
-                     &h->x_dg, &h->x_dg_out, &h->x_chain, &h->x_gc, &h->x_gc_list, &h->x_bin, &h->x_chunk})
+                     &h->x_dg, &h->x_dg_out, &h->x_chain, &h->x_gc, &h->x_gc_list, &h->x_bin, &h->x_chunk,
+                     &h->x_gvis})
     x->release();
   if (h->ctr) hipFree(h->ctr);
   if (h->hctr) hipHostFree(h->hctr);
@@ -2531,11 +2535,40 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
     const uint64_t b = 8 * n_id(r, d) + 4 * (bitmap(r, d) ? words(d) : n_sl(r, d));
     return (b + 7) & ~7ull;
   };
+  // Most marks a round would send find their home already marked (C4 over 8
+  // shards: ~29 M sent per shard and wakeup, ~3.5 M of them new at home), so
+  // while rounds are wide every shard first all-gathers the homes' marked
+  // bitmaps (4 B per 32 shadows of the graph) and sends only the marks whose
+  // homes lack them.  On when the previous round sent at least as many marks
+  // as the bitmaps have words (the first round always), the same decision on
+  // every shard (all-gathered counts).
+  uint64_t gwords = 0, prev_total = ~0ull;
+  for (uint32_t d = 0; d < G; ++d) gwords += words(d);
   for (;;) {
     const auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(xcnt), 0, 4 * MAX_SHARDS * 8, h->stream));
     XSend xs{};
     xs.use_slots = xmode != 0;
+    if (xmode != 0 && h->knobs.xfilter && prev_total >= gwords && gwords) {
+      if (h->x_gvis.ensure(gwords * 4 + 8) != hipSuccess) return CRGC_E_NOMEM;
+      size_t soff[MAX_SHARDS], sb[MAX_SHARDS], roff[MAX_SHARDS], rb[MAX_SHARDS];
+      uint64_t o = 0;
+      for (uint32_t d = 0; d < G; ++d) {
+        xs.gvis_off[d] = o;
+        soff[d] = 0;
+        sb[d] = words(me) * 4;
+        roff[d] = o * 4;
+        rb[d] = words(d) * 4;
+        o += words(d);
+      }
+      xs.gvis_off[G] = o;
+      if (int rc = h->tp->alltoallv(me, h->g.d.vis, soff, sb, h->x_gvis.ptr, roff, rb, h->stream)) {
+        h->poisoned = true;
+        return rc;
+      }
+      *x_bytes += words(me) * 4 * (G - 1);
+      xs.gvis = (const uint32_t *)h->x_gvis.ptr;
+    }
     HIP_TRY(launch_xlist(h->g.d, false, npb, nullptr, xs, h->stream));
     // (with the counts, whether each shard's round was capped with work pending)
     h->h_small[SMALL_PEND_OFF / 8] = capped ? 1 : 0;
@@ -2547,6 +2580,7 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
       for (uint32_t k = 0; k < 2 * G; ++k) total += M[(size_t)r * (2 * G + 1) + k];
       pending += M[(size_t)r * (2 * G + 1) + 2 * G];
     }
+    prev_total = total;
     if (total == 0 && pending == 0) {
       *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       return CRGC_OK;

@@ -257,6 +257,11 @@ struct XSend {
   uint64_t id_off[MAX_SHARDS], sl_off[MAX_SHARDS];
   uint8_t bitmap[MAX_SHARDS];
   int use_slots;
+  // every shard's marked bitmap of its own shadows, as of this round's
+  // exchange (word offsets per shard, G + 1 of them; null: none): a proxy
+  // whose home slot is marked there is not sent
+  const uint32_t *gvis;
+  uint64_t gvis_off[MAX_SHARDS + 1];
 };
 struct XRecv {
   uint32_t G;

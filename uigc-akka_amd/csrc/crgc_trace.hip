@@ -1939,6 +1939,15 @@ __global__ __launch_bounds__(256) void k_xlist(DevGraph g, const uint32_t *buf, 
       hs[u] = v[u] != NO_SLOT && x.use_slots ? g.phs[v[u]] : PHS_NONE;
       k[u] = v[u] == NO_SLOT ? ~0u : ((hs[u] < PHS_ABSENT ? 64u : 0u) | d);
     }
+    if (x.gvis) {  // marks their homes already have stay here
+#pragma unroll
+      for (uint32_t u = 0; u < XU; ++u)
+        if (k[u] != ~0u && (k[u] >> 6)) {
+          const uint32_t d = k[u] & 63;
+          const uint64_t w = x.gvis_off[d] + (hs[u] >> 5);
+          if (w < x.gvis_off[d + 1] && ((x.gvis[w] >> (hs[u] & 31)) & 1u)) k[u] = ~0u;
+        }
+    }
   };
   for (uint64_t blk = p0 + gw; blk < nblk; blk += nw) {
     const uint32_t n = cnt[blk];
