@@ -49,7 +49,7 @@ void free_arrays(Arrays &a) {
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat, d.xbytes,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill,
                 d.nzdeg, d.radj, d.rnew, d.rpool, d.par, d.fx, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
-                d.xp_buf, d.xp_cnt, d.rq_buf, d.rq_cnt, d.phs, d.psh};
+                d.xsent, d.rq_buf, d.rq_cnt, d.phs, d.psh};
   for (void *p : ps)
     if (p) hipFree(p);
   a.allocated = false;
@@ -124,8 +124,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   A(dmalloc(&d.pb[0], c.scap / 32));
   A(dmalloc(&d.pb[1], c.scap / 32));
   if (sharded) {
-    A(dmalloc(&d.xp_buf, c.scap));
-    A(dmalloc(&d.xp_cnt, c.scap / BLK_SLOTS));
+    A(dmalloc(&d.xsent, c.scap / 32));
     A(dmalloc(&d.rq_buf, c.scap));
     A(dmalloc(&d.rq_cnt, c.scap / BLK_SLOTS));
     A(dmalloc(&d.phs, c.scap));
@@ -164,7 +163,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   M(d.pb[1], 0, c.scap / 8);
   if (sharded) {
     M(d.phs, 0xFF, c.scap * 4);  // PHS_NONE: a new generation resolves again
-    M(d.xp_cnt, 0, c.scap / BLK_SLOTS * 4);
+    M(d.xsent, 0, c.scap / 8);
     M(d.rq_cnt, 0, c.scap / BLK_SLOTS * 4);
   }
 #undef M
@@ -2517,8 +2516,8 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
     if (int rc = resolve_home_slots(h, top, xmode, x_bytes)) return rc;
     *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
-  // marked proxies are listed in the proxy region's blocks
-  const uint64_t npb = blocks_of(proxy_top_ub(h)), p0 = h->g.caps.pbase / BLK_SLOTS;
+  // (the export scans the proxy region's blocks: k_xscan)
+  const uint64_t npb = blocks_of(proxy_top_ub(h));
   std::vector<uint64_t> M((size_t)G * (2 * G + 1));  // per shard: ids, slots per destination; pending
   auto n_id = [&](uint32_t r, uint32_t d) { return M[(size_t)r * (2 * G + 1) + d]; };
   auto n_sl = [&](uint32_t r, uint32_t d) { return M[(size_t)r * (2 * G + 1) + G + d]; };
@@ -2602,7 +2601,6 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
     for (uint32_t d = 0; d < G; ++d) any_bitmap |= xs.bitmap[d] != 0;
     if (any_bitmap) HIP_TRY(hipMemsetAsync(h->x_send.ptr, 0, so, h->stream));
     HIP_TRY(launch_xlist(h->g.d, true, npb, (char *)h->x_send.ptr, xs, h->stream));
-    if (npb) HIP_TRY(hipMemsetAsync(h->g.d.xp_cnt + p0, 0, npb * 4, h->stream));
     uint64_t nrecv = 0;
     if (int rc = a2a(h, h->x_send.ptr, B.data(), 1, h->x_recv, false, &nrecv)) return rc;
     *ids_sent += nsend;

@@ -234,8 +234,7 @@ struct DevGraph {
   uint64_t *out_kill; // dense kill ids
   // sharded graphs (n_shards > 1)
   uint32_t n_shards, shard;
-  uint32_t *xp_buf;   // per-block regions: proxy slots marked since the last export
-  uint32_t *xp_cnt;   // per block: listed proxies
+  uint32_t *xsent;    // 1 bit / slot (the proxy region's words): a marked proxy already exported
   uint32_t *rq_buf;   // per-block regions: garbage slots whose kill waits on a remote mark
   uint32_t *rq_cnt;   // per block: listed requests
   uint32_t *phs;      // per proxy slot: its slot at the home shard (PHS_NONE / PHS_ABSENT)

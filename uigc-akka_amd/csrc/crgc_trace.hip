@@ -214,18 +214,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     if (m) g.vis[(uint64_t)blk * 64 + lane] = word | m;
     if (sp_cur && lane == 0) Dc[blk] = 0;
     if (!ROOTS && vbs.proxy(vb)) {
-      // A proxy block: its newly marked proxies join the block's export list
-      // (sent home after the round); proxies have no edges, so nothing else —
+      // A proxy block: its proxies are marked (k_xscan exports the newly
+      // marked ones after the round); proxies have no edges, so nothing else —
       // and they do not count in the level's frontier (a level that only
       // reaches proxies ends the round).
-      const uint32_t cnt = __popc(m);
-      if (__ballot(cnt != 0)) {
-        const uint32_t incl = wave_incl_scan(cnt);
-        const uint32_t n0 = g.xp_cnt[blk];
-        uint32_t pos = n0 + incl - cnt;
-        for (uint32_t mm = m; mm; mm &= mm - 1) g.xp_buf[(uint64_t)blk * BLK_SLOTS + pos++] = (uint32_t)(base + __ffs(mm) - 1);
-        if (lane == 63) g.xp_cnt[blk] = n0 + incl;
-      }
       continue;
     }
 
@@ -307,7 +299,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     // Frontier shadows -> supervisor marks + edge ranges (push levels).
     uint32_t nlight = 0;
     uint2 *region = g.qn_buf + (uint64_t)blk * BLK_SLOTS;
-    uint32_t nprox = sharded ? g.xp_cnt[blk] : 0;
     // FB chunks of 64 frontier shadows at a time: every per-shadow load of the
     // group (flags, degree, segment, supervisor) is issued before any store,
     // then the supervisors' marked words, so a dense block costs two memory
@@ -344,12 +335,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
       }
 #pragma unroll
       for (int b = 0; b < FB; ++b) {
-        if (sharded) {  // newly marked proxies: exported to their home shard after the round
-          const uint64_t pb = __ballot(f[b] & FL_PROXY);
-          if (f[b] & FL_PROXY)
-            g.xp_buf[(uint64_t)blk * BLK_SLOTS + nprox + __popcll(pb & lanemask_lt())] = v[b];
-          nprox += __popcll(pb);
-        }
         n_edges += nz[b];  // this level's frontier out-edges (Beamer's m_f)
         if (sp[b] != NO_SLOT) {
           n_sup++;
@@ -376,7 +361,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
       }
     }
     if (lane == 0 && nlight) g.qn_tag[blk] = tag | nlight;
-    if (sharded && lane == 0) g.xp_cnt[blk] = nprox;
     wave_lds_fence();
   }
   const uint64_t tf = block_sum4(n_front);
@@ -1059,11 +1043,7 @@ __device__ inline void tail_claim_batch(const DevGraph &g, const TailLds &sh, co
 #pragma unroll
   for (int k = 0; k < N; ++k) {
     if ((w[k] >> (t[k] & 31)) & 1u) continue;  // marked already, or not a target
-    if (t[k] >= g.pbase) {  // a proxy (sharded graphs): nothing to walk, listed for the exchange at once
-      const uint32_t pos = atomicAdd(&g.xp_cnt[t[k] >> 11], 1u);
-      g.xp_buf[(uint64_t)(t[k] >> 11) * BLK_SLOTS + pos] = t[k];
-      continue;
-    }
+    if (t[k] >= g.pbase) continue;  // a proxy (sharded graphs): marked, nothing to walk (k_xscan exports it)
     if (keep && *keep == NO_SLOT) {
       *keep = t[k];
       ++claims;
@@ -1128,10 +1108,6 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
         const uint2 adv = g.adj[v];
         const uint32_t supv = investigate ? NO_SLOT : g.sup[v];
         const bool expand = !(f & FL_HALTED);  // (:226-229)
-        if (!vfirst && (f & FL_PROXY)) {  // level L's were listed by k_frontier
-          const uint32_t pos = atomicAdd(&g.xp_cnt[v >> 11], 1u);
-          g.xp_buf[(uint64_t)(v >> 11) * BLK_SLOTS + pos] = v;
-        }
         ad = make_uint2(0, 0);
         uint32_t keep = NO_SLOT;
         // targets: [0] the supervisor (:258-267), [1 ..] the out-edges of a
@@ -1423,12 +1399,15 @@ __global__ __launch_bounds__(256) void k_trace_reset(DevGraph g, uint64_t nh, ui
   const uint64_t nblk = nh + np, p0 = g.pbase / BLK_SLOTS;
   auto at = [&](uint64_t vb) { return vb < nh ? vb : p0 + (vb - nh); };
   uint4 *vis4 = reinterpret_cast<uint4 *>(g.vis);  // 2048 slots = 64 words = 16 uint4 per block
-  for (uint64_t i = t0; i < nblk * 16; i += stride) vis4[at(i / 16) * 16 + i % 16] = make_uint4(0, 0, 0, 0);
+  uint4 *sent4 = reinterpret_cast<uint4 *>(g.xsent);
+  for (uint64_t i = t0; i < nblk * 16; i += stride) {
+    vis4[at(i / 16) * 16 + i % 16] = make_uint4(0, 0, 0, 0);
+    if (sent4 && i >= nh * 16) sent4[at(i / 16) * 16 + i % 16] = make_uint4(0, 0, 0, 0);
+  }
   for (uint64_t vb = t0; vb < nblk; vb += stride) {
     const uint64_t i = at(vb);
     g.qn_tag[i] = 0;
     g.tl_tag[i] = 0;
-    if (g.xp_cnt) g.xp_cnt[i] = 0;
   }
   for (uint64_t i = t0; i < (uint64_t)STAT_WG * 4; i += stride) g.blkstat[i] = 0;
   for (uint64_t i = t0; i < (uint64_t)STAT_WG; i += stride) g.xbytes[i] = 0;
@@ -1905,75 +1884,102 @@ hipError_t launch_resolve(const DevGraph &g, int step, uint64_t mask, uint64_t *
   return hipGetLastError();
 }
 
-// Marked proxies listed by k_frontier / k_tail, by destination: ids of the
-// unresolved (xcnt), home slots of the resolved (xcnt2); then the scatter
-// into the byte layout the host derived from the all-gathered counts.
-// Marked proxies are listed in the proxy region's blocks (k_frontier, k_tail).
+// The proxies marked since the last export (marked, not yet sent: vis &
+// ~xsent over the proxy region), by destination: ids of the unresolved (xcnt),
+// home slots of the resolved (xcnt2); then the scatter into the byte layout the
+// host derived from the all-gathered counts, which records them as sent.  A
+// streaming pass over the region's marked / sent words and, for the new marks
+// only, their home shards and home slots (round 4 listed marked proxies into
+// per-block regions as the level kernels found them and packed the lists: a
+// chain of dependent loads per entry, ~0.8 ms per shard for C4's first round
+// over 8 logical shards against ~0.1 ms for this scan, profiles/r5m).
+// One wave per 2048-proxy block: lane l holds the block's words l (marked and
+// sent); step k covers slots 64k .. 64k+63 (slot 64k + l: word 2k + l / 32,
+// bit l % 32, by one shuffle), so the home-shard and home-slot loads of a step
+// are coalesced; XU steps per load group.
 template <bool SCATTER>
-__global__ __launch_bounds__(256) void k_xlist(DevGraph g, const uint32_t *buf, const uint32_t *cnt, char *send,
-                                               XSend x) {
+__global__ __launch_bounds__(256) void k_xscan(DevGraph g, char *send, XSend x) {
   // per (form, destination): this workgroup's count, then its next position
   __shared__ uint32_t hist[2 * MAX_SHARDS];
   __shared__ unsigned long long base[2 * MAX_SHARDS];
   for (uint32_t d = threadIdx.x; d < 2 * MAX_SHARDS; d += 256) hist[d] = 0;
   __syncthreads();
   const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
-  const uint64_t p0 = g.pbase / BLK_SLOTS;
-  const uint64_t nblk = p0 + (g.ctr->proxy_top + BLK_SLOTS - 1) / BLK_SLOTS;
-  // XU entries per lane in flight: a wave's entries are a chain of dependent
-  // loads (listing -> home shard / home slot), so one at a time left the kernel
-  // latency-bound (round 4: ~600 us per launch at C4 over 8 logical shards)
-  constexpr uint32_t XU = 4;
+  const uint64_t np = g.ctr->proxy_top;
+  const uint64_t nb = (np + BLK_SLOTS - 1) / BLK_SLOTS;
+  const uint64_t w0 = g.pbase / 32;  // the region's first marked word (pbase is block-aligned)
   const uint32_t lane = lane_id();
-  // Entry -> key (form << 6 | destination; form 1: a resolved home slot).
-  // Keys are aggregated per wave (one ballot per distinct key, one LDS atomic
-  // per key and wave): 64 lanes' LDS atomics on G counters serialised, and
-  // ranks from them scattered each destination's run over the segment.
-  auto keys = [&](uint64_t blk, uint32_t i0, uint32_t n, uint32_t (&v)[XU], uint32_t (&k)[XU], uint32_t (&hs)[XU]) {
-    const uint32_t *lb = buf + blk * BLK_SLOTS;
+  constexpr uint32_t XU = 4;
+  // Entry -> key (form << 6 | destination; form 1: a resolved home slot; ~0:
+  // none).  Keys are aggregated per wave (one ballot per distinct key, one LDS
+  // atomic per key and wave).
+  auto pass = [&](bool record, auto &&emit) {
+    for (uint64_t blk = gw; blk < nb; blk += nw) {
+      const uint64_t w = w0 + blk * 64 + lane;
+      const uint32_t mw = g.vis[w], sw = g.xsent[w];
+      const uint32_t nm = mw & ~sw;
+      if (!__ballot(nm != 0)) continue;
+      for (uint32_t k0 = 0; k0 < 32; k0 += XU) {
+        uint32_t v[XU], k[XU], hs[XU];
+        bool any = false;
 #pragma unroll
-    for (uint32_t u = 0; u < XU; ++u) v[u] = i0 + u * 64 + lane < n ? lb[i0 + u * 64 + lane] : NO_SLOT;
-#pragma unroll
-    for (uint32_t u = 0; u < XU; ++u) {
-      const uint32_t d = v[u] != NO_SLOT ? g.psh[v[u]] : 0u;
-      hs[u] = v[u] != NO_SLOT && x.use_slots ? g.phs[v[u]] : PHS_NONE;
-      k[u] = v[u] == NO_SLOT ? ~0u : ((hs[u] < PHS_ABSENT ? 64u : 0u) | d);
-    }
-    if (x.gvis) {  // marks their homes already have stay here
-#pragma unroll
-      for (uint32_t u = 0; u < XU; ++u)
-        if (k[u] != ~0u && (k[u] >> 6)) {
-          const uint32_t d = k[u] & 63;
-          const uint64_t w = x.gvis_off[d] + (hs[u] >> 5);
-          if (w < x.gvis_off[d + 1] && ((x.gvis[w] >> (hs[u] & 31)) & 1u)) k[u] = ~0u;
+        for (uint32_t u = 0; u < XU; ++u) {
+          const uint32_t word = __shfl(nm, 2 * (k0 + u) + (lane >> 5));
+          const uint64_t sl = g.pbase + blk * BLK_SLOTS + (k0 + u) * 64 + lane;
+          v[u] = ((word >> (lane & 31)) & 1u) && sl - g.pbase < np ? (uint32_t)sl : NO_SLOT;
+          any |= __ballot(v[u] != NO_SLOT) != 0;
         }
+        if (!any) continue;
+#pragma unroll
+        for (uint32_t u = 0; u < XU; ++u) {
+          const uint32_t d = v[u] != NO_SLOT ? g.psh[v[u]] : 0u;
+          hs[u] = v[u] != NO_SLOT && x.use_slots ? g.phs[v[u]] : PHS_NONE;
+          k[u] = v[u] == NO_SLOT ? ~0u : ((hs[u] < PHS_ABSENT ? 64u : 0u) | d);
+        }
+        if (x.gvis) {  // marks their homes already have stay here
+#pragma unroll
+          for (uint32_t u = 0; u < XU; ++u)
+            if (k[u] != ~0u && (k[u] >> 6)) {
+              const uint32_t d = k[u] & 63;
+              const uint64_t gwd = x.gvis_off[d] + (hs[u] >> 5);
+              if (gwd < x.gvis_off[d + 1] && ((x.gvis[gwd] >> (hs[u] & 31)) & 1u)) k[u] = ~0u;
+            }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < XU; ++u) emit(v[u], k[u], hs[u]);
+      }
+      if (record && nm) g.xsent[w] = sw | nm;  // (the scatter's last pass only)
     }
   };
-  for (uint64_t blk = p0 + gw; blk < nblk; blk += nw) {
-    const uint32_t n = cnt[blk];
-    for (uint32_t i0 = 0; i0 < n; i0 += 64 * XU) {
-      uint32_t v[XU], k[XU], hs[XU];
-      keys(blk, i0, n, v, k, hs);
-#pragma unroll
-      for (uint32_t u = 0; u < XU; ++u) {
-        for (uint64_t pend = __ballot(k[u] != ~0u); pend;) {
-          const uint32_t kk = __shfl(k[u], __ffsll((unsigned long long)pend) - 1);
-          const uint64_t m = __ballot(k[u] == kk);
-          if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1))
-            atomicAdd(&hist[(kk >> 6) * MAX_SHARDS + (kk & 63)], (uint32_t)__popcll(m));
-          pend &= ~m;
-        }
-      }
-    }
-  }
-  __syncthreads();
   if (!SCATTER) {
+    pass(false, [&](uint32_t, uint32_t key, uint32_t) {
+      for (uint64_t pend = __ballot(key != ~0u); pend;) {
+        const uint32_t kk = __shfl(key, __ffsll((unsigned long long)pend) - 1);
+        const uint64_t m = __ballot(key == kk);
+        if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1))
+          atomicAdd(&hist[(kk >> 6) * MAX_SHARDS + (kk & 63)], (uint32_t)__popcll(m));
+        pend &= ~m;
+      }
+    });
+    __syncthreads();
     for (uint32_t dd = threadIdx.x; dd < g.n_shards; dd += 256) {
       if (hist[dd]) atomicAdd(&g.ctr->xcnt[dd], (unsigned long long)hist[dd]);
       if (hist[MAX_SHARDS + dd]) atomicAdd(&g.ctr->xcnt2[dd], (unsigned long long)hist[MAX_SHARDS + dd]);
     }
     return;
   }
+  // scatter: this workgroup's range of every segment from its counts (a
+  // counting pre-pass over its own blocks, then one global atomic per key)
+  pass(false, [&](uint32_t, uint32_t key, uint32_t) {
+    for (uint64_t pend = __ballot(key != ~0u); pend;) {
+      const uint32_t kk = __shfl(key, __ffsll((unsigned long long)pend) - 1);
+      const uint64_t m = __ballot(key == kk);
+      if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1))
+        atomicAdd(&hist[(kk >> 6) * MAX_SHARDS + (kk & 63)], (uint32_t)__popcll(m));
+      pend &= ~m;
+    }
+  });
+  __syncthreads();
   if (threadIdx.x < g.n_shards) {
     const uint32_t dd = threadIdx.x;
     base[dd] = hist[dd] ? atomicAdd(&g.ctr->xpos[dd], (unsigned long long)hist[dd]) : 0ull;
@@ -1982,40 +1988,32 @@ __global__ __launch_bounds__(256) void k_xlist(DevGraph g, const uint32_t *buf, 
     hist[dd] = hist[MAX_SHARDS + dd] = 0;
   }
   __syncthreads();
-  for (uint64_t blk = p0 + gw; blk < nblk; blk += nw) {
-    const uint32_t n = cnt[blk];
-    for (uint32_t i0 = 0; i0 < n; i0 += 64 * XU) {
-      uint32_t v[XU], k[XU], hs[XU];
-      keys(blk, i0, n, v, k, hs);
-#pragma unroll
-      for (uint32_t u = 0; u < XU; ++u) {
-        // this lane's position: its wave's run of the key, at the key's next
-        // position in this workgroup's range (consecutive lanes, consecutive
-        // addresses: one store per run)
-        uint64_t at = 0;
-        for (uint64_t pend = __ballot(k[u] != ~0u); pend;) {
-          const uint32_t kk = __shfl(k[u], __ffsll((unsigned long long)pend) - 1);
-          const uint64_t m = __ballot(k[u] == kk);
-          const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)m) - 1);
-          const bool bm = (kk >> 6) && x.bitmap[kk & 63];
-          uint32_t r0 = 0;
-          if (lane == leader && !bm) r0 = atomicAdd(&hist[(kk >> 6) * MAX_SHARDS + (kk & 63)], (uint32_t)__popcll(m));
-          r0 = __shfl(r0, leader);
-          if (k[u] == kk) at = base[(kk >> 6) * MAX_SHARDS + (kk & 63)] + r0 + __popcll(m & lanemask_lt());
-          pend &= ~m;
-        }
-        if (k[u] == ~0u) continue;
-        const uint32_t d = k[u] & 63;
-        if (!(k[u] >> 6)) {  // (the id only for the unresolved)
-          ((uint64_t *)(send + x.id_off[d]))[at] = g.vid[v[u]];
-        } else if (x.bitmap[d]) {
-          atomicOr((uint32_t *)(send + x.sl_off[d]) + (hs[u] >> 5), 1u << (hs[u] & 31));
-        } else {
-          ((uint32_t *)(send + x.sl_off[d]))[at] = hs[u];
-        }
-      }
+  pass(true, [&](uint32_t v, uint32_t key, uint32_t hs) {
+    // this lane's position: its wave's run of the key, at the key's next
+    // position in this workgroup's range (consecutive lanes, consecutive
+    // addresses: one store per run)
+    uint64_t at = 0;
+    for (uint64_t pend = __ballot(key != ~0u); pend;) {
+      const uint32_t kk = __shfl(key, __ffsll((unsigned long long)pend) - 1);
+      const uint64_t m = __ballot(key == kk);
+      const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)m) - 1);
+      const bool bm = (kk >> 6) && x.bitmap[kk & 63];
+      uint32_t r0 = 0;
+      if (lane == leader && !bm) r0 = atomicAdd(&hist[(kk >> 6) * MAX_SHARDS + (kk & 63)], (uint32_t)__popcll(m));
+      r0 = __shfl(r0, leader);
+      if (key == kk) at = base[(kk >> 6) * MAX_SHARDS + (kk & 63)] + r0 + __popcll(m & lanemask_lt());
+      pend &= ~m;
     }
-  }
+    if (key == ~0u) return;
+    const uint32_t d = key & 63;
+    if (!(key >> 6)) {  // (the id only for the unresolved)
+      ((uint64_t *)(send + x.id_off[d]))[at] = g.vid[v];
+    } else if (x.bitmap[d]) {
+      atomicOr((uint32_t *)(send + x.sl_off[d]) + (hs >> 5), 1u << (hs & 31));
+    } else {
+      ((uint32_t *)(send + x.sl_off[d]))[at] = hs;
+    }
+  });
 }
 
 hipError_t launch_xlist(const DevGraph &g, bool scatter, uint64_t nblk, char *send, const XSend &x,
@@ -2024,9 +2022,9 @@ hipError_t launch_xlist(const DevGraph &g, bool scatter, uint64_t nblk, char *se
   if (nblk == 0) return hipSuccess;
   const int grid = (int)std::min<uint64_t>((nblk + 3) / 4, 8192);
   if (scatter)
-    hipLaunchKernelGGL(k_xlist<true>, dim3(grid), dim3(256), 0, s, g, g.xp_buf, g.xp_cnt, send, x);
+    hipLaunchKernelGGL(k_xscan<true>, dim3(grid), dim3(256), 0, s, g, send, x);
   else
-    hipLaunchKernelGGL(k_xlist<false>, dim3(grid), dim3(256), 0, s, g, g.xp_buf, g.xp_cnt, send, x);
+    hipLaunchKernelGGL(k_xscan<false>, dim3(grid), dim3(256), 0, s, g, send, x);
   return hipGetLastError();
 }
 
