@@ -49,7 +49,7 @@ void free_arrays(Arrays &a) {
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat, d.xbytes,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill,
                 d.nzdeg, d.radj, d.rnew, d.rpool, d.par, d.fx, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
-                d.xsent, d.rq_buf, d.rq_cnt, d.phs, d.psh};
+                d.xsent, d.xkey, d.rq_buf, d.rq_cnt, d.phs, d.psh};
   for (void *p : ps)
     if (p) hipFree(p);
   a.allocated = false;
@@ -125,6 +125,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   A(dmalloc(&d.pb[1], c.scap / 32));
   if (sharded) {
     A(dmalloc(&d.xsent, c.scap / 32));
+    A(dmalloc(&d.xkey, c.scap));
     A(dmalloc(&d.rq_buf, c.scap));
     A(dmalloc(&d.rq_cnt, c.scap / BLK_SLOTS));
     A(dmalloc(&d.phs, c.scap));
@@ -392,6 +393,7 @@ struct crgc_graph {
   Scratch x_bin;             // the pseudo-root level's binned push: counters, then bin regions
   Scratch x_gc, x_gc_list;   // replicated chain closure of sharded marks (crgc_xchain.hip)
   Scratch x_gvis;            // every shard's marked bitmap of its shadows (mark_all's send filter)
+  Scratch x_wgc;             // k_xscan's per-workgroup counts
   uint64_t *h_small = nullptr;       // pinned host staging for small all-gathers
   uint64_t *h_bounce = nullptr;      // pinned bounce for id lists into partly pinned caller buffers
   uint64_t h_bounce_bytes = 0;
@@ -912,7 +914,7 @@ void crgc_destroy(crgc_graph *h) {
   for (Scratch *x : {&h->x_send, &h->x_slot, &h->x_recv, &h->x_ans, &h->x_ans_back, &h->x_small,
                      &h->x_pack, &h->x_pack_recv, &h->x_route, &h->x_route_send, &h->x_cat,
                      &h->x_dg, &h->x_dg_out, &h->x_chain, &h->x_gc, &h->x_gc_list, &h->x_bin, &h->x_chunk,
-                     &h->x_gvis})
+                     &h->x_gvis, &h->x_wgc})
     x->release();
   if (h->ctr) hipFree(h->ctr);
   if (h->hctr) hipHostFree(h->hctr);
@@ -2568,7 +2570,8 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
       *x_bytes += words(me) * 4 * (G - 1);
       xs.gvis = (const uint32_t *)h->x_gvis.ptr;
     }
-    HIP_TRY(launch_xlist(h->g.d, false, npb, nullptr, xs, h->stream));
+    if (h->x_wgc.ensure((size_t)xscan_grid(npb) * 2 * G * 4 + 8) != hipSuccess) return CRGC_E_NOMEM;
+    HIP_TRY(launch_xlist(h->g.d, false, npb, nullptr, xs, (uint32_t *)h->x_wgc.ptr, h->stream));
     // (with the counts, whether each shard's round was capped with work pending)
     h->h_small[SMALL_PEND_OFF / 8] = capped ? 1 : 0;
     if (int rc = ag_u64(h, {{(char *)h->ctr + CTR_OFF(xcnt), G}, {(char *)h->ctr + CTR_OFF(xcnt2), G},
@@ -2600,7 +2603,7 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
     bool any_bitmap = false;  // (the bitmap segments zeroed by one memset of the send buffer)
     for (uint32_t d = 0; d < G; ++d) any_bitmap |= xs.bitmap[d] != 0;
     if (any_bitmap) HIP_TRY(hipMemsetAsync(h->x_send.ptr, 0, so, h->stream));
-    HIP_TRY(launch_xlist(h->g.d, true, npb, (char *)h->x_send.ptr, xs, h->stream));
+    HIP_TRY(launch_xlist(h->g.d, true, npb, (char *)h->x_send.ptr, xs, (uint32_t *)h->x_wgc.ptr, h->stream));
     uint64_t nrecv = 0;
     if (int rc = a2a(h, h->x_send.ptr, B.data(), 1, h->x_recv, false, &nrecv)) return rc;
     *ids_sent += nsend;

@@ -272,7 +272,8 @@ struct XRecv {
 };
 // (nblk: a bound of the proxy region's blocks, for the grid)
 hipError_t launch_xlist(const DevGraph &g, bool scatter, uint64_t nblk, char *send, const XSend &x,
-                        hipStream_t s);
+                        uint32_t *wgc, hipStream_t s);
+int xscan_grid(uint64_t nblk);  // k_xscan's workgroups (the counts `wgc` holds: 2 G u32 each)
 // The replicated chain closure of deep sharded marks (crgc_xchain.hip).
 struct XcArgs {
   uint32_t G, me;

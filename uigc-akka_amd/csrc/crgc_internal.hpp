@@ -235,6 +235,7 @@ struct DevGraph {
   // sharded graphs (n_shards > 1)
   uint32_t n_shards, shard;
   uint32_t *xsent;    // 1 bit / slot (the proxy region's words): a marked proxy already exported
+  uint8_t *xkey;      // 1 B / slot (proxies): the export key of a new mark (k_xscan)
   uint32_t *rq_buf;   // per-block regions: garbage slots whose kill waits on a remote mark
   uint32_t *rq_cnt;   // per block: listed requests
   uint32_t *phs;      // per proxy slot: its slot at the home shard (PHS_NONE / PHS_ABSENT)

@@ -1892,17 +1892,31 @@ hipError_t launch_resolve(const DevGraph &g, int step, uint64_t mask, uint64_t *
 // only, their home shards and home slots (round 4 listed marked proxies into
 // per-block regions as the level kernels found them and packed the lists: a
 // chain of dependent loads per entry, ~0.8 ms per shard for C4's first round
-// over 8 logical shards against ~0.1 ms for this scan, profiles/r5m).
+// over 8 logical shards).
 // One wave per 2048-proxy block: lane l holds the block's words l (marked and
 // sent); step k covers slots 64k .. 64k+63 (slot 64k + l: word 2k + l / 32,
-// bit l % 32, by one shuffle), so the home-shard and home-slot loads of a step
-// are coalesced; XU steps per load group.
+// bit l % 32, by one shuffle), so the loads of a step are coalesced; XU steps
+// per load group.  The count pass derives each new mark's key (form << 6 |
+// destination; 0xFF: none — its home is marked already) from the home shard,
+// the home slot and the replicated home bitmaps, stores it as a byte and leaves
+// its workgroup's count per key in `wgc`; the scatter pass (same grid, so the
+// same blocks per workgroup) reserves each key's range from those counts and
+// reads the key bytes back, so the random bitmap probes run once.
 template <bool SCATTER>
-__global__ __launch_bounds__(256) void k_xscan(DevGraph g, char *send, XSend x) {
-  // per (form, destination): this workgroup's count, then its next position
+__global__ __launch_bounds__(256) void k_xscan(DevGraph g, char *send, XSend x, uint32_t *wgc) {
   __shared__ uint32_t hist[2 * MAX_SHARDS];
   __shared__ unsigned long long base[2 * MAX_SHARDS];
-  for (uint32_t d = threadIdx.x; d < 2 * MAX_SHARDS; d += 256) hist[d] = 0;
+  const uint32_t G = g.n_shards;
+  uint32_t *mine = wgc + (uint64_t)blockIdx.x * 2 * G;  // this workgroup's counts: [form][destination]
+  for (uint32_t q = threadIdx.x; q < 2 * MAX_SHARDS; q += 256) {
+    hist[q] = 0;
+    if (SCATTER) {
+      const uint32_t f = q / MAX_SHARDS, d = q % MAX_SHARDS;
+      const uint32_t n = d < G ? mine[f * G + d] : 0u;
+      base[q] = n && !(f && x.bitmap[d]) ? atomicAdd(f ? &g.ctr->xpos2[d] : &g.ctr->xpos[d], (unsigned long long)n)
+                                         : 0ull;
+    }
+  }
   __syncthreads();
   const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
   const uint64_t np = g.ctr->proxy_top;
@@ -1910,121 +1924,114 @@ __global__ __launch_bounds__(256) void k_xscan(DevGraph g, char *send, XSend x) 
   const uint64_t w0 = g.pbase / 32;  // the region's first marked word (pbase is block-aligned)
   const uint32_t lane = lane_id();
   constexpr uint32_t XU = 4;
-  // Entry -> key (form << 6 | destination; form 1: a resolved home slot; ~0:
-  // none).  Keys are aggregated per wave (one ballot per distinct key, one LDS
-  // atomic per key and wave).
-  auto pass = [&](bool record, auto &&emit) {
-    for (uint64_t blk = gw; blk < nb; blk += nw) {
-      const uint64_t w = w0 + blk * 64 + lane;
-      const uint32_t mw = g.vis[w], sw = g.xsent[w];
-      const uint32_t nm = mw & ~sw;
-      if (!__ballot(nm != 0)) continue;
-      for (uint32_t k0 = 0; k0 < 32; k0 += XU) {
-        uint32_t v[XU], k[XU], hs[XU];
-        bool any = false;
+  for (uint64_t blk = gw; blk < nb; blk += nw) {
+    const uint64_t w = w0 + blk * 64 + lane;
+    const uint32_t mw = g.vis[w], sw = g.xsent[w];
+    const uint32_t nm = mw & ~sw;
+    if (!__ballot(nm != 0)) continue;
+    for (uint32_t k0 = 0; k0 < 32; k0 += XU) {
+      uint32_t v[XU], key[XU];
+      bool any = false;
 #pragma unroll
-        for (uint32_t u = 0; u < XU; ++u) {
-          const uint32_t word = __shfl(nm, 2 * (k0 + u) + (lane >> 5));
-          const uint64_t sl = g.pbase + blk * BLK_SLOTS + (k0 + u) * 64 + lane;
-          v[u] = ((word >> (lane & 31)) & 1u) && sl - g.pbase < np ? (uint32_t)sl : NO_SLOT;
-          any |= __ballot(v[u] != NO_SLOT) != 0;
-        }
-        if (!any) continue;
+      for (uint32_t u = 0; u < XU; ++u) {
+        const uint32_t word = __shfl(nm, 2 * (k0 + u) + (lane >> 5));
+        const uint64_t sl = g.pbase + blk * BLK_SLOTS + (k0 + u) * 64 + lane;
+        v[u] = ((word >> (lane & 31)) & 1u) && sl - g.pbase < np ? (uint32_t)sl : NO_SLOT;
+        any |= __ballot(v[u] != NO_SLOT) != 0;
+      }
+      if (!any) continue;
+      if (!SCATTER) {
+        uint32_t hs[XU];
 #pragma unroll
         for (uint32_t u = 0; u < XU; ++u) {
           const uint32_t d = v[u] != NO_SLOT ? g.psh[v[u]] : 0u;
           hs[u] = v[u] != NO_SLOT && x.use_slots ? g.phs[v[u]] : PHS_NONE;
-          k[u] = v[u] == NO_SLOT ? ~0u : ((hs[u] < PHS_ABSENT ? 64u : 0u) | d);
+          key[u] = v[u] == NO_SLOT ? ~0u : ((hs[u] < PHS_ABSENT ? 64u : 0u) | d);
         }
         if (x.gvis) {  // marks their homes already have stay here
 #pragma unroll
           for (uint32_t u = 0; u < XU; ++u)
-            if (k[u] != ~0u && (k[u] >> 6)) {
-              const uint32_t d = k[u] & 63;
+            if (key[u] != ~0u && (key[u] >> 6)) {
+              const uint32_t d = key[u] & 63;
               const uint64_t gwd = x.gvis_off[d] + (hs[u] >> 5);
-              if (gwd < x.gvis_off[d + 1] && ((x.gvis[gwd] >> (hs[u] & 31)) & 1u)) k[u] = ~0u;
+              if (gwd < x.gvis_off[d + 1] && ((x.gvis[gwd] >> (hs[u] & 31)) & 1u)) key[u] = ~0u;
             }
         }
 #pragma unroll
-        for (uint32_t u = 0; u < XU; ++u) emit(v[u], k[u], hs[u]);
+        for (uint32_t u = 0; u < XU; ++u) {
+          if (v[u] != NO_SLOT) g.xkey[v[u]] = key[u] == ~0u ? (uint8_t)0xFF : (uint8_t)key[u];
+          for (uint64_t pend = __ballot(key[u] != ~0u); pend;) {
+            const uint32_t kk = __shfl(key[u], __ffsll((unsigned long long)pend) - 1);
+            const uint64_t m = __ballot(key[u] == kk);
+            if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1))
+              atomicAdd(&hist[(kk >> 6) * MAX_SHARDS + (kk & 63)], (uint32_t)__popcll(m));
+            pend &= ~m;
+          }
+        }
+        continue;
       }
-      if (record && nm) g.xsent[w] = sw | nm;  // (the scatter's last pass only)
+      // scatter: the keys back, then the home slot (a resolved mark) or the id
+#pragma unroll
+      for (uint32_t u = 0; u < XU; ++u) {
+        const uint8_t kb = v[u] != NO_SLOT ? g.xkey[v[u]] : (uint8_t)0xFF;
+        key[u] = kb == 0xFF ? ~0u : (uint32_t)kb;
+      }
+      uint64_t val[XU];
+#pragma unroll
+      for (uint32_t u = 0; u < XU; ++u)
+        val[u] = key[u] == ~0u ? 0ull : (key[u] >> 6) ? (uint64_t)g.phs[v[u]] : g.vid[v[u]];
+#pragma unroll
+      for (uint32_t u = 0; u < XU; ++u) {
+        // this lane's position: its wave's run of the key, at the key's next
+        // position in this workgroup's range (consecutive lanes, consecutive
+        // addresses: one store per run)
+        uint64_t at = 0;
+        for (uint64_t pend = __ballot(key[u] != ~0u); pend;) {
+          const uint32_t kk = __shfl(key[u], __ffsll((unsigned long long)pend) - 1);
+          const uint64_t m = __ballot(key[u] == kk);
+          const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)m) - 1);
+          const bool bm = (kk >> 6) && x.bitmap[kk & 63];
+          uint32_t r0 = 0;
+          if (lane == leader && !bm) r0 = atomicAdd(&hist[(kk >> 6) * MAX_SHARDS + (kk & 63)], (uint32_t)__popcll(m));
+          r0 = __shfl(r0, leader);
+          if (key[u] == kk) at = base[(kk >> 6) * MAX_SHARDS + (kk & 63)] + r0 + __popcll(m & lanemask_lt());
+          pend &= ~m;
+        }
+        if (key[u] == ~0u) continue;
+        const uint32_t d = key[u] & 63;
+        if (!(key[u] >> 6)) {  // (the id only for the unresolved)
+          ((uint64_t *)(send + x.id_off[d]))[at] = val[u];
+        } else if (x.bitmap[d]) {
+          const uint32_t hs = (uint32_t)val[u];
+          atomicOr((uint32_t *)(send + x.sl_off[d]) + (hs >> 5), 1u << (hs & 31));
+        } else {
+          ((uint32_t *)(send + x.sl_off[d]))[at] = (uint32_t)val[u];
+        }
+      }
     }
-  };
+    if (SCATTER && nm) g.xsent[w] = sw | nm;
+  }
   if (!SCATTER) {
-    pass(false, [&](uint32_t, uint32_t key, uint32_t) {
-      for (uint64_t pend = __ballot(key != ~0u); pend;) {
-        const uint32_t kk = __shfl(key, __ffsll((unsigned long long)pend) - 1);
-        const uint64_t m = __ballot(key == kk);
-        if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1))
-          atomicAdd(&hist[(kk >> 6) * MAX_SHARDS + (kk & 63)], (uint32_t)__popcll(m));
-        pend &= ~m;
-      }
-    });
     __syncthreads();
-    for (uint32_t dd = threadIdx.x; dd < g.n_shards; dd += 256) {
-      if (hist[dd]) atomicAdd(&g.ctr->xcnt[dd], (unsigned long long)hist[dd]);
-      if (hist[MAX_SHARDS + dd]) atomicAdd(&g.ctr->xcnt2[dd], (unsigned long long)hist[MAX_SHARDS + dd]);
+    for (uint32_t q = threadIdx.x; q < 2 * G; q += 256) {
+      const uint32_t f = q / G, d = q % G, n = hist[f * MAX_SHARDS + d];
+      mine[q] = n;
+      if (n) atomicAdd(f ? &g.ctr->xcnt2[d] : &g.ctr->xcnt[d], (unsigned long long)n);
     }
-    return;
   }
-  // scatter: this workgroup's range of every segment from its counts (a
-  // counting pre-pass over its own blocks, then one global atomic per key)
-  pass(false, [&](uint32_t, uint32_t key, uint32_t) {
-    for (uint64_t pend = __ballot(key != ~0u); pend;) {
-      const uint32_t kk = __shfl(key, __ffsll((unsigned long long)pend) - 1);
-      const uint64_t m = __ballot(key == kk);
-      if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1))
-        atomicAdd(&hist[(kk >> 6) * MAX_SHARDS + (kk & 63)], (uint32_t)__popcll(m));
-      pend &= ~m;
-    }
-  });
-  __syncthreads();
-  if (threadIdx.x < g.n_shards) {
-    const uint32_t dd = threadIdx.x;
-    base[dd] = hist[dd] ? atomicAdd(&g.ctr->xpos[dd], (unsigned long long)hist[dd]) : 0ull;
-    base[MAX_SHARDS + dd] = hist[MAX_SHARDS + dd] && !x.bitmap[dd]
-                                ? atomicAdd(&g.ctr->xpos2[dd], (unsigned long long)hist[MAX_SHARDS + dd]) : 0ull;
-    hist[dd] = hist[MAX_SHARDS + dd] = 0;
-  }
-  __syncthreads();
-  pass(true, [&](uint32_t v, uint32_t key, uint32_t hs) {
-    // this lane's position: its wave's run of the key, at the key's next
-    // position in this workgroup's range (consecutive lanes, consecutive
-    // addresses: one store per run)
-    uint64_t at = 0;
-    for (uint64_t pend = __ballot(key != ~0u); pend;) {
-      const uint32_t kk = __shfl(key, __ffsll((unsigned long long)pend) - 1);
-      const uint64_t m = __ballot(key == kk);
-      const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)m) - 1);
-      const bool bm = (kk >> 6) && x.bitmap[kk & 63];
-      uint32_t r0 = 0;
-      if (lane == leader && !bm) r0 = atomicAdd(&hist[(kk >> 6) * MAX_SHARDS + (kk & 63)], (uint32_t)__popcll(m));
-      r0 = __shfl(r0, leader);
-      if (key == kk) at = base[(kk >> 6) * MAX_SHARDS + (kk & 63)] + r0 + __popcll(m & lanemask_lt());
-      pend &= ~m;
-    }
-    if (key == ~0u) return;
-    const uint32_t d = key & 63;
-    if (!(key >> 6)) {  // (the id only for the unresolved)
-      ((uint64_t *)(send + x.id_off[d]))[at] = g.vid[v];
-    } else if (x.bitmap[d]) {
-      atomicOr((uint32_t *)(send + x.sl_off[d]) + (hs >> 5), 1u << (hs & 31));
-    } else {
-      ((uint32_t *)(send + x.sl_off[d]))[at] = hs;
-    }
-  });
 }
 
+int xscan_grid(uint64_t nblk) { return (int)std::max<uint64_t>(1, std::min<uint64_t>((nblk + 3) / 4, 8192)); }
+
 hipError_t launch_xlist(const DevGraph &g, bool scatter, uint64_t nblk, char *send, const XSend &x,
-                        hipStream_t s) {
+                        uint32_t *wgc, hipStream_t s) {
   launch_begin();
   if (nblk == 0) return hipSuccess;
-  const int grid = (int)std::min<uint64_t>((nblk + 3) / 4, 8192);
+  const int grid = xscan_grid(nblk);
   if (scatter)
-    hipLaunchKernelGGL(k_xscan<true>, dim3(grid), dim3(256), 0, s, g, send, x);
+    hipLaunchKernelGGL(k_xscan<true>, dim3(grid), dim3(256), 0, s, g, send, x, wgc);
   else
-    hipLaunchKernelGGL(k_xscan<false>, dim3(grid), dim3(256), 0, s, g, send, x);
+    hipLaunchKernelGGL(k_xscan<false>, dim3(grid), dim3(256), 0, s, g, send, x, wgc);
   return hipGetLastError();
 }
 

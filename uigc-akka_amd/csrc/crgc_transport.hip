@@ -34,13 +34,18 @@ int LocalTransport::barrier() {
   return broken ? CRGC_E_TIMEOUT : CRGC_OK;
 }
 
+// Every buffer the handles pass through a transport is device memory (their
+// own scratch arrays), so the copies name the direction: a hipMemcpyDefault
+// copy looks both pointers up in the runtime's allocation map on every call,
+// and under rocprofv3's API interception two such lookups from shard threads
+// faulted inside the runtime (profiles/r5n/README.md).
 int LocalTransport::allgather(uint32_t shard, const void *send, void *recv, size_t bytes,
                               hipStream_t s) {
   if (stream_wait(s) != hipSuccess) return DEV_FAIL("transport");  // send is complete
   post[shard].ptr = send;
   if (int rc = barrier()) return rc;
   for (uint32_t r = 0; r < n_shards; ++r)
-    if (bytes && hipMemcpyAsync((char *)recv + (size_t)r * bytes, post[r].ptr, bytes, hipMemcpyDefault,
+    if (bytes && hipMemcpyAsync((char *)recv + (size_t)r * bytes, post[r].ptr, bytes, hipMemcpyDeviceToDevice,
                                 s) != hipSuccess)
       return DEV_FAIL("transport");
   if (stream_wait(s) != hipSuccess) return DEV_FAIL("transport");
@@ -57,7 +62,7 @@ int LocalTransport::alltoallv(uint32_t shard, const void *send, const size_t *so
   for (uint32_t r = 0; r < n_shards; ++r) {
     if (!rbytes[r]) continue;
     const char *src = (const char *)post[r].ptr + post[r].soff[shard];
-    if (hipMemcpyAsync((char *)recv + roff[r], src, rbytes[r], hipMemcpyDefault, s) != hipSuccess)
+    if (hipMemcpyAsync((char *)recv + roff[r], src, rbytes[r], hipMemcpyDeviceToDevice, s) != hipSuccess)
       return DEV_FAIL("transport");
   }
   if (stream_wait(s) != hipSuccess) return DEV_FAIL("transport");
