@@ -14,6 +14,49 @@
 namespace crgc {
 
 // ---- LocalTransport ----------------------------------------------------------
+// A collective's G device copies in one launch (G hipMemcpyAsync calls were
+// ~2.5 us of GPU time and a dispatch each: 2 000 copies per C4 wakeup over 8
+// logical shards, profiles/r5n).  Segment j: bytes [0, n) of src[j] to dst[j];
+// workgroups stride over 16-B units of every segment (byte tails apart).
+struct Segs {
+  const char *src[TRANSPORT_MAX_SHARDS];
+  char *dst[TRANSPORT_MAX_SHARDS];
+  uint64_t n[TRANSPORT_MAX_SHARDS];
+  uint32_t count;
+};
+
+__global__ __launch_bounds__(256) void k_copy_segs(Segs sg) {
+  const uint64_t t0 = (uint64_t)blockIdx.x * 256 + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
+  for (uint32_t j = 0; j < sg.count; ++j) {
+    const char *src = sg.src[j];
+    char *dst = sg.dst[j];
+    const uint64_t n = sg.n[j];
+    // the widest unit both ends are aligned to (segments are 8-B aligned at least)
+    const uintptr_t al = ((uintptr_t)src | (uintptr_t)dst);
+    uint64_t done = 0;
+    if ((al & 15) == 0) {
+      done = n / 16 * 16;
+      for (uint64_t i = t0; i < n / 16; i += stride) ((uint4 *)dst)[i] = ((const uint4 *)src)[i];
+    } else if ((al & 7) == 0) {
+      done = n / 8 * 8;
+      for (uint64_t i = t0; i < n / 8; i += stride) ((uint2 *)dst)[i] = ((const uint2 *)src)[i];
+    } else if ((al & 3) == 0) {
+      done = n / 4 * 4;
+      for (uint64_t i = t0; i < n / 4; i += stride) ((uint32_t *)dst)[i] = ((const uint32_t *)src)[i];
+    }
+    for (uint64_t i = done + t0; i < n; i += stride) dst[i] = src[i];
+  }
+}
+
+static hipError_t copy_segs(const Segs &sg, hipStream_t s) {
+  uint64_t most = 0;
+  for (uint32_t j = 0; j < sg.count; ++j) most = std::max(most, sg.n[j]);
+  if (!most) return hipSuccess;
+  const uint64_t grid = std::min<uint64_t>(std::max<uint64_t>((most / 16 + 255) / 256, 1), 2048);
+  hipLaunchKernelGGL(k_copy_segs, dim3((uint32_t)grid), dim3(256), 0, s, sg);
+  return hipGetLastError();
+}
+
 // A generation barrier with a bound: a shard that never arrives (its caller
 // failed before the collective) breaks the transport instead of hanging the
 // others forever.
@@ -35,19 +78,23 @@ int LocalTransport::barrier() {
 }
 
 // Every buffer the handles pass through a transport is device memory (their
-// own scratch arrays), so the copies name the direction: a hipMemcpyDefault
-// copy looks both pointers up in the runtime's allocation map on every call,
-// and under rocprofv3's API interception two such lookups from shard threads
-// faulted inside the runtime (profiles/r5n/README.md).
+// own scratch arrays), so a kernel copies it: no runtime copy, whose
+// hipMemcpyDefault form looks both pointers up in the runtime's allocation map
+// (under rocprofv3's API interception two such lookups from shard threads
+// faulted inside the runtime, profiles/r5n/README.md).
 int LocalTransport::allgather(uint32_t shard, const void *send, void *recv, size_t bytes,
                               hipStream_t s) {
   if (stream_wait(s) != hipSuccess) return DEV_FAIL("transport");  // send is complete
   post[shard].ptr = send;
   if (int rc = barrier()) return rc;
-  for (uint32_t r = 0; r < n_shards; ++r)
-    if (bytes && hipMemcpyAsync((char *)recv + (size_t)r * bytes, post[r].ptr, bytes, hipMemcpyDeviceToDevice,
-                                s) != hipSuccess)
-      return DEV_FAIL("transport");
+  Segs sg{};
+  for (uint32_t r = 0; r < n_shards && bytes; ++r) {
+    sg.src[sg.count] = (const char *)post[r].ptr;
+    sg.dst[sg.count] = (char *)recv + (size_t)r * bytes;
+    sg.n[sg.count++] = bytes;
+  }
+  (void)hipGetLastError();  // (a soft status of an earlier call is not this launch's)
+  if (copy_segs(sg, s) != hipSuccess) return DEV_FAIL("transport");
   if (stream_wait(s) != hipSuccess) return DEV_FAIL("transport");
   return barrier();  // nobody reuses its send buffer before every peer has copied it
 }
@@ -59,12 +106,15 @@ int LocalTransport::alltoallv(uint32_t shard, const void *send, const size_t *so
   post[shard].ptr = send;
   post[shard].soff = soff;
   if (int rc = barrier()) return rc;
+  Segs sg{};
   for (uint32_t r = 0; r < n_shards; ++r) {
     if (!rbytes[r]) continue;
-    const char *src = (const char *)post[r].ptr + post[r].soff[shard];
-    if (hipMemcpyAsync((char *)recv + roff[r], src, rbytes[r], hipMemcpyDeviceToDevice, s) != hipSuccess)
-      return DEV_FAIL("transport");
+    sg.src[sg.count] = (const char *)post[r].ptr + post[r].soff[shard];
+    sg.dst[sg.count] = (char *)recv + roff[r];
+    sg.n[sg.count++] = rbytes[r];
   }
+  (void)hipGetLastError();  // (a soft status of an earlier call is not this launch's)
+  if (copy_segs(sg, s) != hipSuccess) return DEV_FAIL("transport");
   if (stream_wait(s) != hipSuccess) return DEV_FAIL("transport");
   return barrier();
 }
