@@ -1902,11 +1902,35 @@ hipError_t launch_resolve(const DevGraph &g, int step, uint64_t mask, uint64_t *
 // its workgroup's count per key in `wgc`; the scatter pass (same grid, so the
 // same blocks per workgroup) reserves each key's range from those counts and
 // reads the key bytes back, so the random bitmap probes run once.
+// A load group's keys (XU per lane) by key, without a dependent LDS atomic per
+// key and group step: a uniform loop over the 2G keys ballots each step's
+// lanes of that key into s_m[key][step] and sums them into s_c[key].
+template <int XU>
+__device__ inline void group_keys(const uint32_t (&key)[XU], uint32_t G, uint64_t (*s_m)[XU], uint32_t *s_c) {
+  const uint32_t lane = lane_id();
+  for (uint32_t q = 0; q < 2 * G; ++q) {
+    const uint32_t kq = (q / G) * 64 + (q % G);  // form << 6 | destination
+    uint32_t c = 0;
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+      const uint64_t m = __ballot(key[u] == kq);
+      if (lane == 0) s_m[q][u] = m;
+      c += (uint32_t)__popcll(m);
+    }
+    if (lane == 0) s_c[q] = c;
+  }
+  wave_lds_fence();
+}
+
 template <bool SCATTER>
 __global__ __launch_bounds__(256) void k_xscan(DevGraph g, char *send, XSend x, uint32_t *wgc) {
+  constexpr uint32_t XU = 4;
   __shared__ uint32_t hist[2 * MAX_SHARDS];
   __shared__ unsigned long long base[2 * MAX_SHARDS];
+  __shared__ uint64_t s_m[4][2 * MAX_SHARDS][XU];  // per wave: a load group's lanes by key and step
+  __shared__ uint32_t s_c[4][2 * MAX_SHARDS];      // per wave: the group's count, then its run's start
   const uint32_t G = g.n_shards;
+  const int wv = threadIdx.x >> 6;
   uint32_t *mine = wgc + (uint64_t)blockIdx.x * 2 * G;  // this workgroup's counts: [form][destination]
   for (uint32_t q = threadIdx.x; q < 2 * MAX_SHARDS; q += 256) {
     hist[q] = 0;
@@ -1918,12 +1942,11 @@ __global__ __launch_bounds__(256) void k_xscan(DevGraph g, char *send, XSend x, 
     }
   }
   __syncthreads();
-  const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
+  const uint64_t gw = (uint64_t)blockIdx.x * 4 + wv, nw = (uint64_t)gridDim.x * 4;
   const uint64_t np = g.ctr->proxy_top;
   const uint64_t nb = (np + BLK_SLOTS - 1) / BLK_SLOTS;
   const uint64_t w0 = g.pbase / 32;  // the region's first marked word (pbase is block-aligned)
   const uint32_t lane = lane_id();
-  constexpr uint32_t XU = 4;
   for (uint64_t blk = gw; blk < nb; blk += nw) {
     const uint64_t w = w0 + blk * 64 + lane;
     const uint32_t mw = g.vis[w], sw = g.xsent[w];
@@ -1958,16 +1981,12 @@ __global__ __launch_bounds__(256) void k_xscan(DevGraph g, char *send, XSend x, 
             }
         }
 #pragma unroll
-        for (uint32_t u = 0; u < XU; ++u) {
+        for (uint32_t u = 0; u < XU; ++u)
           if (v[u] != NO_SLOT) g.xkey[v[u]] = key[u] == ~0u ? (uint8_t)0xFF : (uint8_t)key[u];
-          for (uint64_t pend = __ballot(key[u] != ~0u); pend;) {
-            const uint32_t kk = __shfl(key[u], __ffsll((unsigned long long)pend) - 1);
-            const uint64_t m = __ballot(key[u] == kk);
-            if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1))
-              atomicAdd(&hist[(kk >> 6) * MAX_SHARDS + (kk & 63)], (uint32_t)__popcll(m));
-            pend &= ~m;
-          }
-        }
+        group_keys<XU>(key, G, s_m[wv], s_c[wv]);
+        for (uint32_t q = lane; q < 2 * G; q += 64)
+          if (s_c[wv][q]) atomicAdd(&hist[(q / G) * MAX_SHARDS + q % G], s_c[wv][q]);
+        wave_lds_fence();  // s_c is rewritten by the next group
         continue;
       }
       // scatter: the keys back, then the home slot (a resolved mark) or the id
@@ -1980,34 +1999,33 @@ __global__ __launch_bounds__(256) void k_xscan(DevGraph g, char *send, XSend x, 
 #pragma unroll
       for (uint32_t u = 0; u < XU; ++u)
         val[u] = key[u] == ~0u ? 0ull : (key[u] >> 6) ? (uint64_t)g.phs[v[u]] : g.vid[v[u]];
+      // each key's run in this workgroup's range: one LDS atomic per key
+      // present in the group (issued together by lanes q), then every lane's
+      // position = run start + its key's lanes before it in the group
+      group_keys<XU>(key, G, s_m[wv], s_c[wv]);
+      for (uint32_t q = lane; q < 2 * G; q += 64) {
+        const uint32_t c = s_c[wv][q], f = q / G, d = q % G;
+        s_c[wv][q] = c && !(f && x.bitmap[d]) ? atomicAdd(&hist[f * MAX_SHARDS + d], c) : 0u;
+      }
+      wave_lds_fence();
 #pragma unroll
       for (uint32_t u = 0; u < XU; ++u) {
-        // this lane's position: its wave's run of the key, at the key's next
-        // position in this workgroup's range (consecutive lanes, consecutive
-        // addresses: one store per run)
-        uint64_t at = 0;
-        for (uint64_t pend = __ballot(key[u] != ~0u); pend;) {
-          const uint32_t kk = __shfl(key[u], __ffsll((unsigned long long)pend) - 1);
-          const uint64_t m = __ballot(key[u] == kk);
-          const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)m) - 1);
-          const bool bm = (kk >> 6) && x.bitmap[kk & 63];
-          uint32_t r0 = 0;
-          if (lane == leader && !bm) r0 = atomicAdd(&hist[(kk >> 6) * MAX_SHARDS + (kk & 63)], (uint32_t)__popcll(m));
-          r0 = __shfl(r0, leader);
-          if (key[u] == kk) at = base[(kk >> 6) * MAX_SHARDS + (kk & 63)] + r0 + __popcll(m & lanemask_lt());
-          pend &= ~m;
-        }
         if (key[u] == ~0u) continue;
-        const uint32_t d = key[u] & 63;
-        if (!(key[u] >> 6)) {  // (the id only for the unresolved)
-          ((uint64_t *)(send + x.id_off[d]))[at] = val[u];
-        } else if (x.bitmap[d]) {
+        const uint32_t f = key[u] >> 6, d = key[u] & 63, q = f * G + d;
+        if (f && x.bitmap[d]) {
           const uint32_t hs = (uint32_t)val[u];
           atomicOr((uint32_t *)(send + x.sl_off[d]) + (hs >> 5), 1u << (hs & 31));
-        } else {
-          ((uint32_t *)(send + x.sl_off[d]))[at] = (uint32_t)val[u];
+          continue;
         }
+        uint64_t at = base[f * MAX_SHARDS + d] + s_c[wv][q];
+#pragma unroll
+        for (uint32_t u2 = 0; u2 < XU; ++u2)
+          if (u2 < u) at += (uint64_t)__popcll(s_m[wv][q][u2]);
+        at += (uint64_t)__popcll(s_m[wv][q][u] & lanemask_lt());
+        if (!f) ((uint64_t *)(send + x.id_off[d]))[at] = val[u];  // (the id only for the unresolved)
+        else ((uint32_t *)(send + x.sl_off[d]))[at] = (uint32_t)val[u];
       }
+      wave_lds_fence();  // s_m / s_c are rewritten by the next group
     }
     if (SCATTER && nm) g.xsent[w] = sw | nm;
   }
@@ -2048,29 +2066,55 @@ __device__ inline uint32_t import_mark(const DevGraph &g, uint8_t *Fc, uint8_t *
   return 1;
 }
 
+// XI work items per thread, their loads issued together (one item per thread
+// was a chain of three dependent loads: 0.2 ms per shard for C4's second
+// round over 8 logical shards, profiles/r5o).
 __global__ __launch_bounds__(256) void k_ximport(DevGraph g, const char *recv, XRecv x, int L) {
+  constexpr int XI = 4;
   uint8_t *Fc = g.front[L & 1];
   uint8_t *Dc = g.dirty[L & 1];
   const uint64_t top = g.ctr->slot_top;
   uint32_t found = 0;
   const uint64_t total = x.start[x.G], stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += stride) {
-    uint32_t r = 0;
-    while (r + 1 < x.G && x.start[r + 1] <= i) ++r;
-    const uint64_t k = i - x.start[r];
-    const char *seg = recv + x.off[r];
-    if (k < x.n_id[r]) {
-      const uint32_t v = id_find(g, ((const uint64_t *)seg)[k]);
-      if (v < 0xFFFFFFF0u) found += import_mark(g, Fc, Dc, v, top);
-      continue;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * 256 + threadIdx.x; i0 < total; i0 += stride * XI) {
+    uint32_t v[XI];
+#pragma unroll
+    for (int u = 0; u < XI; ++u) {
+      const uint64_t i = i0 + u * stride;
+      v[u] = NO_SLOT;
+      if (i >= total) continue;
+      uint32_t r = 0;
+      while (r + 1 < x.G && x.start[r + 1] <= i) ++r;
+      const uint64_t k = i - x.start[r];
+      const char *seg = recv + x.off[r];
+      if (k < x.n_id[r]) {
+        const uint32_t s = id_find(g, ((const uint64_t *)seg)[k]);
+        if (s < 0xFFFFFFF0u) v[u] = s;
+        continue;
+      }
+      const uint64_t j = k - x.n_id[r];
+      const uint32_t w = ((const uint32_t *)(seg + 8 * x.n_id[r]))[j];
+      if (!x.bitmap[r]) {
+        v[u] = w;
+      } else {
+        for (uint32_t m = w; m; m &= m - 1) found += import_mark(g, Fc, Dc, (uint32_t)(j * 32) + __ffs(m) - 1, top);
+      }
     }
-    const uint64_t j = k - x.n_id[r];
-    const uint32_t w = ((const uint32_t *)(seg + 8 * x.n_id[r]))[j];
-    if (!x.bitmap[r]) {
-      found += import_mark(g, Fc, Dc, w, top);
-    } else {
-      for (uint32_t m = w; m; m &= m - 1) found += import_mark(g, Fc, Dc, (uint32_t)(j * 32) + __ffs(m) - 1, top);
+    uint8_t f[XI];
+    uint32_t vw[XI];
+#pragma unroll
+    for (int u = 0; u < XI; ++u) {
+      const bool in = v[u] < top;
+      f[u] = in ? g.flags[v[u]] : (uint8_t)0;
+      vw[u] = in ? g.vis[v[u] >> 5] : ~0u;
     }
+#pragma unroll
+    for (int u = 0; u < XI; ++u)
+      if (v[u] < top && (f[u] & (FL_ALIVE | FL_PROXY)) == FL_ALIVE && !((vw[u] >> (v[u] & 31)) & 1u)) {
+        Fc[v[u]] = 1;
+        Dc[v[u] >> 11] = 1;
+        ++found;
+      }
   }
   const uint64_t t = block_sum4(found);
   if (threadIdx.x == 0 && t) atomicAdd(&g.ctr->ring[(L - 1) % LEVEL_RING], (unsigned long long)t);
@@ -2099,7 +2143,7 @@ hipError_t launch_ximport(const DevGraph &g, const char *recv, const XRecv &x, i
   launch_begin();
   const uint64_t n = x.start[x.G];
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ximport, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, g, recv, x, level);
+  hipLaunchKernelGGL(k_ximport, dim3(grid_for((n + 3) / 4, 256, 4096)), dim3(256), 0, s, g, recv, x, level);
   return hipGetLastError();
 }
 
