@@ -1902,51 +1902,44 @@ hipError_t launch_resolve(const DevGraph &g, int step, uint64_t mask, uint64_t *
 // its workgroup's count per key in `wgc`; the scatter pass (same grid, so the
 // same blocks per workgroup) reserves each key's range from those counts and
 // reads the key bytes back, so the random bitmap probes run once.
-// A load group's keys (XU per lane) by key, without a dependent LDS atomic per
-// key and group step: a uniform loop over the 2G keys ballots each step's
-// lanes of that key into s_m[key][step] and sums them into s_c[key].
-template <int XU>
-__device__ inline void group_keys(const uint32_t (&key)[XU], uint32_t G, uint64_t (*s_m)[XU], uint32_t *s_c) {
-  const uint32_t lane = lane_id();
-  for (uint32_t q = 0; q < 2 * G; ++q) {
-    const uint32_t kq = (q / G) * 64 + (q % G);  // form << 6 | destination
-    uint32_t c = 0;
-#pragma unroll
-    for (int u = 0; u < XU; ++u) {
-      const uint64_t m = __ballot(key[u] == kq);
-      if (lane == 0) s_m[q][u] = m;
-      c += (uint32_t)__popcll(m);
-    }
-    if (lane == 0) s_c[q] = c;
-  }
-  wave_lds_fence();
-}
-
+// The proxies marked since the last export (marked, not yet sent: vis &
+// ~xsent over the proxy region), by destination: ids of the unresolved (xcnt),
+// home slots of the resolved (xcnt2); then the scatter into the byte layout the
+// host derived from the all-gathered counts, which records them as sent.  A
+// streaming pass over the region's marked / sent words and, for the new marks
+// only, their home shards and home slots (round 4 listed marked proxies into
+// per-block regions as the level kernels found them and packed the lists: a
+// chain of dependent loads per entry, ~0.8 ms per shard for C4's first round
+// over 8 logical shards).
+// One wave per 2048-proxy block: lane l holds the block's words l (marked and
+// sent); step k covers slots 64k .. 64k+63 (slot 64k + l: word 2k + l / 32,
+// bit l % 32, by one shuffle), so the loads of a step are coalesced; XU steps
+// per load group.  The count pass derives each new mark's key (form << 6 |
+// destination; 0xFF: none — its home is marked already) from the home shard,
+// the home slot and the replicated home bitmaps, stores it as a byte and leaves
+// its workgroup's count per key in `wgc`; the scatter pass (same grid, so the
+// same blocks per workgroup) reserves each key's range from those counts and
+// reads the key bytes back, so the random bitmap probes run once.
 template <bool SCATTER>
 __global__ __launch_bounds__(256) void k_xscan(DevGraph g, char *send, XSend x, uint32_t *wgc) {
-  constexpr uint32_t XU = 4;
   __shared__ uint32_t hist[2 * MAX_SHARDS];
   __shared__ unsigned long long base[2 * MAX_SHARDS];
-  __shared__ uint64_t s_m[4][2 * MAX_SHARDS][XU];  // per wave: a load group's lanes by key and step
-  __shared__ uint32_t s_c[4][2 * MAX_SHARDS];      // per wave: the group's count, then its run's start
   const uint32_t G = g.n_shards;
-  const int wv = threadIdx.x >> 6;
   uint32_t *mine = wgc + (uint64_t)blockIdx.x * 2 * G;  // this workgroup's counts: [form][destination]
   for (uint32_t q = threadIdx.x; q < 2 * MAX_SHARDS; q += 256) {
     hist[q] = 0;
-    if (SCATTER) {
+    if (SCATTER) {  // this workgroup's run of each segment: k_xscan_sum's exclusive scan
       const uint32_t f = q / MAX_SHARDS, d = q % MAX_SHARDS;
-      const uint32_t n = d < G ? mine[f * G + d] : 0u;
-      base[q] = n && !(f && x.bitmap[d]) ? atomicAdd(f ? &g.ctr->xpos2[d] : &g.ctr->xpos[d], (unsigned long long)n)
-                                         : 0ull;
+      base[q] = d < G ? mine[f * G + d] : 0ull;
     }
   }
   __syncthreads();
-  const uint64_t gw = (uint64_t)blockIdx.x * 4 + wv, nw = (uint64_t)gridDim.x * 4;
+  const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
   const uint64_t np = g.ctr->proxy_top;
   const uint64_t nb = (np + BLK_SLOTS - 1) / BLK_SLOTS;
   const uint64_t w0 = g.pbase / 32;  // the region's first marked word (pbase is block-aligned)
   const uint32_t lane = lane_id();
+  constexpr uint32_t XU = 4;
   for (uint64_t blk = gw; blk < nb; blk += nw) {
     const uint64_t w = w0 + blk * 64 + lane;
     const uint32_t mw = g.vis[w], sw = g.xsent[w];
@@ -1981,12 +1974,16 @@ __global__ __launch_bounds__(256) void k_xscan(DevGraph g, char *send, XSend x, 
             }
         }
 #pragma unroll
-        for (uint32_t u = 0; u < XU; ++u)
+        for (uint32_t u = 0; u < XU; ++u) {
           if (v[u] != NO_SLOT) g.xkey[v[u]] = key[u] == ~0u ? (uint8_t)0xFF : (uint8_t)key[u];
-        group_keys<XU>(key, G, s_m[wv], s_c[wv]);
-        for (uint32_t q = lane; q < 2 * G; q += 64)
-          if (s_c[wv][q]) atomicAdd(&hist[(q / G) * MAX_SHARDS + q % G], s_c[wv][q]);
-        wave_lds_fence();  // s_c is rewritten by the next group
+          for (uint64_t pend = __ballot(key[u] != ~0u); pend;) {
+            const uint32_t kk = __shfl(key[u], __ffsll((unsigned long long)pend) - 1);
+            const uint64_t m = __ballot(key[u] == kk);
+            if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1))
+              atomicAdd(&hist[(kk >> 6) * MAX_SHARDS + (kk & 63)], (uint32_t)__popcll(m));
+            pend &= ~m;
+          }
+        }
         continue;
       }
       // scatter: the keys back, then the home slot (a resolved mark) or the id
@@ -1999,43 +1996,61 @@ __global__ __launch_bounds__(256) void k_xscan(DevGraph g, char *send, XSend x, 
 #pragma unroll
       for (uint32_t u = 0; u < XU; ++u)
         val[u] = key[u] == ~0u ? 0ull : (key[u] >> 6) ? (uint64_t)g.phs[v[u]] : g.vid[v[u]];
-      // each key's run in this workgroup's range: one LDS atomic per key
-      // present in the group (issued together by lanes q), then every lane's
-      // position = run start + its key's lanes before it in the group
-      group_keys<XU>(key, G, s_m[wv], s_c[wv]);
-      for (uint32_t q = lane; q < 2 * G; q += 64) {
-        const uint32_t c = s_c[wv][q], f = q / G, d = q % G;
-        s_c[wv][q] = c && !(f && x.bitmap[d]) ? atomicAdd(&hist[f * MAX_SHARDS + d], c) : 0u;
-      }
-      wave_lds_fence();
 #pragma unroll
       for (uint32_t u = 0; u < XU; ++u) {
+        // this lane's position: its wave's run of the key, at the key's next
+        // position in this workgroup's range (consecutive lanes, consecutive
+        // addresses: one store per run)
+        uint64_t at = 0;
+        for (uint64_t pend = __ballot(key[u] != ~0u); pend;) {
+          const uint32_t kk = __shfl(key[u], __ffsll((unsigned long long)pend) - 1);
+          const uint64_t m = __ballot(key[u] == kk);
+          const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)m) - 1);
+          const bool bm = (kk >> 6) && x.bitmap[kk & 63];
+          uint32_t r0 = 0;
+          if (lane == leader && !bm) r0 = atomicAdd(&hist[(kk >> 6) * MAX_SHARDS + (kk & 63)], (uint32_t)__popcll(m));
+          r0 = __shfl(r0, leader);
+          if (key[u] == kk) at = base[(kk >> 6) * MAX_SHARDS + (kk & 63)] + r0 + __popcll(m & lanemask_lt());
+          pend &= ~m;
+        }
         if (key[u] == ~0u) continue;
-        const uint32_t f = key[u] >> 6, d = key[u] & 63, q = f * G + d;
-        if (f && x.bitmap[d]) {
+        const uint32_t d = key[u] & 63;
+        if (!(key[u] >> 6)) {  // (the id only for the unresolved)
+          ((uint64_t *)(send + x.id_off[d]))[at] = val[u];
+        } else if (x.bitmap[d]) {
           const uint32_t hs = (uint32_t)val[u];
           atomicOr((uint32_t *)(send + x.sl_off[d]) + (hs >> 5), 1u << (hs & 31));
-          continue;
+        } else {
+          ((uint32_t *)(send + x.sl_off[d]))[at] = (uint32_t)val[u];
         }
-        uint64_t at = base[f * MAX_SHARDS + d] + s_c[wv][q];
-#pragma unroll
-        for (uint32_t u2 = 0; u2 < XU; ++u2)
-          if (u2 < u) at += (uint64_t)__popcll(s_m[wv][q][u2]);
-        at += (uint64_t)__popcll(s_m[wv][q][u] & lanemask_lt());
-        if (!f) ((uint64_t *)(send + x.id_off[d]))[at] = val[u];  // (the id only for the unresolved)
-        else ((uint32_t *)(send + x.sl_off[d]))[at] = (uint32_t)val[u];
       }
-      wave_lds_fence();  // s_m / s_c are rewritten by the next group
     }
     if (SCATTER && nm) g.xsent[w] = sw | nm;
   }
-  if (!SCATTER) {
+  if (!SCATTER) {  // (one global atomic per workgroup and key serialised ~4 400 workgroups on
+                   // 2G words: ~50 us per pass at C4 over 8 logical shards; k_xscan_sum scans)
     __syncthreads();
-    for (uint32_t q = threadIdx.x; q < 2 * G; q += 256) {
-      const uint32_t f = q / G, d = q % G, n = hist[f * MAX_SHARDS + d];
-      mine[q] = n;
-      if (n) atomicAdd(f ? &g.ctr->xcnt2[d] : &g.ctr->xcnt[d], (unsigned long long)n);
-    }
+    for (uint32_t q = threadIdx.x; q < 2 * G; q += 256) mine[q] = hist[(q / G) * MAX_SHARDS + q % G];
+  }
+}
+
+// Per key (one workgroup each): the exclusive scan of the workgroups' counts
+// in place, the total into xcnt / xcnt2.
+__global__ __launch_bounds__(1024) void k_xscan_sum(DevGraph g, uint32_t *wgc, uint32_t nwg) {
+  __shared__ uint32_t s_w[40];
+  const uint32_t G = g.n_shards, q = blockIdx.x;
+  uint32_t run = 0;
+  for (uint32_t w0 = 0; w0 < nwg; w0 += 1024) {
+    const uint32_t w = w0 + threadIdx.x;
+    const uint32_t n = w < nwg ? wgc[(uint64_t)w * 2 * G + q] : 0u;
+    uint32_t tot;
+    const uint32_t ex = tail_scan(n, s_w, tot);
+    if (w < nwg) wgc[(uint64_t)w * 2 * G + q] = run + ex;
+    run += tot;
+  }
+  if (threadIdx.x == 0) {
+    const uint32_t f = q / G, d = q % G;
+    (f ? g.ctr->xcnt2 : g.ctr->xcnt)[d] = run;
   }
 }
 
@@ -2046,10 +2061,12 @@ hipError_t launch_xlist(const DevGraph &g, bool scatter, uint64_t nblk, char *se
   launch_begin();
   if (nblk == 0) return hipSuccess;
   const int grid = xscan_grid(nblk);
-  if (scatter)
+  if (scatter) {
     hipLaunchKernelGGL(k_xscan<true>, dim3(grid), dim3(256), 0, s, g, send, x, wgc);
-  else
+  } else {
     hipLaunchKernelGGL(k_xscan<false>, dim3(grid), dim3(256), 0, s, g, send, x, wgc);
+    hipLaunchKernelGGL(k_xscan_sum, dim3(2 * g.n_shards), dim3(1024), 0, s, g, wgc, (uint32_t)grid);
+  }
   return hipGetLastError();
 }
 
