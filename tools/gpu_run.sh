@@ -23,6 +23,7 @@
 #   c4l8s c2l8s      logical shards on one shared stream with the per-shard level log (all level kernels timed)
 #   c2l8x<k> c4l8x<k>  c2l8 / c4l8 with mark rounds capped at k levels (CRGC_XLEVELS, test hook)
 #   ab:<variants>    tools/ab_bench.sh A/B of env variants on the C2 line
+#   abl:<variants>   the same after 100 warmup wakeups (a grown graph)
 #   ab2l8:<variants> ab4l8:<variants>  tools/ab_l8.sh A/B of env variants on C2 / C4 logical shards
 #   longkt           kernel trace + level log of the long run
 #   long             C2 over 200 wakeups: the steady state, rebuilds / repacks amortized in
@@ -107,6 +108,9 @@ for step in "$@"; do
     ab:*)  # tools/ab_bench.sh (C2 N = 1) over the variants after the colon (separated by spaces)
       read -ra vs <<< "${step#*:}"
       (cd "$ROOT" && bash tools/ab_bench.sh "$TAG/ab_c2" "${vs[@]}" > /dev/null) ;;
+    abl:*)  # the same after 100 warmup wakeups (the live set grown to ~2.1e7: the long run's middle)
+      read -ra vs <<< "${step#*:}"
+      (cd "$ROOT" && AB_ARGS="--steps 10 --warmup 100" bash tools/ab_bench.sh "$TAG/ab_c2l" "${vs[@]}" > /dev/null) ;;
     ab2l8:*|ab4l8:*)  # tools/ab_l8.sh over the variants after the colon (separated by spaces)
       wl=${step%%l8:*}; wl=c${wl#ab}
       read -ra vs <<< "${step#*:}"
