@@ -325,6 +325,31 @@ def test_c4_shape_eight_shards(sharded, oracle_mod, xbits, xlevels, ratio, xfilt
     assert h.total_actors_seen() == o.total_actors_seen()
 
 
+@pytest.mark.parametrize("walk", [{"CRGC_WALK": "0"}, {"CRGC_WALK_START": "64", "CRGC_WALK_MAX": "128"},
+                                  {"CRGC_WALK_START": "65536", "CRGC_WALK_MAX": "65536"}])
+def test_c4_shape_eight_shards_walk_forms(sharded, oracle_mod, walk, monkeypatch):
+    """A mark round's narrow levels by k_tail (one workgroup; CRGC_WALK=0) or by
+    k_walk (WALK_WG workgroups with grid barriers) taking over early and
+    bailing often (64 / 128) or taking every listed level up to its queue's
+    capacity: bit-exact against the unsharded oracle (G = 8, C4-shaped)."""
+    for k, v in walk.items():
+        monkeypatch.setenv(k, v)
+    V = 100_000
+    w = world.World(seed=0x5EED + 14)
+    w.bulk_graph(V, 10 * V, alpha=2.1, n_roots=V // 1000, cap=100000)
+    h, o = sharded(8), oracle_mod.OracleGraph()
+    for b in w.batches(1 << 18):
+        h.merge_entries(b, split=True)
+        o.merge_entries(b)
+    _same(h.trace(True), o.trace(True))
+    for _ in range(2):
+        b = w.wakeup(V // 10, busy=V * 9 // 100, pending=V // 100)
+        h.merge_entries(b, split=True)
+        o.merge_entries(b)
+        _same(h.trace(True), o.trace(True))
+    assert h.export() == o.export()
+
+
 def test_forty_shards_rebuild_homes_above_32(sharded, oracle_mod):
     """Home-slot generations of shards >= 32 (the per-home mask is
     64 bits wide).  Shards 33, 35 and 39 compact between traces, renumbering

@@ -253,6 +253,11 @@ struct Knobs {
   // CRGC_TAIL_MAX set both forms.
   uint32_t tail_start_sharded = 2048;
   uint32_t tail_max_sharded = 4096;
+  // Sharded graphs: k_walk (WALK_WG workgroups) takes a mark round's narrow
+  // levels over instead (CRGC_WALK=0: k_tail with the thresholds above).
+  bool walk = true;              // CRGC_WALK
+  uint32_t walk_start = 16384;   // CRGC_WALK_START
+  uint32_t walk_max = 32768;     // CRGC_WALK_MAX
   uint32_t chain_after = 64;     // CRGC_CHAIN_AFTER
   int kernel_timing = 1;         // CRGC_KERNEL_TIMING: 0 chunks, 1 k_expand, 2 all level kernels
   bool level_log = false;        // CRGC_LEVEL_LOG
@@ -307,6 +312,9 @@ struct Knobs {
     if (const char *m = env("CRGC_TAIL")) tail = atoi(m) != 0;
     if (const char *m = env("CRGC_TAIL_START")) tail_start = tail_start_sharded = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_TAIL_MAX")) tail_max = tail_max_sharded = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_WALK")) walk = atoi(m) != 0;
+    if (const char *m = env("CRGC_WALK_START")) walk_start = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_WALK_MAX")) walk_max = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_CHAIN_AFTER")) chain_after = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_XBITS")) xbits = atoi(m);
     if (const char *m = env("CRGC_BUCKETS_LOG2"))
@@ -504,7 +512,7 @@ int device_error(crgc_graph *h) {
   snprintf(what, sizeof what, "device error flags 0x%llx", (unsigned long long)err);
   note_error(__FILE__, __LINE__, what);
   if (err & (ERR_RESERVED_ID | ERR_TOO_MANY | ERR_BAD_OFFSETS)) return CRGC_E_INVAL;
-  if (err & ERR_SPIN) return CRGC_E_TIMEOUT;
+  if (err & (ERR_SPIN | ERR_WALK_STUCK)) return CRGC_E_TIMEOUT;
   if (err & ERR_QUEUE_FULL) return DEV_FAIL("");
   return CRGC_E_NOMEM;
 }
@@ -2092,14 +2100,18 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
     la.pull_div = 0;
   }
   if (kn.has_sparse) la.sparse_thresh = kn.sparse_thresh;
-  // Narrow frontiers: one workgroup finishes the mark (k_tail).
+  // Narrow frontiers: one workgroup finishes the mark (k_tail), or in a
+  // sharded graph WALK_WG of them (k_walk, to larger frontiers).
   if (kn.tail) la.flags |= LV_TAIL;
+  const bool walk = h->tp && kn.tail && kn.walk;
+  if (walk) la.flags |= LV_WALK;
   // Deep marks: a k_tail walk of chain_after links hands the rest to chain mode
   // (pointer jumping, crgc_chain.hip).  Unsharded graphs only.
   la.chain_after = h->tp ? 0 : kn.chain_after;
   la.xslices = kn.xslices;
-  la.tail_start = std::min<uint32_t>(h->tp ? kn.tail_start_sharded : kn.tail_start, TAIL_QCAP);
-  la.tail_max = std::min<uint32_t>(std::max(h->tp ? kn.tail_max_sharded : kn.tail_max, 1u), TAIL_QCAP);
+  la.tail_start = std::min<uint32_t>(walk ? kn.walk_start : h->tp ? kn.tail_start_sharded : kn.tail_start, TAIL_QCAP);
+  la.tail_max = std::min<uint32_t>(std::max(walk ? kn.walk_max : h->tp ? kn.tail_max_sharded : kn.tail_max, 1u),
+                                   TAIL_QCAP);
   // The pseudo-root level's binned push (crgc_trace.hip k_bin_place / k_bin_apply):
   // up to 256 bins of >= 65536 slots (an LDS bitmap of <= 128 KiB each), BIN_WG
   // place workgroups with a fixed-capacity slice of every bin each; the slices
@@ -2647,7 +2659,7 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
     // A round from a few received marks is usually finished by k_tail in its
     // first level: launch one level first, not four (the rest would only check
     // that the mark is done: ~13 us each)
-    const int first = !capped && items <= h->knobs.tail_start_sharded ? 1 : 4;
+    const int first = !capped && items <= (h->knobs.walk ? h->knobs.walk_start : h->knobs.tail_start_sharded) ? 1 : 4;
     if (int rc = run_levels(h, investigate, location, top, false, L, lr, &end, nullptr, cap, &capped, first))
       return rc;
     ++*rounds;

@@ -165,6 +165,7 @@ constexpr uint32_t LV_PULL = 4;                // dense levels scan in-candidate
 constexpr uint32_t LV_TAIL = 8;                // narrow frontiers go to one workgroup (k_tail)
 constexpr uint32_t LV_INVESTIGATE = 16;        // set by launch_level: no supervisor edges
 constexpr uint32_t LV_ROOTS = 32;              // set by launch_level: the pseudo-root level
+constexpr uint32_t LV_WALK = 64;               // narrow frontiers go to WALK_WG workgroups (k_walk)
 
 struct LevelArgs {
   int level;

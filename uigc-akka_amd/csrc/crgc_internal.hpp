@@ -108,6 +108,7 @@ constexpr uint32_t ERR_UNDO_NEW = 1u << 6;
 constexpr uint32_t ERR_SPIN = 1u << 7;
 constexpr uint32_t ERR_BAD_OFFSETS = 1u << 8;
 constexpr uint32_t ERR_QUEUE_FULL = 1u << 9;
+constexpr uint32_t ERR_WALK_STUCK = 1u << 10;  // k_walk: a grid barrier wait ran out
 
 constexpr int WAVE = 64;
 constexpr int BLK_SLOTS = 2048;          // slots per wave-block (64 lanes x 32)
@@ -158,6 +159,11 @@ struct Counters {
   unsigned long long xpos[MAX_SHARDS];  // scatter cursors
   unsigned long long xcnt2[MAX_SHARDS]; // mark rounds: home slots to send per destination
   unsigned long long xpos2[MAX_SHARDS]; // their scatter cursors
+  // k_walk (the multi-workgroup narrow-frontier walk): queue lengths by level
+  // mod 3, claims and supervisor edges, and its grid barrier
+  unsigned long long walk_n[3];
+  unsigned long long walk_claims, walk_sup;
+  unsigned int walk_bar, walk_gen, walk_fail, walk_pad;
   unsigned long long ring[LEVEL_RING];
 };
 

@@ -973,6 +973,26 @@ constexpr uint32_t TAIL_LQ = 1024;
 constexpr uint32_t TAIL_LIGHT = 16;
 constexpr uint32_t TAIL_LVIS_WORDS = 32 * 1024;  // 128 KiB: graphs of up to 1,048,576 slots
 
+// Exclusive scan over a workgroup of T threads (T / 64 <= 16 waves); `total` gets the sum.
+template <int T>
+__device__ inline uint32_t tail_scan_n(uint32_t v, uint32_t *s_w, uint32_t &total) {
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const uint32_t incl = wave_incl_scan(v);
+  if (lane == 63) s_w[w] = incl;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const uint32_t x = threadIdx.x < T / 64 ? s_w[threadIdx.x] : 0;
+    const uint32_t xi = wave_incl_scan(x);
+    if (threadIdx.x < T / 64) s_w[16 + threadIdx.x] = xi - x;
+    if (threadIdx.x == T / 64 - 1) s_w[32] = xi;
+  }
+  __syncthreads();
+  total = s_w[32];
+  const uint32_t r = s_w[16 + w] + incl - v;
+  __syncthreads();
+  return r;
+}
+
 // Exclusive scan over the workgroup; `total` gets the sum.
 __device__ inline uint32_t tail_scan(uint32_t v, uint32_t *s_w, uint32_t &total) {
   const int lane = lane_id(), w = threadIdx.x >> 6;
@@ -1337,6 +1357,311 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_walk: WALK_WG workgroups finish a sharded mark round's narrow levels in
+// one launch (the multi-workgroup form of k_tail's takeover).  One workgroup
+// walking a shard's narrow levels ran ~1 G edges/s, and every level the level
+// kernels run costs three dependent launches (~25 us with nothing to do:
+// ~30 such levels per shard and C4 wakeup over 8 logical shards,
+// profiles/r5o).  Here each level is a pass over a global queue by all
+// workgroups (a chunk of WALK_T shadows per workgroup and step; light shadows
+// by their own thread, heavy ones' edges shared by the workgroup), claims by
+// atomicOr on the marked bitmap, new shadows appended to the next queue
+// (wave-aggregated), then a grid barrier.  It takes over where k_tail would
+// (the listed frontier of a narrow level), hands back to the level kernels as
+// k_tail does when a level finds more than tail_max shadows, and writes the
+// same controller state.  Every workgroup computes the takeover decision from
+// the same per-workgroup statistics, so all take the same path; WALK_WG is
+// far below one workgroup per CU, and every barrier wait is bounded (a
+// workgroup that never arrives — not resident — fails the mark with
+// ERR_WALK_STUCK instead of hanging the grid).
+// ---------------------------------------------------------------------------
+constexpr int WALK_WG = 64;
+constexpr int WALK_T = 256;
+constexpr uint32_t WALK_LIGHT = 16;
+
+// A load that reads the device-coherent value (past this CU's L1): what
+// other workgroups of the launch wrote before the last barrier.
+template <class T>
+__device__ inline T ld_agent(const T *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Grid barrier over the launch's workgroups: arrival counter, generation word.
+// Returns false when the wait ran out (every workgroup then leaves the walk).
+__device__ inline bool walk_sync(Counters *c, uint32_t nwg, uint32_t &gen) {
+  __shared__ uint32_t s_ok;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t ok = 1;
+    __threadfence();  // this workgroup's queue appends and claims, before the arrival
+    if (atomicAdd(&c->walk_bar, 1u) == nwg - 1) {
+      atomicExch(&c->walk_bar, 0u);
+      __threadfence();
+      atomicAdd(&c->walk_gen, 1u);
+    } else {
+      uint64_t k = 0;
+      while (__hip_atomic_load(&c->walk_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        if (++k > (1ull << 24) || __hip_atomic_load(&c->walk_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          ok = 0;
+          atomicExch(&c->walk_fail, 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __threadfence();  // the other workgroups' writes, after the wait
+    ++gen;
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+__global__ __launch_bounds__(WALK_T) void k_walk(DevGraph g, LevelArgs a) {
+  __shared__ unsigned long long s_red[2 * (WALK_T / 64)];
+  __shared__ uint32_t s_start[WALK_T + 1], s_off[WALK_T], s_w[40];
+  Counters *c = g.ctr;
+  const int L = a.level;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wg = blockIdx.x, nwg = gridDim.x;
+  // the level count and its frontier's out-edges, as k_tail sums them
+  unsigned long long pf = 0, pm = 0;
+  for (uint32_t b = tid; b < a.frontier_grid; b += WALK_T) {
+    pf += g.blkstat[b * 4 + STAT_FRONT];
+    pm += g.blkstat[b * 4 + STAT_MF];
+  }
+  if (c->tail_state) return;
+  for (int d = 32; d > 0; d >>= 1) {
+    pf += __shfl_xor(pf, d);
+    pm += __shfl_xor(pm, d);
+  }
+  if (lane == 0) {
+    s_red[tid >> 6] = pf;
+    s_red[WALK_T / 64 + (tid >> 6)] = pm;
+  }
+  __syncthreads();
+  uint64_t n0 = 0, mf = 0;
+  for (int k = 0; k < WALK_T / 64; ++k) {
+    n0 += s_red[k];
+    mf += s_red[WALK_T / 64 + k];
+  }
+  if (!listing_level(c, L, a) || n0 == 0 || n0 > a.tail_start) {
+    if (wg == 0 && tid == 0) {  // the level kernels go on
+      c->mf_level = mf;
+      c->mf_sum += mf;
+      c->ring[L % LEVEL_RING] = n0;
+      c->marked += n0;
+      c->qh[(L + 1) & 1] = 0;
+      if (n0 == 0) c->mark_done = 1;
+    }
+    return;
+  }
+  uint32_t gen = __hip_atomic_load(&c->walk_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t *qb[2] = {g.tq, g.tq + TAIL_QCAP};
+  uint8_t *Fn = g.front[(L + 1) & 1];  // k_frontier(L)'s supervisor pushes, redone here
+  uint8_t *Dn = g.dirty[(L + 1) & 1];
+  uint8_t *Fb = g.front[L & 1];        // bail: candidates of level L+2
+  uint8_t *Db = g.dirty[L & 1];
+  const bool investigate = a.flags & LV_INVESTIGATE;
+  // Take over: the listed frontier of level L into queue 0 (walk_n[0]); the
+  // other two counts zeroed for the first levels
+  {
+    if (wg == 0 && tid == 0) c->walk_n[1] = c->walk_n[2] = 0;
+    const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
+    const uint32_t want = (uint32_t)(L + 1);
+    for (uint64_t b = (uint64_t)wg * WALK_T + tid; b - tid < nblk; b += (uint64_t)nwg * WALK_T) {
+      const uint32_t t = b < nblk ? g.tl_tag[b] : 0u;
+      const uint32_t cnt = (t >> 12) == want ? (t & 0xFFFu) : 0u;
+      const uint32_t incl = wave_incl_scan(cnt), tot = __shfl(incl, 63);
+      unsigned long long at = 0;
+      if (lane == 63 && tot) at = atomicAdd(&c->walk_n[0], (unsigned long long)tot);
+      at = __shfl(at, 63) + incl - cnt;
+      for (uint32_t i = 0; i < cnt; ++i)
+        if (at + i < TAIL_QCAP) qb[0][at + i] = g.tl_buf[b * BLK_SLOTS + i];
+    }
+  }
+  bool ok = walk_sync(c, nwg, gen);
+  uint32_t claims = 0, n_sup = 0;
+  uint32_t r = 0;  // walk levels done
+  bool bailed = false;
+  uint64_t n_bail = 0;
+  for (; ok; ++r) {
+    const uint64_t n = min(ld_agent(&c->walk_n[r % 3]), (unsigned long long)TAIL_QCAP);
+    const uint32_t *cur = qb[r & 1];
+    uint32_t *nxt = qb[(r + 1) & 1];
+    unsigned long long *nn_ctr = &c->walk_n[(r + 1) % 3];
+    if (wg == 0 && tid == 0) c->walk_n[(r + 2) % 3] = 0;  // read at level r - 1, appended at r + 1
+    // chunks of WALK_T shadows, dealt to the workgroups
+    for (uint64_t c0 = (uint64_t)wg * WALK_T; c0 < n; c0 += (uint64_t)nwg * WALK_T) {
+      const uint64_t i = c0 + tid;
+      const bool have = i < n;
+      const uint32_t v = have ? ld_agent(&cur[i]) : 0u;
+      uint8_t f = 0;
+      uint2 ad = make_uint2(0, 0);
+      uint32_t supv = NO_SLOT;
+      if (have) {
+        f = g.flags[v];
+        ad = g.adj[v];
+        supv = investigate ? NO_SLOT : g.sup[v];
+      }
+      const bool expand = have && !(f & FL_HALTED);  // (:226-229)
+      if (!expand) ad = make_uint2(0, 0);
+      // targets: the supervisor (:258-267), the out-edges of a light shadow (:231-241)
+      uint32_t tg[WALK_LIGHT + 1];
+      uint32_t valid = 0;
+      tg[0] = 0;
+      if (expand && supv < 0xFFFFFFF0u) {
+        if (r == 0) {  // level L's supervisor pushes were made by k_frontier: undo them
+          Fn[supv] = 0;
+          Dn[supv >> 11] = 0;
+        } else {
+          ++n_sup;
+        }
+        tg[0] = supv;
+        valid = 1;
+      }
+      const bool light = ad.y <= WALK_LIGHT;
+#pragma unroll
+      for (uint32_t u = 0; u < WALK_LIGHT; ++u) {
+        const uint64_t ed = (light && u < ad.y) ? g.pool[(uint64_t)ad.x + u] : 0;
+        tg[u + 1] = edge_target(ed);
+        valid |= edge_count(ed) > 0 ? (2u << u) : 0u;
+      }
+      // claims: marked words together, then the atomics of the still unmarked
+      uint32_t w[WALK_LIGHT + 1];
+#pragma unroll
+      for (uint32_t k = 0; k <= WALK_LIGHT; ++k) w[k] = ((valid >> k) & 1u) ? g.vis[tg[k] >> 5] : ~0u;
+      uint32_t go = 0;
+#pragma unroll
+      for (uint32_t k = 0; k <= WALK_LIGHT; ++k) go |= ((w[k] >> (tg[k] & 31)) & 1u) ? 0u : (1u << k);
+      uint32_t mine = 0;  // claimed shadows (not proxies) of this thread, by target index
+#pragma unroll
+      for (uint32_t k = 0; k <= WALK_LIGHT; ++k)
+        if ((go >> k) & 1u) {
+          const uint32_t old = atomicOr(&g.vis[tg[k] >> 5], 1u << (tg[k] & 31));
+          if (!((old >> (tg[k] & 31)) & 1u) && tg[k] < g.pbase) mine |= 1u << k;
+        }
+      // append this thread's claims to the next queue (one atomic per wave)
+      {
+        const uint32_t cnt = __popc(mine);
+        const uint32_t incl = wave_incl_scan(cnt), tot = __shfl(incl, 63);
+        unsigned long long at = 0;
+        if (lane == 63 && tot) at = atomicAdd(nn_ctr, (unsigned long long)tot);
+        at = __shfl(at, 63) + incl - cnt;
+        for (uint32_t m = mine; m; m &= m - 1) {
+          const uint32_t k = __ffs(m) - 1;
+          if (at < TAIL_QCAP) {
+            nxt[at] = tg[k];
+            ++claims;
+          } else {  // no queue room: a candidate of the resume level instead (the level bails)
+            atomicAnd(&g.vis[tg[k] >> 5], ~(1u << (tg[k] & 31)));
+            Fb[tg[k]] = 1;
+            Db[tg[k] >> 11] = 1;
+          }
+          ++at;
+        }
+      }
+      // heavy shadows: the workgroup shares their edges
+      const bool heavy = expand && ad.y > WALK_LIGHT;
+      if (__syncthreads_or(heavy)) {
+        uint32_t total;
+        const uint32_t st = tail_scan_n<WALK_T>(heavy ? ad.y : 0u, s_w, total);
+        s_start[tid] = st;
+        s_off[tid] = ad.x;
+        __syncthreads();
+        for (uint32_t e0 = tid; e0 < total; e0 += WALK_T) {
+          int lo = 0, hi = WALK_T - 1;  // last item whose start <= e0
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_start[mid] <= e0) lo = mid;
+            else hi = mid - 1;
+          }
+          const uint64_t ed = g.pool[(uint64_t)s_off[lo] + (e0 - s_start[lo])];
+          const uint32_t t = edge_target(ed);
+          bool got = false;
+          if (edge_count(ed) > 0 && !((g.vis[t >> 5] >> (t & 31)) & 1u)) {
+            const uint32_t old = atomicOr(&g.vis[t >> 5], 1u << (t & 31));
+            got = !((old >> (t & 31)) & 1u) && t < g.pbase;
+          }
+          const uint64_t bal = __ballot(got);
+          unsigned long long at = 0;
+          if (lane == 0 && bal) at = atomicAdd(nn_ctr, (unsigned long long)__popcll(bal));
+          at = __shfl(at, 0) + __popcll(bal & lanemask_lt());
+          if (got) {
+            if (at < TAIL_QCAP) {
+              nxt[at] = t;
+              ++claims;
+            } else {
+              atomicAnd(&g.vis[t >> 5], ~(1u << (t & 31)));
+              Fb[t] = 1;
+              Db[t >> 11] = 1;
+            }
+          }
+        }
+        __syncthreads();  // s_start / s_off are rewritten by the next chunk
+      }
+    }
+    ok = walk_sync(c, nwg, gen);
+    if (!ok) break;
+    const uint64_t nn = ld_agent(&c->walk_n[(r + 1) % 3]);
+    if (nn == 0) {
+      ++r;
+      break;
+    }
+    if (nn > a.tail_max || nn > (uint64_t)TAIL_QCAP) {
+      // hand the pending shadows to the level kernels as level L+2 candidates
+      const uint64_t m = min(nn, (uint64_t)TAIL_QCAP);
+      for (uint64_t i = (uint64_t)wg * WALK_T + tid; i < m; i += (uint64_t)nwg * WALK_T) {
+        const uint32_t t = ld_agent(&nxt[i]);
+        atomicAnd(&g.vis[t >> 5], ~(1u << (t & 31)));
+        Fb[t] = 1;
+        Db[t >> 11] = 1;
+      }
+      bailed = true;
+      n_bail = m;
+      ++r;
+      break;
+    }
+  }
+  // totals, then the controller state (workgroup 0 after a last barrier)
+  {
+    uint32_t tc, ts;
+    const uint32_t x0 = tail_scan_n<WALK_T>(claims, s_w, tc);
+    const uint32_t x1 = tail_scan_n<WALK_T>(n_sup, s_w, ts);
+    (void)x0;
+    (void)x1;
+    if (tid == 0) {
+      if (tc) atomicAdd(&c->walk_claims, (unsigned long long)tc);
+      if (ts) atomicAdd(&c->walk_sup, (unsigned long long)ts);
+    }
+  }
+  const bool fin = walk_sync(c, nwg, gen) && ok;
+  if (wg != 0 || tid != 0) return;
+  if (!fin) {
+    set_err(c, ERR_WALK_STUCK);
+    c->tail_state = TAIL_DONE;  // the host reads the error word and fails the trace
+    c->mark_done = 1;
+    return;
+  }
+  const uint64_t claimed = ld_agent(&c->walk_claims), sup = ld_agent(&c->walk_sup);
+  c->walk_claims = c->walk_sup = 0;
+  c->ring[L % LEVEL_RING] = n0;
+  c->marked += n0 + claimed - (bailed ? n_bail : 0);  // queued claims undone by a bail
+  g.blkstat[STAT_SUP] += sup;
+  c->tail_from = L;
+  if (bailed) {
+    c->ring[L % LEVEL_RING] = 1;  // level L+2 runs sparse over the dirty blocks
+    c->ring[(L + 1) % LEVEL_RING] = n_bail;
+    c->qh[L & 1] = 0;
+    c->tail_level = L + 2;
+    c->tail_state = TAIL_BAILED;
+  } else {
+    c->tail_level = L + r;  // levels 0 .. L+r-1 were non-empty
+    c->tail_state = TAIL_DONE;
+    c->mark_done = 1;
+  }
+}
+
 int level_grid(uint64_t slot_top) {
   const uint64_t blocks = (slot_top + BLK_SLOTS - 1) / BLK_SLOTS;  // wave-blocks
   uint64_t wg = (blocks + 3) / 4;
@@ -1366,7 +1691,10 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
   else if (investigate) frontier(k_frontier<false, true>);
   else frontier(k_frontier<false, false>);
   // level controller: the level count, and the narrow-frontier takeover
-  hipExtLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, e[2], e[3], 0, g, a);
+  if (a.flags & LV_WALK)
+    hipExtLaunchKernelGGL(k_walk, dim3(WALK_WG), dim3(WALK_T), 0, s, e[2], e[3], 0, g, a);
+  else
+    hipExtLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, e[2], e[3], 0, g, a);
   // 8 WGs of 4 waves per CU
   if (roots && a.nbins) {
     // the pseudo-root level, binned when it is wide: place and apply, timed
