@@ -256,6 +256,7 @@ struct Knobs {
   // Sharded graphs: k_walk (WALK_WG workgroups) takes a mark round's narrow
   // levels over instead (CRGC_WALK=0: k_tail with the thresholds above).
   bool walk = true;              // CRGC_WALK
+  bool walk_unsharded = false;   // CRGC_WALK_UNSHARDED=1: k_walk for unsharded graphs too (no chain mode then)
   uint32_t walk_start = 16384;   // CRGC_WALK_START
   uint32_t walk_max = 32768;     // CRGC_WALK_MAX
   uint32_t chain_after = 64;     // CRGC_CHAIN_AFTER
@@ -313,6 +314,7 @@ struct Knobs {
     if (const char *m = env("CRGC_TAIL_START")) tail_start = tail_start_sharded = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_TAIL_MAX")) tail_max = tail_max_sharded = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_WALK")) walk = atoi(m) != 0;
+    if (const char *m = env("CRGC_WALK_UNSHARDED")) walk_unsharded = atoi(m) != 0;
     if (const char *m = env("CRGC_WALK_START")) walk_start = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_WALK_MAX")) walk_max = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_CHAIN_AFTER")) chain_after = (uint32_t)strtoul(m, nullptr, 10);
@@ -2103,7 +2105,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   // Narrow frontiers: one workgroup finishes the mark (k_tail), or in a
   // sharded graph WALK_WG of them (k_walk, to larger frontiers).
   if (kn.tail) la.flags |= LV_TAIL;
-  const bool walk = h->tp && kn.tail && kn.walk;
+  const bool walk = (h->tp || kn.walk_unsharded) && kn.tail && kn.walk;
   if (walk) la.flags |= LV_WALK;
   // Deep marks: a k_tail walk of chain_after links hands the rest to chain mode
   // (pointer jumping, crgc_chain.hip).  Unsharded graphs only.
