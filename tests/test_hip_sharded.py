@@ -325,13 +325,15 @@ def test_c4_shape_eight_shards(sharded, oracle_mod, xbits, xlevels, ratio, xfilt
     assert h.total_actors_seen() == o.total_actors_seen()
 
 
-@pytest.mark.parametrize("walk", [{"CRGC_WALK": "0"}, {"CRGC_WALK_START": "64", "CRGC_WALK_MAX": "128"},
-                                  {"CRGC_WALK_START": "65536", "CRGC_WALK_MAX": "65536"}])
+@pytest.mark.parametrize("walk", [{"CRGC_WALK": "1"},
+                                  {"CRGC_WALK": "1", "CRGC_WALK_START": "64", "CRGC_WALK_MAX": "128"},
+                                  {"CRGC_WALK": "1", "CRGC_WALK_START": "65536", "CRGC_WALK_MAX": "65536"}])
 def test_c4_shape_eight_shards_walk_forms(sharded, oracle_mod, walk, monkeypatch):
-    """A mark round's narrow levels by k_tail (one workgroup; CRGC_WALK=0) or by
-    k_walk (WALK_WG workgroups with grid barriers) taking over early and
-    bailing often (64 / 128) or taking every listed level up to its queue's
-    capacity: bit-exact against the unsharded oracle (G = 8, C4-shaped)."""
+    """A mark round's narrow levels by k_walk (WALK_WG workgroups with grid
+    barriers; off by default, the level kernels and k_tail run them): at its
+    default thresholds, taking over early and bailing often (64 / 128), or
+    taking every listed level up to its queue's capacity — bit-exact against
+    the unsharded oracle (G = 8, C4-shaped)."""
     for k, v in walk.items():
         monkeypatch.setenv(k, v)
     V = 100_000

@@ -236,7 +236,11 @@ Caps caps_create(uint64_t v0, uint64_t p0, bool proxies, uint64_t e0, uint32_t i
 struct Knobs {
   bool pull = true;              // CRGC_PULL=0: push only
   uint64_t pull_div = 16;        // CRGC_PULL_DIV: pull after a frontier of >= slots / div
-  uint32_t pull_cur_div = 4;     // CRGC_PULL_CUR_DIV
+  // (4 until round 5: on the C2 graph grown to 2.2e7 shadows level 1's
+  // frontier fell under a quarter of the slots and pushed its 6e7 edges in
+  // 0.83 ms where the pull took 0.24 ms; at 8, 2.65 -> 2.08 ms per wakeup there,
+  // profiles/r5r)
+  uint32_t pull_cur_div = 8;     // CRGC_PULL_CUR_DIV
   uint32_t alpha = 0;            // CRGC_ALPHA: Beamer's rule (off by default)
   bool has_pull_thresh = false;  // CRGC_PULL_THRESH: absolute threshold (test hook)
   uint64_t pull_thresh = 0;
@@ -253,9 +257,13 @@ struct Knobs {
   // CRGC_TAIL_MAX set both forms.
   uint32_t tail_start_sharded = 2048;
   uint32_t tail_max_sharded = 4096;
-  // Sharded graphs: k_walk (WALK_WG workgroups) takes a mark round's narrow
-  // levels over instead (CRGC_WALK=0: k_tail with the thresholds above).
-  bool walk = true;              // CRGC_WALK
+  // k_walk (WALK_WG workgroups with grid barriers) in place of k_tail for a
+  // sharded graph's narrow levels: correct, and slower as measured (C4 at half
+  // size over 8 logical shards 33.0 -> 36.4 ms per wakeup, GPU work 38.4 ->
+  // 39.3 ms: as the level controller it runs on every level, and a narrow
+  // level's hub leaves the other workgroups waiting at the barrier,
+  // profiles/r5r), so off by default (CRGC_WALK=1).
+  bool walk = false;             // CRGC_WALK
   bool walk_unsharded = false;   // CRGC_WALK_UNSHARDED=1: k_walk for unsharded graphs too (no chain mode then)
   uint32_t walk_start = 16384;   // CRGC_WALK_START
   uint32_t walk_max = 32768;     // CRGC_WALK_MAX
