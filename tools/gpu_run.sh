@@ -16,6 +16,7 @@
 #   c4l8 c2l8        C4 (at half size: 8 proxy-heavy shards of the full graph need > 288 GB) / C2 over
 #                    8 logical shards on the one GPU (the sharded protocol at scale)
 #   c2rs c4rs        the N>1 bench path itself on one rank (nccl group, RCCL transport, one shard)
+#   ktrs             kernel trace of c2rs
 #   ktl8             kernel trace of c4l8 (every shard's kernels, one process)
 #   ktl8s            ktl8 with every shard on one stream (--shared-stream): the shards' kernels run one at
 #                    a time, so each duration is the kernel's own and their sum is the GPU work per wakeup
@@ -81,6 +82,10 @@ for step in "$@"; do
     c2rs) (cd /tmp && timeout -k 10 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node=1 \
           --master-addr=127.0.0.1 --master-port=29517 "$ROOT/bench.py" --gpus 1 --workload c2 --rehearse-sharded \
           --steps 5 --warmup 2 --no-pcie > "$O/bench_c2rs.json" 2> "$O/bench_c2rs.err") ;;
+    ktrs) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ktrs" -o kt -- \
+          python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr=127.0.0.1 \
+          --master-port=29519 "$ROOT/bench.py" --gpus 1 --workload c2 --rehearse-sharded --steps 5 --warmup 2 \
+          --no-pcie --no-cpu-baseline > "$O/bench_ktrs.json" 2> "$O/bench_ktrs.err") ;;
     c4rs) (cd /tmp && timeout -k 10 1000 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node=1 \
           --master-addr=127.0.0.1 --master-port=29518 "$ROOT/bench.py" --gpus 1 --workload c4 --rehearse-sharded \
           --steps 3 --warmup 1 --no-pcie --no-cpu-baseline > "$O/bench_c4rs.json" 2> "$O/bench_c4rs.err") ;;
