@@ -49,7 +49,7 @@ void free_arrays(Arrays &a) {
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat, d.xbytes,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill,
                 d.nzdeg, d.radj, d.rnew, d.rpool, d.par, d.fx, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
-                d.xsent, d.xkey, d.rq_buf, d.rq_cnt, d.phs, d.psh};
+                d.xsent, d.xkey, d.wpc, d.rq_buf, d.rq_cnt, d.phs, d.psh};
   for (void *p : ps)
     if (p) hipFree(p);
   a.allocated = false;
@@ -118,6 +118,8 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   A(dmalloc(&d.par, c.scap));
   A(dmalloc(&d.fx, c.scap / 32));
   A(dmalloc(&d.tq, 2 * (uint64_t)TAIL_QCAP));
+  d.wpc_cap = (uint64_t)TAIL_QCAP + c.pcap / 256 + 1;  // (WALK_PIECE = 256 edges)
+  A(dmalloc(&d.wpc, d.wpc_cap));
   A(dmalloc(&d.tl_buf, c.scap));
   A(dmalloc(&d.tl_tag, c.scap / BLK_SLOTS));
   A(dmalloc(&d.cm, c.scap / 32));

@@ -162,6 +162,7 @@ struct Counters {
   // k_walk (the multi-workgroup narrow-frontier walk): queue lengths by level
   // mod 3, claims and supervisor edges, and its grid barrier
   unsigned long long walk_n[3];
+  unsigned long long walk_np[2];     // heavy shadows' edge pieces by level parity
   unsigned long long walk_claims, walk_sup;
   unsigned int walk_bar, walk_gen, walk_fail, walk_pad;
   unsigned long long ring[LEVEL_RING];
@@ -242,6 +243,8 @@ struct DevGraph {
   uint32_t n_shards, shard;
   uint32_t *xsent;    // 1 bit / slot (the proxy region's words): a marked proxy already exported
   uint8_t *xkey;      // 1 B / slot (proxies): the export key of a new mark (k_xscan)
+  uint2 *wpc;         // k_walk: a level's heavy-shadow edge pieces {offset, length}
+  uint64_t wpc_cap;   // TAIL_QCAP + pcap / WALK_PIECE: room for any level's pieces
   uint32_t *rq_buf;   // per-block regions: garbage slots whose kill waits on a remote mark
   uint32_t *rq_cnt;   // per block: listed requests
   uint32_t *phs;      // per proxy slot: its slot at the home shard (PHS_NONE / PHS_ABSENT)

@@ -1379,6 +1379,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
 constexpr int WALK_WG = 64;
 constexpr int WALK_T = 256;
 constexpr uint32_t WALK_LIGHT = 16;
+constexpr uint32_t WALK_PIECE = 256;  // edges of a heavy shadow's piece
 
 // A load that reads the device-coherent value (past this CU's L1): what
 // other workgroups of the launch wrote before the last barrier.
@@ -1466,7 +1467,7 @@ __global__ __launch_bounds__(WALK_T) void k_walk(DevGraph g, LevelArgs a) {
   // Take over: the listed frontier of level L into queue 0 (walk_n[0]); the
   // other two counts zeroed for the first levels
   {
-    if (wg == 0 && tid == 0) c->walk_n[1] = c->walk_n[2] = 0;
+    if (wg == 0 && tid == 0) c->walk_n[1] = c->walk_n[2] = c->walk_np[0] = c->walk_np[1] = 0;
     const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
     const uint32_t want = (uint32_t)(L + 1);
     for (uint64_t b = (uint64_t)wg * WALK_T + tid; b - tid < nblk; b += (uint64_t)nwg * WALK_T) {
@@ -1490,7 +1491,10 @@ __global__ __launch_bounds__(WALK_T) void k_walk(DevGraph g, LevelArgs a) {
     const uint32_t *cur = qb[r & 1];
     uint32_t *nxt = qb[(r + 1) & 1];
     unsigned long long *nn_ctr = &c->walk_n[(r + 1) % 3];
-    if (wg == 0 && tid == 0) c->walk_n[(r + 2) % 3] = 0;  // read at level r - 1, appended at r + 1
+    if (wg == 0 && tid == 0) {
+      c->walk_n[(r + 2) % 3] = 0;    // read at level r - 1, appended at r + 1
+      c->walk_np[(r + 1) & 1] = 0;   // read at level r - 1, appended at r + 1
+    }
     // chunks of WALK_T shadows, dealt to the workgroups
     for (uint64_t c0 = (uint64_t)wg * WALK_T; c0 < n; c0 += (uint64_t)nwg * WALK_T) {
       const uint64_t i = c0 + tid;
@@ -1561,44 +1565,65 @@ __global__ __launch_bounds__(WALK_T) void k_walk(DevGraph g, LevelArgs a) {
           ++at;
         }
       }
-      // heavy shadows: the workgroup shares their edges
-      const bool heavy = expand && ad.y > WALK_LIGHT;
-      if (__syncthreads_or(heavy)) {
-        uint32_t total;
-        const uint32_t st = tail_scan_n<WALK_T>(heavy ? ad.y : 0u, s_w, total);
-        s_start[tid] = st;
-        s_off[tid] = ad.x;
-        __syncthreads();
-        for (uint32_t e0 = tid; e0 < total; e0 += WALK_T) {
-          int lo = 0, hi = WALK_T - 1;  // last item whose start <= e0
-          while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_start[mid] <= e0) lo = mid;
-            else hi = mid - 1;
+      // heavy shadows: their edges as pieces of <= WALK_PIECE for every
+      // workgroup after the barrier (a hub walked by its own workgroup kept the
+      // others waiting at the barrier, profiles/r5r)
+      const uint32_t np = (expand && ad.y > WALK_LIGHT) ? (ad.y + WALK_PIECE - 1) / WALK_PIECE : 0u;
+      {
+        const uint32_t incl = wave_incl_scan(np), tot = __shfl(incl, 63);
+        unsigned long long at = 0;
+        if (lane == 63 && tot) at = atomicAdd(&c->walk_np[r & 1], (unsigned long long)tot);
+        at = __shfl(at, 63) + incl - np;
+        for (uint32_t k = 0; k < np; ++k, ++at)
+          if (at < g.wpc_cap)  // (always: a level has <= TAIL_QCAP shadows, pcap edges)
+            g.wpc[at] = make_uint2(ad.x + k * WALK_PIECE, min(WALK_PIECE, ad.y - k * WALK_PIECE));
+      }
+    }
+    ok = walk_sync(c, nwg, gen);
+    if (!ok) break;
+    {
+      // the pieces, one per wave at a time (4 edges per lane in flight)
+      const uint64_t npc = min(ld_agent(&c->walk_np[r & 1]), (unsigned long long)g.wpc_cap);
+      const uint64_t gwv = (uint64_t)wg * (WALK_T / 64) + (tid >> 6), nwv = (uint64_t)nwg * (WALK_T / 64);
+      for (uint64_t pi = gwv; pi < npc; pi += nwv) {
+        const unsigned long long raw = ld_agent(reinterpret_cast<const unsigned long long *>(g.wpc + pi));
+        const uint2 pc = make_uint2((uint32_t)raw, (uint32_t)(raw >> 32));
+        for (uint32_t e0 = 0; e0 < pc.y; e0 += 256) {
+          uint32_t t[4];
+          bool go[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t e = e0 + u * 64 + lane;
+            const uint64_t ed = e < pc.y ? g.pool[(uint64_t)pc.x + e] : 0ull;
+            t[u] = edge_target(ed);
+            go[u] = edge_count(ed) > 0;
           }
-          const uint64_t ed = g.pool[(uint64_t)s_off[lo] + (e0 - s_start[lo])];
-          const uint32_t t = edge_target(ed);
-          bool got = false;
-          if (edge_count(ed) > 0 && !((g.vis[t >> 5] >> (t & 31)) & 1u)) {
-            const uint32_t old = atomicOr(&g.vis[t >> 5], 1u << (t & 31));
-            got = !((old >> (t & 31)) & 1u) && t < g.pbase;
-          }
-          const uint64_t bal = __ballot(got);
-          unsigned long long at = 0;
-          if (lane == 0 && bal) at = atomicAdd(nn_ctr, (unsigned long long)__popcll(bal));
-          at = __shfl(at, 0) + __popcll(bal & lanemask_lt());
-          if (got) {
-            if (at < TAIL_QCAP) {
-              nxt[at] = t;
-              ++claims;
-            } else {
-              atomicAnd(&g.vis[t >> 5], ~(1u << (t & 31)));
-              Fb[t] = 1;
-              Db[t >> 11] = 1;
+          uint32_t w4[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) w4[u] = go[u] ? g.vis[t[u] >> 5] : ~0u;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            bool got = false;
+            if (go[u] && !((w4[u] >> (t[u] & 31)) & 1u)) {
+              const uint32_t old = atomicOr(&g.vis[t[u] >> 5], 1u << (t[u] & 31));
+              got = !((old >> (t[u] & 31)) & 1u) && t[u] < g.pbase;
+            }
+            const uint64_t bal = __ballot(got);
+            unsigned long long at = 0;
+            if (lane == 0 && bal) at = atomicAdd(nn_ctr, (unsigned long long)__popcll(bal));
+            at = __shfl(at, 0) + __popcll(bal & lanemask_lt());
+            if (got) {
+              if (at < TAIL_QCAP) {
+                nxt[at] = t[u];
+                ++claims;
+              } else {
+                atomicAnd(&g.vis[t[u] >> 5], ~(1u << (t[u] & 31)));
+                Fb[t[u]] = 1;
+                Db[t[u] >> 11] = 1;
+              }
             }
           }
         }
-        __syncthreads();  // s_start / s_off are rewritten by the next chunk
       }
     }
     ok = walk_sync(c, nwg, gen);
