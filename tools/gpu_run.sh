@@ -82,10 +82,10 @@ for step in "$@"; do
     c2rs) (cd /tmp && timeout -k 10 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node=1 \
           --master-addr=127.0.0.1 --master-port=29517 "$ROOT/bench.py" --gpus 1 --workload c2 --rehearse-sharded \
           --steps 5 --warmup 2 --no-pcie > "$O/bench_c2rs.json" 2> "$O/bench_c2rs.err") ;;
-    ktrs) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ktrs" -o kt -- \
-          python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr=127.0.0.1 \
-          --master-port=29519 "$ROOT/bench.py" --gpus 1 --workload c2 --rehearse-sharded --steps 5 --warmup 2 \
-          --no-pcie --no-cpu-baseline > "$O/bench_ktrs.json" 2> "$O/bench_ktrs.err") ;;
+    ktrs) (cd /tmp && MASTER_ADDR=127.0.0.1 MASTER_PORT=29519 RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 \
+          timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ktrs" -o kt -- \
+          python3 -u "$ROOT/bench.py" --gpus 1 --workload c2 --rehearse-sharded --steps 5 --warmup 2 \
+          --no-pcie --no-cpu-baseline > "$O/bench_ktrs.json" 2> "$O/bench_ktrs.err") ;;  # (the rank itself, no launcher)
     c4rs) (cd /tmp && timeout -k 10 1000 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node=1 \
           --master-addr=127.0.0.1 --master-port=29518 "$ROOT/bench.py" --gpus 1 --workload c4 --rehearse-sharded \
           --steps 3 --warmup 1 --no-pcie --no-cpu-baseline > "$O/bench_c4rs.json" 2> "$O/bench_c4rs.err") ;;
