@@ -82,9 +82,39 @@ int LocalTransport::barrier() {
 // hipMemcpyDefault form looks both pointers up in the runtime's allocation map
 // (under rocprofv3's API interception two such lookups from shard threads
 // faulted inside the runtime, profiles/r5n/README.md).
+int LocalTransport::events(uint32_t shard) {
+  Post &p = post[shard];
+  if (!p.ready && hipEventCreateWithFlags(&p.ready, hipEventDisableTiming) != hipSuccess) return DEV_FAIL("transport");
+  if (!p.done && hipEventCreateWithFlags(&p.done, hipEventDisableTiming) != hipSuccess) return DEV_FAIL("transport");
+  return CRGC_OK;
+}
+
+// A collective in stream order, with no host wait (round 4 waited for the
+// stream before posting and after copying: two host round trips per collective
+// and shard, most of the logical-shard runs' exchange time): the shard records
+// `ready` behind its send buffer's producers, every shard's stream waits for
+// every peer's `ready` before its copy kernel and records `done` after it, and
+// after the second rendezvous every stream waits for every peer's `done`, so
+// no later work of a shard's stream overwrites a buffer a peer still reads.
+// (The host threads only rendezvous: an event is waited for by the peers only
+// after its record was enqueued, and recorded again only after every peer has
+// enqueued that wait.)
+int LocalTransport::collect(uint32_t shard, const Segs &sg, hipStream_t s) {
+  for (uint32_t r = 0; r < n_shards; ++r)
+    if (r != shard && hipStreamWaitEvent(s, post[r].ready, 0) != hipSuccess) return DEV_FAIL("transport");
+  (void)hipGetLastError();  // (a soft status of an earlier call is not this launch's)
+  if (copy_segs(sg, s) != hipSuccess) return DEV_FAIL("transport");
+  if (hipEventRecord(post[shard].done, s) != hipSuccess) return DEV_FAIL("transport");
+  if (int rc = barrier()) return rc;
+  for (uint32_t r = 0; r < n_shards; ++r)
+    if (r != shard && hipStreamWaitEvent(s, post[r].done, 0) != hipSuccess) return DEV_FAIL("transport");
+  return CRGC_OK;
+}
+
 int LocalTransport::allgather(uint32_t shard, const void *send, void *recv, size_t bytes,
                               hipStream_t s) {
-  if (stream_wait(s) != hipSuccess) return DEV_FAIL("transport");  // send is complete
+  if (int rc = events(shard)) return rc;
+  if (hipEventRecord(post[shard].ready, s) != hipSuccess) return DEV_FAIL("transport");  // send's producers
   post[shard].ptr = send;
   if (int rc = barrier()) return rc;
   Segs sg{};
@@ -93,16 +123,14 @@ int LocalTransport::allgather(uint32_t shard, const void *send, void *recv, size
     sg.dst[sg.count] = (char *)recv + (size_t)r * bytes;
     sg.n[sg.count++] = bytes;
   }
-  (void)hipGetLastError();  // (a soft status of an earlier call is not this launch's)
-  if (copy_segs(sg, s) != hipSuccess) return DEV_FAIL("transport");
-  if (stream_wait(s) != hipSuccess) return DEV_FAIL("transport");
-  return barrier();  // nobody reuses its send buffer before every peer has copied it
+  return collect(shard, sg, s);
 }
 
 int LocalTransport::alltoallv(uint32_t shard, const void *send, const size_t *soff, const size_t *sbytes,
                               void *recv, const size_t *roff, const size_t *rbytes, hipStream_t s) {
   (void)sbytes;
-  if (stream_wait(s) != hipSuccess) return DEV_FAIL("transport");
+  if (int rc = events(shard)) return rc;
+  if (hipEventRecord(post[shard].ready, s) != hipSuccess) return DEV_FAIL("transport");
   post[shard].ptr = send;
   post[shard].soff = soff;
   if (int rc = barrier()) return rc;
@@ -113,10 +141,7 @@ int LocalTransport::alltoallv(uint32_t shard, const void *send, const size_t *so
     sg.dst[sg.count] = (char *)recv + roff[r];
     sg.n[sg.count++] = rbytes[r];
   }
-  (void)hipGetLastError();  // (a soft status of an earlier call is not this launch's)
-  if (copy_segs(sg, s) != hipSuccess) return DEV_FAIL("transport");
-  if (stream_wait(s) != hipSuccess) return DEV_FAIL("transport");
-  return barrier();
+  return collect(shard, sg, s);  // (peers read post[*].soff before the second rendezvous)
 }
 
 // ---- RcclTransport -------------------------------------------------------------

@@ -46,11 +46,17 @@ namespace crgc {
 
 constexpr uint32_t TRANSPORT_MAX_SHARDS = 64;
 
+struct Segs;  // a collective's copies (crgc_transport.hip)
+
 // One process, one host thread per shard.
 struct LocalTransport final : crgc_transport {
   struct Post {
     const void *ptr = nullptr;
     const size_t *soff = nullptr;
+    // stream order across the shards' streams, without host waits: `ready`
+    // recorded behind the send buffer's producers, `done` behind this shard's
+    // copies out of its peers' buffers (created by the shard's own thread)
+    hipEvent_t ready = nullptr, done = nullptr;
   };
   std::mutex m;
   std::condition_variable cv;
@@ -69,6 +75,14 @@ struct LocalTransport final : crgc_transport {
   }
   bool accepts(uint32_t shard, int) const override { return shard < n_shards; }
   int barrier();
+  int events(uint32_t shard);  // the shard's two events, created on first use
+  int collect(uint32_t shard, const Segs &sg, hipStream_t s);
+  ~LocalTransport() override {
+    for (uint32_t r = 0; r < TRANSPORT_MAX_SHARDS; ++r) {
+      if (post[r].ready) hipEventDestroy(post[r].ready);
+      if (post[r].done) hipEventDestroy(post[r].done);
+    }
+  }
   int allgather(uint32_t shard, const void *send, void *recv, size_t bytes, hipStream_t s) override;
   int alltoallv(uint32_t shard, const void *send, const size_t *soff, const size_t *sbytes, void *recv,
                 const size_t *roff, const size_t *rbytes, hipStream_t s) override;
