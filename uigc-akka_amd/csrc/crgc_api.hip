@@ -2571,7 +2571,7 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
   for (uint32_t d = 0; d < G; ++d) gwords += words(d);
   for (;;) {
     const auto t0 = std::chrono::steady_clock::now();
-    HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(xcnt), 0, 4 * MAX_SHARDS * 8, h->stream));
+    HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(xcnt), 0, 3 * MAX_SHARDS * 8, h->stream));  // xcnt .. xcnt2
     XSend xs{};
     xs.use_slots = xmode != 0;
     if (xmode != 0 && h->knobs.xfilter && prev_total >= gwords && gwords) {

@@ -158,7 +158,6 @@ struct Counters {
   unsigned long long xcnt[MAX_SHARDS];  // ids to send per destination shard
   unsigned long long xpos[MAX_SHARDS];  // scatter cursors
   unsigned long long xcnt2[MAX_SHARDS]; // mark rounds: home slots to send per destination
-  unsigned long long xpos2[MAX_SHARDS]; // their scatter cursors
   // k_walk (the multi-workgroup narrow-frontier walk): queue lengths by level
   // mod 3, claims and supervisor edges, and its grid barrier
   unsigned long long walk_n[3];

@@ -2252,27 +2252,10 @@ hipError_t launch_resolve(const DevGraph &g, int step, uint64_t mask, uint64_t *
 // per load group.  The count pass derives each new mark's key (form << 6 |
 // destination; 0xFF: none — its home is marked already) from the home shard,
 // the home slot and the replicated home bitmaps, stores it as a byte and leaves
-// its workgroup's count per key in `wgc`; the scatter pass (same grid, so the
-// same blocks per workgroup) reserves each key's range from those counts and
-// reads the key bytes back, so the random bitmap probes run once.
-// The proxies marked since the last export (marked, not yet sent: vis &
-// ~xsent over the proxy region), by destination: ids of the unresolved (xcnt),
-// home slots of the resolved (xcnt2); then the scatter into the byte layout the
-// host derived from the all-gathered counts, which records them as sent.  A
-// streaming pass over the region's marked / sent words and, for the new marks
-// only, their home shards and home slots (round 4 listed marked proxies into
-// per-block regions as the level kernels found them and packed the lists: a
-// chain of dependent loads per entry, ~0.8 ms per shard for C4's first round
-// over 8 logical shards).
-// One wave per 2048-proxy block: lane l holds the block's words l (marked and
-// sent); step k covers slots 64k .. 64k+63 (slot 64k + l: word 2k + l / 32,
-// bit l % 32, by one shuffle), so the loads of a step are coalesced; XU steps
-// per load group.  The count pass derives each new mark's key (form << 6 |
-// destination; 0xFF: none — its home is marked already) from the home shard,
-// the home slot and the replicated home bitmaps, stores it as a byte and leaves
-// its workgroup's count per key in `wgc`; the scatter pass (same grid, so the
-// same blocks per workgroup) reserves each key's range from those counts and
-// reads the key bytes back, so the random bitmap probes run once.
+// its workgroup's count per key in `wgc`; k_xscan_sum turns those into each
+// workgroup's run of each segment (an exclusive scan), and the scatter pass
+// (same grid, so the same blocks per workgroup) reads the key bytes back, so
+// the random bitmap probes run once.
 template <bool SCATTER>
 __global__ __launch_bounds__(256) void k_xscan(DevGraph g, char *send, XSend x, uint32_t *wgc) {
   __shared__ uint32_t hist[2 * MAX_SHARDS];
