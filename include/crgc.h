@@ -102,6 +102,24 @@ int crgc_transport_rccl(const uint8_t id[128], uint32_t n_shards, uint32_t shard
 /* One process, G shards (possibly on one GPU), one host thread per shard:
  * device-to-device copies.  Shared by the G handles. */
 int crgc_transport_local(uint32_t n_shards, crgc_transport **out);
+/* One process per shard, the bytes moved by the caller's own collectives over
+ * host memory (e.g. torch.distributed gloo, MPI, the JVM's cluster messaging):
+ * the transport stages each exchange in pinned host buffers and calls back on
+ * the calling thread.  Every callback returns 0 on success; any other value
+ * fails the exchange (CRGC_E_DEVICE, the handle poisoned).  For shards that
+ * cannot share a GPU communicator (two ranks on one GPU) and for parity tests
+ * of the multi-process protocol; RCCL is the transport for speed. */
+typedef struct crgc_host_collectives {
+  void *ctx;
+  /* recv[r*bytes .. (r+1)*bytes) = shard r's send[0 .. bytes) */
+  int (*allgather)(void *ctx, uint32_t shard, const void *send, void *recv, size_t bytes);
+  /* send[soff[r] .. +sbytes[r]) goes to shard r; recv[roff[r] .. +rbytes[r])
+   * gets shard r's block for this shard (rbytes[r] = r's sbytes[shard]) */
+  int (*alltoallv)(void *ctx, uint32_t shard, const void *send, const size_t *soff, const size_t *sbytes,
+                   void *recv, const size_t *roff, const size_t *rbytes);
+} crgc_host_collectives;
+int crgc_transport_host(const crgc_host_collectives *c, uint32_t n_shards, uint32_t shard, int32_t device,
+                        crgc_transport **out);
 /* Destroy after every handle using it. */
 void crgc_transport_destroy(crgc_transport *t);
 /* Home shard of an actor id. */

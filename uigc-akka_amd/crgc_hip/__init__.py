@@ -6,8 +6,8 @@ ShadowGraph surface (ShadowGraph.java), bound through ctypes.
 """
 from . import abi
 from .batch import Entry, EntryBatch, DeltaBatch, UndoBatch, TraceResult, RefobInfo, GraphState, HostArena
-from .graph import ShadowGraph, ShardedShadowGraph, Transport, UndoAccumulator, shard_of
+from .graph import HostCollectives, ShadowGraph, ShardedShadowGraph, Transport, UndoAccumulator, shard_of
 
 __all__ = ["abi", "Entry", "EntryBatch", "HostArena", "DeltaBatch", "UndoBatch", "TraceResult", "RefobInfo",
-           "GraphState", "ShadowGraph", "ShardedShadowGraph", "Transport", "UndoAccumulator",
+           "GraphState", "HostCollectives", "ShadowGraph", "ShardedShadowGraph", "Transport", "UndoAccumulator",
            "shard_of"]

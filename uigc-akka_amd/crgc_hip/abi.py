@@ -197,6 +197,16 @@ class CrgcUndoLogOut(C.Structure):
     ]
 
 
+# crgc_host_collectives (include/crgc.h): the caller's host collectives
+HOST_ALLGATHER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_size_t)
+HOST_ALLTOALLV = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.POINTER(C.c_size_t),
+                             C.POINTER(C.c_size_t), C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t))
+
+
+class HostCollectives(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("allgather", HOST_ALLGATHER), ("alltoallv", HOST_ALLTOALLV)]
+
+
 # Entry points declared in include/crgc.h — every one must be exported.
 EXPORTED_SYMBOLS = (
     "crgc_create",
@@ -226,6 +236,7 @@ EXPORTED_SYMBOLS = (
     "crgc_transport_rccl_id",
     "crgc_transport_rccl",
     "crgc_transport_local",
+    "crgc_transport_host",
     "crgc_transport_destroy",
     "crgc_shard_of",
     "crgc_host_register",
@@ -293,6 +304,10 @@ def load_library(path: str | None = None) -> C.CDLL:
                                         C.POINTER(_P)]
     lib.crgc_transport_local.restype = C.c_int
     lib.crgc_transport_local.argtypes = [C.c_uint32, C.POINTER(_P)]
+    if hasattr(lib, "crgc_transport_host"):
+        lib.crgc_transport_host.restype = C.c_int
+        lib.crgc_transport_host.argtypes = [C.POINTER(HostCollectives), C.c_uint32, C.c_uint32, C.c_int32,
+                                            C.POINTER(_P)]
     lib.crgc_transport_destroy.restype = None
     lib.crgc_transport_destroy.argtypes = [_P]
     lib.crgc_shard_of.restype = C.c_uint32

@@ -441,10 +441,72 @@ class Transport:
                          "crgc_transport_rccl")
         return cls(t, lib)
 
+    @classmethod
+    def host(cls, collectives: "HostCollectives", device: int) -> "Transport":
+        """crgc_transport_host: this process's shard over host collectives
+        (`collectives`, e.g. GlooCollectives: torch.distributed over gloo)."""
+        lib = abi.load_library()
+        t = C.c_void_p()
+        ShadowGraph._chk(lib.crgc_transport_host(C.byref(collectives.c), collectives.n_shards,
+                                                 collectives.shard, device, C.byref(t)), "crgc_transport_host")
+        tr = cls(t, lib)
+        tr._keep = collectives  # the callbacks must outlive the transport
+        return tr
+
     def close(self):
         if self.t:
             self.lib.crgc_transport_destroy(self.t)
             self.t = None
+
+
+class HostCollectives:
+    """The callbacks of crgc_transport_host over torch.distributed (any
+    backend with all_gather_into_tensor / all_to_all_single on CPU tensors:
+    gloo).  Buffers are the transport's pinned host staging; the callbacks run
+    on the thread that called into the graph."""
+
+    def __init__(self, n_shards: int, shard: int, group=None):
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+        self.n_shards, self.shard, self.group = n_shards, shard, group
+        np_, torch_, dist_ = np, torch, dist
+
+        def view(addr, n):
+            return np_.ctypeslib.as_array((C.c_uint8 * max(int(n), 1)).from_address(addr))[:int(n)]
+
+        def allgather(_ctx, _shard, send, recv, nbytes):
+            try:
+                src = torch_.from_numpy(view(send, nbytes).copy())
+                out = torch_.empty(int(nbytes) * n_shards, dtype=torch_.uint8)
+                dist_.all_gather_into_tensor(out, src, group=self.group)
+                view(recv, int(nbytes) * n_shards)[:] = out.numpy()
+                return 0
+            except Exception:  # noqa: BLE001 — a failed exchange fails the call, not the process
+                return 1
+
+        def alltoallv(_ctx, _shard, send, soff, sbytes, recv, roff, rbytes):
+            try:
+                sb = [int(sbytes[r]) for r in range(n_shards)]
+                rb = [int(rbytes[r]) for r in range(n_shards)]
+                sn = max([int(soff[r]) + sb[r] for r in range(n_shards) if sb[r]] or [0])
+                rn = max([int(roff[r]) + rb[r] for r in range(n_shards) if rb[r]] or [0])
+                sv = view(send, sn)
+                inp = torch_.from_numpy(np_.concatenate(
+                    [sv[int(soff[r]):int(soff[r]) + sb[r]] for r in range(n_shards)] or [np_.zeros(0, np_.uint8)]))
+                out = torch_.empty(sum(rb), dtype=torch_.uint8)
+                dist_.all_to_all_single(out, inp, rb, sb, group=self.group)
+                rv, o, at = view(recv, rn), out.numpy(), 0
+                for r in range(n_shards):
+                    rv[int(roff[r]):int(roff[r]) + rb[r]] = o[at:at + rb[r]]
+                    at += rb[r]
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+
+        self._ag = abi.HOST_ALLGATHER(allgather)
+        self._a2a = abi.HOST_ALLTOALLV(alltoallv)
+        self.c = abi.HostCollectives(None, self._ag, self._a2a)
 
 
 def shard_of(actor_id: int, n_shards: int) -> int:

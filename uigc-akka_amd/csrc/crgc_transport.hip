@@ -221,6 +221,61 @@ struct RcclTransport final : crgc_transport {
   }
 };
 
+// ---- HostTransport -------------------------------------------------------------
+// One process per shard, the exchange done by the caller's host collectives:
+// every collective copies this shard's bytes to pinned host memory, calls
+// back, and copies what arrived to the device (stream waits on both sides, so
+// the host buffers are free again when the call returns).
+struct HostTransport final : crgc_transport {
+  crgc_host_collectives cb{};
+  uint32_t rank = 0;
+  int device = 0;
+  void *hs = nullptr, *hr = nullptr;
+  size_t hs_bytes = 0, hr_bytes = 0;
+  ~HostTransport() override {
+    if (hs) hipHostFree(hs);
+    if (hr) hipHostFree(hr);
+  }
+  bool accepts(uint32_t shard, int dev) const override { return shard == rank && dev == device; }
+  static bool grow(void *&p, size_t &have, size_t need) {
+    if (need <= have) return true;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    have = 0;
+    const size_t sz = need + need / 4 + 4096;
+    if (hipHostMalloc(&p, sz, hipHostMallocDefault) != hipSuccess) return false;
+    have = sz;
+    return true;
+  }
+  int allgather(uint32_t, const void *send, void *recv, size_t bytes, hipStream_t s) override {
+    if (!bytes) return CRGC_OK;
+    if (!grow(hs, hs_bytes, bytes) || !grow(hr, hr_bytes, bytes * n_shards)) return CRGC_E_NOMEM;
+    if (hipMemcpyAsync(hs, send, bytes, hipMemcpyDeviceToHost, s) != hipSuccess || stream_wait(s) != hipSuccess)
+      return DEV_FAIL("transport: staging");
+    if (cb.allgather(cb.ctx, rank, hs, hr, bytes) != 0) return DEV_FAIL("transport: host all-gather");
+    if (hipMemcpyAsync(recv, hr, bytes * n_shards, hipMemcpyHostToDevice, s) != hipSuccess ||
+        stream_wait(s) != hipSuccess)
+      return DEV_FAIL("transport: staging");
+    return CRGC_OK;
+  }
+  int alltoallv(uint32_t, const void *send, const size_t *soff, const size_t *sbytes, void *recv,
+                const size_t *roff, const size_t *rbytes, hipStream_t s) override {
+    size_t sn = 0, rn = 0;
+    for (uint32_t r = 0; r < n_shards; ++r) {
+      if (sbytes[r]) sn = std::max(sn, soff[r] + sbytes[r]);
+      if (rbytes[r]) rn = std::max(rn, roff[r] + rbytes[r]);
+    }
+    if (!grow(hs, hs_bytes, sn + 1) || !grow(hr, hr_bytes, rn + 1)) return CRGC_E_NOMEM;
+    if (sn && (hipMemcpyAsync(hs, send, sn, hipMemcpyDeviceToHost, s) != hipSuccess || stream_wait(s) != hipSuccess))
+      return DEV_FAIL("transport: staging");
+    if (cb.alltoallv(cb.ctx, rank, hs, soff, sbytes, hr, roff, rbytes) != 0)
+      return DEV_FAIL("transport: host all-to-all");
+    if (rn && (hipMemcpyAsync(recv, hr, rn, hipMemcpyHostToDevice, s) != hipSuccess || stream_wait(s) != hipSuccess))
+      return DEV_FAIL("transport: staging");
+    return CRGC_OK;
+  }
+};
+
 int rccl_unique_id(uint8_t id[128]) {
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
   ncclUniqueId u;
@@ -279,6 +334,21 @@ int crgc_transport_rccl(const uint8_t id[128], uint32_t n_shards, uint32_t shard
   int rc = CRGC_OK;
   *out = crgc::make_rccl_transport(id, n_shards, shard, device, &rc);
   return rc;
+}
+
+int crgc_transport_host(const crgc_host_collectives *c, uint32_t n_shards, uint32_t shard, int32_t device,
+                        crgc_transport **out) {
+  if (!out || !c || !c->allgather || !c->alltoallv || n_shards < 1 || n_shards > crgc::TRANSPORT_MAX_SHARDS ||
+      shard >= n_shards)
+    return CRGC_E_INVAL;
+  crgc::HostTransport *t = new (std::nothrow) crgc::HostTransport();
+  if (!t) return CRGC_E_NOMEM;
+  t->cb = *c;
+  t->n_shards = n_shards;
+  t->rank = shard;
+  t->device = device;
+  *out = t;
+  return CRGC_OK;
 }
 
 void crgc_transport_destroy(crgc_transport *t) { delete t; }
