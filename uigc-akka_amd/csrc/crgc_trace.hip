@@ -159,10 +159,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   const bool lane_pull = pull && !listing && !sharded && !a.alpha;
   uint32_t n_front = 0, n_sup = 0, n_edges = 0;
 
-  // (a sparse level's candidates are shadows only: pushes before it mark
-  // proxies at once, so its scan skips the proxy region)
-  const uint32_t nvb = sp_cur ? vbs.nh : vbs.n;
-  for (uint32_t vb = gw; vb < nvb; vb += nw) {
+  for (uint32_t vb = gw; vb < vbs.n; vb += nw) {
     const uint32_t blk = vbs.at(vb);
     if (sp_cur && Dc[blk] == 0) continue;
     const uint64_t base = (uint64_t)blk * BLK_SLOTS + (uint64_t)lane * 32;
@@ -343,12 +340,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
           n_sup++;
           const uint32_t s = sp[b];
           if (!((sw[b] >> (s & 31)) & 1u)) {
-            if (sp_next && s >= g.pbase) {  // a proxy before a sparse level: marked at once (expand_edges)
-              atomicOr(&g.vis[s >> 5], 1u << (s & 31));
-            } else {
-              Fn[s] = 1;
-              if (sp_next) Dn[s >> 11] = 1;  // blind: no dependent read
-            }
+            Fn[s] = 1;
+            if (sp_next) Dn[s >> 11] = 1;  // blind: no dependent read
           }
         }
         const uint32_t len = ad[b].y;
@@ -402,27 +395,15 @@ __device__ inline void expand_edges(const DevGraph &g, uint8_t *Fn, uint8_t *Dn,
     t[u] = edge_target(ed[u]);
     go[u] = edge_count(ed[u]) > 0 && ((t[u] >> 11) & smask) == slice;
   }
-  if (!sp_next) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      nb += go[u] ? 1 : 0;
-      if (go[u]) Fn[t[u]] = 1;
-    }
-    return;
-  }
-  // a sparse next level: a proxy target (sharded graphs; never below pbase) is
-  // marked at once, so sparse k_frontier levels never scan the proxy region;
-  // a shadow gets its candidate byte and its block's dirty byte, stored blind
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     nb += go[u] ? 1 : 0;
-    if (!go[u]) continue;
-    if (t[u] >= g.pbase) {
-      atomicOr(&g.vis[t[u] >> 5], 1u << (t[u] & 31));
-    } else {
-      Fn[t[u]] = 1;
-      Dn[t[u] >> 11] = 1;
-    }
+    if (go[u]) Fn[t[u]] = 1;
+  }
+  if (sp_next) {  // the block's dirty byte, stored blind like the candidate byte
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (go[u]) Dn[t[u] >> 11] = 1;
   }
 }
 
