@@ -25,6 +25,12 @@ VARIANTS = [
     {"CRGC_TAIL_START": "1000000", "CRGC_TAIL_MAX": "64"},  # early takeover, frequent bails
     {"CRGC_BIN_MIN_SLOTS": "0"},          # the pseudo-root level binned at this size too
     {"CRGC_BIN": "0"},                    # the pseudo-root level's direct push
+    {"CRGC_CBITS": "0"},                  # a pull level's finds as candidate bytes (round-4 form)
+    {"CRGC_ROOTS_CO": "0"},               # the pseudo-root pass's per-lane 128-B count loads
+    {"CRGC_PULL_PRED": "1"},              # the previous trace's pull levels pull again
+    {"CRGC_BIN512": "0", "CRGC_BIN_MIN_SLOTS": "0"},  # binned level 0 with at most 256 bins
+    # candidate bits after every pull (level 0 included) with frequent k_tail bails
+    {"CRGC_ALPHA": "1000000", "CRGC_TAIL_START": "1000000", "CRGC_TAIL_MAX": "64"},
 ]
 
 

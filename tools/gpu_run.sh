@@ -110,6 +110,17 @@ for step in "$@"; do
           -d "$O/kt2l8s" -o kt -- python3 -u "$ROOT/bench.py" --workload c2 --logical-shards 8 --shared-stream \
           --no-cpu-baseline \
           --steps 4 --warmup 2 > "$O/bench_kt2l8s.json" 2> "$O/bench_kt2l8s.err") ;;
+    lv:*)  # per-level kernel times (all three level kernels timed) over env variants, two passes
+      read -ra vs <<< "${step#*:}"
+      for pass in 1 2; do
+        for v in "${vs[@]}"; do
+          envs=(CRGC_TEST_HOOKS=1 CRGC_LEVEL_LOG=1 CRGC_KERNEL_TIMING=2)
+          [ "$v" != "BASE" ] && IFS=',' read -ra ev <<< "$v" && envs+=("${ev[@]}")
+          f="$O/lv_p${pass}_$(echo "$v" | tr '=,/' '___')"
+          (cd /tmp && env "${envs[@]}" timeout -k 10 300 $B > "$f.json" 2> "$f.err")
+          { echo "== pass $pass $v"; python3 "$ROOT/tools/lv_summary.py" "$f.err" 3; } >> "$O/lv_summary.txt"
+        done
+      done ;;
     ab:*)  # tools/ab_bench.sh (C2 N = 1) over the variants after the colon (separated by spaces)
       read -ra vs <<< "${step#*:}"
       (cd "$ROOT" && bash tools/ab_bench.sh "$TAG/ab_c2" "${vs[@]}" > /dev/null) ;;

@@ -48,7 +48,7 @@ void free_arrays(Arrays &a) {
                 d.pool, d.etab, d.vis, d.front[0], d.front[1],
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat, d.xbytes,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill,
-                d.nzdeg, d.radj, d.rnew, d.rpool, d.par, d.fx, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
+                d.nzdeg, d.radj, d.rnew, d.rpool, d.par, d.fx, d.cb, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
                 d.xsent, d.xkey, d.wpc, d.rq_buf, d.rq_cnt, d.phs, d.psh};
   for (void *p : ps)
     if (p) hipFree(p);
@@ -117,6 +117,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   A(dmalloc(&d.rpool, d.rpcap));
   A(dmalloc(&d.par, c.scap));
   A(dmalloc(&d.fx, c.scap / 32));
+  A(dmalloc(&d.cb, c.scap / 32));
   A(dmalloc(&d.tq, 2 * (uint64_t)TAIL_QCAP));
   d.wpc_cap = (uint64_t)TAIL_QCAP + c.pcap / 256 + 1;  // (WALK_PIECE = 256 edges)
   A(dmalloc(&d.wpc, d.wpc_cap));
@@ -161,6 +162,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   M(d.rnew, 0, c.scap * 4);
   M(d.par, 0xFF, c.scap * 4);  // no hints in a new generation
   M(d.fx, 0, c.scap / 8);
+  M(d.cb, 0, c.scap / 8);
   M(d.cm, 0, c.scap / 8);
   M(d.pb[0], 0, c.scap / 8);
   M(d.pb[1], 0, c.scap / 8);
@@ -301,6 +303,10 @@ struct Knobs {
   uint64_t dev_chunk = 0;        // CRGC_DEV_CHUNK: sub-merge size of large device batches (test hook; 0 = 2^20)
   uint32_t spin_us = spin_us_default();  // CRGC_SPIN_US (production): host waits poll this long before blocking (0: block at once)
   bool repack_each = false;      // CRGC_REPACK_EACH_MERGE=1: repack the pools before every merge (test hook)
+  bool pull_pred = false;        // CRGC_PULL_PRED=1: the previous trace's pull levels pull again
+  bool bin512 = true;            // CRGC_BIN512=0: bins of 2^16 slots only up to 256 of them (2^24 slots)
+  bool cbits = true;             // CRGC_CBITS=0: a pull level's finds go out as candidate bytes
+  bool roots_co = true;          // CRGC_ROOTS_CO=0: the pseudo-root pass reads 128 B of counts per lane
   void read() {
     auto env = [](const char *k) { return getenv(k); };
     if (const char *m = env("CRGC_KERNEL_TIMING")) kernel_timing = atoi(m);
@@ -344,6 +350,10 @@ struct Knobs {
       xslices = v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
     }
     if (const char *m = env("CRGC_ROUTE")) route = atoi(m) != 0;
+    if (const char *m = env("CRGC_CBITS")) cbits = atoi(m) != 0;
+    if (const char *m = env("CRGC_BIN512")) bin512 = atoi(m) != 0;
+    if (const char *m = env("CRGC_PULL_PRED")) pull_pred = atoi(m) != 0;
+    if (const char *m = env("CRGC_ROOTS_CO")) roots_co = atoi(m) != 0;
     if (const char *m = env("CRGC_SIDE_STREAM")) side_stream = atoi(m) != 0;
     if (const char *m = env("CRGC_SIDE_PRIO")) side_prio = atoi(m) != 0;
     if (const char *m = env("CRGC_CHUNK_HOST")) chunk_host = atoi(m) != 0;
@@ -397,6 +407,7 @@ struct crgc_graph {
   crgc_trace_stats last_stats{};
   bool have_last = false;
   uint64_t last_levels = 0;  // level launches (after level 0) the previous trace needed
+  uint64_t pull_pred = 0;    // levels (bit L) whose k_expand pulled in the previous trace
   std::vector<hipEvent_t> lvl_ev;  // 6 per level launch: start / stop of its 3 kernels
   std::vector<hipEvent_t> chunk_ev;  // start / stop of every chunk of level launches
   uint64_t *roots_buf = nullptr;
@@ -2106,6 +2117,8 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   la.alpha = kn.alpha;
   la.e_total = h->etab_used + h->atoms_since;
   la.pull_thresh = 0;
+  // unsharded pseudo-root traces: the previous trace's pull levels pull again
+  la.pull_pred = (kn.pull_pred && roots && !investigate && !h->tp) ? h->pull_pred : 0;
   // Test hooks: absolute thresholds (0 disables sparse levels entirely).
   if (kn.has_pull_thresh) {
     la.pull_thresh = kn.pull_thresh;
@@ -2117,6 +2130,8 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   if (kn.tail) la.flags |= LV_TAIL;
   const bool walk = (h->tp || kn.walk_unsharded) && kn.tail && kn.walk;
   if (walk) la.flags |= LV_WALK;
+  if (kn.cbits) la.flags |= LV_CBITS;
+  if (kn.roots_co) la.flags |= LV_ROOTS_CO;
   // Deep marks: a k_tail walk of chain_after links hands the rest to chain mode
   // (pointer jumping, crgc_chain.hip).  Unsharded graphs only.
   la.chain_after = h->tp ? 0 : kn.chain_after;
@@ -2132,13 +2147,18 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   if (roots && kn.bin && !kn.alpha && top > 0 && top >= kn.bin_min) {
     uint32_t lg = 0;
     while (lg < 63 && (1ull << lg) < imax) ++lg;
-    const uint32_t shift = std::max<uint32_t>(16, lg > 8 ? lg - 8 : 0);
+    // Bins of 2^16 slots (u16 offsets: the place pass writes 2 B per target)
+    // up to 512 of them (2^25 slots: the C2 bench graph's range passes 2^24),
+    // else up to 256 wider bins of u32 slots.
+    const bool b16 = kn.bin512 && ((imax + 0xFFFFull) >> 16) <= BIN_MAX;
+    const uint32_t shift = b16 ? 16u : std::max<uint32_t>(16, lg > 8 ? lg - 8 : 0);
     const uint64_t nb = (imax + (1ull << shift) - 1) >> shift;
-    if (shift <= 20 && nb <= BIN_MAX) {
+    if (shift <= 20 && nb <= (b16 ? BIN_MAX : BIN_MAX_WIDE)) {
       const uint64_t nc = nb * BIN_WG;
       const uint64_t want = std::max<uint64_t>(1u << 16, (h->etab_used + h->atoms_since) / 2);
       // (a multiple of 8: the apply pass reads a slice of u16 offsets in 16-B groups)
-      const uint64_t sc = std::min<uint64_t>(std::max<uint64_t>(round_up(want / nc, 8), 16), 1u << 24);
+      // (below 2^23: the place pass packs a clamped reservation into 23 bits)
+      const uint64_t sc = std::min<uint64_t>(std::max<uint64_t>(round_up(want / nc, 8), 16), (1u << 23) - 8);
       const size_t need = Carver::need({16, nc * 4, nc * sc * 4});
       HIP_TRY(h->x_bin.ensure(need));
       Carver cv(h->x_bin.ptr);
@@ -2944,6 +2964,7 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   h->inserted_at_trace = c.inserted;
   h->have_last = true;
   h->last_levels = lr.first_chunk;
+  h->pull_pred = c.pulled;
   st.ms_total =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   h->last_stats = st;

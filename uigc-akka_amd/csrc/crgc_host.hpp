@@ -166,6 +166,8 @@ constexpr uint32_t LV_TAIL = 8;                // narrow frontiers go to one wor
 constexpr uint32_t LV_INVESTIGATE = 16;        // set by launch_level: no supervisor edges
 constexpr uint32_t LV_ROOTS = 32;              // set by launch_level: the pseudo-root level
 constexpr uint32_t LV_WALK = 64;               // narrow frontiers go to WALK_WG workgroups (k_walk)
+constexpr uint32_t LV_CBITS = 128;             // a pull level hands the next level its candidates as bits (cb)
+constexpr uint32_t LV_ROOTS_CO = 256;          // the pseudo-root pass reads receive counts lane-interleaved
 
 struct LevelArgs {
   int level;
@@ -190,9 +192,11 @@ struct LevelArgs {
   uint32_t bin_shift;      // a bin covers slots [b << bin_shift, (b + 1) << bin_shift)
   uint32_t nbins;
   uint32_t bin_grid;       // workgroups of the place pass
+  uint64_t pull_pred;      // bit L: level L pulled in the previous trace, so it pulls again (lists skipped)
 };
 constexpr uint32_t BIN_WG = 512;     // k_bin_place workgroups (16 waves each)
-constexpr uint32_t BIN_MAX = 256;    // bins at most (one LDS counter each)
+constexpr uint32_t BIN_MAX = 512;    // bins at most (one LDS counter and table word each)
+constexpr uint32_t BIN_MAX_WIDE = 256;  // ... when a bin spans more than 2^16 slots
 
 // Chain mode (crgc_chain.hip).
 struct ChainArgs {

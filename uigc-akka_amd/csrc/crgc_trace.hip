@@ -43,9 +43,14 @@ __device__ inline uint64_t pull_span(const Counters *c) { return c->slot_top + c
 // Direction choice for level L (same answer in k_frontier and k_expand): pull
 // when the previous frontier was large; the level is then dense, so every
 // block of the slot range is scanned and `fx` is complete.
+// A level that pulled in the previous trace pulls again (LevelArgs::pull_pred):
+// decided before k_frontier, so it lists no push ranges the pull would not read
+// (a level-1 frontier of 5e6 shadows listed 8 B of ranges each, then pulled).
+template <bool PRED = true>
 __device__ inline bool pull_level(const Counters *c, int L, const LevelArgs &a) {
   if (!(a.flags & LV_PULL) || L < 1) return false;
   if (sparse_level(c, L, a.sparse_thresh) || sparse_level(c, L + 1, a.sparse_thresh)) return false;
+  if (PRED && L < 64 && ((a.pull_pred >> L) & 1ull)) return true;
   const uint64_t prev = c->ring[(L - 1) % LEVEL_RING];
   return a.pull_div ? prev * a.pull_div >= pull_span(c) : prev >= a.pull_thresh;
 }
@@ -66,8 +71,11 @@ __device__ inline bool fx_level(const Counters *c, int L, const LevelArgs &a) {
 // over alpha — a pull level reads in-candidate lists that stop at their first hit
 // and probe a frontier bitmap that stays in the XCD's L2, a push level does a
 // random candidate-byte read-modify-write per edge.
+// (PRED = false: the direction the rules give without the prediction — what
+// the next trace predicts from, so a prediction lapses once its level narrows)
+template <bool PRED = true>
 __device__ inline bool pull_now(const Counters *c, int L, const LevelArgs &a) {
-  if (pull_level(c, L, a)) return true;
+  if (pull_level<PRED>(c, L, a)) return true;
   if (!fx_level(c, L, a)) return false;
   if (!a.alpha) return c->ring[L % LEVEL_RING] * a.pull_cur_div >= pull_span(c);
   const uint64_t mu = a.e_total > c->mf_sum ? a.e_total - c->mf_sum : 0;
@@ -117,6 +125,13 @@ __device__ inline uint32_t flag_bits(const uint4 (&f4)[2], uint8_t bit) {
   return m;
 }
 
+// Bit i of an 8-bit value -> bit 4i.
+__device__ inline uint32_t spread8(uint32_t x) {
+  x = (x | (x << 12)) & 0x000F000Fu;
+  x = (x | (x << 6)) & 0x03030303u;
+  return (x | (x << 3)) & 0x11111111u;
+}
+
 // ---------------------------------------------------------------------------
 // k_frontier: one wave per 2048-slot block.  Candidate bytes (or, at level 0,
 // the pseudo-root predicate) -> new frontier bits -> vis (the wave owns those
@@ -155,6 +170,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   const bool write_fx = pull || fx_level(c, L, a);
   const bool listing = !ROOTS && listing_level(c, L, a);
   const bool sharded = !ROOTS && g.n_shards > 1;
+  // candidates from `cb` (k_expand(L-1) pulled and wrote them as bits)
+  const bool from_cb = !ROOTS && (a.flags & LV_CBITS) && c->cb_level == (unsigned long long)L;
+  const uint64_t st = c->slot_top;
   // pull levels without listing, proxies or Beamer's m_f: the per-lane path below
   const bool lane_pull = pull && !listing && !sharded && !a.alpha;
   uint32_t n_front = 0, n_sup = 0, n_edges = 0;
@@ -181,17 +199,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
             m |= 1u << j;
       } else {
         // isPseudoRoot (:201-203): 32 flag bytes + 32 receive counts per lane
-        int4 r4[8];
-        const int4 *rp = (const int4 *)(g.recv + base);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) r4[q] = rp[q];
-        const int32_t *rb = (const int32_t *)r4;
         uint32_t nz = 0;
+        if (a.flags & LV_ROOTS_CO) {
+          // The block's counts lane-interleaved (load q, lane l: slots
+          // q*256 + 4l .. +3, so a load instruction reads 1 KiB of consecutive
+          // counts, not 16 B of each of 64 lines), then transposed by ballots:
+          // bit k of lane l's nibble of load q belongs to lane q*8 + l/8, bit
+          // 4 (l % 8) + k.
+          const int4 *rp = (const int4 *)(g.recv + (uint64_t)blk * BLK_SLOTS);
+          int4 r4[8];
 #pragma unroll
-        for (int j = 0; j < 32; ++j) nz |= rb[j] != 0 ? (1u << j) : 0u;
+          for (int q = 0; q < 8; ++q) r4[q] = rp[q * 64 + lane];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const uint32_t b0 = (uint32_t)(__ballot(r4[q].x != 0) >> (8 * (lane & 7))) & 0xFFu;
+            const uint32_t b1 = (uint32_t)(__ballot(r4[q].y != 0) >> (8 * (lane & 7))) & 0xFFu;
+            const uint32_t b2 = (uint32_t)(__ballot(r4[q].z != 0) >> (8 * (lane & 7))) & 0xFFu;
+            const uint32_t b3 = (uint32_t)(__ballot(r4[q].w != 0) >> (8 * (lane & 7))) & 0xFFu;
+            const uint32_t w = spread8(b0) | (spread8(b1) << 1) | (spread8(b2) << 2) | (spread8(b3) << 3);
+            if ((lane >> 3) == q) nz = w;
+          }
+        } else {
+          int4 r4[8];
+          const int4 *rp = (const int4 *)(g.recv + base);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) r4[q] = rp[q];
+          const int32_t *rb = (const int32_t *)r4;
+#pragma unroll
+          for (int j = 0; j < 32; ++j) nz |= rb[j] != 0 ? (1u << j) : 0u;
+        }
         m = flag_bits(f4, FL_ALIVE) & ~flag_bits(f4, FL_HALTED) & ~flag_bits(f4, FL_PROXY) &
             (flag_bits(f4, FL_ROOT) | flag_bits(f4, FL_BUSY) | ~flag_bits(f4, FL_INTERNED) | nz);
       }
+    } else if (from_cb) {
+      // the pull level before wrote this level's candidates as bits (words
+      // past slot_top are never written: masked)
+      uint32_t bits = g.cb[(uint64_t)blk * 64 + lane];
+      if (base + 32 > st) bits &= base >= st ? 0u : ((1u << (uint32_t)(st - base)) - 1u);
+      m = bits & ~word;
     } else {
       uint4 *fp = (uint4 *)(Fc + base);
       const uint4 x0 = fp[0], x1 = fp[1];
@@ -430,6 +475,11 @@ __device__ inline void expand_bytes_out(const DevGraph &g, uint32_t nb2) {
   if (threadIdx.x == 0) g.xbytes[blockIdx.x] += s_nb / 2;
 }
 
+// Bits 0, 8, 16, 24 of a pull thread's `found` -> bits 0 .. 3.
+__device__ inline uint32_t found_nibble(uint32_t f) {
+  return (f & 1u) | ((f >> 7) & 2u) | ((f >> 14) & 4u) | ((f >> 21) & 8u);
+}
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_expand(DevGraph g, LevelArgs a) {
   constexpr int U = EXPAND_U;
   __shared__ uint32_t s_start[4][65];
@@ -455,6 +505,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   uint32_t nb2 = 0;
 
   if (pull_now(c, L, a)) {
+    if (L < 64 && blockIdx.x == 0 && threadIdx.x == 0 && pull_now<false>(c, L, a)) c->pulled |= 1ull << L;
     // Pull: each unmarked, not-yet-found shadow looks for an expandable
     // frontier shadow among its in-candidates whose edge to it has a
     // positive count (RC_POS), and stops at the first.  A thread owns 4
@@ -465,10 +516,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     const uint64_t nqh = (c->slot_top + 3) / 4;
     const uint64_t nq = nqh + (c->proxy_top + 3) / 4;
     const uint64_t gs = (uint64_t)gridDim.x * 256;
+    // Candidates as bits (LV_CBITS, unsharded graphs): this pass reads every
+    // slot's candidate byte anyway, so it hands level L+1 the complete set —
+    // supervisor bytes | finds — as words of `cb` (eight threads' nibbles, one
+    // word; every word below slot_top is written) and clears the bytes it
+    // read.  k_frontier(L+1) then reads 1 bit per slot instead of reading and
+    // clearing a byte.
+    const bool to_cb = (a.flags & LV_CBITS) && g.n_shards <= 1 && c->proxy_top == 0;
+    if (to_cb && blockIdx.x == 0 && threadIdx.x == 0) c->cb_level = (unsigned long long)(L + 1);
     // (Loading the hints and in-candidate ranges with the flags while a
     // quarter of the slots are unmarked, and the hints' frontier bits with
     // the lists' first chunks, made level 1 slower: 146 -> 181 us, r3g/ab4.)
-    for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += gs) {
+    // The loop bound is wave-uniform (a wave's 64 quads are consecutive), so
+    // the nibble exchange below runs with every lane.
+    const uint64_t qw0 = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u);
+    for (uint64_t qw = qw0; qw < nq; qw += gs) {
+      const uint64_t q = qw + (uint64_t)lane;
+      uint32_t nib = 0;  // (to_cb) this quad's candidates for level L+1
+      do {
+      if (q >= nq) break;
       const uint64_t v0 = q < nqh ? q * 4 : g.pbase + (q - nqh) * 4;
       const uint32_t fl = *(const uint32_t *)(g.flags + v0);
       const uint32_t cand = *(const uint32_t *)(Fn + v0);
@@ -479,7 +545,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       for (int j = 0; j < 4; ++j)
         todo |= (((fl >> (8 * j)) & FL_ALIVE) && !((cand >> (8 * j)) & 0xFFu) && !((vb >> j) & 1u))
                     ? (1u << j) : 0u;
-      if (!todo) continue;
+      if (to_cb && cand) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nib |= ((cand >> (8 * j)) & 0xFFu) ? (1u << j) : 0u;
+        *(uint32_t *)(Fn + v0) = 0;
+        nb2 += 8;
+      }
+      if (!todo) break;
       uint32_t found = 0;
       // Hints first: the owner a pull level found last time, if its edge is
       // still positive (hints are cleared when it stops being) and it is in
@@ -499,9 +571,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         }
       }
       if (!todo) {
-        *(uint32_t *)(Fn + v0) = cand | found;
-        nb2 += 8;
-        continue;
+        if (to_cb) {
+          nib |= found_nibble(found);
+        } else {
+          *(uint32_t *)(Fn + v0) = cand | found;
+          nb2 += 8;
+        }
+        break;
       }
       const uint4 r01 = *(const uint4 *)(g.radj + v0);
       const uint4 r23 = *(const uint4 *)(g.radj + v0 + 2);
@@ -566,8 +642,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
           if (hit || p[j] >= e[j]) live &= ~(1u << j);
         }
       }
-      if (found) *(uint32_t *)(Fn + v0) = cand | found;
-      nb2 += found ? 8 : 0;
+      if (to_cb) {
+        nib |= found_nibble(found);
+      } else if (found) {
+        *(uint32_t *)(Fn + v0) = cand | found;
+        nb2 += 8;
+      }
+      } while (false);
+      if (to_cb) {
+        // lanes 8k .. 8k+7 hold the nibbles of word (qw + 8k) / 8
+        uint32_t w = nib << (4 * (lane & 7));
+        w |= __shfl_xor(w, 1);
+        w |= __shfl_xor(w, 2);
+        w |= __shfl_xor(w, 4);
+        if ((lane & 7) == 0 && q < nq) {
+          g.cb[q >> 3] = w;
+          nb2 += 8;  // an eighth of a candidate word per slot, times 4 slots, times 2
+        }
+      }
     }
     expand_bytes_out(g, nb2);
     return;
@@ -709,9 +801,11 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
   __shared__ uint32_t s_off[BIN_NW][64];
   __shared__ uint32_t s_ulist[BIN_T], s_utag[BIN_T], s_wcnt[BIN_NW], s_nact;
   __shared__ uint32_t lc[BIN_MAX];  // the next position of each bin's slice of this workgroup
-  // per wave: a bin table (counts, then prefixes, then slice-position offsets)
+  // per wave: a bin table (counts, then prefix | slice reservation << 9 in one
+  // word: a window's prefix is <= 64 U = 256, a reservation is clamped to
+  // bin_slice < 2^23, so BIN_MAX = 512 bins fit the LDS of two tables of 256)
   // and the window's targets sorted by bin
-  __shared__ uint32_t s_wa[BIN_NW][BIN_MAX], s_wb[BIN_NW][BIN_MAX];
+  __shared__ uint32_t s_wa[BIN_NW][BIN_MAX];
   __shared__ uint32_t s_ws[BIN_NW][64 * U];
   Counters *c = g.ctr;
   const bool binned = !c->tail_state && bin_mode(c, a);
@@ -761,26 +855,23 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
       }
     }
     wave_lds_fence();
-    uint32_t *B = s_wb[wv], run = 0;
-    for (uint32_t k0 = 0; k0 < NB; k0 += 64) {  // A: counts -> prefixes; B: slice position - prefix
+    uint32_t run = 0;
+    for (uint32_t k0 = 0; k0 < NB; k0 += 64) {  // A: counts -> prefix | reservation << 9
       const uint32_t k = k0 + lane;
       const uint32_t cnt = k < NB ? A[k] : 0u;
       const uint32_t incl = wave_incl_scan(cnt);
       const uint32_t pre = run + incl - cnt;
-      if (k < NB) {
-        B[k] = (cnt ? atomicAdd(&lc[k], cnt) : 0u) - pre;
-        A[k] = pre;
-      }
+      if (k < NB) A[k] = pre | (min(cnt ? atomicAdd(&lc[k], cnt) : 0u, SC) << 9);
       run += __shfl(incl, 63);
     }
     wave_lds_fence();
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (r[u] != 0xFFFFFFFFu) S[A[t[u] >> a.bin_shift] + r[u]] = t[u];
+      if (r[u] != 0xFFFFFFFFu) S[(A[t[u] >> a.bin_shift] & 511u) + r[u]] = t[u];
     wave_lds_fence();
     for (uint32_t i = lane; i < run; i += 64) {
-      const uint32_t tt = S[i], b = tt >> a.bin_shift;
-      const uint32_t pos = B[b] + i;  // slice position = reservation + rank = B + sorted index
+      const uint32_t tt = S[i], b = tt >> a.bin_shift, e = A[b];
+      const uint32_t pos = (e >> 9) + i - (e & 511u);  // slice position = reservation + rank in the bin
       if (pos < SC) {
         const uint64_t at = ((uint64_t)b * G + wg) * SC + pos;
         if (B16) {
