@@ -28,7 +28,8 @@ VARIANTS = [
     {"CRGC_CBITS": "0"},                  # a pull level's finds as candidate bytes (round-4 form)
     {"CRGC_ROOTS_CO": "0"},               # the pseudo-root pass's per-lane 128-B count loads
     {"CRGC_PULL_PRED": "1"},              # the previous trace's pull levels pull again
-    {"CRGC_BIN512": "0", "CRGC_BIN_MIN_SLOTS": "0"},  # binned level 0 with at most 256 bins
+    {"CRGC_SUPBIN": "0"},                 # binned level 0: supervisor candidate bytes stored at once
+    {"CRGC_BIN512": "1", "CRGC_BIN_MIN_SLOTS": "0"},  # binned level 0 with up to 512 bins of 2^16
     # candidate bits after every pull (level 0 included) with frequent k_tail bails
     {"CRGC_ALPHA": "1000000", "CRGC_TAIL_START": "1000000", "CRGC_TAIL_MAX": "64"},
 ]

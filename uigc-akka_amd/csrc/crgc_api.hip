@@ -304,7 +304,10 @@ struct Knobs {
   uint32_t spin_us = spin_us_default();  // CRGC_SPIN_US (production): host waits poll this long before blocking (0: block at once)
   bool repack_each = false;      // CRGC_REPACK_EACH_MERGE=1: repack the pools before every merge (test hook)
   bool pull_pred = false;        // CRGC_PULL_PRED=1: the previous trace's pull levels pull again
-  bool bin512 = true;            // CRGC_BIN512=0: bins of 2^16 slots only up to 256 of them (2^24 slots)
+  bool supbin = true;            // CRGC_SUPBIN=0: the binned level 0 stores supervisor candidate bytes at once
+  // CRGC_BIN512=1: up to 512 bins of 2^16 slots (u16 offsets) past 2^24 slots; measured slower on
+  // the C2 graph (level 0 expand 162 against 135 us: the per-window bin tables, profiles/r5ae)
+  bool bin512 = false;
   bool cbits = true;             // CRGC_CBITS=0: a pull level's finds go out as candidate bytes
   bool roots_co = true;          // CRGC_ROOTS_CO=0: the pseudo-root pass reads 128 B of counts per lane
   void read() {
@@ -352,6 +355,7 @@ struct Knobs {
     if (const char *m = env("CRGC_ROUTE")) route = atoi(m) != 0;
     if (const char *m = env("CRGC_CBITS")) cbits = atoi(m) != 0;
     if (const char *m = env("CRGC_BIN512")) bin512 = atoi(m) != 0;
+    if (const char *m = env("CRGC_SUPBIN")) supbin = atoi(m) != 0;
     if (const char *m = env("CRGC_PULL_PRED")) pull_pred = atoi(m) != 0;
     if (const char *m = env("CRGC_ROOTS_CO")) roots_co = atoi(m) != 0;
     if (const char *m = env("CRGC_SIDE_STREAM")) side_stream = atoi(m) != 0;
@@ -2132,6 +2136,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   if (walk) la.flags |= LV_WALK;
   if (kn.cbits) la.flags |= LV_CBITS;
   if (kn.roots_co) la.flags |= LV_ROOTS_CO;
+  if (kn.supbin) la.flags |= LV_SUPBIN;
   // Deep marks: a k_tail walk of chain_after links hands the rest to chain mode
   // (pointer jumping, crgc_chain.hip).  Unsharded graphs only.
   la.chain_after = h->tp ? 0 : kn.chain_after;

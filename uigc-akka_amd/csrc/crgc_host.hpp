@@ -167,6 +167,7 @@ constexpr uint32_t LV_INVESTIGATE = 16;        // set by launch_level: no superv
 constexpr uint32_t LV_ROOTS = 32;              // set by launch_level: the pseudo-root level
 constexpr uint32_t LV_WALK = 64;               // narrow frontiers go to WALK_WG workgroups (k_walk)
 constexpr uint32_t LV_CBITS = 128;             // a pull level hands the next level its candidates as bits (cb)
+constexpr uint32_t LV_SUPBIN = 512;            // the binned pseudo-root level's supervisor pushes go through the bins
 constexpr uint32_t LV_ROOTS_CO = 256;          // the pseudo-root pass reads receive counts lane-interleaved
 
 struct LevelArgs {

@@ -169,6 +169,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   const bool pull = !ROOTS && pull_level(c, L, a);
   const bool write_fx = pull || fx_level(c, L, a);
   const bool listing = !ROOTS && listing_level(c, L, a);
+  // The pseudo-root level, binned: its supervisor pushes go to the block's
+  // region of `tl_buf` (no level-0 listing uses it) and k_bin_place bins them
+  // with the edge targets, instead of ~1e6 random candidate-byte stores here.
+  const bool sup_list = ROOTS && !INVESTIGATE && (a.flags & LV_SUPBIN) && a.nbins > 0;
+  uint32_t nsl = 0;
   const bool sharded = !ROOTS && g.n_shards > 1;
   // candidates from `cb` (k_expand(L-1) pulled and wrote them as bits)
   const bool from_cb = !ROOTS && (a.flags & LV_CBITS) && c->cb_level == (unsigned long long)L;
@@ -381,13 +386,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
 #pragma unroll
       for (int b = 0; b < FB; ++b) {
         n_edges += nz[b];  // this level's frontier out-edges (Beamer's m_f)
-        if (sp[b] != NO_SLOT) {
-          n_sup++;
+        const bool push_s = sp[b] != NO_SLOT && !((sw[b] >> (sp[b] & 31)) & 1u);
+        if (sp[b] != NO_SLOT) n_sup++;
+        if (sup_list) {
+          const uint64_t bl = __ballot(push_s);
+          if (push_s) g.tl_buf[(uint64_t)blk * BLK_SLOTS + nsl + __popcll(bl & lanemask_lt())] = sp[b];
+          nsl += __popcll(bl);
+        } else if (push_s) {
           const uint32_t s = sp[b];
-          if (!((sw[b] >> (s & 31)) & 1u)) {
-            Fn[s] = 1;
-            if (sp_next) Dn[s >> 11] = 1;  // blind: no dependent read
-          }
+          Fn[s] = 1;
+          if (sp_next) Dn[s >> 11] = 1;  // blind: no dependent read
         }
         const uint32_t len = ad[b].y;
         const bool light = len > 0 && len <= RANGE_MAX;
@@ -406,6 +414,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
       }
     }
     if (lane == 0 && nlight) g.qn_tag[blk] = tag | nlight;
+    if (sup_list) {
+      if (lane == 0 && nsl) g.tl_tag[blk] = (1u << 12) | nsl;
+      nsl = 0;
+    }
     wave_lds_fence();
   }
   const uint64_t tf = block_sum4(n_front);
@@ -820,7 +832,10 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
   const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
   const uint64_t ncid = nblk * 32;
   const uint64_t nh = min(c->qh[0], (unsigned long long)g.qh_cap);
-  const uint64_t nunits = ncid + nh;
+  // k_frontier(0)'s supervisor pushes (LV_SUPBIN): chunks (block b, k-th 256)
+  // of the blocks' tl_buf regions, after the edge units
+  const uint64_t nsc = ((a.flags & LV_SUPBIN) && !(a.flags & LV_INVESTIGATE)) ? nblk * (BLK_SLOTS / 256) : 0;
+  const uint64_t nunits = ncid + nh + nsc;
   uint32_t nb2 = 0;
   if (binned)
     for (uint32_t k = tid; k < NB; k += BIN_T) lc[k] = 0;
@@ -920,6 +935,19 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         edges(ed);
       }
       wave_lds_fence();
+    } else if (un >= ncid + nh) {  // supervisor pushes: up to 256 of a block's
+      const uint64_t sc = un - ncid - nh;
+      const uint64_t b = sc % nblk;
+      const uint32_t k = (uint32_t)(sc / nblk);
+      const uint32_t cnt = tag & 0xFFFu;
+      uint64_t ed[U];
+#pragma unroll
+      for (int uu = 0; uu < U; ++uu) {
+        const uint32_t i = k * 256 + uu * 64 + lane;
+        ed[uu] = i < cnt ? ((1ull << 32) | g.tl_buf[b * BLK_SLOTS + i]) : 0;  // count 1: a candidate
+        nb2 += i < cnt ? 8 : 0;
+      }
+      edges(ed);
     } else {  // a hub piece
       const uint2 rr = g.qh_buf[un - ncid];
       nb2 += lane == 0 ? 16 : 0;
@@ -948,6 +976,11 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     if (u < ncid) {
       tag = g.qn_tag[u % nblk];
       act = (tag >> 12) == 1u && (tag & 0xFFFu) > (uint32_t)(u / nblk) * 64;
+      nb2 += 8;
+    } else if (u >= ncid + nh && u < nunits) {
+      const uint64_t sc = u - ncid - nh;
+      tag = g.tl_tag[sc % nblk];
+      act = (tag >> 12) == 1u && (tag & 0xFFFu) > (uint32_t)(sc / nblk) * 256;
       nb2 += 8;
     } else if (u < nunits) {
       act = true;
