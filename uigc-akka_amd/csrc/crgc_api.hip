@@ -48,7 +48,7 @@ void free_arrays(Arrays &a) {
                 d.pool, d.etab, d.vis, d.front[0], d.front[1],
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat, d.xbytes,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill,
-                d.nzdeg, d.radj, d.rnew, d.rpool, d.par, d.fx, d.cb, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
+                d.nzdeg, d.radj, d.rnew, d.rpool, d.par, d.fx, d.cb, d.cb2, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
                 d.xsent, d.xkey, d.wpc, d.rq_buf, d.rq_cnt, d.phs, d.psh};
   for (void *p : ps)
     if (p) hipFree(p);
@@ -118,6 +118,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   A(dmalloc(&d.par, c.scap));
   A(dmalloc(&d.fx, c.scap / 32));
   A(dmalloc(&d.cb, c.scap / 32));
+  A(dmalloc(&d.cb2, c.scap / 32));
   A(dmalloc(&d.tq, 2 * (uint64_t)TAIL_QCAP));
   d.wpc_cap = (uint64_t)TAIL_QCAP + c.pcap / 256 + 1;  // (WALK_PIECE = 256 edges)
   A(dmalloc(&d.wpc, d.wpc_cap));
@@ -163,6 +164,7 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   M(d.par, 0xFF, c.scap * 4);  // no hints in a new generation
   M(d.fx, 0, c.scap / 8);
   M(d.cb, 0, c.scap / 8);
+  M(d.cb2, 0, c.scap / 8);
   M(d.cm, 0, c.scap / 8);
   M(d.pb[0], 0, c.scap / 8);
   M(d.pb[1], 0, c.scap / 8);

@@ -153,6 +153,8 @@ struct Counters {
   unsigned long long tail_level;     // DONE: levels traced; BAILED: level to resume at
   unsigned long long tail_from;      // level at which k_tail took over
   unsigned long long cb_level;       // a pull k_expand wrote level cb_level's candidates as bits (cb)
+  unsigned long long cb_two;         // ... and the second half of k_bin_apply's bits is in cb2 (level 1)
+  unsigned long long bin_ovf;        // k_bin_place stored a candidate byte at once (a full slice)
   unsigned long long pulled;         // bit L (L < 64): level L's k_expand pulled (the next trace's prediction)
   unsigned long long qn[2], qh[2];   // per-level edge-range queue lengths
   // sharded graphs
@@ -214,6 +216,7 @@ struct DevGraph {
   uint64_t rpcap;
   uint32_t *fx;              // expandable frontier bitmap (frontier & !halted)
   uint32_t *cb;              // candidates of the level after a pull level, 1 bit / slot (LV_CBITS)
+  uint32_t *cb2;             // level 1: the second k_bin_apply workgroup of each bin's bits
   uint32_t *tq;              // narrow-frontier queues, 2 x TAIL_QCAP slots
   uint32_t *tl_buf;          // per-block regions: a listed level's frontier slots
   uint32_t *tl_tag;          // per block: (level+1) << 12 | listed slots

@@ -177,6 +177,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   const bool sharded = !ROOTS && g.n_shards > 1;
   // candidates from `cb` (k_expand(L-1) pulled and wrote them as bits)
   const bool from_cb = !ROOTS && (a.flags & LV_CBITS) && c->cb_level == (unsigned long long)L;
+  const bool cb_two = from_cb && L == 1 && c->cb_two;
   const uint64_t st = c->slot_top;
   // pull levels without listing, proxies or Beamer's m_f: the per-lane path below
   const bool lane_pull = pull && !listing && !sharded && !a.alpha;
@@ -240,6 +241,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
       // the pull level before wrote this level's candidates as bits (words
       // past slot_top are never written: masked)
       uint32_t bits = g.cb[(uint64_t)blk * 64 + lane];
+      if (cb_two) bits |= g.cb2[(uint64_t)blk * 64 + lane];  // level 1 after a binned level 0
       if (base + 32 > st) bits &= base >= st ? 0u : ((1u << (uint32_t)(st - base)) - 1u);
       m = bits & ~word;
     } else {
@@ -866,7 +868,10 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
       r[u] = 0xFFFFFFFFu;
       if (edge_count(ed[u]) > 0) {
         if (b < NB) r[u] = atomicAdd(&A[b], 1u);
-        else Fn[t[u]] = 1;  // (a slot past the bins: never, slot_top is synced)
+        else {
+          Fn[t[u]] = 1;  // (a slot past the bins: never, slot_top is synced)
+          c->bin_ovf = 1;
+        }
       }
     }
     wave_lds_fence();
@@ -898,6 +903,7 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         }
       } else {
         Fn[tt] = 1;  // past the slice: the byte at once
+        c->bin_ovf = 1;  // (k_frontier(1) then reads the candidate bytes too: k_bin_apply writes bytes)
       }
     }
     wave_lds_fence();  // the table and the sorted window are reused by the next window
@@ -1067,6 +1073,26 @@ __global__ __launch_bounds__(BIN_T) void k_bin_apply(DevGraph g, LevelArgs a) {
   const uint64_t lo = (uint64_t)b << a.bin_shift;
   const uint64_t top = slot_end(g);  // (sharded graphs: bins over the proxy region too)
   const uint64_t hi = min(lo + span, top);
+  // Candidate bits (LV_CBITS, unsharded): when no candidate of level 1 went out
+  // as a byte (no full slice; the supervisor pushes binned too), each of a
+  // bin's two workgroups stores its bitmap as words of cb / cb2, which
+  // k_frontier(1) ORs, instead of a byte per candidate.
+  static_assert(BIN_SPLIT == 2, "one candidate bitmap per k_bin_apply workgroup of a bin");
+  Counters *c = g.ctr;
+  if ((a.flags & LV_CBITS) && g.n_shards <= 1 && c->proxy_top == 0 && c->bin_ovf == 0 &&
+      (a.flags & (LV_SUPBIN | LV_INVESTIGATE))) {
+    uint32_t *dst = h == 0 ? g.cb : g.cb2;
+    const uint64_t w0 = lo >> 5, nwd = (hi - lo + 31) >> 5;
+    for (uint64_t k = tid; k < nwd; k += BIN_T) dst[w0 + k] = bm[k];
+    nb2 += 8 * (uint32_t)((nwd + BIN_T - 1 - tid) / BIN_T);
+    if (blockIdx.x == 0 && tid == 0) {
+      c->cb_level = 1;
+      c->cb_two = 1;
+    }
+    const uint32_t ws = wave_sum(nb2);
+    if (lane_id() == 0 && ws) atomicAdd((unsigned long long *)&g.xbytes[blockIdx.x], (unsigned long long)(ws / 2));
+    return;
+  }
   for (uint64_t q = lo + tid; q < hi; q += BIN_T) {
     const uint32_t rel = (uint32_t)(q - lo);
     if ((bm[rel >> 5] >> (rel & 31)) & 1u) {
