@@ -70,3 +70,23 @@ def test_trace_switches_match_oracle(hip_mod, oracle_results, monkeypatch, env):
     for i in range(WAKEUPS):
         h.merge_entries(w.wakeup_batch(BATCH).to_device())
         assert _key(h.trace(True)) == oracle_results[i + 1], f"wakeup {i}"
+
+
+@pytest.mark.parametrize("env", [{}, {"CRGC_BIN_MIN_SLOTS": "0"}, {"CRGC_BIN_MIN_SLOTS": "0", "CRGC_CBITS": "0"}],
+                         ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()) or "defaults")
+def test_host_batches_binned_level0_match_oracle(hip_mod, oracle_results, monkeypatch, env):
+    """Wakeups merged from pageable host memory: the trace's level grids and
+    level-0 bins are then sized from an upper bound of slot_top (the batch's
+    possible new ids), so bins past the slots in use exist — k_bin_apply must
+    store nothing for them (round 5: a bitmap store sized hi - lo faulted
+    there when hi < lo)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    w = _stream()
+    h = hip_mod.ShadowGraph(vertex_capacity=ACTORS * 2, edge_capacity=EDGES * 2)
+    for b in w.batches(1 << 20):
+        h.merge_entries(b)
+    assert _key(h.trace(True)) == oracle_results[0]
+    for i in range(WAKEUPS):
+        h.merge_entries(w.wakeup_batch(BATCH))
+        assert _key(h.trace(True)) == oracle_results[i + 1], f"wakeup {i}"

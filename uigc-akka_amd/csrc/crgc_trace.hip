@@ -1082,7 +1082,9 @@ __global__ __launch_bounds__(BIN_T) void k_bin_apply(DevGraph g, LevelArgs a) {
   if ((a.flags & LV_CBITS) && g.n_shards <= 1 && c->proxy_top == 0 && c->bin_ovf == 0 &&
       (a.flags & (LV_SUPBIN | LV_INVESTIGATE))) {
     uint32_t *dst = h == 0 ? g.cb : g.cb2;
-    const uint64_t w0 = lo >> 5, nwd = (hi - lo + 31) >> 5;
+    // (bins are sized from an upper bound of slot_top: a bin past the slots
+    // in use has hi < lo and stores nothing)
+    const uint64_t w0 = lo >> 5, nwd = hi > lo ? (hi - lo + 31) >> 5 : 0;
     for (uint64_t k = tid; k < nwd; k += BIN_T) dst[w0 + k] = bm[k];
     nb2 += 8 * (uint32_t)((nwd + BIN_T - 1 - tid) / BIN_T);
     if (blockIdx.x == 0 && tid == 0) {
