@@ -23,6 +23,7 @@
 #   kt2l8s           the same for C2 over 8 logical shards
 #   c4l8s c2l8s      logical shards on one shared stream with the per-shard level log (all level kernels timed)
 #   c2l8x<k> c4l8x<k>  c2l8 / c4l8 with mark rounds capped at k levels (CRGC_XLEVELS, test hook)
+#   lv:<variants>    per-level kernel times (CRGC_KERNEL_TIMING=2) over env variants, two passes (tools/lv_summary.py)
 #   ab:<variants>    tools/ab_bench.sh A/B of env variants on the C2 line
 #   abl:<variants>   the same after 100 warmup wakeups (a grown graph)
 #   ab2l8:<variants> ab4l8:<variants>  tools/ab_l8.sh A/B of env variants on C2 / C4 logical shards
