@@ -178,6 +178,29 @@ def test_power_law_c1_sharded(sharded, oracle_mod):
     assert h.total_actors_seen() == o.total_actors_seen()
 
 
+@pytest.mark.parametrize("supbin", ["1", "0"])
+def test_power_law_sharded_binned_level0(sharded, oracle_mod, monkeypatch, supbin):
+    """Level 0 binned in every shard (CRGC_BIN_MIN_SLOTS=0): the bins cover the
+    proxy region, and with CRGC_SUPBIN the pseudo-roots' supervisor pushes —
+    proxies among them — go through the bins too; host batches make the bins'
+    slot bound an upper bound."""
+    monkeypatch.setenv("CRGC_BIN_MIN_SLOTS", "0")
+    monkeypatch.setenv("CRGC_SUPBIN", supbin)
+    w = world.World(seed=0x5EED + 21)
+    w.bulk_graph(60_000, 600_000, alpha=2.1, n_roots=600)
+    h, o = sharded(3), oracle_mod.OracleGraph()
+    for b in w.batches(1 << 18):
+        h.merge_entries(b, split=True)
+        o.merge_entries(b)
+    _same(h.trace(True), o.trace(True))
+    for _ in range(3):
+        b = w.wakeup_batch(6_000)
+        h.merge_entries(b, split=True)
+        o.merge_entries(b)
+        _same(h.trace(True), o.trace(True))
+    assert h.export() == o.export()
+
+
 def test_c3_chains_sharded(sharded, oracle_mod):
     w = world.World(seed=0x5EED + 3)
     w.chain_graph(n_chains=5, chain_len=300, n_sup_chains=3, sup_depth=100,
