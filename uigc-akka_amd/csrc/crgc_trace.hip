@@ -178,6 +178,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   // candidates from `cb` (k_expand(L-1) pulled and wrote them as bits)
   const bool from_cb = !ROOTS && (a.flags & LV_CBITS) && c->cb_level == (unsigned long long)L;
   const bool cb_two = from_cb && L == 1 && c->cb_two;
+  const bool cb_ovf = cb_two && c->bin_ovf;
   const uint64_t st = c->slot_top;
   // pull levels without listing, proxies or Beamer's m_f: the per-lane path below
   const bool lane_pull = pull && !listing && !sharded && !a.alpha;
@@ -241,7 +242,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
       // the pull level before wrote this level's candidates as bits (words
       // past slot_top are never written: masked)
       uint32_t bits = g.cb[(uint64_t)blk * 64 + lane];
-      if (cb_two) bits |= g.cb2[(uint64_t)blk * 64 + lane];  // level 1 after a binned level 0
+      if (cb_two) {  // level 1 after a binned level 0
+        bits |= g.cb2[(uint64_t)blk * 64 + lane];
+        if (cb_ovf && Dc[blk]) {  // a full slice's targets in this block went out as bytes
+          uint4 *fp = (uint4 *)(Fc + base);
+          const uint4 x0 = fp[0], x1 = fp[1];
+          const uint32_t xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) bits |= ((xs[q] >> (8 * k)) & 0xFFu) ? (1u << (4 * q + k)) : 0u;
+          fp[0] = make_uint4(0, 0, 0, 0);
+          fp[1] = make_uint4(0, 0, 0, 0);
+          wave_lds_fence();  // (every lane has read the block's dirty byte)
+          if (lane == 0) Dc[blk] = 0;
+        }
+      }
       if (base + 32 > st) bits &= base >= st ? 0u : ((1u << (uint32_t)(st - base)) - 1u);
       m = bits & ~word;
     } else {
@@ -829,6 +845,7 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
   const uint32_t NB = a.nbins;
   const uint32_t SC = a.bin_slice;
   uint8_t *Fn = g.front[1];
+  uint8_t *Dn1 = g.dirty[1];  // level 1's blocks with candidate bytes (a full slice's targets)
   const int wv = threadIdx.x >> 6, lane = lane_id(), tid = threadIdx.x;
   const uint64_t G = gridDim.x, wg = blockIdx.x;
   const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
@@ -870,6 +887,7 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         if (b < NB) r[u] = atomicAdd(&A[b], 1u);
         else {
           Fn[t[u]] = 1;  // (a slot past the bins: never, slot_top is synced)
+          Dn1[t[u] >> 11] = 1;
           c->bin_ovf = 1;
         }
       }
@@ -903,7 +921,8 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         }
       } else {
         Fn[tt] = 1;  // past the slice: the byte at once
-        c->bin_ovf = 1;  // (k_frontier(1) then reads the candidate bytes too: k_bin_apply writes bytes)
+        Dn1[tt >> 11] = 1;  // (k_frontier(1) reads the bytes of such blocks besides the bits)
+        c->bin_ovf = 1;
       }
     }
     wave_lds_fence();  // the table and the sorted window are reused by the next window
@@ -1073,13 +1092,14 @@ __global__ __launch_bounds__(BIN_T) void k_bin_apply(DevGraph g, LevelArgs a) {
   const uint64_t lo = (uint64_t)b << a.bin_shift;
   const uint64_t top = slot_end(g);  // (sharded graphs: bins over the proxy region too)
   const uint64_t hi = min(lo + span, top);
-  // Candidate bits (LV_CBITS, unsharded): when no candidate of level 1 went out
-  // as a byte (no full slice; the supervisor pushes binned too), each of a
-  // bin's two workgroups stores its bitmap as words of cb / cb2, which
-  // k_frontier(1) ORs, instead of a byte per candidate.
+  // Candidate bits (LV_CBITS, unsharded; the supervisor pushes binned too): each
+  // of a bin's two workgroups stores its bitmap as words of cb / cb2, which
+  // k_frontier(1) ORs, instead of a byte per candidate.  Targets past a full
+  // slice went out as bytes with their block's dirty byte (dirty[1]), which
+  // k_frontier(1) also reads.
   static_assert(BIN_SPLIT == 2, "one candidate bitmap per k_bin_apply workgroup of a bin");
   Counters *c = g.ctr;
-  if ((a.flags & LV_CBITS) && g.n_shards <= 1 && c->proxy_top == 0 && c->bin_ovf == 0 &&
+  if ((a.flags & LV_CBITS) && g.n_shards <= 1 && c->proxy_top == 0 &&
       (a.flags & (LV_SUPBIN | LV_INVESTIGATE))) {
     uint32_t *dst = h == 0 ? g.cb : g.cb2;
     // (bins are sized from an upper bound of slot_top: a bin past the slots
