@@ -401,7 +401,9 @@ int crgc_export(crgc_graph *g, crgc_graph_export *out);
    are copied by the DMA engines, without the driver's pageable staging copy.
    No reference counterpart (the reference has no device boundary).  The
    buffer must stay valid until crgc_host_unregister or crgc_destroy;
-   registering an overlapping range is CRGC_E_INVAL. */
+   registering an overlapping range is CRGC_E_INVAL.  crgc_host_unregister
+   is safe with crgc_merge_entries_async merges in flight: it waits for the
+   copies and merges queued on the handle before unpinning the range. */
 int crgc_host_register(crgc_graph *g, void *ptr, uint64_t bytes);
 int crgc_host_unregister(crgc_graph *g, void *ptr);
 

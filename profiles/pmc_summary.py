@@ -7,12 +7,28 @@ bytes (rocprofv3 reports KiB).  --last-wakeups N keeps only the dispatches of th
 last N wakeups of a bench run (each starts at a k_ids dispatch), i.e. steady
 state, not the graph's bulk load.  --fetch-factor X scales FETCH_SIZE by the
 calibration factor of the kernel's own access shapes (profiles/calib_summary.py);
-the default 1 reports the raw counter.
+the default 1 reports the raw counter.  --calibrate doubles FETCH_SIZE for the
+kernels whose reads are wide streaming loads (STREAMING below): the calibration
+kernels read 0.50 x the bytes of 16-B and 8-B/lane streaming reads
+(profiles/r2d/calib_summary.txt, /opt/skills/guides/MI355X_MICROARCH.md), while
+random 1-B / 4-B accesses count a line each and stay as counted.
 """
 import argparse
 import collections
 import csv
 import json
+
+
+# Kernels whose fetched bytes are (mostly) coalesced 8/16-B per lane streams
+# over slot, entry or atom arrays; the rest are dominated by random line
+# accesses (id / edge probes, candidate stores), which the counter sees whole.
+STREAMING = {
+    "k_frontier<true, false>", "k_frontier<true, true>",  # flags / recv / sup per slot
+    "k_sweep", "k_sweep_scan", "k_trace_reset",            # per-slot passes
+    "k_entries_atoms", "k_ep_count", "k_ep_scatter",        # the batch and atom streams
+    "k_scan_sums", "k_scan_apply_top", "k_copy_lists", "k_copy_segs", "k_copy_ranges",
+    "k_xscan<false>", "k_xscan<true>",
+}
 
 
 def load(paths, last_wakeups):
@@ -36,6 +52,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--last-wakeups", type=int, default=0)
     ap.add_argument("--fetch-factor", type=float, default=1.0)
+    ap.add_argument("--calibrate", action="store_true",
+                    help="x2 FETCH_SIZE for the STREAMING kernels (overrides --fetch-factor there)")
     ap.add_argument("csv", nargs="+")
     a = ap.parse_args()
     agg = load(a.csv, a.last_wakeups)
@@ -47,8 +65,10 @@ def main():
         n = max(len(f), len(w))
         fm = sum(f) / len(f) if f else None
         wm = sum(w) / len(w) if w else None
+        ff = 2.0 if a.calibrate and k in STREAMING else a.fetch_factor
         out[k] = {"launches": n, "fetch_bytes": fm, "write_bytes": wm,
-                  "fetch_bytes_calibrated": fm * a.fetch_factor if fm is not None else None}
+                  "fetch_bytes_calibrated": fm * ff if fm is not None else None,
+                  "fetch_factor": ff}
         fs = f"{fm:15.0f}" if fm is not None else f"{'-':>15s}"
         ws = f"{wm:15.0f}" if wm is not None else f"{'-':>15s}"
         print(f"{k[:40]:40s} {n:8d} {fs} {ws}")

@@ -10,6 +10,7 @@
 #   pmc              FETCH_SIZE and WRITE_SIZE passes of the same command, one run each
 #   probe            tools/hip_probe.hip: HIP last-error / event / pointer-range semantics
 #   rand             tools/rand_probe.hip: random-access ceilings (loads, atomics, CAS, stores)
+#   evprobe          tools/event_probe.hip: the idle GPU time a timing event costs between launches
 #   c4               C4 unsharded on one GPU (1e8 actors / 1e9 edges, the scaling anchor)
 #   c4q              the C4 line without the OpenMP leg (no set comparison)
 #   kt4              kernel trace of the C4 N = 1 line (load and wakeups)
@@ -64,6 +65,7 @@ for step in "$@"; do
             > "$O/bench_write.json" 2> "$O/bench_write.err") ;;
     probe) (cd "$ROOT" && timeout -k 10 60 ./tools/_build/hip_probe > "$O/hip_probe.txt" 2>&1) ;;
     rand) (cd "$ROOT" && timeout -k 10 120 ./tools/_build/rand_probe > "$O/rand_probe.txt" 2>&1) ;;
+    evprobe) (cd "$ROOT" && timeout -k 10 60 ./tools/_build/event_probe > "$O/event_probe.txt" 2>&1) ;;
     c4) (cd /tmp && CRGC_LEVEL_LOG=1 timeout -k 10 1000 python3 -u "$ROOT/bench.py" --workload c4 --steps 5 \
           --warmup 2 --no-pcie > "$O/bench_c4.json" 2> "$O/bench_c4.err") ;;
     c4q) (cd /tmp && timeout -k 10 900 python3 -u "$ROOT/bench.py" --workload c4 --steps 5 --warmup 2 --no-pcie \
@@ -92,6 +94,8 @@ for step in "$@"; do
           --steps 3 --warmup 1 --no-pcie --no-cpu-baseline > "$O/bench_c4rs.json" 2> "$O/bench_c4rs.err") ;;
     c2l8) (cd /tmp && timeout -k 10 600 python3 -u "$ROOT/bench.py" --workload c2 --logical-shards 8 \
           --steps 5 --warmup 2 > "$O/bench_c2l8.json" 2> "$O/bench_c2l8.err") ;;
+    c2l8log) (cd /tmp && CRGC_LEVEL_LOG=1 timeout -k 10 600 python3 -u "$ROOT/bench.py" --workload c2 --logical-shards 8 \
+          --steps 3 --warmup 1 --no-cpu-baseline > "$O/bench_c2l8log.json" 2> "$O/bench_c2l8log.err") ;;
     c2l8x*|c4l8x*)  # the same with CRGC_XLEVELS=<k> (mark rounds capped at k levels; a test hook)
       k=${step#*x}; wl=${step%%l8x*}
       extra=()

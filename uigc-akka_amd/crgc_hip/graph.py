@@ -271,7 +271,11 @@ class ShadowGraph:
         self._chk(self.lib.crgc_host_register(self.h, buf.ctypes.data, buf.nbytes), "crgc_host_register")
 
     def unregister_host(self, buf: np.ndarray):
+        """Unpin `buf` (crgc_host_unregister): pending entries are merged first, and
+        the call waits for async merges still reading it."""
+        self.flush()
         self._chk(self.lib.crgc_host_unregister(self.h, buf.ctypes.data), "crgc_host_unregister")
+        self._synced()
 
     def compact(self):
         """Compact the graph now (crgc_compact): dense slots, segments in slot order."""

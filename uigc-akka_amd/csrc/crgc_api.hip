@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <functional>
 #include <cstdio>
 #include <cstring>
@@ -284,6 +285,11 @@ struct Knobs {
   // 1 / xclosure_narrow of the graph's slots (0: at any width; a test hook).
   uint32_t xclosure_after = 8;   // CRGC_XCLOSURE_AFTER
   uint32_t xclosure_narrow = 1024;  // CRGC_XCLOSURE_NARROW
+  // A mark round's fixed cost in link bytes (two host round trips, the
+  // all-gathered counts and ~4 near-empty level launches: ~0.1 ms ≈ 4 MB at
+  // ~50 GB/s per xGMI link direction), against which the closure's all-gathers
+  // are priced.  CRGC_XROUND_BYTES
+  uint64_t xround_bytes = 4ull << 20;
   uint32_t xslices = 1;          // CRGC_XSLICES: push-level target slices (1, 2, 4, 8)
   // Sharded marks: a round runs at most this many level launches before its
   // exchange (0: to the shard's local fixpoint).  Pending candidates carry
@@ -344,6 +350,7 @@ struct Knobs {
       buckets_log2 = std::min(10, std::max(1, atoi(m)));
     if (const char *m = env("CRGC_XCLOSURE_AFTER")) xclosure_after = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_XCLOSURE_NARROW")) xclosure_narrow = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_XROUND_BYTES")) xround_bytes = strtoull(m, nullptr, 10);
     if (const char *m = env("CRGC_BIN")) bin = atoi(m) != 0;
     if (const char *m = env("CRGC_BIN_MIN_SLOTS")) bin_min = strtoull(m, nullptr, 10);
     if (const char *m = env("CRGC_XLEVELS")) xlevels = (uint32_t)strtoul(m, nullptr, 10);
@@ -738,8 +745,9 @@ int ensure_capacity(crgc_graph *h, uint64_t ids, uint64_t atoms) {
     return st + ids <= c.pbase && (h->G <= 1 || pt + ids <= c.scap - c.pbase) &&
            (st + pt + ids) * 10 <= c.hcap * 7 && (eu + atoms) * 10 <= c.ecap * 7;
   };
-  // upper bounds since the last sync
-  const uint64_t st = h->slot_top + h->ids_since, pt = h->proxy_top + h->ids_since;
+  // upper bounds since the last sync (an unsharded graph has no proxies: its
+  // pending ids are counted once, in st)
+  const uint64_t st = h->slot_top + h->ids_since, pt = h->G > 1 ? h->proxy_top + h->ids_since : 0;
   const uint64_t eu = h->etab_used + h->atoms_since;
   const uint64_t grow = 2 * (h->etab_used + h->atoms_since) + 6 * h->atoms_since;
   // (+ 4 reverse-candidate entries per new shadow: k_ids' first segments)
@@ -2633,6 +2641,7 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
       for (uint32_t k = 0; k < 2 * G; ++k) total += M[(size_t)r * (2 * G + 1) + k];
       pending += M[(size_t)r * (2 * G + 1) + 2 * G];
     }
+    const uint64_t last_total = prev_total;
     prev_total = total;
     if (total == 0 && pending == 0) {
       *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -2679,8 +2688,29 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
       uint64_t n_all = 0, marks = total;
       for (uint32_t d = 0; d < G; ++d) n_all += h->peer_top[d];
       // (never with candidates pending: the closure starts from marks only)
-      if (xmode != 0 && pending == 0 && kn.xclosure_after && *rounds >= kn.xclosure_after &&
-          (kn.xclosure_narrow == 0 || marks * kn.xclosure_narrow <= n_all) && n_all < 0xF0000000ull) {
+      bool closure = xmode != 0 && pending == 0 && kn.xclosure_after && *rounds >= kn.xclosure_after &&
+                     (kn.xclosure_narrow == 0 || marks * kn.xclosure_narrow <= n_all) && n_all < 0xF0000000ull;
+      // ... and only when the rounds it saves would cost more than it does.  Its
+      // five all-gathers bring every shard ~8.4 B per slot of the rest of the
+      // graph; a further round costs a fixed exchange and level floor
+      // (xround_bytes, in link bytes) plus its marks.  A chain's marks per round
+      // stay level (rounds left: unbounded); a shallow graph's last rounds shrink
+      // geometrically (C2 over 8 shards: the closure fired at round 8 and moved
+      // 1.05 GB per wakeup, profiles/r5aq), leaving ~log(marks)/log(ratio).
+      // The test hook xclosure_narrow = 0 forces it.
+      if (closure && kn.xclosure_narrow != 0) {
+        const double cbytes = 8.375 * (double)n_all * (double)(G - 1) / (double)G;
+        double left = 1e30;
+        if (marks == 0) left = 1;
+        else if (last_total != ~0ull && 2 * marks < last_total)
+          left = std::log((double)marks) / std::log((double)last_total / (double)marks) + 1.0;
+        closure = left * ((double)kn.xround_bytes + 4.0 * (double)marks) >= cbytes;
+        if (kn.level_log)
+          fprintf(stderr, "[crgc] shard %u round %llu: marks %llu (last %llu), closure %.1f MB vs %.1f rounds left: %s\n",
+                  me, (unsigned long long)*rounds, (unsigned long long)marks, (unsigned long long)last_total,
+                  cbytes / 1e6, left > 1e29 ? -1.0 : left, closure ? "closure" : "rounds");
+      }
+      if (closure) {
         *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         const auto t1 = std::chrono::steady_clock::now();
         const int rc = xclosure(h, investigate, xr, rounds, x_bytes);
@@ -3537,9 +3567,16 @@ int crgc_host_unregister(crgc_graph *h, void *ptr) {
   for (size_t i = 0; i < h->pinned.size(); ++i)
     if (h->pinned[i].first == (char *)ptr) {
       DeviceGuard dg(h->device);
-      // merges read registered buffers by DMA until they return; nothing is in flight here
+      // An async merge (crgc_merge_entries_async) returns while k_copy_ranges on
+      // the copy stream may still read this range over PCIe, and its merges on
+      // the graph's stream read the staged copy: wait for both before the pages
+      // are unpinned (a queued kernel reading unpinned pages faults the GPU).
+      const hipError_t ec = stream_wait(h->cpy, h->knobs.spin_us);
+      const hipError_t es = h->poisoned ? hipSuccess : hsync(h);
       hipHostUnregister(ptr);
       h->pinned.erase(h->pinned.begin() + (long)i);
+      if (ec != hipSuccess) return map_hip(ec);
+      if (es != hipSuccess) return map_hip(es);
       return CRGC_OK;
     }
   return CRGC_E_INVAL;

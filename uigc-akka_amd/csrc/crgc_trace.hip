@@ -1888,9 +1888,17 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
   else if (investigate) frontier(k_frontier<false, true>);
   else frontier(k_frontier<false, false>);
   // level controller: the level count, and the narrow-frontier takeover
-  if (a.flags & LV_WALK)
-    hipExtLaunchKernelGGL(k_walk, dim3(WALK_WG), dim3(WALK_T), 0, s, e[2], e[3], 0, g, a);
-  else
+  if (a.flags & LV_WALK) {
+    // k_walk's grid barriers need all WALK_WG workgroups resident at once:
+    // a cooperative launch guarantees it (or fails) even when other handles'
+    // streams share the GPU (logical shards, side streams)
+    if (e[2]) (void)hipEventRecord(e[2], s);
+    void *args[] = {(void *)&g, (void *)&a};
+    const hipError_t ce =
+        hipLaunchCooperativeKernel((const void *)k_walk, dim3(WALK_WG), dim3(WALK_T), args, 0, s);
+    if (ce != hipSuccess) return ce;
+    if (e[3]) (void)hipEventRecord(e[3], s);
+  } else
     hipExtLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, e[2], e[3], 0, g, a);
   // 8 WGs of 4 waves per CU
   if (roots && a.nbins) {

@@ -22,6 +22,7 @@ struct Segs {
   const char *src[TRANSPORT_MAX_SHARDS];
   char *dst[TRANSPORT_MAX_SHARDS];
   uint64_t n[TRANSPORT_MAX_SHARDS];
+  uint32_t from[TRANSPORT_MAX_SHARDS];  // the shard whose buffer src points into
   uint32_t count;
 };
 
@@ -84,6 +85,7 @@ int LocalTransport::barrier() {
 // faulted inside the runtime, profiles/r5n/README.md).
 int LocalTransport::events(uint32_t shard) {
   Post &p = post[shard];
+  if (hipGetDevice(&p.device) != hipSuccess) return DEV_FAIL("transport");
   if (!p.ready && hipEventCreateWithFlags(&p.ready, hipEventDisableTiming) != hipSuccess) return DEV_FAIL("transport");
   if (!p.done && hipEventCreateWithFlags(&p.done, hipEventDisableTiming) != hipSuccess) return DEV_FAIL("transport");
   return CRGC_OK;
@@ -99,11 +101,29 @@ int LocalTransport::events(uint32_t shard) {
 // (The host threads only rendezvous: an event is waited for by the peers only
 // after its record was enqueued, and recorded again only after every peer has
 // enqueued that wait.)
+//
+// Shards on other GPUs (one handle per GPU in one process):
+// a kernel here cannot read a peer GPU's memory unless peer access is enabled,
+// so their segments go through the runtime's peer copy instead; segments on
+// this shard's own GPU stay in the copy kernel.
 int LocalTransport::collect(uint32_t shard, const Segs &sg, hipStream_t s) {
   for (uint32_t r = 0; r < n_shards; ++r)
     if (r != shard && hipStreamWaitEvent(s, post[r].ready, 0) != hipSuccess) return DEV_FAIL("transport");
   (void)hipGetLastError();  // (a soft status of an earlier call is not this launch's)
-  if (copy_segs(sg, s) != hipSuccess) return DEV_FAIL("transport");
+  const int mine = post[shard].device;
+  Segs same{};
+  for (uint32_t j = 0; j < sg.count; ++j) {
+    const int dev = post[sg.from[j]].device;
+    if (dev == mine) {
+      same.src[same.count] = sg.src[j];
+      same.dst[same.count] = sg.dst[j];
+      same.n[same.count] = sg.n[j];
+      same.from[same.count++] = sg.from[j];
+    } else if (sg.n[j] && hipMemcpyPeerAsync(sg.dst[j], mine, sg.src[j], dev, sg.n[j], s) != hipSuccess) {
+      return DEV_FAIL("transport: peer copy");
+    }
+  }
+  if (copy_segs(same, s) != hipSuccess) return DEV_FAIL("transport");
   if (hipEventRecord(post[shard].done, s) != hipSuccess) return DEV_FAIL("transport");
   if (int rc = barrier()) return rc;
   for (uint32_t r = 0; r < n_shards; ++r)
@@ -121,6 +141,7 @@ int LocalTransport::allgather(uint32_t shard, const void *send, void *recv, size
   for (uint32_t r = 0; r < n_shards && bytes; ++r) {
     sg.src[sg.count] = (const char *)post[r].ptr;
     sg.dst[sg.count] = (char *)recv + (size_t)r * bytes;
+    sg.from[sg.count] = r;
     sg.n[sg.count++] = bytes;
   }
   return collect(shard, sg, s);
@@ -139,6 +160,7 @@ int LocalTransport::alltoallv(uint32_t shard, const void *send, const size_t *so
     if (!rbytes[r]) continue;
     sg.src[sg.count] = (const char *)post[r].ptr + post[r].soff[shard];
     sg.dst[sg.count] = (char *)recv + roff[r];
+    sg.from[sg.count] = r;
     sg.n[sg.count++] = rbytes[r];
   }
   return collect(shard, sg, s);  // (peers read post[*].soff before the second rendezvous)

@@ -57,6 +57,7 @@ struct LocalTransport final : crgc_transport {
     // recorded behind the send buffer's producers, `done` behind this shard's
     // copies out of its peers' buffers (created by the shard's own thread)
     hipEvent_t ready = nullptr, done = nullptr;
+    int device = 0;  // the GPU of the shard's handle (read at every collective)
   };
   std::mutex m;
   std::condition_variable cv;
