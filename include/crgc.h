@@ -214,8 +214,11 @@ typedef struct crgc_trace_stats {
   uint64_t ids_sent;       /* marked proxies sent to other shards (any form)*/
   double ms_exchange;      /* host wall time spent in exchanges             */
   /* the k_expand roofline */
-  uint64_t expand_launches;/* k_expand dispatches of this trace             */
-  uint64_t expand_bytes;   /* bytes k_expand read + wrote, by element width  */
+  uint64_t expand_launches;/* level expands of this trace that were timed: by
+                              default (CRGC_KERNEL_TIMING=3) the wide levels
+                              0 and 1; ms_expand and expand_bytes cover
+                              exactly these launches                         */
+  uint64_t expand_bytes;   /* bytes they read + wrote, by element width      */
   /* sharded graphs: bytes this shard sent in mark rounds (ids, home slots,
      frontier bitmaps) and in the home-slot resolution before them */
   uint64_t exchange_bytes;
@@ -405,6 +408,21 @@ int crgc_export(crgc_graph *g, crgc_graph_export *out);
    is safe with crgc_merge_entries_async merges in flight: it waits for the
    copies and merges queued on the handle before unpinning the range. */
 int crgc_host_register(crgc_graph *g, void *ptr, uint64_t bytes);
+
+/* Slot and table usage (a diagnostic; no reference counterpart): the dense
+   per-slot passes of a trace (pseudo-roots, frontier scans, sweep) scale with
+   slot_top — live shadows plus the slots of collected ones not yet reused or
+   compacted away — not with the live count.  Counters as of a host
+   synchronisation this call makes. */
+typedef struct crgc_usage {
+  uint64_t slot_top, slot_cap;    /* home slots in use (dead ones included), capacity */
+  uint64_t proxy_top, proxy_cap;  /* proxy region (sharded graphs)                    */
+  uint64_t free_slots;            /* swept slots waiting for reuse by new shadows     */
+  uint64_t pool_top, pool_cap;    /* edge pool entries                                */
+  uint64_t etab_used, etab_cap;   /* edge-table keys                                  */
+  uint64_t rebuilds, grows, repacks;
+} crgc_usage;
+int crgc_usage_of(crgc_graph *g, crgc_usage *out);
 int crgc_host_unregister(crgc_graph *g, void *ptr);
 
 /* Human-readable text for a status code. */

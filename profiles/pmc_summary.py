@@ -48,6 +48,38 @@ def load(paths, last_wakeups):
     return agg
 
 
+def wide_expand(paths, last_wakeups):
+    """Bytes per wakeup of the wide levels' expand — level 0 (k_bin_place +
+    k_bin_apply) and level 1 (the first k_expand after them) — the launches the
+    library times by default (CRGC_KERNEL_TIMING=3): {counter: mean bytes}."""
+    out = {}
+    for p in paths:
+        rows = list(csv.DictReader(open(p)))
+        rows.sort(key=lambda r: int(r.get("Dispatch_Id") or 0))
+        per = []  # per wakeup (each starts at a k_ids dispatch)
+        cur, seen_bin, seen_l1 = None, False, False
+        for r in rows:
+            k = r["Kernel_Name"]
+            if "k_ids" in k:
+                cur, seen_bin, seen_l1 = {}, False, False
+                per.append(cur)
+                continue
+            if cur is None:
+                continue
+            name = r["Counter_Name"]
+            if "k_bin_place" in k or "k_bin_apply" in k:
+                seen_bin = True
+                cur[name] = cur.get(name, 0.0) + float(r["Counter_Value"]) * 1024.0
+            elif "k_expand" in k and seen_bin and not seen_l1:
+                seen_l1 = True
+                cur[name] = cur.get(name, 0.0) + float(r["Counter_Value"]) * 1024.0
+        per = [w for w in per if w][-last_wakeups:] if last_wakeups else [w for w in per if w]
+        for w in per:
+            for n, v in w.items():
+                out.setdefault(n, []).append(v)
+    return {n: sum(v) / len(v) for n, v in out.items()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--last-wakeups", type=int, default=0)
@@ -72,6 +104,10 @@ def main():
         fs = f"{fm:15.0f}" if fm is not None else f"{'-':>15s}"
         ws = f"{wm:15.0f}" if wm is not None else f"{'-':>15s}"
         print(f"{k[:40]:40s} {n:8d} {fs} {ws}")
+    wide = wide_expand(a.csv, a.last_wakeups)
+    if wide:
+        print(f"wide-level expand (levels 0 + 1) per wakeup: {wide}")
+        out["_wide_expand_per_wakeup"] = wide
     print(json.dumps(out))
 
 

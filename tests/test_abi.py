@@ -24,7 +24,7 @@ def test_header_declares_exactly_the_exported_list():
 def test_struct_layout_matches_c_compiler(tmp_path):
     prog = tmp_path / "sz.c"
     structs = ["crgc_config", "crgc_entry_batch", "crgc_delta_batch", "crgc_undo_log",
-               "crgc_trace_stats", "crgc_trace_out", "crgc_graph_export"]
+               "crgc_trace_stats", "crgc_trace_out", "crgc_graph_export", "crgc_usage"]
     prog.write_text('#include <stdio.h>\n#include "%s"\nint main(void){%s return 0;}\n' % (
         HEADER, "".join('printf("%%zu\\n", sizeof(%s));' % s for s in structs)))
     exe = tmp_path / "sz"
@@ -32,7 +32,7 @@ def test_struct_layout_matches_c_compiler(tmp_path):
     sizes = [int(x) for x in subprocess.check_output([str(exe)]).split()]
     py = [C.sizeof(t) for t in (abi.CrgcConfig, abi.CrgcEntryBatch, abi.CrgcDeltaBatch,
                                 abi.CrgcUndoLog, abi.CrgcTraceStats, abi.CrgcTraceOut,
-                                abi.CrgcGraphExport)]
+                                abi.CrgcGraphExport, abi.CrgcUsage)]
     assert sizes == py
 
 

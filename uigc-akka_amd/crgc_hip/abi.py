@@ -203,6 +203,12 @@ HOST_ALLTOALLV = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.POIN
                              C.POINTER(C.c_size_t), C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t))
 
 
+class CrgcUsage(C.Structure):
+    _fields_ = [(n, _U64) for n in ("slot_top", "slot_cap", "proxy_top", "proxy_cap", "free_slots",
+                                   "pool_top", "pool_cap", "etab_used", "etab_cap",
+                                   "rebuilds", "grows", "repacks")]
+
+
 class HostCollectives(C.Structure):
     _fields_ = [("ctx", C.c_void_p), ("allgather", HOST_ALLGATHER), ("alltoallv", HOST_ALLTOALLV)]
 
@@ -241,6 +247,7 @@ EXPORTED_SYMBOLS = (
     "crgc_shard_of",
     "crgc_host_register",
     "crgc_host_unregister",
+    "crgc_usage_of",
 )
 
 
@@ -264,6 +271,8 @@ def _declare(lib: C.CDLL, prefix: str) -> None:
         sig["compact"] = (C.c_int, [g])
         sig["sync"] = (C.c_int, [g])
         sig["merge_entries_async"] = (C.c_int, [g, P(CrgcEntryBatch)])
+        if hasattr(lib, "crgc_usage_of") or not os.environ.get("CRGC_LIB_AB"):  # an A/B build may predate it
+            sig["usage_of"] = (C.c_int, [g, P(CrgcUsage)])
     for name, (res, args) in sig.items():
         fn = getattr(lib, prefix + name)
         fn.restype = res

@@ -277,6 +277,13 @@ class ShadowGraph:
         self._chk(self.lib.crgc_host_unregister(self.h, buf.ctypes.data), "crgc_host_unregister")
         self._synced()
 
+    def usage(self) -> dict:
+        """Slot and table usage (crgc_usage_of): slot_top counts the slots of
+        collected shadows not yet reused; the dense trace passes scale with it."""
+        u = abi.CrgcUsage()
+        self._chk(self.lib.crgc_usage_of(self.h, C.byref(u)), "crgc_usage_of")
+        return {n: int(getattr(u, n)) for n, _ in abi.CrgcUsage._fields_}
+
     def compact(self):
         """Compact the graph now (crgc_compact): dense slots, segments in slot order."""
         self.flush()

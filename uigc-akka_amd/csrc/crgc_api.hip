@@ -275,7 +275,13 @@ struct Knobs {
   uint32_t walk_start = 16384;   // CRGC_WALK_START
   uint32_t walk_max = 32768;     // CRGC_WALK_MAX
   uint32_t chain_after = 64;     // CRGC_CHAIN_AFTER
-  int kernel_timing = 1;         // CRGC_KERNEL_TIMING: 0 chunks, 1 k_expand, 2 all level kernels
+  // CRGC_KERNEL_TIMING: 0 chunks only, 1 every level's expand, 2 all level
+  // kernels, 3 (default) the expand of the wide levels 0 and 1 only.  A timing
+  // event carried by a dispatch costs ~5 us of idle GPU around it
+  // (tools/event_probe.hip, profiles/r6a): ~60 us per C2 wakeup with every
+  // expand timed, most of it on narrow levels that carry ~20 % of the
+  // expand's device time.
+  int kernel_timing = 3;
   bool level_log = false;        // CRGC_LEVEL_LOG
   uint64_t level_timeout_s = 300;  // CRGC_LEVEL_TIMEOUT_S
   int xbits = 1;                 // CRGC_XBITS: sharded mark form (0 ids, 1 cheaper, 2 bitmaps)
@@ -395,6 +401,9 @@ struct crgc_graph {
   // exact values as of the last synchronisation + upper-bound increments since
   uint64_t slot_top = 0, pool_top = 0, rpool_top = 0, etab_used = 0, live = 0;
   uint64_t proxy_top = 0;  // proxy region slots in use (sharded graphs), as of the last synchronisation
+  uint64_t n_rebuild = 0, n_grow = 0, n_repack = 0;  // crgc_usage_of
+  bool walk_ok = false;  // CRGC_WALK: k_walk's workgroups fit the device at once (walk_fits)
+  std::vector<uint8_t> lvl_timed;  // per level launch of the current run_levels: timed (events)
   uint64_t ids_since = 0, atoms_since = 0;
   uint64_t inserted_at_trace = 0;  // Counters::inserted when `live` was exact
   Scratch stage, work;
@@ -620,6 +629,7 @@ int grow(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   }
   free_arrays(h->g);
   h->g = dst;
+  ++h->n_grow;
   if (int rc = device_error(h)) return rc;
   return CRGC_OK;
 }
@@ -681,6 +691,7 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms, bool may_grow = false) 
   }
   free_arrays(h->g);
   h->g = dst;
+  ++h->n_rebuild;
   ++h->slot_gen;  // other shards' cached home slots of this shard are stale now
   h->live = h->slot_top;
   h->inserted_at_trace = h->hctr->inserted;
@@ -723,6 +734,7 @@ int repack(crgc_graph *h) {
   hipFree(h->g.d.rpool);
   h->g.d.pool = pool2;
   h->g.d.rpool = rpool2;
+  ++h->n_repack;
   if (h->knobs.level_log)
     fprintf(stderr, "[crgc] repack: pool %llu -> %llu, candidate pool %llu -> %llu (of %llu)\n",
             (unsigned long long)old_p, (unsigned long long)h->pool_top, (unsigned long long)old_r,
@@ -865,6 +877,7 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
   h->F = (cfg && cfg->entry_field_size) ? cfg->entry_field_size : 4;
   h->DGS = (cfg && cfg->delta_graph_size) ? cfg->delta_graph_size : 64;
   h->knobs.read();
+  if (h->knobs.walk) h->walk_ok = walk_fits(h->device);
   // A transport makes the handle a shard (a transport with n_shards == 1 runs
   // the sharded protocol on one shard: a self-check of the transport).
   if (cfg && (cfg->n_shards > 1 || cfg->transport)) {
@@ -2077,6 +2090,7 @@ static int run_chains(crgc_graph *h, bool investigate, uint64_t top) {
 
 struct LevelRun {
   uint64_t levels = 0, roots = 0, launches = 0, depth = 0;
+  uint64_t timed = 0;  // level launches whose expand carried timing events (crgc_trace_stats.expand_launches)
   uint64_t first_chunk = 0;  // level launches after level 0 that this trace needed
   double ms = 0, ms_f = 0, ms_t = 0, ms_e = 0;
   uint64_t time_fail = 0;              // event pairs the runtime could not time
@@ -2142,7 +2156,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   // Narrow frontiers: one workgroup finishes the mark (k_tail), or in a
   // sharded graph WALK_WG of them (k_walk, to larger frontiers).
   if (kn.tail) la.flags |= LV_TAIL;
-  const bool walk = (h->tp || kn.walk_unsharded) && kn.tail && kn.walk;
+  const bool walk = (h->tp || kn.walk_unsharded) && kn.tail && kn.walk && h->walk_ok;
   if (walk) la.flags |= LV_WALK;
   if (kn.cbits) la.flags |= LV_CBITS;
   if (kn.roots_co) la.flags |= LV_ROOTS_CO;
@@ -2202,14 +2216,22 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
     return hipSuccess;
   };
   size_t nl = 0, nc = 0;
+  h->lvl_timed.clear();
   auto launch = [&](int level, bool rootk) -> hipError_t {
     hipEvent_t ev[6] = {};
-    if (timing) {
+    // (mode 3: levels 0 and 1 of a trace from the pseudo-roots; a sharded
+    // round's levels after its first are narrow)
+    const bool timed = timing == 1 || timing == 2 || (timing == 3 && level <= 1);
+    h->lvl_timed.push_back(timed ? 1 : 0);
+    if (timed) {
       if (hipError_t r = new_event(h->lvl_ev, 6 * (nl + 1))) return r;
-      for (int k = timing >= 2 ? 0 : 4; k < 6; ++k) ev[k] = h->lvl_ev[6 * nl + k];
+      for (int k = timing == 2 ? 0 : 4; k < 6; ++k) ev[k] = h->lvl_ev[6 * nl + k];
     }
     la.level = level;
+    if (timing && !timed) la.flags |= LV_NOBYTES;
+    else la.flags &= ~LV_NOBYTES;
     hipError_t r = launch_level(h->g.d, la, rootk, investigate, vtop, h->stream, ev);
+    if (timed) ++lr.timed;
     ++nl;
     return r;
   };
@@ -2344,7 +2366,8 @@ static void collect_times(crgc_graph *h, LevelRun &lr, size_t nl, size_t nc, int
   }
   for (size_t i = 0; i < (timing ? nl : 0); ++i) {
     float t[3] = {0, 0, 0};
-    for (int k = timing >= 2 ? 0 : 2; k < 3; ++k)
+    if (i >= h->lvl_timed.size() || !h->lvl_timed[i]) continue;
+    for (int k = timing == 2 ? 0 : 2; k < 3; ++k)
       t[k] = elapsed_ms(h->lvl_ev[6 * i + 2 * k], h->lvl_ev[6 * i + 2 * k + 1], &lr.time_fail);
     lr.ms_f += t[0];
     lr.ms_t += t[1];
@@ -2980,7 +3003,7 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   crgc_trace_stats st{};
   st.edges_scanned = c.edges_scanned;
   st.sup_edges = c.sup_edges;
-  st.expand_launches = lr.launches;
+  st.expand_launches = lr.timed;  // (the launches whose expand was timed: ms_expand, expand_bytes)
   st.expand_bytes = c.expand_bytes;
   st.levels = lr.levels;
   st.launches = lr.launches;
@@ -3580,6 +3603,28 @@ int crgc_host_unregister(crgc_graph *h, void *ptr) {
       return CRGC_OK;
     }
   return CRGC_E_INVAL;
+}
+
+int crgc_usage_of(crgc_graph *h, crgc_usage *out) {
+  if (int rc = check_graph(h)) return rc;
+  if (!out) return CRGC_E_INVAL;
+  DeviceGuard dg(h->device);
+  HIP_TRY(sync_counters(h));
+  const Caps &c = h->g.caps;
+  *out = crgc_usage{};
+  out->slot_top = h->slot_top;
+  out->slot_cap = c.pbase;
+  out->proxy_top = h->proxy_top;
+  out->proxy_cap = c.scap - c.pbase;
+  out->free_slots = 0;
+  out->pool_top = h->pool_top;
+  out->pool_cap = c.pcap;
+  out->etab_used = h->etab_used;
+  out->etab_cap = c.ecap;
+  out->rebuilds = h->n_rebuild;
+  out->grows = h->n_grow;
+  out->repacks = h->n_repack;
+  return CRGC_OK;
 }
 
 int crgc_compact(crgc_graph *h) {

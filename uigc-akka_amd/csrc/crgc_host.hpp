@@ -169,6 +169,7 @@ constexpr uint32_t LV_WALK = 64;               // narrow frontiers go to WALK_WG
 constexpr uint32_t LV_CBITS = 128;             // a pull level hands the next level its candidates as bits (cb)
 constexpr uint32_t LV_SUPBIN = 512;            // the binned pseudo-root level's supervisor pushes go through the bins
 constexpr uint32_t LV_ROOTS_CO = 256;          // the pseudo-root pass reads receive counts lane-interleaved
+constexpr uint32_t LV_NOBYTES = 1024;          // an untimed level expand: its bytes stay out of the roofline
 
 struct LevelArgs {
   int level;
@@ -250,6 +251,7 @@ hipError_t launch_trace_reset(const DevGraph &g, uint64_t nh, uint64_t np, uint3
 hipError_t launch_sweep(const DevGraph &g, int should_kill, uint64_t slot_top, hipStream_t s,
                         int phase = 3);
 int level_grid(uint64_t slot_top);
+bool walk_fits(int device);
 hipError_t launch_publish(const Counters *c, Counters *hdst, uint32_t r0, uint32_t rn, hipStream_t s);
 hipError_t launch_copy_lists(const DevGraph &g, uint64_t *gdst, uint64_t gcap, uint64_t *kdst, uint64_t kcap,
                              hipStream_t s);

@@ -691,7 +691,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         }
       }
     }
-    expand_bytes_out(g, nb2);
+    expand_bytes_out(g, (a.flags & LV_NOBYTES) ? 0u : nb2);
     return;
   }
 
@@ -778,7 +778,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       nb2 += 2 * nb;
     }
   }
-  expand_bytes_out(g, nb2);
+  expand_bytes_out(g, (a.flags & LV_NOBYTES) ? 0u : nb2);
 }
 
 
@@ -1032,7 +1032,7 @@ __global__ __launch_bounds__(BIN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) v
   }
   if (binned)
     for (uint32_t k = tid; k < NB; k += BIN_T) a.bin_cnt[(uint64_t)k * G + wg] = min(lc[k], SC);
-  expand_bytes_out(g, nb2);
+  expand_bytes_out(g, (a.flags & LV_NOBYTES) ? 0u : nb2);
 }
 
 // BIN_SPLIT workgroups per bin, each over every BIN_SPLIT-th slice into a
@@ -1859,6 +1859,19 @@ __global__ __launch_bounds__(WALK_T) void k_walk(DevGraph g, LevelArgs a) {
   }
 }
 
+// Whether k_walk's WALK_WG workgroups can all be resident on `device` (its
+// grid barriers assume so).  Occupancy alone cannot promise it while other
+// streams keep CUs busy: CRGC_WALK stays a test hook, off by default.
+bool walk_fits(int device) {
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_walk, WALK_T, 0) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return (int64_t)per_cu * cus >= WALK_WG;
+}
+
 int level_grid(uint64_t slot_top) {
   const uint64_t blocks = (slot_top + BLK_SLOTS - 1) / BLK_SLOTS;  // wave-blocks
   uint64_t wg = (blocks + 3) / 4;
@@ -1889,15 +1902,12 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
   else frontier(k_frontier<false, false>);
   // level controller: the level count, and the narrow-frontier takeover
   if (a.flags & LV_WALK) {
-    // k_walk's grid barriers need all WALK_WG workgroups resident at once:
-    // a cooperative launch guarantees it (or fails) even when other handles'
-    // streams share the GPU (logical shards, side streams)
-    if (e[2]) (void)hipEventRecord(e[2], s);
-    void *args[] = {(void *)&g, (void *)&a};
-    const hipError_t ce =
-        hipLaunchCooperativeKernel((const void *)k_walk, dim3(WALK_WG), dim3(WALK_T), args, 0, s);
-    if (ce != hipSuccess) return ce;
-    if (e[3]) (void)hipEventRecord(e[3], s);
+    // (k_walk's grid barriers assume its WALK_WG workgroups are resident at
+    // once: the host enables it only when occupancy allows, walk_fits(); a
+    // workgroup that still never arrives fails the mark with ERR_WALK_STUCK.
+    // A cooperative launch would guarantee residency, but a process that had
+    // made one crashed in the runtime's exit handlers, profiles/r6a)
+    hipExtLaunchKernelGGL(k_walk, dim3(WALK_WG), dim3(WALK_T), 0, s, e[2], e[3], 0, g, a);
   } else
     hipExtLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, e[2], e[3], 0, g, a);
   // 8 WGs of 4 waves per CU
