@@ -154,8 +154,8 @@ def test_c3_chains_eight_shards(hip_mod, oracle_mod):
         g.close()
 
 
-@pytest.mark.parametrize("reg_chunks", ["1", "2"])
-def test_large_host_batches_chunked_and_registered(hip_mod, oracle_mod, monkeypatch, reg_chunks):
+@pytest.mark.parametrize("reg_chunks,sdma", [("1", "0"), ("2", "0"), ("1", "1"), ("2", "1")])
+def test_large_host_batches_chunked_and_registered(hip_mod, oracle_mod, monkeypatch, reg_chunks, sdma):
     """Host batches of >= 2^19 entries take the merge's host paths (crgc_api.hip
     crgc_merge_entries): a pageable batch is copied and merged in chunks, one
     merge per chunk with its own epoch (merge_entries_chunked); a batch in a
@@ -166,6 +166,7 @@ def test_large_host_batches_chunked_and_registered(hip_mod, oracle_mod, monkeypa
     from crgc_hip import HostArena
     monkeypatch.setenv("CRGC_BIN_MIN_SLOTS", "0")  # and the pseudo-root level binned at this size
     monkeypatch.setenv("CRGC_CHUNK_REG", reg_chunks)
+    monkeypatch.setenv("CRGC_REG_SDMA", sdma)  # 1: the chunks by DMA (one span each) instead of k_copy_ranges
     w = world.World(seed=0x5EED + 7)
     w.bulk_graph(200_000, 2_000_000)
     hp, hr, o = hip_mod.ShadowGraph(), hip_mod.ShadowGraph(), oracle_mod.OracleGraph()
@@ -191,13 +192,15 @@ def test_large_host_batches_chunked_and_registered(hip_mod, oracle_mod, monkeypa
     hr.unregister_host(arena.buf)
 
 
-def test_drain_loop_chunks_merged_async_from_registered_arena(hip_mod, oracle_mod):
+@pytest.mark.parametrize("sdma", ["0", "1"])
+def test_drain_loop_chunks_merged_async_from_registered_arena(hip_mod, oracle_mod, monkeypatch, sdma):
     """crgc_merge_entries_async: the drain loop packs a wakeup's entries into a
     registered arena chunk by chunk (LocalGC.scala:152-172) and hands each chunk
     over as soon as it is packed; the merges run while the next chunk is packed,
     and the arena is reused only after the trace.  Chunks merge in call order,
     so the graph equals the oracle's after the whole batch, and the traces too."""
     from crgc_hip import HostArena
+    monkeypatch.setenv("CRGC_REG_SDMA", sdma)
     w = world.World(seed=0x5EED + 9)
     w.bulk_graph(100_000, 1_000_000)
     h, o = hip_mod.ShadowGraph(), oracle_mod.OracleGraph()

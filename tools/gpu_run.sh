@@ -27,6 +27,7 @@
 #   lv:<variants>    per-level kernel times (CRGC_KERNEL_TIMING=2) over env variants, two passes (tools/lv_summary.py)
 #   ab:<variants>    tools/ab_bench.sh A/B of env variants on the C2 line
 #   abl:<variants>   the same after 100 warmup wakeups (a grown graph)
+#   abp:<variants>   tools/ab_pcie.sh A/B of env variants on the PCIe-inclusive legs (registered, drain loop)
 #   ab2l8:<variants> ab4l8:<variants>  tools/ab_l8.sh A/B of env variants on C2 / C4 logical shards
 #   longkt           kernel trace + level log of the long run
 #   long             C2 over 200 wakeups: the steady state, rebuilds / repacks amortized in
@@ -132,6 +133,9 @@ for step in "$@"; do
     abl:*)  # the same after 100 warmup wakeups (the live set grown to ~2.1e7: the long run's middle)
       read -ra vs <<< "${step#*:}"
       (cd "$ROOT" && AB_ARGS="--steps 10 --warmup 100" bash tools/ab_bench.sh "$TAG/ab_c2l" "${vs[@]}" > /dev/null) ;;
+    abp:*)  # tools/ab_pcie.sh: the PCIe-inclusive legs (pageable, registered, drain loop) over env variants
+      read -ra vs <<< "${step#*:}"
+      (cd "$ROOT" && bash tools/ab_pcie.sh "$TAG/ab_pcie" "${vs[@]}" > /dev/null) ;;
     ab2l8:*|ab4l8:*)  # tools/ab_l8.sh over the variants after the colon (separated by spaces)
       wl=${step%%l8:*}; wl=c${wl#ab}
       read -ra vs <<< "${step#*:}"

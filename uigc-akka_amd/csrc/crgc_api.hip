@@ -324,6 +324,11 @@ struct Knobs {
   bool bin512 = false;
   bool cbits = true;             // CRGC_CBITS=0: a pull level's finds go out as candidate bytes
   bool roots_co = true;          // CRGC_ROOTS_CO=0: the pseudo-root pass reads 128 B of counts per lane
+  // CRGC_REG_SDMA=1: a registered batch's chunk is copied by the DMA engines
+  // (one hipMemcpyAsync of the span its arrays occupy in the caller's arena)
+  // instead of read over PCIe by k_copy_ranges, which shares the memory
+  // pipeline with the merge kernels beside it (profiles/r4ab)
+  bool reg_sdma = false;
   void read() {
     auto env = [](const char *k) { return getenv(k); };
     if (const char *m = env("CRGC_KERNEL_TIMING")) kernel_timing = atoi(m);
@@ -378,6 +383,7 @@ struct Knobs {
     if (const char *m = env("CRGC_CHUNK_HOST")) chunk_host = atoi(m) != 0;
     if (const char *m = env("CRGC_CHUNK_MAX")) chunk_max = std::min<uint32_t>(8, std::max(2, atoi(m)));
     if (const char *m = env("CRGC_CHUNK_REG")) chunk_reg = std::min<uint32_t>(8, std::max(1, atoi(m)));
+    if (const char *m = env("CRGC_REG_SDMA")) reg_sdma = atoi(m) != 0;
     if (const char *m = env("CRGC_DEV_CHUNK")) {  // 0: the default
       dev_chunk = strtoull(m, nullptr, 10);
       if (dev_chunk) dev_chunk = std::max<uint64_t>(64, dev_chunk);
@@ -1558,6 +1564,11 @@ static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint3
   };
   Part p[CHUNK_MAX];
   size_t total = 0;
+  // (CRGC_REG_SDMA: a chunk's arrays as one span of the caller's arena, copied
+  // by one DMA; its staging region keeps the host addresses' offsets mod 256)
+  const bool sdma = registered && h->knobs.reg_sdma;
+  const char *span_lo[CHUNK_MAX] = {};
+  size_t span_at[CHUNK_MAX] = {}, span_len[CHUNK_MAX] = {};
   for (uint32_t j = 0; j < K; ++j) {
     Part &q = p[j];
     q.lo = (n * j / K) & ~63ull;  // 64-entry boundaries: every per-entry array's chunk is 64-B aligned
@@ -1572,6 +1583,27 @@ static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint3
                            b->created_owner + q.c0, b->created_target + q.c0, b->spawned_off + q.lo,
                            b->spawned + q.s0, b->updated_off + q.lo, b->updated_ref + q.u0,
                            b->updated_info + q.u0};
+    if (sdma) {
+      const char *lo = nullptr, *hi = nullptr;
+      size_t sum = 0;
+      for (int i = 0; i < 11; ++i)
+        if (sz[i]) {
+          const char *c = (const char *)src[i];
+          if (!lo || c < lo) lo = c;
+          if (!hi || c + sz[i] > hi) hi = c + sz[i];
+          sum += sz[i];
+        }
+      if (lo && (size_t)(hi - lo) <= 2 * sum + (1u << 20)) {  // a packed arena: one span
+        total = (total + 255) & ~(size_t)255;
+        span_lo[j] = lo;
+        span_at[j] = total + ((uintptr_t)lo & 255);
+        span_len[j] = (size_t)(hi - lo);
+        for (int i = 0; i < 11; ++i)
+          q.off[i] = sz[i] ? span_at[j] + (size_t)((const char *)src[i] - lo) : span_at[j];
+        total = span_at[j] + span_len[j];
+        continue;
+      }
+    }
     for (int i = 0; i < 11; ++i) {
       total = (total + 255) & ~(size_t)255;
       // a kernel copy wants the source's alignment mod 16 (the body in 16-B groups)
@@ -1597,7 +1629,10 @@ static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint3
                            b->updated_info + q.u0};
     const size_t sz[11] = {m * 8, m * 2, m, (m + 1) * 4, (q.c1 - q.c0) * 8, (q.c1 - q.c0) * 8, (m + 1) * 4,
                            (q.s1 - q.s0) * 8, (m + 1) * 4, (q.u1 - q.u0) * 8, (q.u1 - q.u0) * 2};
-    if (registered) {  // read over PCIe by a kernel (k_copy_ranges): no per-copy runtime overhead
+    if (span_lo[j]) {  // CRGC_REG_SDMA: the chunk's span in one DMA from the registered arena
+      hipError_t e = hipMemcpyAsync(base + span_at[j], span_lo[j], span_len[j], hipMemcpyHostToDevice, h->cpy);
+      if (e != hipSuccess) return e;
+    } else if (registered && !sdma) {  // read over PCIe by a kernel (k_copy_ranges): no per-copy runtime overhead
       HostCopy hc{};
       for (int i = 0; i < 11; ++i)
         if (sz[i]) {
