@@ -424,3 +424,65 @@ def test_failure_detail_names_the_call(hip_mod):
     g = hip_mod.ShadowGraph(vertex_capacity=1024, edge_capacity=4096)
     g.trace(True)
     assert abi.last_error_detail() == ""
+
+
+@pytest.mark.parametrize("reuse", ["1", "0"])
+def test_swept_slots_reused_match_oracle(hip_mod, oracle_mod, monkeypatch, reuse):
+    """Slot reuse (crgc_reuse.hip, round 6): after every committed sweep the
+    garbage slots are purged of their edges (keys tombstoned, in-edges left
+    with count 0, candidates and pull hints made inert), reset, and taken by
+    the next merges' new shadows — the reference's shadowMap.remove
+    (ShadowGraph.java:276) for dense slots.  A RandomSpec stream collects
+    thousands of actors while spawning new ones, so most slots are reused, some
+    several times; the graph and every trace must equal the oracle's, and the
+    slot range must stay near the live set.  CRGC_SLOT_REUSE=0 is the control
+    (slots reclaimed by rebuilds only)."""
+    monkeypatch.setenv("CRGC_SLOT_REUSE", reuse)
+    w = kats.RandomWorld(seed=31, max_actors=3000, wake_every=40)
+    h, o = _pair(hip_mod, oracle_mod, vertex_capacity=1 << 16, edge_capacity=1 << 16)
+    peak_live, collected = 0, 0
+    for batch in w.steps():
+        h.merge_entries(batch)
+        o.merge_entries(batch)
+        assert h.export() == o.export()
+        rh, ro = h.trace(True), o.trace(True)
+        _same_trace(rh, ro)
+        w.kill(ro.kill_set())
+        peak_live = max(peak_live, ro.n_live)
+        collected += len(ro.garbage)
+    assert h.total_actors_seen() == o.total_actors_seen()
+    u = h.usage()
+    seen = h.total_actors_seen()
+    assert collected > seen // 2  # most actors were collected along the way
+    if reuse == "1":
+        # new shadows took collected shadows' slots: the range stays near the
+        # peak live set (plus one wakeup's new shadows), far below the actors seen
+        assert u["slot_top"] <= 2 * peak_live + 256 < seen, (u, peak_live, seen)
+    else:
+        assert u["free_slots"] == 0 and u["slot_top"] == seen, (u, seen)  # (no rebuild below 65536 slots)
+    assert u["rebuilds"] == 0, u
+
+
+def test_swept_slots_reused_with_halted_supervisors(hip_mod, oracle_mod):
+    """Halted live shadows are never expanded (ShadowGraph.java:226-229), so a
+    sweep can collect their supervisors; before those slots are reused the
+    halted shadows' supervisor pointers become SLOT_DEAD (k_sup_fix), and the
+    exported supervisor stays the dead actor.  Entries, deltas and an undo log
+    (which halts a node's actors) over many wakeups, compared with the oracle
+    after every step."""
+    h, o = _pair(hip_mod, oracle_mod, vertex_capacity=4096, edge_capacity=4096)
+    fz = fuzz.Fuzz(57)
+    for step in range(24):
+        eb = fz.entries(300)
+        h.merge_entries(eb); o.merge_entries(eb)
+        if step % 3 == 1:
+            db = fz.deltas(6)
+            h.merge_deltas(db); o.merge_deltas(db)
+        if step in (6, 15):
+            ub = fz.undo(o.export().vertices.keys())
+            h.merge_undo(ub); o.merge_undo(ub)
+        assert h.export() == o.export()
+        _same_trace(h.trace(True), o.trace(True))
+        fz.sync(o.export())
+    assert h.total_actors_seen() == o.total_actors_seen()
+    assert h.export() == o.export()

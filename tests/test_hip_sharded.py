@@ -350,7 +350,12 @@ def test_c4_shape_eight_shards(sharded, oracle_mod, xbits, xlevels, ratio, xfilt
 
 @pytest.mark.parametrize("walk", [{"CRGC_WALK": "1"},
                                   {"CRGC_WALK": "1", "CRGC_WALK_START": "64", "CRGC_WALK_MAX": "128"},
-                                  {"CRGC_WALK": "1", "CRGC_WALK_START": "65536", "CRGC_WALK_MAX": "65536"}])
+                                  {"CRGC_WALK": "1", "CRGC_WALK_START": "65536", "CRGC_WALK_MAX": "65536"},
+                                  # k_tail (no k_walk) bounded by edge volume: tiny bounds, so
+                                  # takeovers are refused or bail at their first hubs (round 6)
+                                  {"CRGC_TAIL_EDGES": "64"},
+                                  {"CRGC_TAIL_EDGES": "512", "CRGC_TAIL_START": "65536",
+                                   "CRGC_TAIL_MAX": "65536"}])
 def test_c4_shape_eight_shards_walk_forms(sharded, oracle_mod, walk, monkeypatch):
     """A mark round's narrow levels by k_walk (WALK_WG workgroups with grid
     barriers; off by default, the level kernels and k_tail run them): at its

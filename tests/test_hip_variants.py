@@ -32,6 +32,10 @@ VARIANTS = [
     {"CRGC_BIN512": "1", "CRGC_BIN_MIN_SLOTS": "0"},  # binned level 0 with up to 512 bins of 2^16
     # candidate bits after every pull (level 0 included) with frequent k_tail bails
     {"CRGC_ALPHA": "1000000", "CRGC_TAIL_START": "1000000", "CRGC_TAIL_MAX": "64"},
+    # k_tail bounded by edge volume: no takeover of a frontier with more out-edges,
+    # and a walk whose round reaches hubs with more hands them back (round 6)
+    {"CRGC_TAIL_EDGES": "64"},
+    {"CRGC_TAIL_EDGES": "256", "CRGC_TAIL_START": "1000000", "CRGC_TAIL_MAX": "65536"},
 ]
 
 

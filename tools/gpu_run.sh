@@ -112,10 +112,13 @@ for step in "$@"; do
           -d "$O/ktl8s" -o kt -- python3 -u "$ROOT/bench.py" --workload c4 --logical-shards 8 --shared-stream \
           --actors 50000000 --edges 500000000 --batch 5000000 --no-cpu-baseline \
           --steps 2 --warmup 1 > "$O/bench_ktl8s.json" 2> "$O/bench_ktl8s.err") ;;
-    kt2l8s) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
-          -d "$O/kt2l8s" -o kt -- python3 -u "$ROOT/bench.py" --workload c2 --logical-shards 8 --shared-stream \
+    kt2l8s|kt2l8s:*)  # kt2l8s:K=V,K2=V2 runs it under those (test-hook) env settings
+      envs=(CRGC_TEST_HOOKS=1); sfx=""
+      if [ "$step" != kt2l8s ]; then IFS=',' read -ra ev <<< "${step#*:}"; envs+=("${ev[@]}"); sfx="_$(echo "${step#*:}" | tr '=,/' '___')"; fi
+      (cd /tmp && env "${envs[@]}" timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$O/kt2l8s$sfx" -o kt -- python3 -u "$ROOT/bench.py" --workload c2 --logical-shards 8 --shared-stream \
           --no-cpu-baseline \
-          --steps 4 --warmup 2 > "$O/bench_kt2l8s.json" 2> "$O/bench_kt2l8s.err") ;;
+          --steps 4 --warmup 2 > "$O/bench_kt2l8s$sfx.json" 2> "$O/bench_kt2l8s$sfx.err") ;;
     lv:*)  # per-level kernel times (all three level kernels timed) over env variants, two passes
       read -ra vs <<< "${step#*:}"
       for pass in 1 2; do

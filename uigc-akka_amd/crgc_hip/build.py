@@ -10,7 +10,7 @@ CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(PKG, "lib")
 SOURCES = ["crgc_api.hip", "crgc_merge.hip", "crgc_trace.hip", "crgc_rebuild.hip",
            "crgc_transport.hip", "crgc_route.hip", "crgc_delta.hip",
-           "crgc_undo.hip", "crgc_chain.hip", "crgc_edges.hip", "crgc_xchain.hip"]
+           "crgc_undo.hip", "crgc_chain.hip", "crgc_edges.hip", "crgc_xchain.hip", "crgc_reuse.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall",
          "-Wno-unused-function", "-Wno-unused-result", "-Wno-unused-value", "-munsafe-fp-atomics"]

@@ -50,7 +50,7 @@ void free_arrays(Arrays &a) {
                 d.dirty[0], d.dirty[1], d.out_a, d.out_b, d.qn_buf, d.qh_buf, d.qn_tag, d.blkstat, d.xbytes,
                 d.sweep_cnt, d.sweep_off, d.out_ids, d.out_kill,
                 d.nzdeg, d.radj, d.rnew, d.rpool, d.par, d.fx, d.cb, d.cb2, d.tq, d.tl_buf, d.tl_tag, d.cm, d.pb[0], d.pb[1],
-                d.xsent, d.xkey, d.wpc, d.rq_buf, d.rq_cnt, d.phs, d.psh};
+                d.xsent, d.xkey, d.wpc, d.rq_buf, d.rq_cnt, d.phs, d.psh, d.freel, d.freel2, d.gslot};
   for (void *p : ps)
     if (p) hipFree(p);
   a.allocated = false;
@@ -58,7 +58,7 @@ void free_arrays(Arrays &a) {
 }
 
 hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, uint32_t n_shards,
-                        uint32_t shard, bool sharded) {
+                        uint32_t shard, bool sharded, bool reuse) {
   a.caps = c;
   DevGraph &d = a.d;
   d = DevGraph{};
@@ -128,6 +128,11 @@ hipError_t alloc_arrays(Arrays &a, const Caps &c, Counters *ctr, hipStream_t s, 
   A(dmalloc(&d.cm, c.scap / 32));
   A(dmalloc(&d.pb[0], c.scap / 32));
   A(dmalloc(&d.pb[1], c.scap / 32));
+  if (reuse && !sharded) {  // slot reuse (crgc_reuse.hip): the free list, its successor, garbage slots
+    A(dmalloc(&d.freel, c.scap));
+    A(dmalloc(&d.freel2, c.scap));
+    A(dmalloc(&d.gslot, c.scap));
+  }
   if (sharded) {
     A(dmalloc(&d.xsent, c.scap / 32));
     A(dmalloc(&d.xkey, c.scap));
@@ -264,6 +269,12 @@ struct Knobs {
   // CRGC_TAIL_MAX set both forms.
   uint32_t tail_start_sharded = 2048;
   uint32_t tail_max_sharded = 4096;
+  // k_tail walks frontiers of at most this many out-edges per round (0: no
+  // bound).  A shard's hubs are mostly edges to proxies, each a global claim
+  // by the one workgroup: C2 over 8 logical shards spent 2.1 of its 3.4 ms of
+  // k_tail per wakeup in ~11 walks of 230-275 us (profiles/r6b).  CRGC_TAIL_EDGES
+  uint32_t tail_edges = 0;
+  uint32_t tail_edges_sharded = 32768;
   // k_walk (WALK_WG workgroups with grid barriers) in place of k_tail for a
   // sharded graph's narrow levels: correct, and slower as measured (C4 at half
   // size over 8 logical shards 33.0 -> 36.4 ms per wakeup, GPU work 38.4 ->
@@ -324,11 +335,17 @@ struct Knobs {
   bool bin512 = false;
   bool cbits = true;             // CRGC_CBITS=0: a pull level's finds go out as candidate bytes
   bool roots_co = true;          // CRGC_ROOTS_CO=0: the pseudo-root pass reads 128 B of counts per lane
-  // CRGC_REG_SDMA=1: a registered batch's chunk is copied by the DMA engines
-  // (one hipMemcpyAsync of the span its arrays occupy in the caller's arena)
-  // instead of read over PCIe by k_copy_ranges, which shares the memory
-  // pipeline with the merge kernels beside it (profiles/r4ab)
-  bool reg_sdma = false;
+  // A registered batch's chunk is copied by the DMA engines (one
+  // hipMemcpyAsync of the span its arrays occupy in the caller's arena) rather
+  // than read over PCIe by k_copy_ranges, which shares the memory pipeline with
+  // the merge kernels beside it (profiles/r4ab): registered C2 wakeup 2.09 /
+  // 2.14 against 2.17 / 2.27 ms, merge call 0.81 / 0.84 against 0.91 / 0.99 ms,
+  // interleaved on one box (profiles/r6c).  CRGC_REG_SDMA=0: the kernel copy.
+  bool reg_sdma = true;
+  // CRGC_SLOT_REUSE=0: collected shadows' slots are reclaimed only by a rebuild
+  // (round 5); by default the sweep's garbage slots are purged of their edges
+  // and taken by the next merges' new shadows (crgc_reuse.hip)
+  bool slot_reuse = true;
   void read() {
     auto env = [](const char *k) { return getenv(k); };
     if (const char *m = env("CRGC_KERNEL_TIMING")) kernel_timing = atoi(m);
@@ -351,6 +368,7 @@ struct Knobs {
     if (const char *m = env("CRGC_TAIL")) tail = atoi(m) != 0;
     if (const char *m = env("CRGC_TAIL_START")) tail_start = tail_start_sharded = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_TAIL_MAX")) tail_max = tail_max_sharded = (uint32_t)strtoul(m, nullptr, 10);
+    if (const char *m = env("CRGC_TAIL_EDGES")) tail_edges = tail_edges_sharded = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_WALK")) walk = atoi(m) != 0;
     if (const char *m = env("CRGC_WALK_UNSHARDED")) walk_unsharded = atoi(m) != 0;
     if (const char *m = env("CRGC_WALK_START")) walk_start = (uint32_t)strtoul(m, nullptr, 10);
@@ -384,6 +402,7 @@ struct Knobs {
     if (const char *m = env("CRGC_CHUNK_MAX")) chunk_max = std::min<uint32_t>(8, std::max(2, atoi(m)));
     if (const char *m = env("CRGC_CHUNK_REG")) chunk_reg = std::min<uint32_t>(8, std::max(1, atoi(m)));
     if (const char *m = env("CRGC_REG_SDMA")) reg_sdma = atoi(m) != 0;
+    if (const char *m = env("CRGC_SLOT_REUSE")) slot_reuse = atoi(m) != 0;
     if (const char *m = env("CRGC_DEV_CHUNK")) {  // 0: the default
       dev_chunk = strtoull(m, nullptr, 10);
       if (dev_chunk) dev_chunk = std::max<uint64_t>(64, dev_chunk);
@@ -471,6 +490,10 @@ struct crgc_graph {
   };
   std::vector<Pinned> pinned;
 };
+
+// Slot reuse (crgc_reuse.hip): unsharded graphs (a sharded graph's proxies
+// cache their homes' slots), unless CRGC_SLOT_REUSE=0.
+static bool reuse_on(const crgc_graph *h) { return h->G <= 1 && !h->tp && h->knobs.slot_reuse; }
 
 namespace {
 thread_local int api_depth = 0;
@@ -606,7 +629,7 @@ int grow(crgc_graph *h, uint64_t ids, uint64_t atoms) {
             (unsigned long long)c.hcap, (unsigned long long)h->g.caps.ecap, (unsigned long long)c.ecap,
             (unsigned long long)h->g.caps.pcap, (unsigned long long)c.pcap);
   Arrays dst;
-  HIP_TRY(alloc_arrays(dst, c, h->ctr, h->stream, h->G, h->shard, h->tp != nullptr));
+  HIP_TRY(alloc_arrays(dst, c, h->ctr, h->stream, h->G, h->shard, h->tp != nullptr, reuse_on(h)));
   const DevGraph &o = h->g.d;
   DevGraph &d = dst.d;
   hipError_t e = hipSuccess;
@@ -623,9 +646,12 @@ int grow(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   cp(d.nzdeg, o.nzdeg, top * 4);
   cp(d.radj, o.radj, top * 8);
   cp(d.par, o.par, top * 4);
+  if (d.freel && o.freel) cp(d.freel, o.freel, top * 4);  // (the list holds slots below slot_top)
   cp(d.pool, o.pool, h->pool_top * 8);
   cp(d.rpool, o.rpool, h->rpool_top * 4);
   if (e == hipSuccess) e = launch_grow_tables(o, d, h->stream);
+  // (the re-hashed id table has no tombstones left: reused slots' ids no longer load it)
+  if (e == hipSuccess) e = hipMemsetAsync((char *)h->ctr + CTR_OFF(reused), 0, 8, h->stream);
   if (e == hipSuccess) e = carry_lists(h, dst);
   if (e == hipSuccess) e = sync_counters(h);
   if (e != hipSuccess) {
@@ -669,7 +695,7 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms, bool may_grow = false) 
             (unsigned long long)h->etab_used, (unsigned long long)h->g.caps.ecap, (unsigned long long)c.scap,
             (unsigned long long)c.pcap, (unsigned long long)c.ecap);
   Arrays dst;
-  HIP_TRY(alloc_arrays(dst, c, h->ctr, h->stream, h->G, h->shard, h->tp != nullptr));
+  HIP_TRY(alloc_arrays(dst, c, h->ctr, h->stream, h->G, h->shard, h->tp != nullptr, reuse_on(h)));
   Scratch tmp;
   const size_t need = Carver::need({h->g.caps.scap * 4 + 4, c.scap * 8, rebuild_scan_tmp_bytes(c.scap)});
   if (tmp.ensure(need) != hipSuccess) {
@@ -683,7 +709,8 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms, bool may_grow = false) 
   hipError_t e = hipMemsetAsync(offs, 0, c.scap * 8, h->stream);
   // new generation counters: slot_top, pool_top, etab_used, the proxy region's restart
   for (size_t off : {CTR_OFF(slot_top), CTR_OFF(pool_top), CTR_OFF(rpool_top), CTR_OFF(etab_used),
-                     CTR_OFF(proxy_top), CTR_OFF(proxy_dead), CTR_OFF(res_top)})
+                     CTR_OFF(proxy_top), CTR_OFF(proxy_dead), CTR_OFF(res_top), CTR_OFF(free_n),
+                     CTR_OFF(free_used), CTR_OFF(reused)})
     if (e == hipSuccess) e = hipMemsetAsync((char *)h->ctr + off, 0, 8, h->stream);
   // src keeps a view of the old counters' bounds via src_top / src_ptop (passed by value)
   if (e == hipSuccess) e = launch_rebuild(h->g.d, src_top, src_ptop, dst.d, map, offs, scan_tmp, h->stream);
@@ -758,10 +785,14 @@ int ensure_capacity(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   };
   // (new shadows fill the shadows' region, new proxies the proxy region; `ids`
   // bounds either)
+  // (slot reuse: the id table also holds the tombstones of the collected ids
+  // whose slots new shadows took since its last rehash — reused, plus the
+  // merges' takes since the last reclaim — which slot_top no longer bounds)
+  const uint64_t tomb = h->g.d.freel ? h->hctr->reused + h->hctr->free_used : 0;
   auto rest_fits = [&](uint64_t st, uint64_t pt, uint64_t eu) {
     const Caps &c = h->g.caps;
     return st + ids <= c.pbase && (h->G <= 1 || pt + ids <= c.scap - c.pbase) &&
-           (st + pt + ids) * 10 <= c.hcap * 7 && (eu + atoms) * 10 <= c.ecap * 7;
+           (st + pt + ids + tomb) * 10 <= c.hcap * 7 && (eu + atoms) * 10 <= c.ecap * 7;
   };
   // upper bounds since the last sync (an unsharded graph has no proxies: its
   // pending ids are counted once, in st)
@@ -954,7 +985,7 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
     // like the shadows' region
     const uint64_t p0 = cfg && cfg->proxy_capacity ? cfg->proxy_capacity : v0;
     Caps c = caps_create(v0, p0, h->G > 1, e0, h->knobs.idtab_x2);
-    if (hipError_t e = alloc_arrays(h->g, c, h->ctr, h->stream, h->G, h->shard, h->tp != nullptr)) {
+    if (hipError_t e = alloc_arrays(h->g, c, h->ctr, h->stream, h->G, h->shard, h->tp != nullptr, reuse_on(h))) {
       rc = map_hip(e);
       break;
     }
@@ -2201,6 +2232,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   la.chain_after = h->tp ? 0 : kn.chain_after;
   la.xslices = kn.xslices;
   la.tail_start = std::min<uint32_t>(walk ? kn.walk_start : h->tp ? kn.tail_start_sharded : kn.tail_start, TAIL_QCAP);
+  la.tail_edge_max = walk ? 0u : h->tp ? kn.tail_edges_sharded : kn.tail_edges;
   la.tail_max = std::min<uint32_t>(std::max(walk ? kn.walk_max : h->tp ? kn.tail_max_sharded : kn.tail_max, 1u),
                                    TAIL_QCAP);
   // The pseudo-root level's binned push (crgc_trace.hip k_bin_place / k_bin_apply):
@@ -3064,6 +3096,13 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   h->last_stats = st;
   out->stats = st;
+  // Reclaim the garbage slots for the next merges' new shadows
+  // (crgc_reuse.hip): queued behind the trace, so it runs while the caller
+  // takes the results, and the next merge on this stream starts after it.
+  if (rc == CRGC_OK && h->g.d.freel && c.n_garbage) {
+    HIP_TRY(launch_reclaim(h->g.d, h->slot_top, c.n_garbage, c.free_n, h->stream));
+    std::swap(h->g.d.freel, h->g.d.freel2);
+  }
   // Keep the slot space dense: rebuild once dead slots outnumber live ones in
   // the shadows' region, or (sharded graphs) in the proxy region.
   const uint64_t ptop = c.proxy_top;
@@ -3651,7 +3690,7 @@ int crgc_usage_of(crgc_graph *h, crgc_usage *out) {
   out->slot_cap = c.pbase;
   out->proxy_top = h->proxy_top;
   out->proxy_cap = c.scap - c.pbase;
-  out->free_slots = 0;
+  out->free_slots = h->hctr->free_n - std::min(h->hctr->free_used, h->hctr->free_n);
   out->pool_top = h->pool_top;
   out->pool_cap = c.pcap;
   out->etab_used = h->etab_used;

@@ -178,6 +178,8 @@ struct LevelArgs {
   uint32_t pull_div;       // else: after a frontier of >= slot_top / pull_div shadows
   uint32_t tail_start;     // k_tail takes over after a level of <= this many shadows
   uint32_t tail_max;       // ... whose candidates number <= this, and bails above it
+  uint32_t tail_edge_max;  // ... and whose frontier has <= this many out-edges; a later round of the
+                           // walk with more bails too (one workgroup's global claims: ~1 G edges/s); 0: no bound
   uint32_t frontier_grid;  // workgroups of k_frontier (set by launch_level)
   uint32_t flags;          // LV_*
   uint32_t pull_cur_div;   // alpha == 0: k_expand also pulls once the current frontier is >= slot_top / div
@@ -328,6 +330,10 @@ size_t rebuild_scan_tmp_bytes(uint64_t n);
 // grow: both hash tables of `src` re-hashed into `dst`'s (larger) ones; the
 // caller copies the per-slot arrays and the pools (same slots, same offsets)
 hipError_t launch_grow_tables(const DevGraph &src, const DevGraph &dst, hipStream_t s);
+// crgc_reuse.hip: after a committed sweep, purge the garbage slots and list
+// them free for the next merges (unsharded graphs; no-op without a free list)
+hipError_t launch_reclaim(const DevGraph &g, uint64_t slot_top, uint64_t n_garbage, uint64_t n_free,
+                          hipStream_t s);
 // the pools alone, packed into pool2 / rpool2 (pp / rp: scap u64 each; scan_tmp:
 // 2 x rebuild_scan_tmp_bytes(scap)); slots and tables unchanged
 hipError_t launch_repack(const DevGraph &g, uint64_t top, uint64_t ptop, uint64_t *pp, uint64_t *rp, void *scan_tmp,

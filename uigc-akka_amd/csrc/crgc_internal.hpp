@@ -130,6 +130,13 @@ struct Counters {
   unsigned long long proxy_dead;     // ... of which invalidated (their home collected the actor)
   unsigned long long res_top;        // proxies below pbase + res_top have asked their homes (resolution)
   unsigned long long alive_cnt[2];   // a rebuild's kept shadows / proxies (k_rb_count_alive)
+  // Slot reuse (unsharded graphs, crgc_reuse.hip): slots of collected shadows,
+  // purged of their edges after the sweep, wait in DevGraph::freel[0 .. free_n)
+  // for the next merges' new shadows, which take them in order (free_used).
+  unsigned long long free_n;
+  unsigned long long free_used;
+  unsigned long long reused;         // slots taken from the list since the id table's last rehash
+                                     // (their collected ids' tombstones load the table)
   // per-merge lists (reset together before every edge pipeline)
   unsigned long long err;
   unsigned long long spin_max;
@@ -205,6 +212,9 @@ struct DevGraph {
   unsigned long long *vseq;  // last-write-wins tag for busy/root
   unsigned long long *sseq;  // last-write-wins tag for supervisor
   uint32_t *nzdeg;           // out-edges with count != 0 (reference `outgoing.size()`)
+  // slot reuse (unsharded; nullptr when off): the free list, the next one being
+  // built (ping-pong), and the last sweep's garbage slots (dense)
+  uint32_t *freel, *freel2, *gslot;
   // reverse candidates (pull BFS): owners that ever created an edge key to the
   // slot; a candidate is verified against the forward count when used
   uint2 *radj;               // {offset, rlen | log2(capacity) << RLEN_BITS} into rpool (rseg_*)

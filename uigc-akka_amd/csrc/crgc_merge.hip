@@ -116,9 +116,24 @@ __global__ __launch_bounds__(IDS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 
       // otherwise all go through k_rv_grow's overflow path (crgc_edges.hip §3).
       // Homes take slots from slot_top, proxies (sharded graphs) from proxy_top
       // in their own region above pbase.
+      // Slot reuse (unsharded): new shadows take the swept slots of the free
+      // list first (crgc_reuse.hip; the list is fixed during a merge, so the
+      // taken count may pass its end), then fresh slots from slot_top.
+      uint32_t nfree = 0;
+      unsigned long long kf = 0;
+      const bool reuse = g.freel != nullptr;
+      if (reuse) {
+        unsigned long long *const fc[1] = {&g.ctr->free_used};
+        const uint64_t fn = g.ctr->free_n;
+        const uint32_t vf[1] = {nhome};
+        unsigned long long bf[1];
+        block_append<1>(fc, vf, bf);
+        kf = bf[0];
+        nfree = kf >= fn ? 0u : (uint32_t)min<uint64_t>(nhome, fn - kf);
+      }
       unsigned long long *const ctrs[4] = {&g.ctr->slot_top, &g.ctr->inserted, &g.ctr->rpool_top,
                                            &g.ctr->proxy_top};
-      const uint32_t v[4] = {nhome, nhome, nins * IDS_RCAP, nins - nhome};
+      const uint32_t v[4] = {nhome - nfree, nhome, nins * IDS_RCAP, nins - nhome};
       unsigned long long base[4];
       block_append<4>(ctrs, v, base);
       unsigned long long kh = base[0], kp = base[3], ro = base[2];
@@ -127,7 +142,13 @@ __global__ __launch_bounds__(IDS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 
       for (int j = 0; j < IDS_K; ++j) {
         if (st[j] != RS_INSERTED) continue;
         const bool home = is_home(g, id[j]);
-        const uint64_t s = region_slot(g, home, home ? kh++ : kp++);
+        uint64_t s;
+        if (home && nfree) {  // a purged slot of a collected shadow (reset by k_free_list)
+          s = g.freel[kf++];
+          --nfree;
+        } else {
+          s = region_slot(g, home, home ? kh++ : kp++);
+        }
         if (s == ~0ull) {
           set_err(g.ctr, ERR_SLOTS_FULL);
           slot[j] = SLOT_INVALID;

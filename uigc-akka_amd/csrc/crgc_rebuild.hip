@@ -393,7 +393,7 @@ __global__ __launch_bounds__(256) void k_gr_edges(DevGraph src, DevGraph dst) {
   for (uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x; b < src.ecap_tab; b += stride) {
     const uint4 k4 = load_bucket(&src.etab[b]);
     const uint64_t key = bucket_key(k4);
-    if (key == KEY_EMPTY) continue;
+    if (key == KEY_EMPTY || key == KEY_TOMB) continue;  // (TOMB: an edge of a reused slot, purged)
     uint64_t h = mix64(key) & dst.emask;
     for (uint64_t p = 0; p < dst.ecap_tab; ++p) {
       if (atomicCAS((unsigned long long *)&dst.etab[h].key, (unsigned long long)KEY_EMPTY,

@@ -1279,10 +1279,14 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
   uint8_t *Db = g.dirty[L & 1];
   bool first = true;
   __shared__ uint32_t s_deep;  // a walk ran chain_after links: hand the rest to chain mode
+  __shared__ uint32_t s_bail;  // this round's hubs had more than tail_edge_max edges: they went back
+  __shared__ uint32_t s_back;  // ... this many of them, as candidates of level L+2
+  if (threadIdx.x == 0) s_back = 0;
   for (;;) {
     if (threadIdx.x == 0) {
       *sh.next = 0;
       s_deep = 0;
+      s_bail = 0;
     }
     __syncthreads();
     for (uint32_t c0 = 0; c0 < n; c0 += TAIL_THREADS) {
@@ -1346,6 +1350,26 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
       if (__syncthreads_or(heavy)) {  // heavy shadows: the workgroup shares their edges
         uint32_t total;
         const uint32_t st = tail_scan(heavy ? ad.y : 0u, sh.w, total);
+        if (!first && a.tail_edge_max && total > a.tail_edge_max) {
+          // Hubs reached by the walk (a sharded graph's hubs: mostly edges to
+          // proxies, each a global claim): this one workgroup would take
+          // ~1 us per 1000 edges, the level kernels spread them over the
+          // chip.  The hubs go back unexpanded, as candidates of level L+2
+          // (k_frontier marks them again and k_expand walks their edges), and
+          // the round ends in a bail.  (They were claimed, and counted, in the
+          // previous round; the first round's frontier was bounded at the
+          // takeover.)
+          if (heavy) {
+            atomicAnd(LV ? &sh.vis[v >> 5] : &g.vis[v >> 5], ~(1u << (v & 31)));
+            Fb[v] = 1;
+            Db[v >> 11] = 1;
+            --o.claims;
+            atomicAdd(&s_back, 1u);
+          }
+          if (threadIdx.x == 0) s_bail = 1;
+          __syncthreads();
+          continue;
+        }
         sh.start[threadIdx.x] = st;
         sh.off[threadIdx.x] = ad.x;
         __syncthreads();
@@ -1376,8 +1400,8 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
     const uint32_t nn = *sh.next;
     first = false;
     ++o.rounds;
-    if (nn == 0) break;
-    if (nn > a.tail_max) {
+    if (nn == 0 && !s_bail) break;
+    if (nn > a.tail_max || s_bail) {
       // hand the pending shadows to the level kernels as level L+2 candidates
       const uint32_t m = min(nn, (uint32_t)TAIL_QCAP);
       for (uint32_t i = threadIdx.x; i < m; i += TAIL_THREADS) {
@@ -1387,7 +1411,7 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
         Db[t >> 11] = 1;
       }
       o.bailed = true;
-      n = m;
+      n = m + s_back;  // (the hubs handed back are candidates of level L+2 too)
       break;
     }
     if (s_deep && nn <= a.tail_max) {
@@ -1446,7 +1470,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(DevGraph g, LevelArgs a) 
     n0 += s_red[k];
     mf += s_red[16 + k];
   }
-  if (!listing_level(c, L, a) || n0 == 0 || n0 > a.tail_start) {
+  if (!listing_level(c, L, a) || n0 == 0 || n0 > a.tail_start || (a.tail_edge_max && mf > a.tail_edge_max)) {
     if (threadIdx.x == 0) {  // the level kernels go on
       c->mf_level = mf;
       c->mf_sum += mf;
@@ -2181,6 +2205,7 @@ __global__ __launch_bounds__(256) void k_sweep_gather(DevGraph g) {
         id_find(g, id, &bucket);
         if (bucket != KEY_EMPTY) g.htab[bucket].key = KEY_TOMB;
         g.flags[v] = 0;
+        if (g.gslot) g.gslot[go + i] = v;  // slot reuse: purged and listed free (crgc_reuse.hip)
       }
     }
     for (uint32_t i = lane_id(); i < kn; i += 64) g.out_kill[ko + i] = g.vid[ka[i]];
