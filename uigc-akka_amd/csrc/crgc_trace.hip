@@ -1294,6 +1294,7 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
       bool have = i < n;
       uint32_t v = have ? cur.get(i) : 0;
       bool vfirst = first;
+      bool vsup = false;  // the last shadow walked had its supervisor edge counted here (n_sup)
       uint2 ad = make_uint2(0, 0);
       uint32_t steps = 0;
       while (have) {
@@ -1314,12 +1315,14 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
         if (expand) {
           ad = adv;
           const uint32_t s = supv;
+          vsup = false;
           if (s < 0xFFFFFFF0u) {
             if (vfirst) {
               Fn[s] = 0;
               Dn[s >> 11] = 0;
             } else {
               ++o.n_sup;
+              vsup = true;
             }
             tg[0] = s;
             valid = 1;
@@ -1364,6 +1367,7 @@ __device__ inline void tail_rounds(const DevGraph &g, const LevelArgs &a, const 
             Fb[v] = 1;
             Db[v >> 11] = 1;
             --o.claims;
+            if (vsup) --o.n_sup;  // k_frontier(L+2) follows (and counts) its supervisor edge again
             atomicAdd(&s_back, 1u);
           }
           if (threadIdx.x == 0) s_bail = 1;
