@@ -473,6 +473,7 @@ struct crgc_graph {
   Scratch x_gvis;            // every shard's marked bitmap of its shadows (mark_all's send filter)
   Scratch x_wgc;             // k_xscan's per-workgroup counts
   uint64_t *h_small = nullptr;       // pinned host staging for small all-gathers
+  uint64_t *h_small_dev = nullptr;   // its device view (ag_u64 reads host words from it)
   uint64_t *h_bounce = nullptr;      // pinned bounce for id lists into partly pinned caller buffers
   uint64_t h_bounce_bytes = 0;
   char *h_route = nullptr;           // pinned RoutePart / ConcatPart tables
@@ -979,6 +980,10 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
       rc = DEV_FAIL("");
       break;
     }
+    if (hipHostGetDevicePointer((void **)&h->h_small_dev, h->h_small, 0) != hipSuccess) {
+      (void)hipGetLastError();  // (ag_u64 then copies host words by the runtime)
+      h->h_small_dev = nullptr;
+    }
     const uint64_t v0 = cfg && cfg->vertex_capacity ? cfg->vertex_capacity : (1u << 16);
     const uint64_t e0 = cfg && cfg->edge_capacity ? cfg->edge_capacity : 8 * v0;
     // a shard's proxy region from its own hint (ABI 5); without one it is sized
@@ -1126,6 +1131,8 @@ struct SideFork {
 namespace {
 // ---- sharded graphs: collective helpers ---------------------------------------
 // All-gather K u64 per shard: `parts` device sources concatenated -> out[G*K] (host).
+constexpr size_t SMALL_BYTES = 8 * (size_t)MAX_SHARDS * (MAX_SHARDS + 8);  // h_small
+
 static int ag_u64(crgc_graph *h, std::initializer_list<std::pair<const void *, uint32_t>> parts,
                   uint64_t *out) {
   uint32_t K = 0;
@@ -1133,10 +1140,25 @@ static int ag_u64(crgc_graph *h, std::initializer_list<std::pair<const void *, u
   const size_t bytes = (size_t)K * 8;
   if (h->x_small.ensure(bytes * (h->G + 1)) != hipSuccess) return CRGC_E_NOMEM;
   char *snd = (char *)h->x_small.ptr, *rcv = snd + bytes;
-  size_t at = 0;
+  // one gather kernel (device words, or host words through h_small's device view)
+  const uint64_t *src[8];
+  uint32_t cnt[8], k = 0;
+  bool kern = parts.size() <= 8 && h->h_small_dev;
   for (auto &p : parts) {
-    HIP_TRY(hipMemcpyAsync(snd + at, p.first, (size_t)p.second * 8, hipMemcpyDefault, h->stream));
-    at += (size_t)p.second * 8;
+    if (!kern) break;
+    const char *c = (const char *)p.first, *hs = (const char *)h->h_small;
+    if (c >= hs && c < hs + SMALL_BYTES) c = (const char *)h->h_small_dev + (c - hs);
+    src[k] = (const uint64_t *)c;
+    cnt[k++] = p.second;
+  }
+  if (kern) {
+    HIP_TRY(gather_u64_parts(src, cnt, k, (uint64_t *)snd, h->stream));
+  } else {
+    size_t at = 0;
+    for (auto &p : parts) {
+      HIP_TRY(hipMemcpyAsync(snd + at, p.first, (size_t)p.second * 8, hipMemcpyDefault, h->stream));
+      at += (size_t)p.second * 8;
+    }
   }
   if (int rc = h->tp->allgather(h->shard, snd, rcv, bytes, h->stream)) {
     h->poisoned = true;
@@ -1155,6 +1177,7 @@ static int ag_u64(crgc_graph *h, std::initializer_list<std::pair<const void *, u
 // All-gather K host u64 per shard -> out[G*K] (host).
 static int ag_host(crgc_graph *h, const uint64_t *vals, uint32_t K, uint64_t *out) {
   memcpy(h->h_small, vals, (size_t)K * 8);
+  if (h->h_small_dev && (size_t)K * 8 <= SMALL_BYTES) return ag_u64(h, {{h->h_small, K}}, out);
   if (h->x_small.ensure((size_t)K * 8 * (h->G + 2)) != hipSuccess) return CRGC_E_NOMEM;
   char *tmp = (char *)h->x_small.ptr + (size_t)K * 8 * (h->G + 1);
   HIP_TRY(hipMemcpyAsync(tmp, h->h_small, (size_t)K * 8, hipMemcpyHostToDevice, h->stream));
@@ -1274,7 +1297,6 @@ extern "C" {
 // they fit: a copy into pageable memory is staged and waited for inside the
 // runtime, on its blocking wait (not our polling one, crgc_internal.hpp).
 // `off` keeps a read clear of the words an all-gather in flight uses.
-constexpr size_t SMALL_BYTES = 8 * (size_t)MAX_SHARDS * (MAX_SHARDS + 8);
 constexpr size_t SMALL_XFLAG_OFF = SMALL_BYTES / 2;
 constexpr size_t SMALL_PEND_OFF = SMALL_BYTES - 64;  // a mark round's pending word (mark_all)
 static hipError_t d2h_small(crgc_graph *h, void *dst, const void *src, size_t bytes, size_t off = 0) {
@@ -1833,7 +1855,12 @@ static int merge_entries(crgc_graph *h, const crgc_entry_batch *b, bool async) {
   if (int rc = check_graph(h)) return rc;
   DeviceGuard dg(h->device);
   uint64_t C = 0, S = 0, U = 0;
-  const int vrc = entry_counts(h, b, h->tp, &C, &S, &U);
+  // A routed sharded merge needs no exact record counts of a device batch (the
+  // route kernels read the offsets and check them against n*F, as an unsharded
+  // merge does): one host round trip less per merge.  The all-gather form
+  // sizes its copies by them.
+  const bool routed = h->tp && h->route && h->G <= ROUTE_MAX_SHARDS && h->F <= ROUTE_MAX_F;
+  const int vrc = entry_counts(h, b, h->tp && !routed, &C, &S, &U);
   if (!h->tp) {
     if (vrc) return vrc;
     if (b->memory == CRGC_MEM_DEVICE && b->n_entries > (h->knobs.dev_chunk ? h->knobs.dev_chunk : DEV_CHUNK) &&
@@ -1855,8 +1882,7 @@ static int merge_entries(crgc_graph *h, const crgc_entry_batch *b, bool async) {
     }
     return merge_entries_one(h, b, C, S, U);
   }
-  if (h->route && h->G <= ROUTE_MAX_SHARDS && h->F <= ROUTE_MAX_F)
-    return merge_entries_routed(h, b, vrc, C, S, U);
+  if (routed) return merge_entries_routed(h, b, vrc, C, S, U);
   // Sharded: every shard applies its part of every shard's batch, in shard order.
   const uint64_t n = vrc ? 0 : b->n_entries;
   const uint64_t hdr[5] = {(uint64_t)(int64_t)vrc, n, C, S, U};

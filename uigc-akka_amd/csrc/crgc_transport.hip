@@ -58,6 +58,37 @@ static hipError_t copy_segs(const Segs &sg, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Small all-gathers' send words (counters, flags, host words) gathered into
+// one buffer by one kernel: a runtime copy per part was a ~3 us blit kernel
+// each (~50 per shard and C2 wakeup over 8 logical shards, profiles/r6b).
+// Parts are device memory or pinned host memory's device view.
+struct U64Parts {
+  const uint64_t *p[8];
+  uint32_t n[8];
+  uint32_t k;
+};
+
+__global__ __launch_bounds__(256) void k_gather_u64(U64Parts a, uint64_t *dst) {
+  uint32_t off = 0;
+  for (uint32_t j = 0; j < a.k; ++j) {
+    for (uint32_t i = threadIdx.x; i < a.n[j]; i += 256) dst[off + i] = a.p[j][i];
+    off += a.n[j];
+  }
+}
+
+hipError_t gather_u64_parts(const uint64_t *const *src, const uint32_t *n, uint32_t k, uint64_t *dst,
+                            hipStream_t s) {
+  if (k > 8) return hipErrorInvalidValue;
+  U64Parts a{};
+  for (uint32_t j = 0; j < k; ++j) {
+    a.p[j] = src[j];
+    a.n[j] = n[j];
+  }
+  a.k = k;
+  hipLaunchKernelGGL(k_gather_u64, dim3(1), dim3(256), 0, s, a, dst);
+  return hipGetLastError();
+}
+
 // A generation barrier with a bound: a shard that never arrives (its caller
 // failed before the collective) breaks the transport instead of hanging the
 // others forever.

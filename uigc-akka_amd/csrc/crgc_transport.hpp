@@ -89,6 +89,10 @@ struct LocalTransport final : crgc_transport {
                 const size_t *roff, const size_t *rbytes, hipStream_t s) override;
 };
 
+// One kernel gathering k <= 8 parts of u64 words (device or pinned-host views) into dst.
+hipError_t gather_u64_parts(const uint64_t *const *src, const uint32_t *n, uint32_t k, uint64_t *dst,
+                            hipStream_t s);
+
 // Created by crgc_transport_rccl (crgc_transport.hip); RCCL types stay there.
 crgc_transport *make_rccl_transport(const uint8_t id[128], uint32_t n_shards, uint32_t shard,
                                     int device, int *rc);
