@@ -13,6 +13,11 @@
 //   trace: pseudo-roots by a parallel scan; level-synchronous top-down BFS
 //          with per-thread frontiers over out-edges with count > 0 and
 //          supervisor edges, halted shadows marked but not expanded; sweep.
+// Since round 6 it also merges DeltaGraph batches (ShadowGraph.mergeDelta,
+// :127-156: the same atomics and last-write-wins tags, flags only when
+// interned) and UndoLogs (mergeUndoLog, :158-174: the CME decided first, the
+// node's shadows halted, admitted fields applied), so the full-size C5 GPU test
+// has a checker.
 // Collected slots are never reused (the incarnation rule E9 holds as in the
 // HIP graph: edges to them have count <= 0 or come from halted owners).
 // Not the product.  tests/test_omp_graph_cpu.py pins its garbage / kill sets to
@@ -135,6 +140,60 @@ inline void atomic_max(uint64_t *p, uint64_t v) {
   }
 }
 
+// The slot of a live id, or NONE (no insert: mergeUndoLog's existence checks).
+uint32_t lookup(const Graph &g, uint64_t id) {
+  uint64_t h = mix(id) & (g.hcap - 1);
+  for (uint64_t p = 0; p < g.hcap; ++p) {
+    const uint64_t k = g.hkey[h];
+    if (k == id) return g.hval[h];
+    if (k == K_EMPTY) return NONE;
+    h = (h + 1) & (g.hcap - 1);
+  }
+  return NONE;
+}
+
+// outgoing[o][t] += c for every atom (owner << 32 | target, c): sorted,
+// reduced, merged per owner into its target-sorted vector; a zero count is
+// removed (updateOutgoing, ShadowGraph.java:64-73).
+void apply_atoms(Graph &g, std::vector<std::pair<uint64_t, int32_t>> &atoms) {
+  __gnu_parallel::sort(atoms.begin(), atoms.end(),
+                       [](const auto &x, const auto &y) { return x.first < y.first; });
+  std::vector<std::pair<uint64_t, int32_t>> red;
+  red.reserve(atoms.size());
+  for (auto &a : atoms) {
+    if (!red.empty() && red.back().first == a.first) red.back().second = (int32_t)((uint32_t)red.back().second + (uint32_t)a.second);
+    else red.push_back(a);
+  }
+  std::vector<uint64_t> runs;  // first atom of each owner's run
+  for (uint64_t k = 0; k < red.size(); ++k)
+    if (k == 0 || (red[k].first >> 32) != (red[k - 1].first >> 32)) runs.push_back(k);
+  runs.push_back(red.size());
+  const uint64_t n_runs = runs.size() - 1;
+#pragma omp parallel for schedule(dynamic, 64)
+  for (uint64_t r = 0; r < n_runs; ++r) {
+    const uint32_t o = (uint32_t)(red[runs[r]].first >> 32);
+    std::vector<Edge> &cur = g.out[o];
+    std::vector<Edge> nxt;
+    nxt.reserve(cur.size() + (runs[r + 1] - runs[r]));
+    uint64_t a = runs[r], e = 0;
+    while (a < runs[r + 1] || e < cur.size()) {
+      const uint32_t ta = a < runs[r + 1] ? (uint32_t)red[a].first : ~0u;
+      const uint32_t te = e < cur.size() ? cur[e].t : ~0u;
+      if (te < ta) {
+        nxt.push_back(cur[e++]);
+      } else {
+        int32_t c = red[a].second;
+        if (te == ta) c = (int32_t)((uint32_t)c + (uint32_t)cur[e++].c);
+        if (c) nxt.push_back({ta, c});
+        ++a;
+      }
+    }
+    cur.swap(nxt);
+  }
+}
+
+inline bool reserved(uint64_t id) { return id >= K_TOMB || (id >> 48) == 0xFFFFull; }
+
 }  // namespace
 
 extern "C" {
@@ -204,40 +263,105 @@ int omp_graph_merge(void *h, const crgc_entry_batch *b, int threads) {
   for (uint64_t i = 0; i < n; ++i)
     for (uint32_t k = b->updated_off[i]; k < b->updated_off[i + 1]; ++k)
       if (b->updated_info[k] & 1) atoms.push_back({((uint64_t)me[i] << 32) | ut[k], -1});
-  __gnu_parallel::sort(atoms.begin(), atoms.end(),
-                       [](const auto &x, const auto &y) { return x.first < y.first; });
-  std::vector<std::pair<uint64_t, int32_t>> red;
-  red.reserve(atoms.size());
-  for (auto &a : atoms) {
-    if (!red.empty() && red.back().first == a.first) red.back().second += a.second;
-    else red.push_back(a);
+  apply_atoms(g, atoms);
+  return 0;
+}
+
+// N x ShadowGraph.mergeDelta in batch order (ShadowGraph.java:127-156).
+// Returns 0 or CRGC_E_INVAL.
+int omp_graph_merge_deltas(void *h, const crgc_delta_batch *b, int threads) {
+  Graph &g = *(Graph *)h;
+  if (!b || b->memory != CRGC_MEM_HOST) return CRGC_E_INVAL;
+  if (threads > 0) omp_set_num_threads(threads);
+  const uint64_t n = b->n_shadows;
+  if (!n) return 0;
+  const uint64_t O = b->out_off[n];
+  for (uint64_t i = 0; i < n; ++i) {
+    if (reserved(b->id[i]) || (b->supervisor[i] != CRGC_NO_ACTOR && reserved(b->supervisor[i])) ||
+        b->out_off[i + 1] < b->out_off[i])
+      return CRGC_E_INVAL;
   }
-  std::vector<uint64_t> runs;  // first atom of each owner's run
-  for (uint64_t k = 0; k < red.size(); ++k)
-    if (k == 0 || (red[k].first >> 32) != (red[k - 1].first >> 32)) runs.push_back(k);
-  runs.push_back(red.size());
-  const uint64_t n_runs = runs.size() - 1;
-#pragma omp parallel for schedule(dynamic, 64)
-  for (uint64_t r = 0; r < n_runs; ++r) {
-    const uint32_t o = (uint32_t)(red[runs[r]].first >> 32);
-    std::vector<Edge> &cur = g.out[o];
-    std::vector<Edge> nxt;
-    nxt.reserve(cur.size() + (runs[r + 1] - runs[r]));
-    uint64_t a = runs[r], e = 0;
-    while (a < runs[r + 1] || e < cur.size()) {
-      const uint32_t ta = a < runs[r + 1] ? (uint32_t)red[a].first : ~0u;
-      const uint32_t te = e < cur.size() ? cur[e].t : ~0u;
-      if (te < ta) {
-        nxt.push_back(cur[e++]);
-      } else {
-        int32_t c = red[a].second;
-        if (te == ta) c = (int32_t)((uint32_t)c + (uint32_t)cur[e++].c);
-        if (c) nxt.push_back({ta, c});  // updateOutgoing: a zero count is removed (:64-73)
-        ++a;
-      }
+  for (uint64_t k = 0; k < O; ++k)
+    if (reserved(b->out_target[k])) return CRGC_E_INVAL;
+  reserve(g, 2 * n + O);
+  const uint64_t ep = ++g.epoch;
+  std::vector<uint32_t> me(n), su(n), ot(O);
+#pragma omp parallel for schedule(static)
+  for (uint64_t i = 0; i < n; ++i) {
+    me[i] = resolve(g, b->id[i]);
+    su[i] = b->supervisor[i] != CRGC_NO_ACTOR ? resolve(g, b->supervisor[i]) : NONE;
+  }
+#pragma omp parallel for schedule(static)
+  for (uint64_t k = 0; k < O; ++k) ot[k] = resolve(g, b->out_target[k]);
+#pragma omp parallel for schedule(static)
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t tag = (ep << 32) | (i + 1);
+    const uint32_t s = me[i];
+    if (b->recv_count[i]) atomic_add(&g.recv[s], b->recv_count[i]);
+    if (b->flags[i] & CRGC_DELTA_INTERNED) {  // interned |= ; busy / root only when interned (:139-146)
+      __atomic_fetch_or(&g.flags[s], INTERNED, __ATOMIC_RELAXED);
+      atomic_max(&g.vseq[s], tag);
     }
-    cur.swap(nxt);
+    if (su[i] != NONE) atomic_max(&g.sseq[s], tag);
   }
+#pragma omp parallel for schedule(static)
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t tag = (ep << 32) | (i + 1);
+    const uint32_t s = me[i];
+    if ((b->flags[i] & CRGC_DELTA_INTERNED) && g.vseq[s] == tag) {
+      uint8_t f = (uint8_t)(g.flags[s] & ~(BUSY | ROOT));
+      if (b->flags[i] & CRGC_DELTA_BUSY) f |= BUSY;
+      if (b->flags[i] & CRGC_DELTA_ROOT) f |= ROOT;
+      g.flags[s] = f;
+    }
+    if (su[i] != NONE && g.sseq[s] == tag) g.sup[s] = su[i];
+  }
+  std::vector<std::pair<uint64_t, int32_t>> atoms;
+  atoms.reserve(O);
+  for (uint64_t i = 0; i < n; ++i)
+    for (uint32_t k = b->out_off[i]; k < b->out_off[i + 1]; ++k)
+      atoms.push_back({((uint64_t)me[i] << 32) | ot[k], b->out_count[k]});
+  apply_atoms(g, atoms);
+  return 0;
+}
+
+// ShadowGraph.mergeUndoLog (ShadowGraph.java:158-174).  Returns 0,
+// CRGC_E_INVAL (a reserved or repeated actor), or CRGC_E_UNDO_NEW_SHADOW (the
+// reference's ConcurrentModificationException: an admitted actor's created ref
+// names an unknown actor) with the graph unchanged.
+int omp_graph_merge_undo(void *h, const crgc_undo_log *log, int threads) {
+  Graph &g = *(Graph *)h;
+  if (!log || log->memory != CRGC_MEM_HOST) return CRGC_E_INVAL;
+  if (threads > 0) omp_set_num_threads(threads);
+  const uint64_t n = log->n_fields;
+  std::vector<uint64_t> ids(log->actor, log->actor + n);
+  for (uint64_t f = 0; f < n; ++f)
+    if (reserved(ids[f])) return CRGC_E_INVAL;
+  std::sort(ids.begin(), ids.end());
+  for (uint64_t f = 1; f < n; ++f)
+    if (ids[f] == ids[f - 1]) return CRGC_E_INVAL;  // UndoLog.admitted: one field per actor
+  std::vector<uint32_t> me(n);
+  int cme = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(| : cme)
+  for (uint64_t f = 0; f < n; ++f) {
+    me[f] = lookup(g, log->actor[f]);
+    if (me[f] == NONE) continue;  // not a shadow here: the log's field is not applied
+    for (uint32_t k = log->created_off[f]; k < log->created_off[f + 1]; ++k)
+      if (lookup(g, log->created_target[k]) == NONE) cme = 1;
+  }
+  if (cme) return CRGC_E_UNDO_NEW_SHADOW;
+  const uint64_t top = g.slot_top;
+#pragma omp parallel for schedule(static)
+  for (uint64_t v = 0; v < top; ++v)
+    if ((g.flags[v] & ALIVE) && (uint16_t)(g.vid[v] >> 48) == log->node_location) g.flags[v] |= HALTED;
+  std::vector<std::pair<uint64_t, int32_t>> atoms;
+  for (uint64_t f = 0; f < n; ++f) {
+    if (me[f] == NONE) continue;
+    if (log->message_count[f]) atomic_add(&g.recv[me[f]], log->message_count[f]);
+    for (uint32_t k = log->created_off[f]; k < log->created_off[f + 1]; ++k)
+      atoms.push_back({((uint64_t)me[f] << 32) | lookup(g, log->created_target[k]), log->created_count[k]});
+  }
+  apply_atoms(g, atoms);
   return 0;
 }
 

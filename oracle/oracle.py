@@ -145,6 +145,8 @@ class OmpGraph:
         lib.omp_graph_create.argtypes = [C.c_uint32, C.c_uint64]
         lib.omp_graph_destroy.argtypes = [C.c_void_p]
         lib.omp_graph_merge.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        lib.omp_graph_merge_deltas.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        lib.omp_graph_merge_undo.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
         lib.omp_graph_trace.argtypes = ([C.c_void_p, C.c_int, C.c_int] + [C.POINTER(C.c_uint64)] * 5 +
                                         [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64])
         self.lib, self.threads = lib, threads
@@ -166,6 +168,19 @@ class OmpGraph:
         rc = self.lib.omp_graph_merge(self.h, C.addressof(batch.struct()), self.threads)
         if rc:
             raise abi.CrgcError(rc, "omp_graph_merge")
+
+    def merge_deltas(self, batch):
+        """N x ShadowGraph.mergeDelta (DeltaBatch in host memory)."""
+        rc = self.lib.omp_graph_merge_deltas(self.h, C.addressof(batch.struct()), self.threads)
+        if rc:
+            raise abi.CrgcError(rc, "omp_graph_merge_deltas")
+
+    def merge_undo(self, log):
+        """ShadowGraph.mergeUndoLog (UndoBatch in host memory); CRGC_E_UNDO_NEW_SHADOW
+        is the reference's ConcurrentModificationException, the graph unchanged."""
+        rc = self.lib.omp_graph_merge_undo(self.h, C.addressof(log.struct()), self.threads)
+        if rc:
+            raise abi.CrgcError(rc, "omp_graph_merge_undo")
 
     def trace(self, should_kill: bool = True, ids: bool = False) -> dict:
         """Counts; with ids=True also 'garbage_ids' / 'kill_ids' (unsorted)."""

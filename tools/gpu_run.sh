@@ -44,7 +44,7 @@ for step in "$@"; do
     tests|tests:*)
       K=()
       [ "$step" != tests ] && K=(-k "${step#tests:}")
-      (cd "$ROOT" && timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 150 \
+      (cd "$ROOT" && timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --durations=25 --timeout 150 \
         --timeout-method thread "${K[@]}" > "$O/gpu_tests.log" 2>&1) ;;
     smoke) (cd "$ROOT" && timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1) ;;
     c2) (cd /tmp && timeout -k 10 480 python3 "$ROOT/bench.py" > "$O/bench_c2.json" 2> "$O/bench_c2.err") ;;
