@@ -116,7 +116,7 @@ def test_c5_full_size_cluster_stream_and_downed_node_match_openmp(hip_mod, oracl
         w.bulk_graph(V, E, alpha=2.1, n_roots=max(1, V // 1000), cap=100000)
     h = hip_mod.ShadowGraph(vertex_capacity=int(nodes * V * 1.2), edge_capacity=int(nodes * E * 1.2))
     p = oracle_mod.OmpGraph(threads=THREADS, vertex_hint=int(nodes * V * 1.5))
-    p.reserve_ids(1 << 20)
+    p.reserve_ids(nodes * V)  # the downed node's trace reports up to all its shadows
     accs = [h.undo_accumulator(k + 1) for k in range(1, nodes)]
     for k, w in enumerate(ws):
         for b in w.batches(1 << 20):
