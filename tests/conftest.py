@@ -13,6 +13,10 @@ for sub in ("uigc-akka_amd", "workload", "oracle", "tests"):
 # which the library reads only under this gate (crgc_api.hip Knobs); with no
 # hook variable set, every default is the production one.
 os.environ["CRGC_TEST_HOOKS"] = "1"
+# Slot reuse purges the swept slots after every sweep in the suite (the
+# library batches them, CRGC_SLOT_REUSE_DIV=16), so every unsharded parity test
+# runs its reused slots through the next merges.
+os.environ.setdefault("CRGC_SLOT_REUSE_DIV", "0")
 
 
 def pytest_configure(config):

@@ -115,6 +115,34 @@ def test_power_law_wakeups_match_oracle(hip_mod, oracle_mod, actors, edges, batc
     assert h.total_actors_seen() == o.total_actors_seen()
 
 
+@pytest.mark.parametrize("div", ["16", "0"])
+def test_slot_reuse_batches_through_grows(hip_mod, oracle_mod, monkeypatch, div):
+    """Slot reuse as the library runs it (CRGC_SLOT_REUSE_DIV=16: the swept
+    slots wait listed until they are 1/16 of the range, then one purge) on a
+    power-law graph loaded in small batches into a graph at its minimum
+    capacity, so it grows in place (crgc_api.hip grow) with garbage slots
+    still listed, then wakeups that collect and spawn; every trace and the
+    final graph equal to the oracle's (ShadowGraph.java:205-289, :276)."""
+    monkeypatch.setenv("CRGC_SLOT_REUSE_DIV", div)
+    w = world.World(seed=0x5EED + 9)
+    w.bulk_graph(40_000, 400_000, alpha=2.1, n_roots=400)
+    h = hip_mod.ShadowGraph(vertex_capacity=1000, edge_capacity=10_000)
+    o = oracle_mod.OracleGraph()
+    for b in w.batches(1 << 13):
+        h.merge_entries(b)
+        o.merge_entries(b)
+        _same(h.trace(True), o.trace(True))
+    for _ in range(8):
+        b = w.wakeup_batch(4000)
+        h.merge_entries(b.to_device())
+        o.merge_entries(b)
+        _same(h.trace(True), o.trace(True))
+    assert h.export() == o.export()
+    assert h.total_actors_seen() == o.total_actors_seen()
+    u = h.usage()
+    assert u["grows"] >= 1, u
+
+
 @pytest.mark.parametrize("chain_after", ["64", "0", "2"])
 def test_c3_deep_chains_and_dead_rings(hip_mod, oracle_mod, monkeypatch, chain_after):
     """Chains walked by k_tail (CRGC_CHAIN_AFTER=0) or handed to chain mode

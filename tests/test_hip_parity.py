@@ -426,8 +426,8 @@ def test_failure_detail_names_the_call(hip_mod):
     assert abi.last_error_detail() == ""
 
 
-@pytest.mark.parametrize("reuse", ["1", "0"])
-def test_swept_slots_reused_match_oracle(hip_mod, oracle_mod, monkeypatch, reuse):
+@pytest.mark.parametrize("reuse,div", [("1", "0"), ("1", "16"), ("0", "0")])
+def test_swept_slots_reused_match_oracle(hip_mod, oracle_mod, monkeypatch, reuse, div):
     """Slot reuse (crgc_reuse.hip, round 6): after every committed sweep the
     garbage slots are purged of their edges (keys tombstoned, in-edges left
     with count 0, candidates and pull hints made inert), reset, and taken by
@@ -436,8 +436,12 @@ def test_swept_slots_reused_match_oracle(hip_mod, oracle_mod, monkeypatch, reuse
     thousands of actors while spawning new ones, so most slots are reused, some
     several times; the graph and every trace must equal the oracle's, and the
     slot range must stay near the live set.  CRGC_SLOT_REUSE=0 is the control
-    (slots reclaimed by rebuilds only)."""
+    (slots reclaimed by rebuilds only).  div = 0 purges after every sweep (the
+    suite's default, tests/conftest.py); 16 (the library default) lists the
+    garbage slots and purges them in batches of 1/16 of the slot range
+    (tests/test_hip_configs.py also grows a graph with slots listed)."""
     monkeypatch.setenv("CRGC_SLOT_REUSE", reuse)
+    monkeypatch.setenv("CRGC_SLOT_REUSE_DIV", div)
     w = kats.RandomWorld(seed=31, max_actors=3000, wake_every=40)
     h, o = _pair(hip_mod, oracle_mod, vertex_capacity=1 << 16, edge_capacity=1 << 16)
     peak_live, collected = 0, 0

@@ -55,7 +55,7 @@ for step in "$@"; do
     c3) (cd /tmp && timeout -k 10 300 python3 "$ROOT/bench.py" --workload c3 > "$O/bench_c3.json" 2> "$O/bench_c3.err") ;;
     c5) (cd /tmp && timeout -k 10 420 python3 "$ROOT/bench.py" --workload c5 --steps 5 --warmup 2 --no-cpu-baseline \
           > "$O/bench_c5.json" 2> "$O/bench_c5.err") ;;
-    levels) (cd /tmp && CRGC_LEVEL_LOG=1 CRGC_KERNEL_TIMING=2 timeout -k 10 420 $B > "$O/levels.json" 2> "$O/levels.err") ;;
+    levels) (cd /tmp && CRGC_LEVEL_LOG=1 CRGC_KERNEL_TIMING=2 timeout -k 10 420 $B --timing-every 1 > "$O/levels.json" 2> "$O/levels.err") ;;
     kt) (cd /tmp && timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o kt -- $B \
           > "$O/bench_kt.json" 2> "$O/bench_kt.err") ;;
     ktp) (cd /tmp && timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ktp" -o kt -- \
@@ -126,7 +126,7 @@ for step in "$@"; do
           envs=(CRGC_TEST_HOOKS=1 CRGC_LEVEL_LOG=1 CRGC_KERNEL_TIMING=2)
           [ "$v" != "BASE" ] && IFS=',' read -ra ev <<< "$v" && envs+=("${ev[@]}")
           f="$O/lv_p${pass}_$(echo "$v" | tr '=,/' '___')"
-          (cd /tmp && env "${envs[@]}" timeout -k 10 300 $B > "$f.json" 2> "$f.err")
+          (cd /tmp && env "${envs[@]}" timeout -k 10 300 $B --timing-every 1 > "$f.json" 2> "$f.err")
           { echo "== pass $pass $v"; python3 "$ROOT/tools/lv_summary.py" "$f.err" 3; } >> "$O/lv_summary.txt"
         done
       done ;;

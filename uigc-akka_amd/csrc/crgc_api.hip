@@ -236,8 +236,10 @@ Caps caps_create(uint64_t v0, uint64_t p0, bool proxies, uint64_t e0, uint32_t i
 //
 // Production reads only the documented keys:
 //   CRGC_LEVEL_TIMEOUT_S  wall bound of one trace's level loop (default 300 s)
-//   CRGC_KERNEL_TIMING    0: chunk events only, 1 (default): k_expand's dispatch
-//                         events too (the roofline's live timing), 2: every level kernel
+//   CRGC_KERNEL_TIMING    0: chunk events only, 1: k_expand's dispatch events too,
+//                         2: every level kernel, 3 (default): the expand of the wide
+//                         levels 0 and 1 (the roofline's live timing)
+//   CRGC_TIMING_EVERY     k: only every k-th trace carries timing events (default 1)
 //   CRGC_LEVEL_LOG        per-level device times on stderr (diagnostics)
 //   CRGC_SPIN_US          host waits poll the stream this long before blocking
 //                         (default 20000; 0 blocks at once; crgc_internal.hpp)
@@ -293,6 +295,12 @@ struct Knobs {
   // expand timed, most of it on narrow levels that carry ~20 % of the
   // expand's device time.
   int kernel_timing = 3;
+  // CRGC_TIMING_EVERY=k: only every k-th trace carries timing events (its
+  // level chunks, timed expands and sweep; the others report 0 ms and 0 timed
+  // launches).  Each event costs ~5 us of idle GPU (r6a), ~45 us per C2 wakeup
+  // in all (profiles/r6d/c2_last_wakeup_timeline.txt); a sample of the traces
+  // is enough for the device-time figures.
+  uint32_t timing_every = 1;
   bool level_log = false;        // CRGC_LEVEL_LOG
   uint64_t level_timeout_s = 300;  // CRGC_LEVEL_TIMEOUT_S
   int xbits = 1;                 // CRGC_XBITS: sharded mark form (0 ids, 1 cheaper, 2 bitmaps)
@@ -338,17 +346,22 @@ struct Knobs {
   // A registered batch's chunk is copied by the DMA engines (one
   // hipMemcpyAsync of the span its arrays occupy in the caller's arena) rather
   // than read over PCIe by k_copy_ranges, which shares the memory pipeline with
-  // the merge kernels beside it (profiles/r4ab): registered C2 wakeup 2.09 /
-  // 2.14 against 2.17 / 2.27 ms, merge call 0.81 / 0.84 against 0.91 / 0.99 ms,
-  // interleaved on one box (profiles/r6c).  CRGC_REG_SDMA=0: the kernel copy.
+  // the merge kernels beside it (profiles/r4ab): registered C2 wakeup 2.13 /
+  // 2.19 against 2.32 / 2.31 ms, merge call 0.82 / 0.85 against 0.95 / 0.99 ms,
+  // interleaved on one box (profiles/r6e/ab_pcie).  CRGC_REG_SDMA=0: the kernel copy.
   bool reg_sdma = true;
   // CRGC_SLOT_REUSE=0: collected shadows' slots are reclaimed only by a rebuild
   // (round 5); by default the sweep's garbage slots are purged of their edges
   // and taken by the next merges' new shadows (crgc_reuse.hip)
   bool slot_reuse = true;
+  // The listed garbage slots are purged and freed in one batch once they make up
+  // 1 / reuse_div of the slot range (0: after every committed sweep, the test
+  // suite's setting).  CRGC_SLOT_REUSE_DIV
+  uint32_t reuse_div = 16;
   void read() {
     auto env = [](const char *k) { return getenv(k); };
     if (const char *m = env("CRGC_KERNEL_TIMING")) kernel_timing = atoi(m);
+    if (const char *m = env("CRGC_TIMING_EVERY")) timing_every = std::max<uint32_t>(1, (uint32_t)strtoul(m, nullptr, 10));
     level_log = env("CRGC_LEVEL_LOG") != nullptr;
     if (const char *m = env("CRGC_LEVEL_TIMEOUT_S")) level_timeout_s = std::max<uint64_t>(1, strtoull(m, nullptr, 10));
     const char *hooks = env("CRGC_TEST_HOOKS");
@@ -403,6 +416,7 @@ struct Knobs {
     if (const char *m = env("CRGC_CHUNK_REG")) chunk_reg = std::min<uint32_t>(8, std::max(1, atoi(m)));
     if (const char *m = env("CRGC_REG_SDMA")) reg_sdma = atoi(m) != 0;
     if (const char *m = env("CRGC_SLOT_REUSE")) slot_reuse = atoi(m) != 0;
+    if (const char *m = env("CRGC_SLOT_REUSE_DIV")) reuse_div = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_DEV_CHUNK")) {  // 0: the default
       dev_chunk = strtoull(m, nullptr, 10);
       if (dev_chunk) dev_chunk = std::max<uint64_t>(64, dev_chunk);
@@ -427,6 +441,10 @@ struct crgc_graph {
   uint64_t slot_top = 0, pool_top = 0, rpool_top = 0, etab_used = 0, live = 0;
   uint64_t proxy_top = 0;  // proxy region slots in use (sharded graphs), as of the last synchronisation
   uint64_t n_rebuild = 0, n_grow = 0, n_repack = 0;  // crgc_usage_of
+  uint64_t pend_n = 0;        // slot reuse: committed garbage slots listed in gslot, not purged yet
+  uint64_t n_traces = 0;      // crgc_trace calls (timing_every)
+  bool timed = true;          // the current mark carries timing events
+  bool halted_seen = false;   // an undo log was merged: live shadows may be halted (k_sup_fix)
   bool walk_ok = false;  // CRGC_WALK: k_walk's workgroups fit the device at once (walk_fits)
   std::vector<uint8_t> lvl_timed;  // per level launch of the current run_levels: timed (events)
   uint64_t ids_since = 0, atoms_since = 0;
@@ -647,7 +665,8 @@ int grow(crgc_graph *h, uint64_t ids, uint64_t atoms) {
   cp(d.nzdeg, o.nzdeg, top * 4);
   cp(d.radj, o.radj, top * 8);
   cp(d.par, o.par, top * 4);
-  if (d.freel && o.freel) cp(d.freel, o.freel, top * 4);  // (the list holds slots below slot_top)
+  if (d.freel && o.freel) cp(d.freel, o.freel, top * 4);  // (the lists hold slots below slot_top)
+  if (d.gslot && o.gslot) cp(d.gslot, o.gslot, h->pend_n * 4);
   cp(d.pool, o.pool, h->pool_top * 8);
   cp(d.rpool, o.rpool, h->rpool_top * 4);
   if (e == hipSuccess) e = launch_grow_tables(o, d, h->stream);
@@ -725,6 +744,7 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms, bool may_grow = false) 
   }
   free_arrays(h->g);
   h->g = dst;
+  h->pend_n = 0;  // (the rebuild dropped every collected slot)
   ++h->n_rebuild;
   ++h->slot_gen;  // other shards' cached home slots of this shard are stale now
   h->live = h->slot_top;
@@ -2114,6 +2134,7 @@ int crgc_merge_undo(crgc_graph *h, const crgc_undo_log *log) {
   }
   HIP_TRY(sync_counters(h));
   if (int rc = device_error(h)) return rc;
+  h->halted_seen = true;  // (k_undo_halt: the downed location's shadows)
   HIP_TRY(launch_undo_apply(h->g.d, a, h->slot_top, h->stream));
   if (int rc = run_edges(h, a.atom_o, a.atom_t, a.atom_d, nc, wc)) return rc;
   note_merge(h, nc, nc);
@@ -2298,7 +2319,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
   //   CRGC_KERNEL_TIMING=1 (default): k_expand's start / stop carried by its dispatch;
   //   CRGC_KERNEL_TIMING=2: all three level kernels (each timed dispatch costs a few us);
   //   CRGC_KERNEL_TIMING=0: chunks only.
-  const int timing = kn.kernel_timing;
+  const int timing = h->timed ? kn.kernel_timing : 0;
   auto new_event = [&](std::vector<hipEvent_t> &v, size_t n) -> hipError_t {
     while (v.size() < n) {
       hipEvent_t e;
@@ -2321,7 +2342,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
       for (int k = timing == 2 ? 0 : 4; k < 6; ++k) ev[k] = h->lvl_ev[6 * nl + k];
     }
     la.level = level;
-    if (timing && !timed) la.flags |= LV_NOBYTES;
+    if (!timed) la.flags |= LV_NOBYTES;
     else la.flags &= ~LV_NOBYTES;
     hipError_t r = launch_level(h->g.d, la, rootk, investigate, vtop, h->stream, ev);
     if (timed) ++lr.timed;
@@ -2329,6 +2350,7 @@ static int run_levels(crgc_graph *h, bool investigate, uint16_t location, uint64
     return r;
   };
   auto chunk_event = [&]() -> hipError_t {
+    if (!h->timed) return hipSuccess;
     if (hipError_t r = new_event(h->chunk_ev, nc + 1)) return r;
     return hipEventRecord(h->chunk_ev[nc++], h->stream);
   };
@@ -3037,6 +3059,8 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   // exact value from the device counters, so no synchronisation is needed here.
   const uint64_t top = h->slot_top + h->ids_since;
   reset_trace_counters(h);
+  h->timed = h->n_traces++ % h->knobs.timing_every == 0;
+  h->g.d.gslot_at = h->pend_n;  // this sweep's garbage slots are listed after the pending ones
   LevelRun lr;
   uint64_t rounds = 0, ids_sent = 0, x_bytes = 0;
   double ms_x = 0;
@@ -3051,9 +3075,9 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
     if (out->garbage_ids) (void)host_kind(h, out->garbage_ids, out->garbage_cap * 8, &dg);
     if (out->kill_ids) (void)host_kind(h, out->kill_ids, out->kill_cap * 8, &dk);
     auto sweep = [&]() -> hipError_t {
-      hipError_t e = hipEventRecord(h->ev[1], h->stream);
+      hipError_t e = h->timed ? hipEventRecord(h->ev[1], h->stream) : hipSuccess;
       if (e == hipSuccess) e = launch_sweep(h->g.d, should_kill ? 1 : 0, top, h->stream);
-      if (e == hipSuccess) e = hipEventRecord(h->ev[2], h->stream);
+      if (e == hipSuccess && h->timed) e = hipEventRecord(h->ev[2], h->stream);
       if (e == hipSuccess && (dg || dk))
         e = launch_copy_lists(h->g.d, dg, dg ? out->garbage_cap : 0, dk, dk ? out->kill_cap : 0, h->stream);
       return e;  // the counters come back with the chunk's k_publish
@@ -3068,9 +3092,9 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
              (!out->kill_ids || (dk && cc.n_kill <= out->kill_cap));
   } else {
     if (int rc = mark_all(h, false, 0, top, lr, &rounds, &ids_sent, &ms_x, &x_bytes)) return rc;
-    HIP_TRY(hipEventRecord(h->ev[1], h->stream));
+    if (h->timed) HIP_TRY(hipEventRecord(h->ev[1], h->stream));
     if (int rc = sweep_sharded(h, should_kill ? 1 : 0, top, &ms_x)) return rc;
-    HIP_TRY(hipEventRecord(h->ev[2], h->stream));
+    if (h->timed) HIP_TRY(hipEventRecord(h->ev[2], h->stream));
     HIP_TRY(sync_counters(h));
   }
   const Counters &c = *h->hctr;
@@ -3108,7 +3132,7 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   st.ids_sent = ids_sent;
   st.exchange_bytes = x_bytes;
   st.ms_exchange = ms_x;
-  st.ms_sweep = elapsed_ms(h->ev[1], h->ev[2], &lr.time_fail);
+  st.ms_sweep = h->timed ? elapsed_ms(h->ev[1], h->ev[2], &lr.time_fail) : 0.f;
   st.time_query_failures = lr.time_fail;
   st.direct_lists = direct ? 1 : 0;
   st.pseudo_roots = lr.roots;
@@ -3122,12 +3146,18 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   h->last_stats = st;
   out->stats = st;
-  // Reclaim the garbage slots for the next merges' new shadows
-  // (crgc_reuse.hip): queued behind the trace, so it runs while the caller
-  // takes the results, and the next merge on this stream starts after it.
+  // Reclaim the listed garbage slots for the next merges' new shadows
+  // (crgc_reuse.hip) once they are 1 / reuse_div of the range: queued behind
+  // the trace, so it runs while the caller takes the results, and the next
+  // merge on this stream starts after it.
   if (rc == CRGC_OK && h->g.d.freel && c.n_garbage) {
-    HIP_TRY(launch_reclaim(h->g.d, h->slot_top, c.n_garbage, c.free_n, h->stream));
-    std::swap(h->g.d.freel, h->g.d.freel2);
+    h->pend_n += c.n_garbage;
+    const uint32_t div = h->knobs.reuse_div;
+    if (div == 0 || h->pend_n * div >= h->slot_top) {
+      HIP_TRY(launch_reclaim(h->g.d, h->slot_top, h->pend_n, c.free_n, h->halted_seen, h->stream));
+      std::swap(h->g.d.freel, h->g.d.freel2);
+      h->pend_n = 0;
+    }
   }
   // Keep the slot space dense: rebuild once dead slots outnumber live ones in
   // the shadows' region, or (sharded graphs) in the proxy region.
@@ -3635,6 +3665,7 @@ int crgc_count_reachable_from(crgc_graph *h, uint16_t location, int64_t *out) {
   HIP_TRY(sync_counters(h));
   if (int rc = device_error(h)) return rc;
   reset_trace_counters(h);
+  h->timed = true;
   LevelRun lr;
   uint64_t rounds = 0, sent = 0, x_bytes = 0;
   double ms_x = 0;

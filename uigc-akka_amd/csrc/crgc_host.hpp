@@ -330,10 +330,11 @@ size_t rebuild_scan_tmp_bytes(uint64_t n);
 // grow: both hash tables of `src` re-hashed into `dst`'s (larger) ones; the
 // caller copies the per-slot arrays and the pools (same slots, same offsets)
 hipError_t launch_grow_tables(const DevGraph &src, const DevGraph &dst, hipStream_t s);
-// crgc_reuse.hip: after a committed sweep, purge the garbage slots and list
-// them free for the next merges (unsharded graphs; no-op without a free list)
-hipError_t launch_reclaim(const DevGraph &g, uint64_t slot_top, uint64_t n_garbage, uint64_t n_free,
-                          hipStream_t s);
+// crgc_reuse.hip: after a committed sweep, purge the listed garbage slots
+// gslot[0, n_purge) and list them free for the next merges (unsharded graphs;
+// no-op without a free list); sup_fix: some live shadow may be halted
+hipError_t launch_reclaim(const DevGraph &g, uint64_t slot_top, uint64_t n_purge, uint64_t n_free,
+                          bool sup_fix, hipStream_t s);
 // the pools alone, packed into pool2 / rpool2 (pp / rp: scap u64 each; scan_tmp:
 // 2 x rebuild_scan_tmp_bytes(scap)); slots and tables unchanged
 hipError_t launch_repack(const DevGraph &g, uint64_t top, uint64_t ptop, uint64_t *pp, uint64_t *rp, void *scan_tmp,

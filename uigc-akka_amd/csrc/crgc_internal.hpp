@@ -213,8 +213,10 @@ struct DevGraph {
   unsigned long long *sseq;  // last-write-wins tag for supervisor
   uint32_t *nzdeg;           // out-edges with count != 0 (reference `outgoing.size()`)
   // slot reuse (unsharded; nullptr when off): the free list, the next one being
-  // built (ping-pong), and the last sweep's garbage slots (dense)
+  // built (ping-pong), and the committed sweeps' garbage slots not purged yet
+  // (dense; a sweep appends its own from gslot_at)
   uint32_t *freel, *freel2, *gslot;
+  uint64_t gslot_at;
   // reverse candidates (pull BFS): owners that ever created an edge key to the
   // slot; a candidate is verified against the forward count when used
   uint2 *radj;               // {offset, rlen | log2(capacity) << RLEN_BITS} into rpool (rseg_*)

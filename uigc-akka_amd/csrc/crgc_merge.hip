@@ -121,7 +121,16 @@ __global__ __launch_bounds__(IDS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 
       // taken count may pass its end), then fresh slots from slot_top.
       uint32_t nfree = 0;
       unsigned long long kf = 0;
-      const bool reuse = g.freel != nullptr;
+      // Once the list is used up (free_used only grows during a merge, so an
+      // older value can only say "not yet"), a round skips its append: a
+      // wakeup's first few hundred rounds use it up (C2: ~2e4 swept slots for
+      // ~1.3e5 new shadows), and the append costs every later round a counter
+      // round trip.  The same decision for the whole workgroup.
+      const bool reuse =
+          g.freel != nullptr &&
+          __syncthreads_or(threadIdx.x == 0 &&
+                           __hip_atomic_load(&g.ctr->free_used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                               __hip_atomic_load(&g.ctr->free_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       if (reuse) {
         unsigned long long *const fc[1] = {&g.ctr->free_used};
         const uint64_t fn = g.ctr->free_n;
@@ -271,8 +280,8 @@ __global__ __launch_bounds__(256) void k_entries_atoms(DevGraph g, EntryArgs a) 
 // conflict region, where k_entries_lww rewrites the field from the true
 // winner (the tag's entry).  Most shadows appear once per batch, so the winners
 // need no second random pass over every entry's tag.
-__device__ inline void entry_flags(const DevGraph &g, uint32_t me, uint8_t ef) {
-  uint8_t f = g.flags[me] & (uint8_t)~(FL_BUSY | FL_ROOT);
+__device__ inline void entry_flags(const DevGraph &g, uint32_t me, uint8_t ef, uint8_t f0) {
+  uint8_t f = f0 & (uint8_t)~(FL_BUSY | FL_ROOT);
   f |= FL_INTERNED | FL_LOCAL;
   if (ef & CRGC_ENTRY_BUSY) f |= FL_BUSY;
   if (ef & CRGC_ENTRY_ROOT) f |= FL_ROOT;
@@ -298,9 +307,14 @@ __global__ __launch_bounds__(256) void k_entries_vertex(DevGraph g, EntryArgs a)
     const bool self_home = !sh || is_home(g, a.self[i]);
     // Local information (:77-82): recv delta and the busy/root LWW tag.
     if (vs(me) && self_home) {
+      // The flag byte is read beside the tag's atomic, not after it returns:
+      // only the slot's first tagger of this merge writes it here (the
+      // others go to the conflict list), so the early read is the value that
+      // writer would read.
+      const uint8_t f0 = g.flags[me];
       if (rc != 0) atomicAdd(&g.recv[me], (int32_t)rc);
       const unsigned long long old = atomicMax(&g.vseq[me], tag);
-      if ((old >> 32) != a.epoch) entry_flags(g, me, a.flags[i]);
+      if ((old >> 32) != a.epoch) entry_flags(g, me, a.flags[i], f0);
       else cv[atomicAdd(&s_nv, 1u)] = me;
     }
     // Spawned actors (:96-104): child.supervisor = self, last write wins.
@@ -337,7 +351,7 @@ __global__ __launch_bounds__(256) void k_entries_lww(DevGraph g, EntryArgs a) {
   for (uint32_t k = threadIdx.x; k < nv; k += 256) {
     const uint32_t me = cv[k];
     const uint64_t w = (uint64_t)(g.vseq[me] & 0xFFFFFFFFull) - 1;  // the winning entry
-    entry_flags(g, me, a.flags[w]);
+    entry_flags(g, me, a.flags[w], g.flags[me]);
   }
   for (uint32_t k = threadIdx.x; k < ns; k += 256) {
     const uint32_t cs = cs_[k];

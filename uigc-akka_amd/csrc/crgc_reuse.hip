@@ -5,11 +5,16 @@
 // dense and every per-slot pass of a trace (pseudo-roots, dense frontier
 // scans, sweep) covers [0, slot_top): without reuse a collected shadow's slot
 // is reclaimed only by a rebuild, and a long run's slot range outgrows its live
-// set (C2 over 200 wakeups: 4.17e7 slots for 3.15e7 live shadows, profiles/r6c).
-// So after a committed sweep (no NPE, the mark done) the garbage slots are
-// purged and listed free; the next merges' new shadows take them first
-// (k_ids).  Unsharded graphs only: a sharded graph's proxies cache their
-// homes' slots.
+// set (C2 over 200 wakeups: 4.17e7 slots for 3.15e7 live shadows, profiles/r5ao).
+// So the committed sweeps' garbage slots (no NPE, the mark done) are listed
+// (gslot), and once they make up 1/reuse_div of the slot range they are purged
+// in one batch and listed free; the next merges' new shadows take them first
+// (k_ids).  Purging at every sweep cost more than the dead slots it saves the
+// per-slot passes on a short run (a purged slot ~1 ns once, a dead slot
+// ~10 ps per trace: C2 1.249 / 1.273 against 1.177 / 1.216 ms per wakeup
+// with reuse off, profiles/r6e); a dead slot waiting for its batch is exactly
+// round 5's collected slot.  Unsharded graphs only: a sharded graph's proxies
+// cache their homes' slots.
 //
 // What a reused slot must not inherit (the incarnation rule):
 //   * its out-edges: their edge-table keys (slot << 32 | target) are
@@ -27,8 +32,9 @@
 // Collected ids stay tombstoned in the id table until its next rehash, so a
 // reappearing id is a new incarnation (a new shadow), exactly as before.
 //
-//   k_purge        one wave per garbage slot: out-edges, then in-edges
-//   k_sup_fix      halted live shadows whose supervisor was collected
+//   k_purge        one wave per listed garbage slot: out-edges, then in-edges
+//   k_sup_fix      halted live shadows whose supervisor was collected (only
+//                  once an undo log has halted shadows)
 //   k_free_list    the untaken rest of the free list, then the garbage slots
 //                  (reset), into the next list; k_free_commit its counts
 #include "crgc_host.hpp"
@@ -51,10 +57,9 @@ __device__ inline uint64_t etab_find(const DevGraph &g, uint32_t owner, uint32_t
 
 __device__ inline bool reclaim_commit(const Counters *c) { return c->mark_done && c->npe == 0; }
 
-__global__ __launch_bounds__(256) void k_purge(DevGraph g) {
+__global__ __launch_bounds__(256) void k_purge(DevGraph g, uint64_t ng) {
   const Counters *c = g.ctr;
   if (!reclaim_commit(c)) return;
-  const uint64_t ng = c->n_garbage;
   const uint32_t lane = lane_id();
   const uint64_t nw = (uint64_t)gridDim.x * 4;
   for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < ng; i += nw) {
@@ -93,7 +98,7 @@ __global__ __launch_bounds__(256) void k_purge(DevGraph g) {
 // so theirs are the only supervisor pointers a sweep can leave dangling.
 __global__ __launch_bounds__(256) void k_sup_fix(DevGraph g) {
   const Counters *c = g.ctr;
-  if (!reclaim_commit(c) || c->n_garbage == 0) return;
+  if (!reclaim_commit(c)) return;
   const uint64_t top = c->slot_top;
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < top; v += stride) {
@@ -106,10 +111,10 @@ __global__ __launch_bounds__(256) void k_sup_fix(DevGraph g) {
 // The next free list: the entries the merges since the last sweep did not take,
 // then this sweep's garbage slots, each reset to a fresh slot's state
 // (alloc_arrays' defaults).
-__global__ __launch_bounds__(256) void k_free_list(DevGraph g) {
+__global__ __launch_bounds__(256) void k_free_list(DevGraph g, uint64_t n_purged) {
   const Counters *c = g.ctr;
   const uint64_t fn = c->free_n, fu = min((uint64_t)c->free_used, fn), rem = fn - fu;
-  const uint64_t ng = reclaim_commit(c) ? c->n_garbage : 0;
+  const uint64_t ng = reclaim_commit(c) ? n_purged : 0;
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < rem + ng; i += stride) {
     if (i < rem) {
@@ -129,24 +134,24 @@ __global__ __launch_bounds__(256) void k_free_list(DevGraph g) {
   }
 }
 
-__global__ void k_free_commit(Counters *c) {
+__global__ void k_free_commit(Counters *c, uint64_t n_purged) {
   const uint64_t fn = c->free_n, fu = min((uint64_t)c->free_used, fn);
-  const uint64_t ng = reclaim_commit(c) ? c->n_garbage : 0;
+  const uint64_t ng = reclaim_commit(c) ? n_purged : 0;
   c->reused += fu;  // taken slots: their collected ids' tombstones stay in the id table
   c->free_n = fn - fu + ng;
   c->free_used = 0;
 }
 
-hipError_t launch_reclaim(const DevGraph &g, uint64_t slot_top, uint64_t n_garbage, uint64_t n_free,
-                          hipStream_t s) {
+hipError_t launch_reclaim(const DevGraph &g, uint64_t slot_top, uint64_t n_purge, uint64_t n_free,
+                          bool sup_fix, hipStream_t s) {
   launch_begin();
   if (!g.freel) return hipSuccess;
-  if (n_garbage) {
-    hipLaunchKernelGGL(k_purge, dim3(grid_for(n_garbage, 4, 4096)), dim3(256), 0, s, g);
-    hipLaunchKernelGGL(k_sup_fix, dim3(grid_for(slot_top, 256, 4096)), dim3(256), 0, s, g);
+  if (n_purge) {
+    hipLaunchKernelGGL(k_purge, dim3(grid_for(n_purge, 4, 4096)), dim3(256), 0, s, g, n_purge);
+    if (sup_fix) hipLaunchKernelGGL(k_sup_fix, dim3(grid_for(slot_top, 256, 4096)), dim3(256), 0, s, g);
   }
-  hipLaunchKernelGGL(k_free_list, dim3(grid_for(n_garbage + n_free, 256, 4096)), dim3(256), 0, s, g);
-  hipLaunchKernelGGL(k_free_commit, dim3(1), dim3(1), 0, s, g.ctr);
+  hipLaunchKernelGGL(k_free_list, dim3(grid_for(n_purge + n_free, 256, 4096)), dim3(256), 0, s, g, n_purge);
+  hipLaunchKernelGGL(k_free_commit, dim3(1), dim3(1), 0, s, g.ctr, n_purge);
   return hipGetLastError();
 }
 

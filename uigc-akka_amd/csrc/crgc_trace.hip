@@ -1934,7 +1934,7 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a0, bool roots, bool
     // once: the host enables it only when occupancy allows, walk_fits(); a
     // workgroup that still never arrives fails the mark with ERR_WALK_STUCK.
     // A cooperative launch would guarantee residency, but a process that had
-    // made one crashed in the runtime's exit handlers, profiles/r6a)
+    // made one crashed in the runtime's exit handlers in a round-6 test run)
     hipExtLaunchKernelGGL(k_walk, dim3(WALK_WG), dim3(WALK_T), 0, s, e[2], e[3], 0, g, a);
   } else
     hipExtLaunchKernelGGL(k_tail, dim3(1), dim3(TAIL_THREADS), 0, s, e[2], e[3], 0, g, a);
@@ -2209,7 +2209,7 @@ __global__ __launch_bounds__(256) void k_sweep_gather(DevGraph g) {
         id_find(g, id, &bucket);
         if (bucket != KEY_EMPTY) g.htab[bucket].key = KEY_TOMB;
         g.flags[v] = 0;
-        if (g.gslot) g.gslot[go + i] = v;  // slot reuse: purged and listed free (crgc_reuse.hip)
+        if (g.gslot) g.gslot[g.gslot_at + go + i] = v;  // slot reuse: purged, listed free (crgc_reuse.hip)
       }
     }
     for (uint32_t i = lane_id(); i < kn; i += 64) g.out_kill[ko + i] = g.vid[ka[i]];

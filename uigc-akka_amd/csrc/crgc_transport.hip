@@ -60,7 +60,7 @@ static hipError_t copy_segs(const Segs &sg, hipStream_t s) {
 
 // Small all-gathers' send words (counters, flags, host words) gathered into
 // one buffer by one kernel: a runtime copy per part was a ~3 us blit kernel
-// each (~50 per shard and C2 wakeup over 8 logical shards, profiles/r6b).
+// each (~50 per shard and C2 wakeup over 8 logical shards in a round-6 kernel trace).
 // Parts are device memory or pinned host memory's device view.
 struct U64Parts {
   const uint64_t *p[8];
