@@ -443,6 +443,7 @@ struct crgc_graph {
   uint64_t n_rebuild = 0, n_grow = 0, n_repack = 0;  // crgc_usage_of
   uint64_t pend_n = 0;        // slot reuse: committed garbage slots listed in gslot, not purged yet
   uint64_t n_traces = 0;      // crgc_trace calls (timing_every)
+  bool free_avail = false;    // slot reuse: the free list may hold untaken slots (ids_view)
   bool timed = true;          // the current mark carries timing events
   bool halted_seen = false;   // an undo log was merged: live shadows may be halted (k_sup_fix)
   bool walk_ok = false;  // CRGC_WALK: k_walk's workgroups fit the device at once (walk_fits)
@@ -513,6 +514,15 @@ struct crgc_graph {
 // Slot reuse (crgc_reuse.hip): unsharded graphs (a sharded graph's proxies
 // cache their homes' slots), unless CRGC_SLOT_REUSE=0.
 static bool reuse_on(const crgc_graph *h) { return h->G <= 1 && !h->tp && h->knobs.slot_reuse; }
+
+// The graph as k_ids sees it: without the free list while the host knows it is
+// empty (k_ids then takes every new slot from slot_top with no free-list step;
+// a per-round check on the device cost ~14 us per C2 merge, profiles/r6g).
+static DevGraph ids_view(const crgc_graph *h) {
+  DevGraph d = h->g.d;
+  if (!h->free_avail) d.freel = nullptr;
+  return d;
+}
 
 namespace {
 thread_local int api_depth = 0;
@@ -745,6 +755,7 @@ int rebuild(crgc_graph *h, uint64_t ids, uint64_t atoms, bool may_grow = false) 
   free_arrays(h->g);
   h->g = dst;
   h->pend_n = 0;  // (the rebuild dropped every collected slot)
+  h->free_avail = false;
   ++h->n_rebuild;
   ++h->slot_gen;  // other shards' cached home slots of this shard are stale now
   h->live = h->slot_top;
@@ -1425,7 +1436,7 @@ static int merge_entries_one(crgc_graph *h, const crgc_entry_batch *b, uint64_t 
   a.conf_n = wc.take<uint32_t>(2 * nb256);
   // a batch refused for its offsets writes no atoms and the edge pipeline
   // skips it (EdgeArgs::err), so the atom arrays need no clearing
-  HIP_TRY(launch_entries(h->g.d, a, h->stream, 0));
+  HIP_TRY(launch_entries(ids_view(h), a, h->stream, 0));
   {
     SideFork sf(h);
     HIP_TRY(sf.fork());
@@ -1995,7 +2006,7 @@ static int merge_deltas_one(crgc_graph *h, const crgc_delta_batch *b, uint64_t n
   a.atom_o = wc.take<uint32_t>(std::max<uint64_t>(nout, 1));
   a.atom_t = wc.take<uint32_t>(std::max<uint64_t>(nout, 1));
   a.atom_d = wc.take<int32_t>(std::max<uint64_t>(nout, 1));
-  HIP_TRY(launch_deltas(h->g.d, a, nout, h->stream, 0));
+  HIP_TRY(launch_deltas(ids_view(h), a, nout, h->stream, 0));
   {
     SideFork sf(h);
     HIP_TRY(sf.fork());
@@ -3150,6 +3161,7 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
   // (crgc_reuse.hip) once they are 1 / reuse_div of the range: queued behind
   // the trace, so it runs while the caller takes the results, and the next
   // merge on this stream starts after it.
+  bool reclaimed = false;
   if (rc == CRGC_OK && h->g.d.freel && c.n_garbage) {
     h->pend_n += c.n_garbage;
     const uint32_t div = h->knobs.reuse_div;
@@ -3157,7 +3169,15 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
       HIP_TRY(launch_reclaim(h->g.d, h->slot_top, h->pend_n, c.free_n, h->halted_seen, h->stream));
       std::swap(h->g.d.freel, h->g.d.freel2);
       h->pend_n = 0;
+      h->free_avail = true;
+      reclaimed = true;
     }
+  }
+  // Whether the merges since the last purge used the free list up: read only
+  // while it may still hold slots (the traces after a batch purge).
+  if (rc == CRGC_OK && h->free_avail && !reclaimed && h->g.d.freel) {
+    HIP_TRY(sync_counters(h));
+    h->free_avail = h->hctr->free_used < h->hctr->free_n;
   }
   // Keep the slot space dense: rebuild once dead slots outnumber live ones in
   // the shadows' region, or (sharded graphs) in the proxy region.

@@ -121,16 +121,9 @@ __global__ __launch_bounds__(IDS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 
       // taken count may pass its end), then fresh slots from slot_top.
       uint32_t nfree = 0;
       unsigned long long kf = 0;
-      // Once the list is used up (free_used only grows during a merge, so an
-      // older value can only say "not yet"), a round skips its append: a
-      // wakeup's first few hundred rounds use it up (C2: ~2e4 swept slots for
-      // ~1.3e5 new shadows), and the append costs every later round a counter
-      // round trip.  The same decision for the whole workgroup.
-      const bool reuse =
-          g.freel != nullptr &&
-          __syncthreads_or(threadIdx.x == 0 &&
-                           __hip_atomic_load(&g.ctr->free_used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                               __hip_atomic_load(&g.ctr->free_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      // (the host passes no free list while it knows the list is empty:
+      // crgc_api.hip ids_view)
+      const bool reuse = g.freel != nullptr;
       if (reuse) {
         unsigned long long *const fc[1] = {&g.ctr->free_used};
         const uint64_t fn = g.ctr->free_n;
