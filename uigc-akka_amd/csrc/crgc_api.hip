@@ -3087,10 +3087,13 @@ int crgc_trace(crgc_graph *h, int should_kill, crgc_trace_out *out) {
     if (out->kill_ids) (void)host_kind(h, out->kill_ids, out->kill_cap * 8, &dk);
     auto sweep = [&]() -> hipError_t {
       hipError_t e = h->timed ? hipEventRecord(h->ev[1], h->stream) : hipSuccess;
-      if (e == hipSuccess) e = launch_sweep(h->g.d, should_kill ? 1 : 0, top, h->stream);
+      HostLists hl;
+      hl.g = dg;
+      hl.gcap = dg ? out->garbage_cap : 0;
+      hl.k = dk;
+      hl.kcap = dk ? out->kill_cap : 0;
+      if (e == hipSuccess) e = launch_sweep(h->g.d, should_kill ? 1 : 0, top, h->stream, 3, hl);
       if (e == hipSuccess && h->timed) e = hipEventRecord(h->ev[2], h->stream);
-      if (e == hipSuccess && (dg || dk))
-        e = launch_copy_lists(h->g.d, dg, dg ? out->garbage_cap : 0, dk, dk ? out->kill_cap : 0, h->stream);
       return e;  // the counters come back with the chunk's k_publish
     };
     int end = 0;

@@ -247,11 +247,18 @@ hipError_t launch_level(const DevGraph &g, const LevelArgs &a, bool roots, bool 
 // nh blocks of the shadows' own slots and np of the proxy region
 hipError_t launch_trace_reset(const DevGraph &g, uint64_t nh, uint64_t np, uint32_t ctr_from, uint32_t ctr_words,
                               hipStream_t s);
+// The caller's device-writable host buffers for the garbage / kill ids (page-
+// locked or registered; null: none), filled by k_sweep_gather beside out_ids /
+// out_kill when the lists fit and no NPE was seen.
+struct HostLists {
+  uint64_t *g = nullptr, *k = nullptr;
+  uint64_t gcap = 0, kcap = 0;
+};
 // sweep + id compaction + removal of the garbage (skipped on a reference NPE)
 // phase 1: classify + counts (k_sweep, k_sweep_scan); phase 2: ids + commit
 // (k_sweep_gather); 3: both
 hipError_t launch_sweep(const DevGraph &g, int should_kill, uint64_t slot_top, hipStream_t s,
-                        int phase = 3);
+                        int phase = 3, const HostLists &hl = HostLists{});
 int level_grid(uint64_t slot_top);
 bool walk_fits(int device);
 hipError_t launch_publish(const Counters *c, Counters *hdst, uint32_t r0, uint32_t rn, hipStream_t s);

@@ -2187,10 +2187,14 @@ __global__ __launch_bounds__(1024) void k_sweep_scan(DevGraph g, uint32_t sweep_
   }
 }
 
-__global__ __launch_bounds__(256) void k_sweep_gather(DevGraph g) {
+__global__ __launch_bounds__(256) void k_sweep_gather(DevGraph g, HostLists hl) {
   Counters *c = g.ctr;
   if (!c->mark_done) return;
   const bool commit = c->npe == 0;
+  // the ids straight into the caller's host buffers as well, when they fit (one
+  // kernel less than a copy behind the gather; the host checks the counts)
+  uint64_t *const hg = (hl.g && commit && c->n_garbage <= hl.gcap) ? hl.g : nullptr;
+  uint64_t *const hk = (hl.k && commit && c->n_kill <= hl.kcap) ? hl.k : nullptr;
   const uint64_t nblk = (c->slot_top + BLK_SLOTS - 1) / BLK_SLOTS;
   const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const uint64_t nw = (uint64_t)gridDim.x * 4;
@@ -2204,6 +2208,7 @@ __global__ __launch_bounds__(256) void k_sweep_gather(DevGraph g) {
       const uint32_t v = ga[i];
       const uint64_t id = g.vid[v];
       g.out_ids[go + i] = id;
+      if (hg) hg[go + i] = id;
       if (commit) {
         uint64_t bucket = KEY_EMPTY;
         id_find(g, id, &bucket);
@@ -2212,7 +2217,11 @@ __global__ __launch_bounds__(256) void k_sweep_gather(DevGraph g) {
         if (g.gslot) g.gslot[g.gslot_at + go + i] = v;  // slot reuse: purged, listed free (crgc_reuse.hip)
       }
     }
-    for (uint32_t i = lane_id(); i < kn; i += 64) g.out_kill[ko + i] = g.vid[ka[i]];
+    for (uint32_t i = lane_id(); i < kn; i += 64) {
+      const uint64_t id = g.vid[ka[i]];
+      g.out_kill[ko + i] = id;
+      if (hk) hk[ko + i] = id;
+    }
   }
 }
 
@@ -2263,14 +2272,14 @@ hipError_t launch_publish(const Counters *c, Counters *hdst, uint32_t r0, uint32
 }
 
 hipError_t launch_sweep(const DevGraph &g, int should_kill, uint64_t slot_top, hipStream_t s,
-                        int phase) {
+                        int phase, const HostLists &hl) {
   launch_begin();
   const int grid = level_grid(slot_top);
   if (phase & 1) {
     hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(256), 0, s, g, should_kill);
     hipLaunchKernelGGL(k_sweep_scan, dim3(1), dim3(1024), 0, s, g, (uint32_t)grid);
   }
-  if (phase & 2) hipLaunchKernelGGL(k_sweep_gather, dim3(grid), dim3(256), 0, s, g);
+  if (phase & 2) hipLaunchKernelGGL(k_sweep_gather, dim3(grid), dim3(256), 0, s, g, hl);
   return hipGetLastError();
 }
 
