@@ -460,6 +460,13 @@ struct crgc_graph {
   // them merge on `stream` (merge_entries_chunked).
   hipStream_t cpy = nullptr;
   hipEvent_t ev_cstart = nullptr, ev_chunk[8] = {};
+  // Host-batch chunk merges stage into two areas in turn: a call's copy waits
+  // only for the merges that last read its area (ev_cfree), so a drain loop's
+  // next chunk is copied while the previous one merges
+  Scratch cstage[2];
+  hipEvent_t ev_cfree[2] = {};
+  bool cfree_rec[2] = {false, false};
+  int cstage_k = 0;
   // CRGC_SIDE_STREAM=1 (read at create): the edge pipeline beside the vertex
   // updates.  Off: both halves are bound by random memory operations, so the
   // overlap bought nothing (merge 0.578-0.587 ms alone vs 0.588-0.598 ms with
@@ -989,6 +996,8 @@ int crgc_create(const crgc_config *cfg, crgc_graph **out) {
       rc = DEV_FAIL("");
     for (auto &e : h->ev_chunk)
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = DEV_FAIL("");
+    for (auto &e : h->ev_cfree)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = DEV_FAIL("");
     // CRGC_SIDE_PRIO=1: the side stream (the merge's critical path) at the
     // device's highest priority, so its workgroups dispatch first
     const int side_prio = h->knobs.side_prio ? prio_hi : 0;
@@ -1041,6 +1050,7 @@ void crgc_destroy(crgc_graph *h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   free_arrays(h->g);
   h->stage.release();
+  for (Scratch &x : h->cstage) x.release();
   h->work.release();
   for (Scratch *x : {&h->x_send, &h->x_slot, &h->x_recv, &h->x_ans, &h->x_ans_back, &h->x_small,
                      &h->x_pack, &h->x_pack_recv, &h->x_route, &h->x_route_send, &h->x_cat,
@@ -1064,6 +1074,8 @@ void crgc_destroy(crgc_graph *h) {
   }
   if (h->ev_cstart) hipEventDestroy(h->ev_cstart);
   for (auto &e : h->ev_chunk)
+    if (e) hipEventDestroy(e);
+  for (auto &e : h->ev_cfree)
     if (e) hipEventDestroy(e);
   if (h->ev_fork) hipEventDestroy(h->ev_fork);
   if (h->ev_join) hipEventDestroy(h->ev_join);
@@ -1696,14 +1708,18 @@ static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint3
       total += sz[i];
     }
   }
-  // (a larger staging area frees the old one: let the work queued on it finish first —
-  // an async merge's copies and merges may still read it)
-  if (total + 256 > h->stage.bytes) HIP_TRY(hsync(h));
-  if (h->stage.ensure(total + 256) != hipSuccess) return CRGC_E_NOMEM;
-  char *base = (char *)h->stage.ptr;
-  // the staging area is free once the work already queued on the graph's stream is done
-  HIP_TRY(hipEventRecord(h->ev_cstart, h->stream));
-  HIP_TRY(hipStreamWaitEvent(h->cpy, h->ev_cstart, 0));
+  // This call's staging area (two in turn): free once the merges of the call
+  // that last used it are done (ev_cfree, recorded behind them on the graph's
+  // stream), so its copy can run beside the previous call's merge.  (A larger
+  // area frees the old one: let the work queued on it finish first — an async
+  // merge's copies and merges may still read it.)
+  const int sk = h->cstage_k;
+  h->cstage_k ^= 1;
+  Scratch &stg = h->cstage[sk];
+  if (total + 256 > stg.bytes) HIP_TRY(hsync(h));
+  if (stg.ensure(total + 256) != hipSuccess) return CRGC_E_NOMEM;
+  char *base = (char *)stg.ptr;
+  if (h->cfree_rec[sk]) HIP_TRY(hipStreamWaitEvent(h->cpy, h->ev_cfree[sk], 0));
   auto copy_chunk = [&](uint32_t j) -> hipError_t {
     const Part &q = p[j];
     const uint64_t m = q.hi - q.lo;
@@ -1775,6 +1791,12 @@ static int merge_entries_chunked(crgc_graph *h, const crgc_entry_batch *b, uint3
     v.updated_info = (const int16_t *)(base + q.off[10]);
     v.memory = CRGC_MEM_DEVICE;
     rc = merge_entries_one(h, &v, q.c1 - q.c0, q.s1 - q.s0, q.u1 - q.u0);
+  }
+  // the area is free again once these merges are done
+  if (hipError_t e = hipEventRecord(h->ev_cfree[sk], h->stream)) {
+    if (rc == CRGC_OK) rc = map_hip(e);
+  } else {
+    h->cfree_rec[sk] = true;
   }
   // the caller's buffers are read only during the call (async: until the
   // next trace or sync, which wait for the graph's stream and so for these
