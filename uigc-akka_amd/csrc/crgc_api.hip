@@ -2775,6 +2775,7 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
   // every shard (all-gathered counts).
   uint64_t gwords = 0, prev_total = ~0ull;
   for (uint32_t d = 0; d < G; ++d) gwords += words(d);
+  std::vector<uint64_t> hist;  // marks sent per round (the closure's shape test)
   for (;;) {
     const auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(xcnt), 0, 3 * MAX_SHARDS * 8, h->stream));  // xcnt .. xcnt2
@@ -2812,8 +2813,8 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
       for (uint32_t k = 0; k < 2 * G; ++k) total += M[(size_t)r * (2 * G + 1) + k];
       pending += M[(size_t)r * (2 * G + 1) + 2 * G];
     }
-    const uint64_t last_total = prev_total;
     prev_total = total;
+    hist.push_back(total);
     if (total == 0 && pending == 0) {
       *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       return CRGC_OK;
@@ -2861,25 +2862,34 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
       // (never with candidates pending: the closure starts from marks only)
       bool closure = xmode != 0 && pending == 0 && kn.xclosure_after && *rounds >= kn.xclosure_after &&
                      (kn.xclosure_narrow == 0 || marks * kn.xclosure_narrow <= n_all) && n_all < 0xF0000000ull;
-      // ... and only when the rounds it saves would cost more than it does.  Its
-      // five all-gathers bring every shard ~8.4 B per slot of the rest of the
-      // graph; a further round costs a fixed exchange and level floor
-      // (xround_bytes, in link bytes) plus its marks.  A chain's marks per round
-      // stay level (rounds left: unbounded); a shallow graph's last rounds shrink
-      // geometrically (C2 over 8 shards: the closure fired at round 8 and moved
-      // 1.05 GB per wakeup, profiles/r5aq), leaving ~log(marks)/log(ratio).
-      // The test hook xclosure_narrow = 0 forces it.
+      // ... and only for a chain-shaped mark, when the rounds it saves would cost
+      // more than it does.  Its five all-gathers bring every shard ~8.4 B per
+      // slot of the rest of the graph; a further round costs a fixed exchange
+      // and level floor (xround_bytes, in link bytes) plus its marks.  A
+      // chain's marks per round stay level: over the last XC_WINDOW rounds no
+      // round sent less than half the round before (rounds left: from their
+      // mean ratio, unbounded when level).  A shallow graph's last rounds fall
+      // off faster: on C2 over 8 logical shards a closure at round 8 (the
+      // round-5 rule, and a one-ratio test this round) moved 1.05 GB per
+      // wakeup and still ended at round 9, 15.6 / 17.0 against 13.5 / 13.5 ms
+      // without it (profiles/r6j).  The test hook xclosure_narrow = 0 forces it.
       if (closure && kn.xclosure_narrow != 0) {
+        constexpr size_t XC_WINDOW = 3;
         const double cbytes = 8.375 * (double)n_all * (double)(G - 1) / (double)G;
+        bool chain = hist.size() > XC_WINDOW;
+        double lr = 0;  // mean log ratio of the window's rounds
+        for (size_t k = hist.size() - std::min(hist.size(), XC_WINDOW); chain && k < hist.size(); ++k) {
+          if (k == 0 || hist[k - 1] == 0 || 2 * hist[k] < hist[k - 1]) chain = false;
+          else lr += std::log((double)hist[k] / (double)hist[k - 1]) / (double)XC_WINDOW;
+        }
         double left = 1e30;
         if (marks == 0) left = 1;
-        else if (last_total != ~0ull && 2 * marks < last_total)
-          left = std::log((double)marks) / std::log((double)last_total / (double)marks) + 1.0;
-        closure = left * ((double)kn.xround_bytes + 4.0 * (double)marks) >= cbytes;
+        else if (chain && lr < -0.05) left = std::log((double)marks) / -lr + 1.0;
+        closure = chain && left * ((double)kn.xround_bytes + 4.0 * (double)marks) >= cbytes;
         if (kn.level_log)
-          fprintf(stderr, "[crgc] shard %u round %llu: marks %llu (last %llu), closure %.1f MB vs %.1f rounds left: %s\n",
-                  me, (unsigned long long)*rounds, (unsigned long long)marks, (unsigned long long)last_total,
-                  cbytes / 1e6, left > 1e29 ? -1.0 : left, closure ? "closure" : "rounds");
+          fprintf(stderr, "[crgc] shard %u round %llu: marks %llu, closure %.1f MB, chain-shaped %d, %.1f rounds left: %s\n",
+                  me, (unsigned long long)*rounds, (unsigned long long)marks, cbytes / 1e6, chain ? 1 : 0,
+                  left > 1e29 ? -1.0 : left, closure ? "closure" : "rounds");
       }
       if (closure) {
         *ms_x += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
