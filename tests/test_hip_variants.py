@@ -94,3 +94,25 @@ def test_host_batches_binned_level0_match_oracle(hip_mod, oracle_results, monkey
     for i in range(WAKEUPS):
         h.merge_entries(w.wakeup_batch(BATCH))
         assert _key(h.trace(True)) == oracle_results[i + 1], f"wakeup {i}"
+
+
+def test_sampled_timing_matches_oracle(hip_mod, oracle_results, monkeypatch):
+    """CRGC_TIMING_EVERY=2 (round 6): only every other trace carries timing
+    events; the traces in between report no device times and no timed
+    launches.  What is marked never depends on it."""
+    monkeypatch.setenv("CRGC_TIMING_EVERY", "2")
+    w = _stream()
+    h = hip_mod.ShadowGraph(vertex_capacity=ACTORS * 2, edge_capacity=EDGES * 2)
+    for b in w.batches(1 << 20):
+        h.merge_entries(b)
+    rs = [h.trace(True)]
+    assert _key(rs[0]) == oracle_results[0]
+    for i in range(WAKEUPS):
+        h.merge_entries(w.wakeup_batch(BATCH).to_device())
+        rs.append(h.trace(True))
+        assert _key(rs[-1]) == oracle_results[i + 1], f"wakeup {i}"
+    for k, r in enumerate(rs):
+        if k % 2 == 0:
+            assert r.ms_mark > 0 and r.expand_launches > 0, k
+        else:
+            assert r.ms_mark == 0 and r.ms_sweep == 0 and r.expand_launches == 0, k
