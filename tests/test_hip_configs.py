@@ -143,10 +143,10 @@ def test_slot_reuse_batches_through_grows(hip_mod, oracle_mod, monkeypatch, div)
     assert u["grows"] >= 1, u
 
 
-@pytest.mark.parametrize("chain_after", ["64", "0", "2"])
+@pytest.mark.parametrize("chain_after", ["16", "64", "0", "2"])
 def test_c3_deep_chains_and_dead_rings(hip_mod, oracle_mod, monkeypatch, chain_after):
     """Chains walked by k_tail (CRGC_CHAIN_AFTER=0) or handed to chain mode
-    (pointer jumping) after 64 / 2 links: the same marks."""
+    (pointer jumping) after 16 (the default) / 64 / 2 links: the same marks."""
     monkeypatch.setenv("CRGC_CHAIN_AFTER", chain_after)
     w = world.World(seed=0x5EED + 3)
     w.chain_graph(n_chains=20, chain_len=3000, n_sup_chains=5, sup_depth=400,

@@ -287,7 +287,10 @@ struct Knobs {
   bool walk_unsharded = false;   // CRGC_WALK_UNSHARDED=1: k_walk for unsharded graphs too (no chain mode then)
   uint32_t walk_start = 16384;   // CRGC_WALK_START
   uint32_t walk_max = 32768;     // CRGC_WALK_MAX
-  uint32_t chain_after = 64;     // CRGC_CHAIN_AFTER
+  // CRGC_CHAIN_AFTER: a k_tail walk of this many links hands the rest of the
+  // mark to chain mode.  16 (64 until round 6): C3 1.112 / 1.086 -> 0.968 /
+  // 1.059 ms per trace, C2 and C1 unchanged (profiles/r6u)
+  uint32_t chain_after = 16;
   // CRGC_KERNEL_TIMING: 0 chunks only, 1 every level's expand, 2 all level
   // kernels, 3 (default) the expand of the wide levels 0 and 1 only.  A timing
   // event carried by a dispatch costs ~5 us of idle GPU around it
