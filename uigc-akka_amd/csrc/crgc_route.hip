@@ -90,36 +90,55 @@ __global__ __launch_bounds__(RT_THREADS) void k_route_count(RouteArgs a) {
 }
 
 // One workgroup per destination: exclusive prefixes of the four counts over
-// the blocks, and the destination's totals.
-__global__ __launch_bounds__(256) void k_route_scan(RouteArgs a) {
-  __shared__ uint32_t s_w[4][4];
+// the blocks, and the destination's totals.  A thread takes RS_K consecutive
+// blocks, so a C2 wakeup's ~3 900 blocks are one pass of 1024 threads (a
+// 256-thread loop over them was 16 dependent rounds, 25 us: profiles/r6o).
+constexpr int RS_THREADS = 1024, RS_K = 4;
+__global__ __launch_bounds__(RS_THREADS) void k_route_scan(RouteArgs a) {
+  __shared__ uint32_t s_w[RS_THREADS / 64][4];
   __shared__ uint64_t s_carry[4];
   const uint32_t d = blockIdx.x;
   const int lane = lane_id(), wv = threadIdx.x >> 6;
   if (threadIdx.x < 4) s_carry[threadIdx.x] = 0;
   __syncthreads();
-  for (uint64_t b0 = 0; b0 < a.nblk; b0 += 256) {
-    const uint64_t b = b0 + threadIdx.x;
-    const uint64_t p = b < a.nblk ? a.blk_tot[(uint64_t)d * a.nblk + b] : 0;
-    uint32_t f[4], inc[4];
+  const uint64_t *bt = a.blk_tot + (uint64_t)d * a.nblk;
+  uint64_t *bp = a.blk_pre + (uint64_t)d * a.nblk * 4;
+  for (uint64_t b0 = 0; b0 < a.nblk; b0 += (uint64_t)RS_THREADS * RS_K) {
+    const uint64_t b = b0 + (uint64_t)threadIdx.x * RS_K;
+    uint64_t p[RS_K];
+#pragma unroll
+    for (int k = 0; k < RS_K; ++k) p[k] = b + k < a.nblk ? bt[b + k] : 0ull;
+    uint32_t f[4] = {0, 0, 0, 0}, inc[4];  // (a pass's sums stay below 4096 x 2^16)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      f[q] = (uint32_t)((p >> (16 * q)) & 0xFFFFu);
+#pragma unroll
+      for (int k = 0; k < RS_K; ++k) f[q] += (uint32_t)((p[k] >> (16 * q)) & 0xFFFFu);
       inc[q] = wave_incl_scan(f[q]);
     }
     if (lane == 63)
       for (int q = 0; q < 4; ++q) s_w[wv][q] = inc[q];
     __syncthreads();
+    uint64_t pre[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      uint64_t pre = s_carry[q];
-      for (int w = 0; w < wv; ++w) pre += s_w[w][q];
-      if (b < a.nblk) a.blk_pre[((uint64_t)d * a.nblk + b) * 4 + q] = pre + inc[q] - f[q];
+      pre[q] = s_carry[q] + inc[q] - f[q];
+      for (int w = 0; w < wv; ++w) pre[q] += s_w[w][q];
+    }
+#pragma unroll
+    for (int k = 0; k < RS_K; ++k) {
+      if (b + k >= a.nblk) break;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bp[(b + k) * 4 + q] = pre[q];
+        pre[q] += (p[k] >> (16 * q)) & 0xFFFFu;
+      }
     }
     __syncthreads();
-    if (threadIdx.x < 4)
-      s_carry[threadIdx.x] += (uint64_t)s_w[0][threadIdx.x] + s_w[1][threadIdx.x] + s_w[2][threadIdx.x] +
-                             s_w[3][threadIdx.x];
+    if (threadIdx.x < 4) {
+      uint64_t t = 0;
+      for (int w = 0; w < RS_THREADS / 64; ++w) t += s_w[w][threadIdx.x];
+      s_carry[threadIdx.x] += t;
+    }
     __syncthreads();
   }
   if (threadIdx.x < 4) a.totals[d * 4 + threadIdx.x] = s_carry[threadIdx.x];
@@ -209,7 +228,7 @@ hipError_t launch_route(const RouteArgs &a, int phase, const RoutePart *parts, h
   const int blocks = (int)a.nblk;
   if (phase == 0) {
     hipLaunchKernelGGL(k_route_count, dim3(blocks), dim3(RT_THREADS), 0, s, a);
-    hipLaunchKernelGGL(k_route_scan, dim3(a.G), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_route_scan, dim3(a.G), dim3(RS_THREADS), 0, s, a);
   } else {
     hipLaunchKernelGGL(k_route_scatter, dim3(blocks), dim3(RT_THREADS), 0, s, a, parts);
   }
