@@ -274,7 +274,9 @@ struct Knobs {
   // k_tail walks frontiers of at most this many out-edges per round (0: no
   // bound).  A shard's hubs are mostly edges to proxies, each a global claim
   // by the one workgroup: C2 over 8 logical shards spent 2.1 of its 3.4 ms of
-  // k_tail per wakeup in ~11 walks of 230-275 us (profiles/r6b).  CRGC_TAIL_EDGES
+  // k_tail per wakeup in ~11 walks of 230-275 us in an early round-6 run (its
+  // record was lost); with the bound k_tail averages 14.5 us per launch there
+  // (profiles/r6i/c2l8s_kernels_per_wakeup.txt).  CRGC_TAIL_EDGES
   uint32_t tail_edges = 0;
   uint32_t tail_edges_sharded = 32768;
   // k_walk (WALK_WG workgroups with grid barriers) in place of k_tail for a
@@ -294,13 +296,13 @@ struct Knobs {
   // CRGC_KERNEL_TIMING: 0 chunks only, 1 every level's expand, 2 all level
   // kernels, 3 (default) the expand of the wide levels 0 and 1 only.  A timing
   // event carried by a dispatch costs ~5 us of idle GPU around it
-  // (tools/event_probe.hip, profiles/r6a): ~60 us per C2 wakeup with every
+  // (tools/event_probe.hip, profiles/r6g/event_probe.txt): ~60 us per C2 wakeup with every
   // expand timed, most of it on narrow levels that carry ~20 % of the
   // expand's device time.
   int kernel_timing = 3;
   // CRGC_TIMING_EVERY=k: only every k-th trace carries timing events (its
   // level chunks, timed expands and sweep; the others report 0 ms and 0 timed
-  // launches).  Each event costs ~5 us of idle GPU (r6a), ~45 us per C2 wakeup
+  // launches).  Each event costs ~5 us of idle GPU (r6g), ~45 us per C2 wakeup
   // in all (profiles/r6d/c2_last_wakeup_timeline.txt); a sample of the traces
   // is enough for the device-time figures.
   uint32_t timing_every = 1;
