@@ -348,6 +348,31 @@ def test_c4_shape_eight_shards(sharded, oracle_mod, xbits, xlevels, ratio, xfilt
     assert h.total_actors_seen() == o.total_actors_seen()
 
 
+@pytest.mark.parametrize("xq,ratio", [("1", "32"), ("8", "32"), ("8", "1")])
+def test_c4_shape_eight_shards_xscan_units(sharded, oracle_mod, xq, ratio, monkeypatch):
+    """The export scan (k_xscan) with a wave per whole proxy block (1) or per
+    eighth of one (8; the default is a quarter), as lists and as bitmaps
+    (CRGC_XBITMAP_RATIO=1): bit-exact against the unsharded oracle on G = 8."""
+    monkeypatch.setenv("CRGC_XSCAN_Q", xq)
+    monkeypatch.setenv("CRGC_XBITMAP_RATIO", ratio)
+    V = 200_000
+    w = world.World(seed=0x5EED + 5)
+    w.bulk_graph(V, 10 * V, alpha=2.1, n_roots=V // 1000, cap=100000)
+    h, o = sharded(8), oracle_mod.OracleGraph()
+    for b in w.batches(1 << 18):
+        h.merge_entries(b, split=True)
+        o.merge_entries(b)
+    _same(h.trace(True), o.trace(True))
+    for _ in range(3):
+        b = w.wakeup(V // 10, busy=V * 9 // 100, pending=V // 100)
+        h.merge_entries(b, split=True)
+        o.merge_entries(b)
+        rh = h.trace(True)
+        _same(rh, o.trace(True))
+        assert rh.rounds >= 2 and rh.ids_sent > 0
+    assert h.export() == o.export()
+
+
 @pytest.mark.parametrize("walk", [{"CRGC_WALK": "1"},
                                   {"CRGC_WALK": "1", "CRGC_WALK_START": "64", "CRGC_WALK_MAX": "128"},
                                   {"CRGC_WALK": "1", "CRGC_WALK_START": "65536", "CRGC_WALK_MAX": "65536"},

@@ -327,6 +327,11 @@ struct Knobs {
   uint32_t xlevels = 0;          // CRGC_XLEVELS
   uint32_t idtab_x2 = 3;         // CRGC_IDTAB_X2: id-table buckets per slot x 2 (caps_regions)
   bool xfilter = true;           // CRGC_XFILTER=0: send every newly marked proxy (mark_all)
+  // CRGC_ROUND_CHUNK (test hook): levels a sharded mark round launches before
+  // its first host check when it starts from more than tail_start_sharded marks
+  // (0: as many as the previous round needed, 1 .. 4)
+  uint32_t round_chunk = 4;
+  uint32_t xscan_q = 4;          // CRGC_XSCAN_Q (test hook): k_xscan's units per proxy block (1, 2, 4, 8)
   uint64_t xbitmap_ratio = 32;   // CRGC_XBITMAP_RATIO: a mark round's home slots as a bitmap above
                                  // this many list bytes per bitmap byte (mark_all; 32: never)
   bool bin = true;               // CRGC_BIN=0: the pseudo-root level pushes candidate bytes directly
@@ -403,6 +408,11 @@ struct Knobs {
     if (const char *m = env("CRGC_XLEVELS")) xlevels = (uint32_t)strtoul(m, nullptr, 10);
     if (const char *m = env("CRGC_XFILTER")) xfilter = atoi(m) != 0;
     if (const char *m = env("CRGC_XBITMAP_RATIO")) xbitmap_ratio = std::max<uint64_t>(1, strtoull(m, nullptr, 10));
+    if (const char *m = env("CRGC_ROUND_CHUNK")) round_chunk = std::min<uint32_t>((uint32_t)strtoul(m, nullptr, 10), 64);
+    if (const char *m = env("CRGC_XSCAN_Q")) {
+      const uint32_t v = (uint32_t)strtoul(m, nullptr, 10);
+      if (v == 1 || v == 2 || v == 4 || v == 8) xscan_q = v;
+    }
     if (const char *m = env("CRGC_IDTAB_X2")) idtab_x2 = std::max<uint32_t>(1, (uint32_t)strtoul(m, nullptr, 10));
     if (const char *m = env("CRGC_XSLICES")) {
       const uint32_t v = (uint32_t)strtoul(m, nullptr, 10);
@@ -2567,7 +2577,7 @@ static int resolve_home_slots(crgc_graph *h, uint64_t top, int xmode, uint64_t *
   if (xmode == 0) return CRGC_OK;  // ids only: nothing to resolve
   const uint64_t ptop = proxy_top_ub(h);  // (grids over the proxy region)
   if (mask) HIP_TRY(launch_resolve(h->g.d, 0, mask, nullptr, nullptr, nullptr, 0, nullptr, ptop, h->stream));
-  HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(xcnt), 0, 2 * MAX_SHARDS * 8, h->stream));
+  HIP_TRY(launch_zero_u64((char *)h->ctr + CTR_OFF(xcnt), 2 * MAX_SHARDS, h->stream));
   HIP_TRY(launch_resolve(h->g.d, 1, 0, nullptr, nullptr, nullptr, 0, nullptr, ptop, h->stream));
   std::vector<uint64_t> M((size_t)G * G);
   if (int rc = ag_u64(h, {{(char *)h->ctr + CTR_OFF(xcnt), G}}, M.data())) return rc;
@@ -2781,11 +2791,15 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
   uint64_t gwords = 0, prev_total = ~0ull;
   for (uint32_t d = 0; d < G; ++d) gwords += words(d);
   std::vector<uint64_t> hist;  // marks sent per round (the closure's shape test)
+  int prev_used = 4;           // level launches the previous round needed (CRGC_ROUND_CHUNK=0)
   for (;;) {
     const auto t0 = std::chrono::steady_clock::now();
-    HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(xcnt), 0, 3 * MAX_SHARDS * 8, h->stream));  // xcnt .. xcnt2
+    // xcnt / xcnt2: k_xscan_sum writes every destination's totals; zeroed
+    // only when there is no proxy block to scan
+    if (npb == 0) HIP_TRY(launch_zero_u64((char *)h->ctr + CTR_OFF(xcnt), 3 * MAX_SHARDS, h->stream));
     XSend xs{};
     xs.use_slots = xmode != 0;
+    xs.xq = h->knobs.xscan_q;
     if (xmode != 0 && h->knobs.xfilter && prev_total >= gwords && gwords) {
       if (h->x_gvis.ensure(gwords * 4 + 8) != hipSuccess) return CRGC_E_NOMEM;
       size_t soff[MAX_SHARDS], sb[MAX_SHARDS], roff[MAX_SHARDS], rb[MAX_SHARDS];
@@ -2806,7 +2820,7 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
       *x_bytes += words(me) * 4 * (G - 1);
       xs.gvis = (const uint32_t *)h->x_gvis.ptr;
     }
-    if (h->x_wgc.ensure((size_t)xscan_grid(npb) * 2 * G * 4 + 8) != hipSuccess) return CRGC_E_NOMEM;
+    if (h->x_wgc.ensure((size_t)xscan_grid(npb, xs.xq) * 2 * G * 4 + 8) != hipSuccess) return CRGC_E_NOMEM;
     HIP_TRY(launch_xlist(h->g.d, false, npb, nullptr, xs, (uint32_t *)h->x_wgc.ptr, h->stream));
     // (with the counts, whether each shard's round was capped with work pending)
     h->h_small[SMALL_PEND_OFF / 8] = capped ? 1 : 0;
@@ -2914,9 +2928,11 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
     // A round from a few received marks is usually finished by k_tail in its
     // first level: launch one level first, not four (the rest would only check
     // that the mark is done: ~13 us each)
-    const int first = !capped && items <= (h->knobs.walk ? h->knobs.walk_start : h->knobs.tail_start_sharded) ? 1 : 4;
+    const int wide = h->knobs.round_chunk ? (int)h->knobs.round_chunk : std::max(1, std::min(4, prev_used));
+    const int first = !capped && items <= (h->knobs.walk ? h->knobs.walk_start : h->knobs.tail_start_sharded) ? 1 : wide;
     if (int rc = run_levels(h, investigate, location, top, false, L, lr, &end, nullptr, cap, &capped, first))
       return rc;
+    prev_used = std::max(1, end - L + 1);  // (its levels with marks and the empty one that ended it)
     ++*rounds;
   }
 }
@@ -3025,7 +3041,7 @@ static int sweep_sharded(crgc_graph *h, int should_kill, uint64_t top, double *m
   const uint32_t G = h->G, me = h->shard;
   const uint64_t nblk = round_up(std::min<uint64_t>(top, h->g.caps.scap), BLK_SLOTS) / BLK_SLOTS;
   HIP_TRY(launch_sweep(h->g.d, should_kill, top, h->stream, 1));
-  HIP_TRY(hipMemsetAsync((char *)h->ctr + CTR_OFF(xcnt), 0, 2 * MAX_SHARDS * 8, h->stream));
+  HIP_TRY(launch_zero_u64((char *)h->ctr + CTR_OFF(xcnt), 2 * MAX_SHARDS, h->stream));
   HIP_TRY(launch_list(h->g.d, 1, false, h->g.d.rq_buf, h->g.d.rq_cnt, nblk, nullptr, nullptr, h->stream));
   const auto t0 = std::chrono::steady_clock::now();
   // one all-gather: every shard's NPE count, garbage count (k_sweep_scan has it)

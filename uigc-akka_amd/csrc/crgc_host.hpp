@@ -274,6 +274,7 @@ struct XSend {
   uint64_t id_off[MAX_SHARDS], sl_off[MAX_SHARDS];
   uint8_t bitmap[MAX_SHARDS];
   int use_slots;
+  uint32_t xq;  // k_xscan's units per 2048-proxy block (1, 2, 4 or 8; a wave each)
   // every shard's marked bitmap of its own shadows, as of this round's
   // exchange (word offsets per shard, G + 1 of them; null: none): a proxy
   // whose home slot is marked there is not sent
@@ -290,7 +291,7 @@ struct XRecv {
 // (nblk: a bound of the proxy region's blocks, for the grid)
 hipError_t launch_xlist(const DevGraph &g, bool scatter, uint64_t nblk, char *send, const XSend &x,
                         uint32_t *wgc, hipStream_t s);
-int xscan_grid(uint64_t nblk);  // k_xscan's workgroups (the counts `wgc` holds: 2 G u32 each)
+int xscan_grid(uint64_t nblk, uint32_t xq);  // k_xscan's workgroups (the counts `wgc` holds: 2 G u32 each)
 // The replicated chain closure of deep sharded marks (crgc_xchain.hip).
 struct XcArgs {
   uint32_t G, me;
@@ -313,6 +314,9 @@ hipError_t launch_xclosure(const DevGraph &g, const XcArgs &x, int step, const v
                            uint32_t fi, int first, hipStream_t s);
 hipError_t launch_ximport(const DevGraph &g, const char *recv, const XRecv &x, int level, hipStream_t s);
 hipError_t launch_round_start(Counters *c, int level, bool fresh, hipStream_t s);
+// n words from p zeroed by one dispatch (a small hipMemsetAsync is up to three
+// fill kernels, ~3.6 us each, several per sharded mark round: profiles/r6y)
+hipError_t launch_zero_u64(void *p, uint32_t n, hipStream_t s);
 // home-slot resolution: 0 reset(mask), 1 count unresolved, 2 list them (ids, slots),
 // 3 answer asked ids (at the home), 4 store the answers, 5 every proxy so far has asked
 // (n_proxy: a bound of the proxy slots, for the grids)

@@ -2474,8 +2474,8 @@ hipError_t launch_resolve(const DevGraph &g, int step, uint64_t mask, uint64_t *
 // per-block regions as the level kernels found them and packed the lists: a
 // chain of dependent loads per entry, ~0.8 ms per shard for C4's first round
 // over 8 logical shards).
-// One wave per 2048-proxy block: lane l holds the block's words l (marked and
-// sent); step k covers slots 64k .. 64k+63 (slot 64k + l: word 2k + l / 32,
+// One wave per quarter q of a 2048-proxy block: lane l holds the block's word l
+// (marked and sent) when l / 16 == q; step k (8q .. 8q + 7) covers slots 64k .. 64k+63 (slot 64k + l: word 2k + l / 32,
 // bit l % 32, by one shuffle), so the loads of a step are coalesced; XU steps
 // per load group.  The count pass derives each new mark's key (form << 6 |
 // destination; 0xFF: none — its home is marked already) from the home shard,
@@ -2504,12 +2504,25 @@ __global__ __launch_bounds__(256) void k_xscan(DevGraph g, char *send, XSend x, 
   const uint64_t w0 = g.pbase / 32;  // the region's first marked word (pbase is block-aligned)
   const uint32_t lane = lane_id();
   constexpr uint32_t XU = 4;
-  for (uint64_t blk = gw; blk < nb; blk += nw) {
+  // A wave's unit is 1 / xq of a block (xq = 4: 512 slots, words 16q .. 16q +
+  // 15, steps 8q .. 8q + 7): a new mark's key is a chain of dependent loads
+  // (psh, phs, the home bitmap), so xq times the waves hide xq times the
+  // latency (a wave per block walked its 32 steps alone: 22 / 40 us per count /
+  // scatter pass on C2 over 8 logical shards, profiles/r6i; 13 / 18 us at 4)
+  const uint32_t XQ = x.xq, wpu = 64 / XQ, spu = 32 / XQ;
+  const uint64_t nu = nb * XQ;
+  for (uint64_t un = gw; un < nu; un += nw) {
+    const uint64_t blk = un / XQ;
+    const uint32_t q = (uint32_t)(un % XQ);
     const uint64_t w = w0 + blk * 64 + lane;
-    const uint32_t mw = g.vis[w], sw = g.xsent[w];
+    uint32_t mw = 0, sw = 0;
+    if (lane / wpu == q) {  // this lane's word is in the unit
+      mw = g.vis[w];
+      sw = g.xsent[w];
+    }
     const uint32_t nm = mw & ~sw;
     if (!__ballot(nm != 0)) continue;
-    for (uint32_t k0 = 0; k0 < 32; k0 += XU) {
+    for (uint32_t k0 = spu * q; k0 < spu * q + spu; k0 += XU) {
       uint32_t v[XU], key[XU];
       bool any = false;
 #pragma unroll
@@ -2599,17 +2612,30 @@ __global__ __launch_bounds__(256) void k_xscan(DevGraph g, char *send, XSend x, 
 }
 
 // Per key (one workgroup each): the exclusive scan of the workgroups' counts
-// in place, the total into xcnt / xcnt2.
+// in place, the total into xcnt / xcnt2.  XS consecutive workgroups' counts per
+// thread: up to 4096 workgroups in one pass (one per thread was a pass per
+// 1024, 8.4 us at C2 over 8 logical shards with quarter-block units).
 __global__ __launch_bounds__(1024) void k_xscan_sum(DevGraph g, uint32_t *wgc, uint32_t nwg) {
+  constexpr uint32_t XS = 4;
   __shared__ uint32_t s_w[40];
   const uint32_t G = g.n_shards, q = blockIdx.x;
   uint32_t run = 0;
-  for (uint32_t w0 = 0; w0 < nwg; w0 += 1024) {
-    const uint32_t w = w0 + threadIdx.x;
-    const uint32_t n = w < nwg ? wgc[(uint64_t)w * 2 * G + q] : 0u;
+  for (uint32_t w0 = 0; w0 < nwg; w0 += 1024 * XS) {
+    const uint32_t wb = w0 + threadIdx.x * XS;
+    uint32_t n[XS], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < XS; ++k) {
+      n[k] = wb + k < nwg ? wgc[(uint64_t)(wb + k) * 2 * G + q] : 0u;
+      sum += n[k];
+    }
     uint32_t tot;
-    const uint32_t ex = tail_scan(n, s_w, tot);
-    if (w < nwg) wgc[(uint64_t)w * 2 * G + q] = run + ex;
+    uint32_t ex = run + tail_scan(sum, s_w, tot);
+#pragma unroll
+    for (uint32_t k = 0; k < XS; ++k)
+      if (wb + k < nwg) {
+        wgc[(uint64_t)(wb + k) * 2 * G + q] = ex;
+        ex += n[k];
+      }
     run += tot;
   }
   if (threadIdx.x == 0) {
@@ -2618,13 +2644,13 @@ __global__ __launch_bounds__(1024) void k_xscan_sum(DevGraph g, uint32_t *wgc, u
   }
 }
 
-int xscan_grid(uint64_t nblk) { return (int)std::max<uint64_t>(1, std::min<uint64_t>((nblk + 3) / 4, 8192)); }
+int xscan_grid(uint64_t nblk, uint32_t xq) { return (int)std::max<uint64_t>(1, std::min<uint64_t>((nblk * xq + 3) / 4, 8192)); }
 
 hipError_t launch_xlist(const DevGraph &g, bool scatter, uint64_t nblk, char *send, const XSend &x,
                         uint32_t *wgc, hipStream_t s) {
   launch_begin();
   if (nblk == 0) return hipSuccess;
-  const int grid = xscan_grid(nblk);
+  const int grid = xscan_grid(nblk, x.xq);
   if (scatter) {
     hipLaunchKernelGGL(k_xscan<true>, dim3(grid), dim3(256), 0, s, g, send, x, wgc);
   } else {
@@ -2717,6 +2743,17 @@ __global__ void k_round_start(Counters *c, int L, int fresh) {
 hipError_t launch_round_start(Counters *c, int level, bool fresh, hipStream_t s) {
   launch_begin();
   hipLaunchKernelGGL(k_round_start, dim3(1), dim3(1), 0, s, c, level, fresh ? 1 : 0);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_zero_u64(unsigned long long *p, uint32_t n) {
+  for (uint32_t i = threadIdx.x; i < n; i += 256) p[i] = 0;
+}
+
+hipError_t launch_zero_u64(void *p, uint32_t n, hipStream_t s) {
+  launch_begin();
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_zero_u64, dim3(1), dim3(256), 0, s, (unsigned long long *)p, n);
   return hipGetLastError();
 }
 
