@@ -351,7 +351,7 @@ def test_c4_shape_eight_shards(sharded, oracle_mod, xbits, xlevels, ratio, xfilt
 @pytest.mark.parametrize("xq,ratio", [("1", "32"), ("8", "32"), ("8", "1")])
 def test_c4_shape_eight_shards_xscan_units(sharded, oracle_mod, xq, ratio, monkeypatch):
     """The export scan (k_xscan) with a wave per whole proxy block (1) or per
-    eighth of one (8; the default is a quarter), as lists and as bitmaps
+    eighth of one (8; by default a quarter, fewer units on large proxy regions), as lists and as bitmaps
     (CRGC_XBITMAP_RATIO=1): bit-exact against the unsharded oracle on G = 8."""
     monkeypatch.setenv("CRGC_XSCAN_Q", xq)
     monkeypatch.setenv("CRGC_XBITMAP_RATIO", ratio)
