@@ -332,9 +332,8 @@ struct Knobs {
   // (0: as many as the previous round needed, 1 .. 4)
   uint32_t round_chunk = 4;
   // CRGC_XSCAN_Q (test hook): k_xscan's units (waves) per proxy block, 1, 2, 4 or 8; 0 (default):
-  // 4 while that keeps the scan under ~2048 workgroups, fewer above (C2 over 8 logical shards: 4,
-  // 66 -> 38 us per shard and round; C4 at half size: 1, whose ~1150 workgroups already hide the
-  // latency and whose count scan grows with the grid, profiles/r6ac)
+  // 4 while the grid stays within its 8192-workgroup cap, fewer above (C2 over 8 logical shards:
+  // 66 -> 38 us per shard and round; C4 at half size 148.6 -> 135.9 us, profiles/r6ac, r6ad)
   uint32_t xscan_q = 0;
   uint64_t xbitmap_ratio = 32;   // CRGC_XBITMAP_RATIO: a mark round's home slots as a bitmap above
                                  // this many list bytes per bitmap byte (mark_all; 32: never)
@@ -2806,7 +2805,7 @@ static int mark_all(crgc_graph *h, bool investigate, uint16_t location, uint64_t
     xs.xq = h->knobs.xscan_q;
     if (xs.xq == 0) {
       xs.xq = 4;
-      while (xs.xq > 1 && npb * xs.xq > 8192) xs.xq /= 2;
+      while (xs.xq > 1 && npb * xs.xq > 32768) xs.xq /= 2;
     }
     if (xmode != 0 && h->knobs.xfilter && prev_total >= gwords && gwords) {
       if (h->x_gvis.ensure(gwords * 4 + 8) != hipSuccess) return CRGC_E_NOMEM;

@@ -2613,10 +2613,11 @@ __global__ __launch_bounds__(256) void k_xscan(DevGraph g, char *send, XSend x, 
 
 // Per key (one workgroup each): the exclusive scan of the workgroups' counts
 // in place, the total into xcnt / xcnt2.  XS consecutive workgroups' counts per
-// thread: up to 4096 workgroups in one pass (one per thread was a pass per
-// 1024, 8.4 us at C2 over 8 logical shards with quarter-block units).
+// thread: k_xscan's largest grid (8192) in one pass (one per thread was a pass
+// per 1024: 8.4 us at C2 over 8 logical shards, 15.3 at C4 half size with
+// quarter-block units, profiles/r6y, r6ac).
 __global__ __launch_bounds__(1024) void k_xscan_sum(DevGraph g, uint32_t *wgc, uint32_t nwg) {
-  constexpr uint32_t XS = 4;
+  constexpr uint32_t XS = 8;
   __shared__ uint32_t s_w[40];
   const uint32_t G = g.n_shards, q = blockIdx.x;
   uint32_t run = 0;
