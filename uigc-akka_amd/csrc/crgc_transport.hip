@@ -270,7 +270,7 @@ struct RcclTransport final : crgc_transport {
       }
       void abort() { t->abort(); }
     } q{this, s};
-    return poll_wait(q, std::chrono::seconds(timeout_s));
+    return poll_wait(q, std::chrono::seconds(timeout_s), std::chrono::microseconds(spin_us_default()));
   }
 };
 

@@ -46,9 +46,11 @@ int post_alltoallv(Ops &ops, uint32_t n_ranks, uint32_t rank, const size_t *sbyt
 }
 
 // Q: int query() (0 done, 1 pending, < 0 failed), bool async_error(),
-// void abort().  Polls until the work is done, fails, or `timeout` passes.
+// void abort().  Polls until the work is done, fails, or `timeout` passes;
+// yields between polls for the first `spin`, then sleeps 20 us between them.
 template <class Q, class Clock = std::chrono::steady_clock>
-int poll_wait(Q &q, std::chrono::nanoseconds timeout) {
+int poll_wait(Q &q, std::chrono::nanoseconds timeout,
+              std::chrono::nanoseconds spin = std::chrono::microseconds(256)) {
   const auto t0 = Clock::now();
   for (uint64_t it = 0;; ++it) {
     const int st = q.query();
@@ -68,9 +70,11 @@ int poll_wait(Q &q, std::chrono::nanoseconds timeout) {
         return CRGC_E_TIMEOUT;
       }
     }
-    // a wakeup's exchange normally completes in microseconds: spin briefly,
-    // then yield the pinned GC thread's core
-    if (it > 256) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    // a wakeup's exchange normally completes in microseconds: spin (the caller's
+    // bound), then yield the pinned GC thread's core.  A sleep ends ~50-80 us
+    // late: after 256 polls (round 5) the wait behind a sharded wakeup's level
+    // run (~1 ms) left ~90 us of idle GPU (profiles/r6ad/c2rs_last_wakeup_timeline.txt)
+    if (Clock::now() - t0 > spin) std::this_thread::sleep_for(std::chrono::microseconds(20));
     else std::this_thread::yield();
   }
 }
