@@ -5,6 +5,7 @@
 #include <chrono>
 #include <cstring>
 #include <new>
+#include <thread>
 
 #include "../../include/crgc.h"
 #include "crgc_internal.hpp"
@@ -91,19 +92,35 @@ hipError_t gather_u64_parts(const uint64_t *const *src, const uint32_t *n, uint3
 
 // A generation barrier with a bound: a shard that never arrives (its caller
 // failed before the collective) breaks the transport instead of hanging the
-// others forever.
+// others forever.  The waiters first spin (yielding) for the host-wait bound
+// (CRGC_SPIN_US) on the generation, then sleep on the condition variable: a
+// sleeper's wake-up costs tens of microseconds, and a sharded wakeup passes
+// ~50 rendezvous (two per collective).
 int LocalTransport::barrier() {
-  std::unique_lock<std::mutex> lk(m);
-  if (broken) return CRGC_E_TIMEOUT;
-  const uint64_t gen = generation;
-  if (++arrived == n_shards) {
-    arrived = 0;
-    ++generation;
-    cv.notify_all();
-    return CRGC_OK;
+  uint64_t gen;
+  {
+    std::unique_lock<std::mutex> lk(m);
+    if (broken) return CRGC_E_TIMEOUT;
+    gen = generation;
+    if (++arrived == n_shards) {
+      arrived = 0;
+      ++generation;
+      gen_seen.store(generation, std::memory_order_release);
+      cv.notify_all();
+      return CRGC_OK;
+    }
   }
+  const auto t0 = std::chrono::steady_clock::now();
+  const auto spin = std::chrono::microseconds(spin_us_default());
+  while (std::chrono::steady_clock::now() - t0 < spin) {
+    if (gen_seen.load(std::memory_order_acquire) != gen) return CRGC_OK;
+    if (broken_seen.load(std::memory_order_acquire)) return CRGC_E_TIMEOUT;
+    std::this_thread::yield();
+  }
+  std::unique_lock<std::mutex> lk(m);
   if (!cv.wait_for(lk, std::chrono::seconds(wait_s), [&] { return generation != gen || broken; })) {
     broken = true;
+    broken_seen.store(true, std::memory_order_release);
     cv.notify_all();
   }
   return broken ? CRGC_E_TIMEOUT : CRGC_OK;

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstddef>
@@ -64,6 +65,9 @@ struct LocalTransport final : crgc_transport {
   uint32_t arrived = 0;
   uint64_t generation = 0;
   bool broken = false;
+  // generation / broken for the waiters' spin phase (stored under m)
+  std::atomic<uint64_t> gen_seen{0};
+  std::atomic<bool> broken_seen{false};
   Post post[TRANSPORT_MAX_SHARDS];
 
   // A shard that never arrives (its caller failed before the collective)
