@@ -108,6 +108,24 @@ static void wait_cases() {
     s.fault_after = 3;
     CHECK(poll_wait(s, seconds(5)) == CRGC_E_DEVICE && s.aborted);
   }
+  {
+    FakeStream s;  // drains after many polls, all inside a long spin window: no 20-us sleeps
+    s.done_after = 20000;
+    const auto t0 = steady_clock::now();
+    CHECK(poll_wait(s, seconds(5), seconds(2)) == CRGC_OK && !s.aborted);
+    CHECK(steady_clock::now() - t0 < milliseconds(400));  // 20 000 sleeps would take >= 0.4 s
+  }
+  {
+    FakeStream s;  // no spin window: sleeps between polls, still completes
+    s.done_after = 30;
+    CHECK(poll_wait(s, seconds(5), nanoseconds(0)) == CRGC_OK && !s.aborted);
+  }
+  {
+    FakeStream s;  // a spin window longer than the bound: the bound still ends the wait
+    const auto t0 = steady_clock::now();
+    CHECK(poll_wait(s, milliseconds(50), seconds(10)) == CRGC_E_TIMEOUT && s.aborted);
+    CHECK(steady_clock::now() - t0 < seconds(5));
+  }
 }
 
 int main() {
